@@ -1,0 +1,203 @@
+"""Capture golden vectors from the reference monodepth2 hot path.
+
+Run in the build container only (the reference never travels to the GPU box):
+
+    python tests/golden/make_golden.py [--ref /root/reference]
+
+It imports the reference's own `trainer.py` / `layers.py` (stubbing the four
+modules that are absent here and unused by the hot path: tensorboardX, IPython,
+torchvision, skimage — SURVEY.md §8(c)), builds a minimal `self` carrying the
+state `generate_images_pred` / `compute_losses` read (trainer.py:43, 145-159), and
+runs the UNMODIFIED methods `Trainer.generate_images_pred` (trainer.py:341-391) and
+`Trainer.compute_losses` (trainer.py:407-496) followed by `backward()`.
+
+The tie-break noise drawn at trainer.py:468 is injected by temporarily replacing
+`torch.randn` with a function that hands out pre-drawn unit-normal tensors in call
+order (one per scale); the same tensors are stored in the fixture.
+
+Poses go through the reference's `transformation_from_parameters`
+(layers.py:28-45) with `invert=(f < 0)` exactly like trainer.py:294-295, so the
+fixtures also pin gradients w.r.t. axisangle/translation.
+
+Outputs: tests/golden/<case>.npz with inputs (disp_s, colours, K, inv_K,
+axisangle, translation, stereo_T, noise) and outputs (loss/s, loss, warped colours,
+samples, depth, identity_selection, argmin) and gradients (disp_s, axisangle,
+translation, cam_T_cam).  Full-size cases store scalars and gradient checksums only.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from monodepth2_amd.data import synthetic_batch, synthetic_hotpath  # noqa: E402
+
+CASES = {
+    # name: (B, H, W, frame_ids, flags, pose_scale, keep_full)
+    "mono_b2_64x128": (2, 64, 128, [0, -1, 1], {}, 0.05, True),
+    "stereo_b2_64x128": (2, 64, 128, [0, -1, 1, "s"], {}, 0.05, True),
+    "mono_bigpose_b2_64x96": (2, 64, 96, [0, -1, 1], {}, 0.4, True),
+    "no_ssim_b2_32x64": (2, 32, 64, [0, -1, 1], {"no_ssim": True}, 0.05, True),
+    "avg_reproj_b2_32x64": (2, 32, 64, [0, -1, 1], {"avg_reprojection": True}, 0.05, True),
+    "no_automask_b2_32x64": (2, 32, 64, [0, -1, 1], {"disable_automasking": True}, 0.05, True),
+    "no_automask_avg_b2_32x64": (2, 32, 64, [0, -1, 1],
+                                 {"disable_automasking": True, "avg_reprojection": True}, 0.05, True),
+    "v1_multiscale_b2_64x128": (2, 64, 128, [0, -1, 1], {"v1_multiscale": True}, 0.05, True),
+    "full_mono_b2_192x640": (2, 192, 640, [0, -1, 1], {}, 0.01, False),
+}
+
+
+def _stub_modules():
+    for name in ["tensorboardX", "IPython", "torchvision", "torchvision.models",
+                 "torchvision.transforms", "skimage", "skimage.transform"]:
+        if name not in sys.modules:
+            m = types.ModuleType(name)
+            sys.modules[name] = m
+    sys.modules["tensorboardX"].SummaryWriter = object
+    sys.modules["IPython"].embed = lambda *a, **k: None
+    tv = sys.modules["torchvision"]
+    tv.models = sys.modules["torchvision.models"]
+    tv.transforms = sys.modules["torchvision.transforms"]
+
+    class _ResNet(torch.nn.Module):       # only needed so networks/ imports
+        def __init__(self, *a, **k):
+            super().__init__()
+    tv.models.ResNet = _ResNet
+    tv.models.resnet = types.SimpleNamespace(BasicBlock=object, Bottleneck=object, model_urls={})
+    for n in ["resnet18", "resnet34", "resnet50", "resnet101", "resnet152"]:
+        setattr(tv.models, n, lambda *a, **k: None)
+
+
+def import_reference(ref):
+    _stub_modules()
+    sys.path.insert(0, ref)
+    import trainer as ref_trainer  # noqa: E402
+    import layers as ref_layers    # noqa: E402
+    return ref_trainer, ref_layers
+
+
+def run_case(ref_trainer, ref_layers, name, spec, seed=0):
+    B, H, W, frame_ids, flags, pose_scale, keep_full = spec
+    scales = [0, 1, 2, 3]
+    S = len(frame_ids) - 1
+    inputs = synthetic_batch(B, H, W, frame_ids, 4, seed=seed)
+    hp = synthetic_hotpath(B, H, W, num_src=S, seed=seed, pose_scale=pose_scale)
+    disps = {s: hp["disps"][s].clone().requires_grad_(True) for s in scales}
+    temporal = [f for f in frame_ids[1:] if f != "s"]
+    axis = hp["axisangle"][:len(temporal)].clone().requires_grad_(True)
+    trans = hp["translation"][:len(temporal)].clone().requires_grad_(True)
+
+    opt = types.SimpleNamespace(
+        scales=scales, frame_ids=list(frame_ids), height=H, width=W,
+        v1_multiscale=flags.get("v1_multiscale", False), min_depth=0.1, max_depth=100.0,
+        pose_model_type="separate_resnet", disable_automasking=flags.get("disable_automasking", False),
+        no_ssim=flags.get("no_ssim", False), avg_reprojection=flags.get("avg_reprojection", False),
+        predictive_mask=False, disparity_smoothness=1e-3, batch_size=B)
+    self = types.SimpleNamespace(opt=opt, device=torch.device("cpu"), num_scales=len(scales))
+    self.ssim = ref_layers.SSIM()
+    self.backproject_depth, self.project_3d = {}, {}
+    for s in scales:
+        h, w = H // 2 ** s, W // 2 ** s
+        self.backproject_depth[s] = ref_layers.BackprojectDepth(B, h, w)
+        self.project_3d[s] = ref_layers.Project3D(B, h, w)
+    self.compute_reprojection_loss = types.MethodType(
+        ref_trainer.Trainer.compute_reprojection_loss, self)
+
+    outputs = {("disp", s): disps[s] for s in scales}
+    camT = {}
+    for i, f in enumerate(temporal):
+        T = ref_layers.transformation_from_parameters(axis[i], trans[i], invert=(f < 0))
+        T.retain_grad()
+        outputs[("cam_T_cam", 0, f)] = T
+        camT[f] = T
+
+    # noise injection (trainer.py:468)
+    gen = torch.Generator().manual_seed(seed + 12345)
+    drawn = []
+    real_randn = torch.randn
+
+    def fake_randn(shape, device=None, **kw):
+        n = real_randn(*shape, generator=gen)
+        drawn.append(n.clone())
+        return n
+
+    ref_trainer.torch.randn = fake_randn
+    try:
+        ref_trainer.Trainer.generate_images_pred(self, inputs, outputs)
+        losses = ref_trainer.Trainer.compute_losses(self, inputs, outputs)
+    finally:
+        ref_trainer.torch.randn = real_randn
+    losses["loss"].backward()
+
+    rec = {"B": B, "H": H, "W": W, "S": S, "seed": seed, "pose_scale": pose_scale,
+           "frame_ids": np.array([str(f) for f in frame_ids]),
+           "flags": np.array(sorted(k for k, v in flags.items() if v))}
+    for s in scales:
+        rec[f"loss_{s}"] = losses[f"loss/{s}"].detach().numpy()
+        rec[f"grad_disp_{s}"] = disps[s].grad.numpy()
+    rec["loss"] = losses["loss"].detach().numpy()
+    rec["grad_axisangle"] = axis.grad.numpy()
+    rec["grad_translation"] = trans.grad.numpy()
+    for f in temporal:
+        rec[f"grad_T_{f}"] = camT[f].grad.numpy()
+        rec[f"T_{f}"] = camT[f].detach().numpy()
+    if keep_full:
+        for s in scales:
+            rec[f"disp_{s}"] = hp["disps"][s].numpy()
+            for f in frame_ids:
+                if s == 0 or f == 0 or flags.get("v1_multiscale"):
+                    rec[f"color_{f}_{s}"] = inputs[("color", f, s)].numpy()
+            rec[f"K_{s}"] = inputs[("K", s)].numpy()
+            rec[f"inv_K_{s}"] = inputs[("inv_K", s)].numpy()
+            rec[f"depth_{s}"] = outputs[("depth", 0, s)].detach().numpy()
+            for f in frame_ids[1:]:
+                rec[f"warp_{f}_{s}"] = outputs[("color", f, s)].detach().numpy()
+                rec[f"sample_{f}_{s}"] = outputs[("sample", f, s)].detach().numpy()
+            if not opt.disable_automasking:
+                rec[f"identity_selection_{s}"] = outputs[f"identity_selection/{s}"].numpy().astype(np.uint8)
+        rec["axisangle"] = axis.detach().numpy()
+        rec["translation"] = trans.detach().numpy()
+        if "stereo_T" in inputs:
+            rec["stereo_T"] = inputs["stereo_T"].numpy()
+        for i, n in enumerate(drawn):
+            rec[f"noise_{i}"] = n.numpy()
+    else:
+        for i, n in enumerate(drawn):
+            rec[f"noise_shape_{i}"] = np.array(n.shape)
+        rec["noise_seed"] = seed + 12345
+        for s in scales:
+            g = disps[s].grad
+            rec[f"grad_disp_sum_{s}"] = g.double().sum().numpy()
+            rec[f"grad_disp_abs_{s}"] = g.double().abs().sum().numpy()
+            if not opt.disable_automasking:
+                rec[f"identity_selection_mean_{s}"] = outputs[f"identity_selection/{s}"].double().mean().numpy()
+    return rec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+    torch.set_num_threads(8)
+    ref_trainer, ref_layers = import_reference(args.ref)
+    for name, spec in CASES.items():
+        if args.only and name != args.only:
+            continue
+        rec = run_case(ref_trainer, ref_layers, name, spec)
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **rec)
+        print(f"{name}: loss={float(rec['loss']):.7f} -> {os.path.relpath(path, REPO)} "
+              f"({os.path.getsize(path) / 1e6:.2f} MB)")
+
+
+if __name__ == "__main__":
+    main()
