@@ -1,0 +1,132 @@
+/*
+ * md2hot.h — C ABI of the MI355X (gfx950) monodepth2 photometric hot path.
+ *
+ * One fused operator replaces the body of
+ *   Trainer.generate_images_pred   /root/reference/trainer.py:341-391
+ *   Trainer.compute_losses         /root/reference/trainer.py:407-496
+ *   (+ compute_reprojection_loss   trainer.py:393-405, and the layers.py
+ *    primitives they call: disp_to_depth 16-25, BackprojectDepth 139-168,
+ *    Project3D 171-193, get_smooth_loss 202-215, SSIM 218-248)
+ * and the autograd backward of all of it (dL/ddisp_s for every scale and
+ * dL/dcam_T_cam for every source frame).
+ *
+ * The reference exposes no FFI: its boundary is the two Python methods above.
+ * This header is what the Python host side (monodepth2_amd/_lib.py, ctypes)
+ * binds; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Every tensor is fp32, contiguous NCHW, device memory owned by the caller
+ *    (PyTorch's caching allocator).  The library never allocates: scratch
+ *    lives in `workspace` (md2_workspace_bytes) and must be the SAME buffer for
+ *    a forward and its backward (the forward leaves per-image statistics there).
+ *  - Work is enqueued on `stream` (a hipStream_t); no host synchronisation, no
+ *    device malloc, so every call is hipGraph-capturable.
+ *  - Return 0 on success, a negative code otherwise; md2_last_error() then
+ *    describes the failure (thread-local).  Nothing in the library aborts.
+ *  - Results are deterministic: every reduction is a fixed-order tree.
+ */
+#ifndef MD2HOT_H
+#define MD2HOT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MD2_ABI_VERSION 1
+#define MD2_MAX_SCALES 4
+#define MD2_MAX_SRC 3
+
+#define MD2_OK 0
+#define MD2_ERR_ARG (-1)
+#define MD2_ERR_HIP (-2)
+
+/* opt.* switches of the reference (options.py:104-118) */
+#define MD2_NO_SSIM          (1u << 0) /* --no_ssim             trainer.py:399-403      */
+#define MD2_AVG_REPROJECTION (1u << 1) /* --avg_reprojection    trainer.py:441-442,461  */
+#define MD2_NO_AUTOMASK      (1u << 2) /* --disable_automasking trainer.py:432,466,480  */
+#define MD2_V1_MULTISCALE    (1u << 3) /* --v1_multiscale       trainer.py:347-352,417  */
+#define MD2_T_PER_SCALE      (1u << 4) /* a cam_T_cam per scale (posecnn, trainer.py:366-375) */
+
+typedef struct md2_desc {
+    int32_t batch;               /* B: images per rank (opt.batch_size)                  */
+    int32_t height, width;       /* opt.height / opt.width (full resolution)             */
+    int32_t num_src;             /* S = len(frame_ids) - 1, 1..3                          */
+    int32_t num_scales;          /* len(opt.scales) (scales are 0..num_scales-1), 1..4   */
+    uint32_t flags;              /* MD2_* above                                          */
+    float min_depth, max_depth;  /* opt.min_depth / opt.max_depth                        */
+    float disparity_smoothness;  /* opt.disparity_smoothness                             */
+    uint32_t reserved;
+    uint64_t seed;               /* tie-break noise seed when tensors.noise == NULL      */
+} md2_desc;
+
+/*
+ * Operands.  "loss resolution" of scale s is (H, W) normally and
+ * (H>>s, W>>s) with MD2_V1_MULTISCALE (trainer.py:347-352).
+ */
+typedef struct md2_tensors {
+    /* outputs[("disp", s)]: (B,1,H>>s,W>>s) */
+    const float* disp[MD2_MAX_SCALES];
+    /* inputs[("color", frame, s)]: (B,3,H>>s,W>>s); frame 0 = target (frame_ids[0]),
+     * frames 1..S = frame_ids[1:].  Targets are read at every scale (smoothness,
+     * trainer.py:423,488); sources only at the loss resolution of each scale. */
+    const float* color[MD2_MAX_SCALES][1 + MD2_MAX_SRC];
+    /* inputs[("K", s)] / inputs[("inv_K", s)]: (B,4,4); only [0] unless V1_MULTISCALE */
+    const float* K[MD2_MAX_SCALES];
+    const float* inv_K[MD2_MAX_SCALES];
+    /* cam_T_cam per source frame, stacked: (S,B,4,4); with MD2_T_PER_SCALE
+     * (num_scales,S,B,4,4).  The stereo frame passes inputs["stereo_T"]. */
+    const float* T;
+    /* Optional unit-normal tie-break noise (trainer.py:468), per scale packed
+     * back to back, scale s shaped (B, C, h_s, w_s) with C = S (or 1 with
+     * AVG_REPROJECTION) at the loss resolution.  NULL: drawn in-kernel from seed. */
+    const float* noise;
+} md2_tensors;
+
+int md2_abi_version(void);
+const char* md2_last_error(void);
+
+/* Scratch needed by one forward + backward pair (bytes, 256-B aligned). */
+size_t md2_workspace_bytes(const md2_desc* desc);
+
+/* Bytes of the per-pixel selection map the forward writes (one uint8 per
+ * loss-resolution pixel per scale, scales packed back to back). */
+size_t md2_select_bytes(const md2_desc* desc);
+
+/*
+ * Forward.  Writes loss_out[0..num_scales-1] = losses["loss/s"] and
+ * loss_out[num_scales] = losses["loss"] (trainer.py:492-495), and select_out:
+ * per pixel the argmin index into torch.cat((identity, reprojection), 1)
+ * (trainer.py:471-478); identity_selection = select > (C-1) (trainer.py:481).
+ */
+int md2_photometric_fwd(const md2_desc* desc, const md2_tensors* t,
+                        float* loss_out, uint8_t* select_out,
+                        void* workspace, void* stream);
+
+/*
+ * Backward.  grad_loss: device (num_scales+1) upstream gradients of loss_out.
+ * Writes (overwrites) grad_disp[s] shaped like disp[s], and grad_T shaped like
+ * T.  select and workspace must come from the matching forward.
+ */
+int md2_photometric_bwd(const md2_desc* desc, const md2_tensors* t,
+                        const float* grad_loss, const uint8_t* select,
+                        float* const* grad_disp, float* grad_T,
+                        void* workspace, void* stream);
+
+/*
+ * Materialise what generate_images_pred stores in `outputs` (trainer.py:356,
+ * 382, 384-387) for logging / evaluation steps.  Any pointer may be NULL.
+ *   depth_out[s]          (B,1,h_s,w_s)           outputs[("depth", 0, s)]
+ *   sample_out[s*S + f]   (B,h_s,w_s,2)           outputs[("sample", frame, s)]
+ *   color_out[s*S + f]    (B,3,h_s,w_s)           outputs[("color", frame, s)]
+ */
+int md2_generate_images(const md2_desc* desc, const md2_tensors* t,
+                        float* const* depth_out, float* const* sample_out,
+                        float* const* color_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MD2HOT_H */

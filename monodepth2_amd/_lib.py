@@ -1,0 +1,96 @@
+"""ctypes binding of the C ABI in include/md2hot.h (libmd2hot.so).
+
+There is deliberately no fallback: if the library is missing or fails to load,
+`lib()` raises.  The library must be loaded after `import torch` so that its
+libamdhip64.so.7 dependency resolves to the HIP runtime torch already loaded.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+from .build import LIB_PATH
+
+MAX_SCALES = 4
+MAX_SRC = 3
+ABI_VERSION = 1
+
+NO_SSIM = 1 << 0
+AVG_REPROJECTION = 1 << 1
+NO_AUTOMASK = 1 << 2
+V1_MULTISCALE = 1 << 3
+T_PER_SCALE = 1 << 4
+
+_vp = ctypes.c_void_p
+
+
+class Desc(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("height", ctypes.c_int32), ("width", ctypes.c_int32),
+                ("num_src", ctypes.c_int32), ("num_scales", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("min_depth", ctypes.c_float), ("max_depth", ctypes.c_float),
+                ("disparity_smoothness", ctypes.c_float), ("reserved", ctypes.c_uint32),
+                ("seed", ctypes.c_uint64)]
+
+
+class Tensors(ctypes.Structure):
+    _fields_ = [("disp", _vp * MAX_SCALES),
+                ("color", (_vp * (1 + MAX_SRC)) * MAX_SCALES),
+                ("K", _vp * MAX_SCALES),
+                ("inv_K", _vp * MAX_SCALES),
+                ("T", _vp),
+                ("noise", _vp)]
+
+
+_lock = threading.Lock()
+_lib = None
+
+EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_select_bytes",
+           "md2_photometric_fwd", "md2_photometric_bwd", "md2_generate_images"]
+
+
+def _declare(L):
+    L.md2_abi_version.restype = ctypes.c_int
+    L.md2_abi_version.argtypes = []
+    L.md2_last_error.restype = ctypes.c_char_p
+    L.md2_last_error.argtypes = []
+    L.md2_workspace_bytes.restype = ctypes.c_size_t
+    L.md2_workspace_bytes.argtypes = [ctypes.POINTER(Desc)]
+    L.md2_select_bytes.restype = ctypes.c_size_t
+    L.md2_select_bytes.argtypes = [ctypes.POINTER(Desc)]
+    L.md2_photometric_fwd.restype = ctypes.c_int
+    L.md2_photometric_fwd.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(Tensors), _vp, _vp, _vp, _vp]
+    L.md2_photometric_bwd.restype = ctypes.c_int
+    L.md2_photometric_bwd.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(Tensors), _vp, _vp,
+                                      ctypes.POINTER(_vp), _vp, _vp, _vp]
+    L.md2_generate_images.restype = ctypes.c_int
+    L.md2_generate_images.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(Tensors),
+                                      ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp]
+
+
+def lib():
+    """The loaded library; raises RuntimeError if it is not built or not loadable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"{LIB_PATH} is not built. Build it with `python -m monodepth2_amd.build` "
+                    "(hipcc --offload-arch=gfx950); there is no CPU fallback.")
+            L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            _declare(L)
+            v = L.md2_abi_version()
+            if v != ABI_VERSION:
+                raise RuntimeError(f"libmd2hot ABI {v} != expected {ABI_VERSION}")
+            _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().md2_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,1294 @@
+// md2hot.hip — hand-written CDNA4 (gfx950) kernels for the monodepth2 photometric
+// hot path, behind the C ABI declared in include/md2hot.h.
+//
+// Reference semantics (all /root/reference/...):
+//   upsample disp_s to (H,W), bilinear, align_corners=False      trainer.py:350-351
+//   depth = 1 / (1/max_depth + (1/min_depth - 1/max_depth) disp)  layers.py:16-25
+//   cam = depth * inv_K[:3,:3] @ [x,y,1];  c = (K@T)[:3] @ [cam;1]  layers.py:163-168, 182-185
+//   pix = c.xy / (c.z + 1e-7), normalised by (W-1),(H-1) to [-1,1] layers.py:187-192
+//   warp = grid_sample(color_f, pix, bilinear, border, align_corners=False)  trainer.py:384-387
+//   reproj = 0.85 mean_c SSIM(warp, target) + 0.15 mean_c |target - warp|  trainer.py:393-405
+//   SSIM: reflection pad 1, 3x3 box means, C1=1e-4, C2=9e-4, clamp [0,1]  layers.py:218-248
+//   per-pixel min over cat(identity + 1e-5 noise, reproj)  trainer.py:432-482
+//   smoothness on disp/mean(disp), edge-aware, weight w/2^s       trainer.py:486-490, layers.py:202-215
+//
+// Execution layout: one wave = one column strip of 64 lanes
+// (lane <-> image column, 1 halo lane each side in the forward, 2 in the
+// backward) x ROWS image rows walked top to bottom with a 3-row sliding window.
+// Horizontal 3-tap sums use cross-lane shuffles, vertical ones the register
+// window, so the SSIM stencil needs no LDS and no materialised warped image.
+// Every HBM-sized intermediate of the eager reference (warped images, grids,
+// SSIM maps, candidate stacks) stays in registers.
+//
+// Determinism: no float atomics.  Per-wave partial sums go to the workspace and
+// are reduced in a fixed order by single-block finalize kernels.
+
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "md2hot.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWave * kWavesPerBlock;
+constexpr int kFwdCols = kWave - 2;  // output columns per forward strip
+constexpr int kBwdCols = kWave - 4;  // output columns per backward strip
+constexpr int kRowsF = 8;            // output rows per forward wave
+constexpr int kRowsB = 8;            // output rows per backward wave
+constexpr int kSmoothChunk = 2048;   // pixels per smoothness partial
+constexpr float kC1 = 0.0001f;       // 0.01 ** 2   layers.py:231
+constexpr float kC2 = 0.0009f;       // 0.03 ** 2   layers.py:232
+constexpr float kInv9 = 1.0f / 9.0f;
+
+// ----------------------------------------------------------------------------
+// small device helpers
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ int reflect_clamp(int i, int n) {
+    i = i < 0 ? -i : i;
+    i = i >= n ? 2 * (n - 1) - i : i;
+    return min(max(i, 0), n - 1);
+}
+
+__device__ __forceinline__ float shfl_prev(float v) { return __shfl_up(v, 1, kWave); }
+__device__ __forceinline__ float shfl_next(float v) { return __shfl_down(v, 1, kWave); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+__device__ __forceinline__ float signf(float v) { return (v > 0.f) ? 1.f : ((v < 0.f) ? -1.f : 0.f); }
+
+// counter-based normal deviate for the tie-break noise (trainer.py:468)
+__device__ __forceinline__ uint32_t mix64to32(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return (uint32_t)x;
+}
+__device__ __forceinline__ float hash_normal(uint64_t seed, uint64_t idx) {
+    const uint64_t h = seed * 0x9E3779B97F4A7C15ULL + idx * 0xD1B54A32D192ED03ULL;
+    const uint32_t a = mix64to32(h), c = mix64to32(h ^ 0x5851F42D4C957F2DULL);
+    const float u1 = (float)(a >> 8) * (1.0f / 16777216.0f) + (0.5f / 16777216.0f);
+    const float u2 = (float)(c >> 8) * (1.0f / 16777216.0f);
+    return sqrtf(-2.0f * __logf(u1)) * __cosf(6.28318530718f * u2);
+}
+
+// ----------------------------------------------------------------------------
+// per-(image, frame) camera: P = (K @ T)[:3] and inv_K[:3,:3]   layers.py:164,183
+// ----------------------------------------------------------------------------
+struct Cam {
+    float iK[9];
+    float P[12];
+};
+
+__device__ __forceinline__ void load_cam(Cam& cm, const float* K, const float* iK, const float* T) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            cm.P[i * 4 + j] = K[i * 4 + 0] * T[0 * 4 + j] + K[i * 4 + 1] * T[1 * 4 + j] +
+                              K[i * 4 + 2] * T[2 * 4 + j] + K[i * 4 + 3] * T[3 * 4 + j];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) cm.iK[i * 3 + j] = iK[i * 4 + j];
+}
+
+// everything a warp of one (image, frame, scale) needs
+struct WarpCtx {
+    const float* disp;  // (dh, dw) disparity of this image at its native scale
+    int dh, dw, upsh;   // upsample factor 2^upsh to the loss resolution
+    const float* src;   // (3, h, w) source colours at the loss resolution
+    int h, w;
+    float min_disp, range;
+    Cam cm;
+};
+
+// bilinear upsample, align_corners=False (ATen area_pixel_compute_source_index)
+__device__ __forceinline__ float disp_at(const WarpCtx& c, int y, int x) {
+    if (c.upsh == 0) return c.disp[y * c.dw + x];
+    const float sc = 1.0f / (float)(1 << c.upsh);
+    const float sy = fmaxf(((float)y + 0.5f) * sc - 0.5f, 0.f);
+    const float sx = fmaxf(((float)x + 0.5f) * sc - 0.5f, 0.f);
+    const int y0 = min((int)sy, c.dh - 1), x0 = min((int)sx, c.dw - 1);
+    const int y1 = y0 + (y0 < c.dh - 1 ? 1 : 0), x1 = x0 + (x0 < c.dw - 1 ? 1 : 0);
+    const float ly1 = fminf(fmaxf(sy - (float)y0, 0.f), 1.f), lx1 = fminf(fmaxf(sx - (float)x0, 0.f), 1.f);
+    const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+    const float* r0 = c.disp + y0 * c.dw;
+    const float* r1 = c.disp + y1 * c.dw;
+    return ly0 * (lx0 * r0[x0] + lx1 * r0[x1]) + ly1 * (lx0 * r1[x0] + lx1 * r1[x1]);
+}
+
+// one projected sample: the forward values the backward chain needs
+struct Sample {
+    float depth;
+    float ray[3];   // inv_K[:3,:3] @ [x, y, 1]
+    float pt[3];    // depth * ray
+    float cam[3];   // P @ [pt; 1]
+    float den;      // cam.z + eps
+    float gmx, gmy; // grid-sample input gradient multipliers (size/2, 0 when clipped)
+    int x0, y0;
+    float tx, ty;   // fractional position inside the source cell
+};
+
+__device__ __forceinline__ void project(const WarpCtx& c, int y, int x, Sample& s) {
+    const float d = disp_at(c, y, x);
+    s.depth = 1.0f / (c.min_disp + c.range * d);
+    const float fx = (float)x, fy = (float)y;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        s.ray[i] = c.cm.iK[i * 3 + 0] * fx + c.cm.iK[i * 3 + 1] * fy + c.cm.iK[i * 3 + 2];
+        s.pt[i] = s.depth * s.ray[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        s.cam[i] = c.cm.P[i * 4 + 0] * s.pt[0] + c.cm.P[i * 4 + 1] * s.pt[1] +
+                   c.cm.P[i * 4 + 2] * s.pt[2] + c.cm.P[i * 4 + 3];
+    s.den = s.cam[2] + 1e-7f;
+    const float px = s.cam[0] / s.den, py = s.cam[1] / s.den;
+    const float gx = (px / (float)(c.w - 1) - 0.5f) * 2.f;
+    const float gy = (py / (float)(c.h - 1) - 0.5f) * 2.f;
+    // unnormalise (align_corners=False) and clip (padding_mode="border")
+    const float hw = 0.5f * (float)c.w, hh = 0.5f * (float)c.h;
+    const float ix = (gx + 1.f) * hw - 0.5f, iy = (gy + 1.f) * hh - 0.5f;
+    const float xmax = (float)(c.w - 1), ymax = (float)(c.h - 1);
+    const float ixc = fminf(fmaxf(ix, 0.f), xmax), iyc = fminf(fmaxf(iy, 0.f), ymax);
+    s.gmx = (ix > 0.f && ix < xmax) ? hw : 0.f;  // borders count as out of bounds
+    s.gmy = (iy > 0.f && iy < ymax) ? hh : 0.f;
+    const float fx0 = floorf(ixc), fy0 = floorf(iyc);
+    s.x0 = (int)fx0;
+    s.y0 = (int)fy0;
+    s.tx = ixc - fx0;
+    s.ty = iyc - fy0;
+}
+
+// the four (masked) source corners of a sample for the 3 channels
+struct Corners {
+    float nw[3], ne[3], sw[3], se[3];
+};
+
+__device__ __forceinline__ void gather(const WarpCtx& c, const Sample& s, Corners& v) {
+    const bool vx1 = s.x0 + 1 < c.w, vy1 = s.y0 + 1 < c.h;
+    const int x1 = vx1 ? s.x0 + 1 : s.x0, y1 = vy1 ? s.y0 + 1 : s.y0;
+    const int HW = c.h * c.w;
+    const int o00 = s.y0 * c.w + s.x0, o01 = s.y0 * c.w + x1, o10 = y1 * c.w + s.x0, o11 = y1 * c.w + x1;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        const float* p = c.src + ch * HW;
+        v.nw[ch] = p[o00];
+        v.ne[ch] = vx1 ? p[o01] : 0.f;
+        v.sw[ch] = vy1 ? p[o10] : 0.f;
+        v.se[ch] = (vx1 && vy1) ? p[o11] : 0.f;
+    }
+}
+
+__device__ __forceinline__ void interp(const Sample& s, const Corners& v, float out[3]) {
+    const float e = 1.f - s.tx, so = 1.f - s.ty;
+    const float wnw = so * e, wne = so * s.tx, wsw = s.ty * e, wse = s.ty * s.tx;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) out[ch] = v.nw[ch] * wnw + v.ne[ch] * wne + v.sw[ch] * wsw + v.se[ch] * wse;
+}
+
+__device__ __forceinline__ void warp_value(const WarpCtx& c, int y, int x, float out[3]) {
+    Sample s;
+    project(c, y, x, s);
+    Corners v;
+    gather(c, s, v);
+    interp(s, v, out);
+}
+
+// ----------------------------------------------------------------------------
+// SSIM pieces
+// ----------------------------------------------------------------------------
+struct H5 {  // horizontal 3-tap sums of x, x^2, x*y, y, y^2 for one channel
+    float x, xx, xy, y, yy;
+};
+
+__device__ __forceinline__ H5 hsum(float x, float y) {
+    const float xl = shfl_prev(x), xr = shfl_next(x);
+    const float yl = shfl_prev(y), yr = shfl_next(y);
+    H5 o;
+    o.x = xl + x + xr;
+    o.xx = xl * xl + x * x + xr * xr;
+    o.xy = xl * yl + x * y + xr * yr;
+    o.y = yl + y + yr;
+    o.yy = yl * yl + y * y + yr * yr;
+    return o;
+}
+
+__device__ __forceinline__ float ssim_from_sums(const H5& a, const H5& b, const H5& c) {
+    const float mx = (a.x + b.x + c.x) * kInv9, my = (a.y + b.y + c.y) * kInv9;
+    const float sx = (a.xx + b.xx + c.xx) * kInv9 - mx * mx;
+    const float sy = (a.yy + b.yy + c.yy) * kInv9 - my * my;
+    const float sxy = (a.xy + b.xy + c.xy) * kInv9 - mx * my;
+    const float n = (2.f * mx * my + kC1) * (2.f * sxy + kC2);
+    const float d = (mx * mx + my * my + kC1) * (sx + sy + kC2);
+    return fminf(fmaxf((1.f - n / d) * 0.5f, 0.f), 1.f);
+}
+
+// dL/d(box mean of x), dL/d(box mean of x^2), dL/d(box mean of x*y) at one pixel,
+// given dL/dSSIM (layers.py:238-248 differentiated by hand)
+__device__ __forceinline__ void ssim_adjoint(const H5& a, const H5& b, const H5& c, float gS, float& dA,
+                                             float& dB, float& dC) {
+    const float mx = (a.x + b.x + c.x) * kInv9, my = (a.y + b.y + c.y) * kInv9;
+    const float sx = (a.xx + b.xx + c.xx) * kInv9 - mx * mx;
+    const float sy = (a.yy + b.yy + c.yy) * kInv9 - my * my;
+    const float sxy = (a.xy + b.xy + c.xy) * kInv9 - mx * my;
+    const float n1 = 2.f * mx * my + kC1, n2 = 2.f * sxy + kC2;
+    const float d1 = mx * mx + my * my + kC1, d2 = sx + sy + kC2;
+    const float n = n1 * n2, d = d1 * d2;
+    const float raw = (1.f - n / d) * 0.5f;
+    const float g = (raw >= 0.f && raw <= 1.f) ? gS : 0.f;  // clamp passes [0,1] inclusive
+    const float dn = -0.5f * g / d;
+    const float dd = 0.5f * g * n / (d * d);
+    dA = dn * (2.f * my * (n2 - n1)) + dd * (2.f * mx * (d2 - d1));
+    dB = dd * d1;
+    dC = dn * 2.f * n1;
+}
+
+// ----------------------------------------------------------------------------
+// kernel arguments
+// ----------------------------------------------------------------------------
+struct PhotoArgs {
+    int B, h, w, S, nsc;                    // loss resolution of this launch
+    int strips, rowblocks, wpi;             // wave grid per image
+    int gscale[MD2_MAX_SCALES];             // global scale index of each local scale
+    int num_scales;                         // global number of scales
+    const float* disp[MD2_MAX_SCALES];      // per local scale
+    int dh[MD2_MAX_SCALES], dw[MD2_MAX_SCALES], upsh[MD2_MAX_SCALES];
+    const float* tgt;                       // (B,3,h,w)
+    const float* src[MD2_MAX_SRC];          // (B,3,h,w)
+    const float* K;                         // (B,4,4)
+    const float* iK;                        // (B,4,4)
+    const float* T[MD2_MAX_SCALES];         // per local scale (S,B,4,4)
+    const float* noise[MD2_MAX_SCALES];     // per local scale (B,C,h,w) or null
+    uint64_t seed;
+    float min_disp, range;
+    uint32_t flags;
+    float* photo_part[MD2_MAX_SCALES];      // fwd: per local scale [B*wpi]
+    uint8_t* sel[MD2_MAX_SCALES];           // per local scale (B,h,w)
+    // backward only
+    const float* grad_loss;                 // (num_scales + 1)
+    float* dfull[MD2_MAX_SCALES];           // per local scale (B,h,w)
+    float* dP_part[MD2_MAX_SCALES];         // per local scale [S][B*wpi][12]
+};
+
+__device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int b, WarpCtx& c) {
+    const int HW = a.h * a.w;
+    c.dh = a.dh[ls];
+    c.dw = a.dw[ls];
+    c.upsh = a.upsh[ls];
+    c.disp = a.disp[ls] + (size_t)b * c.dh * c.dw;
+    c.src = a.src[f] + (size_t)b * 3 * HW;
+    c.h = a.h;
+    c.w = a.w;
+    c.min_disp = a.min_disp;
+    c.range = a.range;
+    load_cam(c.cm, a.K + b * 16, a.iK + b * 16, a.T[ls] + ((size_t)f * a.B + b) * 16);
+}
+
+// ----------------------------------------------------------------------------
+// forward: one pass of reprojection losses for kRowsF output rows of one strip.
+// `emit(i, v)` receives the loss of output row r0+i at this lane's column; the
+// row loop stays rolled (the per-row state lives in LDS, see photo_fwd_kernel).
+// ----------------------------------------------------------------------------
+template <bool SSIM_ON, bool WARPED, class Emit>
+__device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float* tgt, int r0, int cc, Emit emit) {
+    const int h = c.h, w = c.w, HW = h * w;
+    if (!SSIM_ON) {
+        for (int i = 0; i < kRowsF; ++i) {
+            const int rr = reflect_clamp(r0 + i, h);
+            float x[3];
+            if (WARPED) {
+                warp_value(c, rr, cc, x);
+            } else {
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) x[ch] = c.src[ch * HW + rr * w + cc];
+            }
+            float l1 = 0.f;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) l1 += fabsf(tgt[ch * HW + rr * w + cc] - x[ch]);
+            emit(i, l1 / 3.f);
+        }
+        return;
+    }
+    H5 hA[3], hB[3];
+    float xB[3], yB[3];
+    for (int k = 0; k < kRowsF + 2; ++k) {
+        const int rr = reflect_clamp(r0 - 1 + k, h);
+        float x[3], y[3];
+        if (WARPED) {
+            warp_value(c, rr, cc, x);
+        } else {
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) x[ch] = c.src[ch * HW + rr * w + cc];
+        }
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) y[ch] = tgt[ch * HW + rr * w + cc];
+        H5 hc[3];
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) hc[ch] = hsum(x[ch], y[ch]);
+        if (k >= 2) {
+            float ss = 0.f, l1 = 0.f;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                ss += ssim_from_sums(hA[ch], hB[ch], hc[ch]);
+                l1 += fabsf(yB[ch] - xB[ch]);
+            }
+            emit(k - 2, 0.85f * (ss / 3.f) + 0.15f * (l1 / 3.f));
+        }
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            hA[ch] = hB[ch];
+            hB[ch] = hc[ch];
+            xB[ch] = x[ch];
+            yB[ch] = y[ch];
+        }
+    }
+}
+
+// per-wave LDS state, lane-major so every access is one conflict-free ds op
+template <int NS>
+struct FwdState {
+    float ident[NS][kRowsF][kWave];
+    float best[kRowsF][kWave];
+    float accum[kRowsF][kWave];
+    int code[kRowsF][kWave];
+};
+
+template <int NS, bool SSIM_ON>
+__global__ __launch_bounds__(kBlock, 2) void photo_fwd_kernel(PhotoArgs a) {
+    __shared__ FwdState<NS> lds[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    FwdState<NS>& L = lds[threadIdx.x >> 6];
+    const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    if (wv >= a.B * a.wpi) return;
+    const int b = wv / a.wpi, rem = wv - b * a.wpi;
+    const int rb = rem / a.strips, st = rem - rb * a.strips;
+    const int r0 = rb * kRowsF;
+    const int h = a.h, w = a.w, HW = h * w;
+    const int c = st * kFwdCols - 1 + lane;
+    const int cc = reflect_clamp(c, w);
+    const bool colok = lane >= 1 && lane <= kFwdCols && c < w;
+    const float* tgt = a.tgt + (size_t)b * 3 * HW;
+    const bool automask = !(a.flags & MD2_NO_AUTOMASK);
+    const bool avg = (a.flags & MD2_AVG_REPROJECTION) != 0;
+    const int C = avg ? 1 : NS;
+
+    // identity reprojection losses (trainer.py:432-439); scale-invariant here
+    if (automask) {
+        for (int f = 0; f < NS; ++f) {
+            WarpCtx ctx;
+            ctx.src = a.src[f] + (size_t)b * 3 * HW;
+            ctx.h = h;
+            ctx.w = w;
+            reproj_rows<SSIM_ON, false>(ctx, tgt, r0, cc, [&](int i, float v) { L.ident[f][i][lane] = v; });
+        }
+    }
+
+    for (int ls = 0; ls < a.nsc; ++ls) {
+        const int gsc = a.gscale[ls];
+        const float* nz = a.noise[ls];
+        for (int i = 0; i < kRowsF; ++i) {
+            float best = INFINITY;
+            int code = 0;
+            if (automask) {
+                const int r = min(r0 + i, h - 1);
+                for (int ch = 0; ch < C; ++ch) {
+                    float v;
+                    if (avg) {
+                        v = 0.f;
+                        for (int f = 0; f < NS; ++f) v += L.ident[f][i][lane];
+                        v = v / (float)NS;
+                    } else {
+                        v = L.ident[ch][i][lane];
+                    }
+                    const size_t nidx = (((size_t)b * C + ch) * h + r) * w + cc;
+                    const float n = nz ? nz[nidx]
+                                       : hash_normal(a.seed, ((uint64_t)gsc << 56) ^ (uint64_t)nidx);
+                    v = v + n * 1e-5f;
+                    if (v < best) {
+                        best = v;
+                        code = ch;
+                    }
+                }
+            }
+            L.best[i][lane] = best;
+            L.code[i][lane] = code;
+            L.accum[i][lane] = 0.f;
+        }
+        for (int f = 0; f < NS; ++f) {
+            WarpCtx ctx;
+            make_ctx(a, ls, f, b, ctx);
+            const int cand = (automask ? NS : 0) + f;
+            reproj_rows<SSIM_ON, true>(ctx, tgt, r0, cc, [&](int i, float v) {
+                if (avg) {
+                    L.accum[i][lane] += v;
+                } else if (v < L.best[i][lane]) {
+                    L.best[i][lane] = v;
+                    L.code[i][lane] = cand;
+                }
+            });
+        }
+        float lsum = 0.f;
+        uint8_t* sel = a.sel[ls] + (size_t)b * HW;
+        for (int i = 0; i < kRowsF; ++i) {
+            float best = L.best[i][lane];
+            int code = L.code[i][lane];
+            if (avg) {
+                const float ra = L.accum[i][lane] / (float)NS;
+                if (automask) {
+                    if (ra < best) {
+                        best = ra;
+                        code = 1;
+                    }
+                } else {
+                    best = ra;
+                }
+            }
+            const int r = r0 + i;
+            if (colok && r < h) {
+                lsum += best;
+                sel[r * w + c] = (uint8_t)code;
+            }
+        }
+        lsum = wave_sum(lsum);
+        if (lane == 0) a.photo_part[ls][wv] = lsum;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// backward: SSIM/L1 adjoint -> grid_sample backward -> projection chain
+// ----------------------------------------------------------------------------
+struct Coef {  // horizontally folded SSIM adjoint of one row, 3 channels
+    float A[3], B[3], C[3];
+    float g;     // per-pixel loss weight at this row (centre lane)
+};
+
+// weight of the reflection-padded 3-tap adjoint: how often neighbour (i-1) / (i+1)
+// contributes to position i (reflection pad folds index -1 onto 1 and n onto n-2)
+__device__ __forceinline__ float fold_lo(int i) { return i == 0 ? 0.f : (i == 1 ? 2.f : 1.f); }
+__device__ __forceinline__ float fold_hi(int i, int n) { return i == n - 1 ? 0.f : (i == n - 2 ? 2.f : 1.f); }
+
+__device__ __forceinline__ float pick(float wgt, float v) { return wgt == 0.f ? 0.f : wgt * v; }
+
+template <int NS>
+__device__ __forceinline__ float frame_weight(int code, int f, bool automask, bool avg) {
+    if (avg) {
+        if (automask) return code == 1 ? 1.f / (float)NS : 0.f;
+        return 1.f / (float)NS;
+    }
+    return code == (automask ? NS : 0) + f ? 1.f : 0.f;
+}
+
+template <int NS, bool SSIM_ON>
+__global__ __launch_bounds__(kBlock, 2) void photo_bwd_kernel(PhotoArgs a) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    if (wv >= a.B * a.wpi) return;
+    const int b = wv / a.wpi, rem = wv - b * a.wpi;
+    const int rb = rem / a.strips, st = rem - rb * a.strips;
+    const int r0 = rb * kRowsB;
+    const int h = a.h, w = a.w, HW = h * w;
+    const int c = st * kBwdCols - 2 + lane;
+    const int cc = reflect_clamp(c, w);
+    const bool colok = lane >= 2 && lane < 2 + kBwdCols && c < w;
+    const bool colreal = c >= 0 && c < w;
+    const float wl = fold_lo(c), wr = fold_hi(c, w);
+    const float* tgt = a.tgt + (size_t)b * 3 * HW;
+    const bool automask = !(a.flags & MD2_NO_AUTOMASK);
+    const bool avg = (a.flags & MD2_AVG_REPROJECTION) != 0;
+    const float l1w = SSIM_ON ? 0.15f : 1.0f;
+    const float inv_count = 1.0f / ((float)a.B * (float)HW);
+
+    for (int ls = 0; ls < a.nsc; ++ls) {
+        const int gsc = a.gscale[ls];
+        const float gscale = (a.grad_loss[gsc] + a.grad_loss[a.num_scales] / (float)a.num_scales) * inv_count;
+        const uint8_t* sel = a.sel[ls] + (size_t)b * HW;
+        float* dfull = a.dfull[ls] + (size_t)b * HW;
+        for (int f = 0; f < NS; ++f) {
+            WarpCtx ctx;
+            make_ctx(a, ls, f, b, ctx);
+            float dP[12];
+#pragma unroll
+            for (int j = 0; j < 12; ++j) dP[j] = 0.f;
+            H5 hA[3], hB[3];
+            float x1[3] = {0.f, 0.f, 0.f}, y1[3] = {0.f, 0.f, 0.f};  // row r-1
+            float x2[3] = {0.f, 0.f, 0.f}, y2[3] = {0.f, 0.f, 0.f};  // row r-2
+            Coef cA, cB;
+            for (int k = 0; k < kRowsB + 4; ++k) {
+                const int r = r0 - 2 + k;
+                const int rr = reflect_clamp(r, h);
+                float x[3], y[3];
+                warp_value(ctx, rr, cc, x);
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) y[ch] = tgt[ch * HW + rr * w + cc];
+                H5 hc[3];
+                if (SSIM_ON) {
+#pragma unroll
+                    for (int ch = 0; ch < 3; ++ch) hc[ch] = hsum(x[ch], y[ch]);
+                }
+                if (k >= 2) {
+                    // coefficient row p = r - 1
+                    const int p = r - 1;
+                    float gp = 0.f;
+                    if (colreal && p >= 0 && p < h) gp = gscale * frame_weight<NS>(sel[p * w + c], f, automask, avg);
+                    Coef cC;
+                    cC.g = gp;
+                    if (SSIM_ON) {
+                        const float gS = gp * (0.85f / 3.f);
+#pragma unroll
+                        for (int ch = 0; ch < 3; ++ch) {
+                            float dA, dB, dC;
+                            ssim_adjoint(hA[ch], hB[ch], hc[ch], gS, dA, dB, dC);
+                            if (gp == 0.f) dA = dB = dC = 0.f;
+                            cC.A[ch] = pick(wl, shfl_prev(dA)) + dA + pick(wr, shfl_next(dA));
+                            cC.B[ch] = pick(wl, shfl_prev(dB)) + dB + pick(wr, shfl_next(dB));
+                            cC.C[ch] = pick(wl, shfl_prev(dC)) + dC + pick(wr, shfl_next(dC));
+                        }
+                    }
+                    if (k >= 4) {
+                        // output row q = r - 2 (coefficient rows q-1, q, q+1 = cA, cB, cC)
+                        const int q = r - 2;
+                        if (colok && q < h) {
+                            float gw[3];
+                            const float l1c = cB.g * (l1w / 3.f);
+#pragma unroll
+                            for (int ch = 0; ch < 3; ++ch) {
+                                float g = l1c * signf(x2[ch] - y2[ch]);
+                                if (SSIM_ON) {
+                                    const float wu = fold_lo(q), wd = fold_hi(q, h);
+                                    const float aA = pick(wu, cA.A[ch]) + cB.A[ch] + pick(wd, cC.A[ch]);
+                                    const float aB = pick(wu, cA.B[ch]) + cB.B[ch] + pick(wd, cC.B[ch]);
+                                    const float aC = pick(wu, cA.C[ch]) + cB.C[ch] + pick(wd, cC.C[ch]);
+                                    g += (aA + 2.f * x2[ch] * aB + y2[ch] * aC) * kInv9;
+                                }
+                                gw[ch] = g;
+                            }
+                            if (gw[0] != 0.f || gw[1] != 0.f || gw[2] != 0.f) {
+                                Sample sm;
+                                project(ctx, q, c, sm);
+                                Corners v;
+                                gather(ctx, sm, v);
+                                const float e = 1.f - sm.tx, so = 1.f - sm.ty;
+                                float gix = 0.f, giy = 0.f;
+#pragma unroll
+                                for (int ch = 0; ch < 3; ++ch) {
+                                    gix += ((v.ne[ch] - v.nw[ch]) * so + (v.se[ch] - v.sw[ch]) * sm.ty) * gw[ch];
+                                    giy += ((v.sw[ch] - v.nw[ch]) * e + (v.se[ch] - v.ne[ch]) * sm.tx) * gw[ch];
+                                }
+                                gix *= sm.gmx;
+                                giy *= sm.gmy;
+                                const float dpx = gix * 2.f / (float)(w - 1);
+                                const float dpy = giy * 2.f / (float)(h - 1);
+                                float dc[3];
+                                dc[0] = dpx / sm.den;
+                                dc[1] = dpy / sm.den;
+                                dc[2] = -(dpx * sm.cam[0]) / (sm.den * sm.den) - (dpy * sm.cam[1]) / (sm.den * sm.den);
+#pragma unroll
+                                for (int i = 0; i < 3; ++i) {
+#pragma unroll
+                                    for (int j = 0; j < 3; ++j) dP[i * 4 + j] += dc[i] * sm.pt[j];
+                                    dP[i * 4 + 3] += dc[i];
+                                }
+                                float ddepth = 0.f;
+#pragma unroll
+                                for (int j = 0; j < 3; ++j) {
+                                    const float dpt = ctx.cm.P[0 * 4 + j] * dc[0] + ctx.cm.P[1 * 4 + j] * dc[1] +
+                                                      ctx.cm.P[2 * 4 + j] * dc[2];
+                                    ddepth += dpt * sm.ray[j];
+                                }
+                                const float dd = -ddepth * (sm.depth * sm.depth) * ctx.range;
+                                if (f == 0) dfull[q * w + c] = dd;
+                                else dfull[q * w + c] += dd;
+                            } else {
+                                if (f == 0) dfull[q * w + c] = 0.f;
+                            }
+                        }
+                    }
+                    cA = cB;
+                    cB = cC;
+                }
+                if (SSIM_ON) {
+#pragma unroll
+                    for (int ch = 0; ch < 3; ++ch) {
+                        hA[ch] = hB[ch];
+                        hB[ch] = hc[ch];
+                    }
+                }
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    x2[ch] = x1[ch];
+                    y2[ch] = y1[ch];
+                    x1[ch] = x[ch];
+                    y1[ch] = y[ch];
+                }
+            }
+            // one 12-float partial of dL/dP per (wave, frame)
+            float* dst = a.dP_part[ls] + ((size_t)f * a.B * a.wpi + wv) * 12;
+#pragma unroll
+            for (int j = 0; j < 12; ++j) {
+                const float t = wave_sum(dP[j]);
+                if (lane == 0) dst[j] = t;
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// smoothness (trainer.py:486-490, layers.py:202-215) — forward partial sums
+// ----------------------------------------------------------------------------
+struct SmoothArgs {
+    int B, num_scales;
+    int hs[MD2_MAX_SCALES], ws[MD2_MAX_SCALES], chunks[MD2_MAX_SCALES];
+    int block_base[MD2_MAX_SCALES + 1];
+    const float* disp[MD2_MAX_SCALES];
+    const float* img[MD2_MAX_SCALES];   // target colour at the native scale
+    float* part[MD2_MAX_SCALES];        // [B][chunks][3]
+};
+
+__device__ __forceinline__ float edge_weight(const float* img, int HW, int o0, int o1) {
+    const float g = (fabsf(img[o0] - img[o1]) + fabsf(img[HW + o0] - img[HW + o1]) +
+                     fabsf(img[2 * HW + o0] - img[2 * HW + o1])) / 3.f;
+    return expf(-g);
+}
+
+__device__ __forceinline__ void block_sum3(float& a, float& b, float& c) {
+    __shared__ float red[3][kWavesPerBlock];
+    a = wave_sum(a);
+    b = wave_sum(b);
+    c = wave_sum(c);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[0][wid] = a;
+        red[1][wid] = b;
+        red[2][wid] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+        b = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        c = red[2][0] + red[2][1] + red[2][2] + red[2][3];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void smooth_fwd_kernel(SmoothArgs a) {
+    int s = 0;
+    while (s + 1 < a.num_scales && (int)blockIdx.x >= a.block_base[s + 1]) ++s;
+    const int local = blockIdx.x - a.block_base[s];
+    const int b = local / a.chunks[s], chunk = local - b * a.chunks[s];
+    const int hs = a.hs[s], ws = a.ws[s], HW = hs * ws;
+    const float* d = a.disp[s] + (size_t)b * HW;
+    const float* img = a.img[s] + (size_t)b * 3 * HW;
+    float sd = 0.f, sx = 0.f, sy = 0.f;
+    const int p0 = chunk * kSmoothChunk;
+    for (int p = p0 + threadIdx.x; p < min(p0 + kSmoothChunk, HW); p += kBlock) {
+        const int i = p / ws, j = p - i * ws;
+        const float v = d[p];
+        sd += v;
+        if (j + 1 < ws) sx += fabsf(v - d[p + 1]) * edge_weight(img, HW, p, p + 1);
+        if (i + 1 < hs) sy += fabsf(v - d[p + ws]) * edge_weight(img, HW, p, p + ws);
+    }
+    block_sum3(sd, sx, sy);
+    if (threadIdx.x == 0) {
+        float* o = a.part[s] + ((size_t)b * a.chunks[s] + chunk) * 3;
+        o[0] = sd;
+        o[1] = sx;
+        o[2] = sy;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// forward finalize: fixed-order reduction of all partials -> losses + stats
+// ----------------------------------------------------------------------------
+struct FinalArgs {
+    int B, num_scales;
+    int lh[MD2_MAX_SCALES], lw[MD2_MAX_SCALES];          // loss resolution per scale
+    int hs[MD2_MAX_SCALES], ws[MD2_MAX_SCALES], chunks[MD2_MAX_SCALES];
+    int nphoto[MD2_MAX_SCALES];                           // partial count per scale
+    const float* photo_part[MD2_MAX_SCALES];
+    const float* smooth_part[MD2_MAX_SCALES];
+    float* stats;                                         // [scale][B][4]
+    float smoothness;
+    float* loss_out;
+};
+
+__global__ __launch_bounds__(kBlock) void finalize_fwd_kernel(FinalArgs a) {
+    __shared__ double red[kBlock];
+    __shared__ double sm_loss[MD2_MAX_SCALES];
+    const int t = threadIdx.x;
+    for (int s = 0; s < a.num_scales; ++s) {
+        double acc = 0.0;
+        for (int i = t; i < a.nphoto[s]; i += kBlock) acc += (double)a.photo_part[s][i];
+        red[t] = acc;
+        __syncthreads();
+        for (int o = kBlock / 2; o > 0; o >>= 1) {
+            if (t < o) red[t] += red[t + o];
+            __syncthreads();
+        }
+        double photo = red[0];
+        __syncthreads();
+        // smoothness: per image, chunks in order
+        double sm = 0.0;
+        const int hs = a.hs[s], ws = a.ws[s];
+        if (t < a.B) {
+            double sd = 0.0, sx = 0.0, sy = 0.0;
+            const float* p = a.smooth_part[s] + (size_t)t * a.chunks[s] * 3;
+            for (int k = 0; k < a.chunks[s]; ++k) {
+                sd += p[3 * k];
+                sx += p[3 * k + 1];
+                sy += p[3 * k + 2];
+            }
+            const double m = sd / ((double)hs * ws) + 1e-7;
+            sm = sx / m / ((double)a.B * hs * (ws - 1)) + sy / m / ((double)a.B * (hs - 1) * ws);
+            float* st = a.stats + ((size_t)s * a.B + t) * 4;
+            st[0] = (float)m;
+            st[1] = (float)sx;
+            st[2] = (float)sy;
+            st[3] = 0.f;
+        }
+        red[t] = sm;
+        __syncthreads();
+        for (int o = kBlock / 2; o > 0; o >>= 1) {
+            if (t < o) red[t] += red[t + o];
+            __syncthreads();
+        }
+        if (t == 0) {
+            const double photo_mean = photo / ((double)a.B * a.lh[s] * a.lw[s]);
+            sm_loss[s] = photo_mean + (double)a.smoothness * red[0] / (double)(1 << s);
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        double total = 0.0;
+        for (int s = 0; s < a.num_scales; ++s) {
+            a.loss_out[s] = (float)sm_loss[s];
+            total += sm_loss[s];
+        }
+        a.loss_out[a.num_scales] = (float)(total / a.num_scales);
+    }
+}
+
+// ----------------------------------------------------------------------------
+// dL/ddisp_s: adjoint of the bilinear upsample (gather form) + smoothness grad
+// ----------------------------------------------------------------------------
+struct DispGradArgs {
+    int B, num_scales, scale;
+    int hs, ws;          // native resolution of this scale
+    int lh, lw;          // loss resolution (= (hs<<upsh, ws<<upsh))
+    int upsh;
+    const float* dfull;  // (B, lh, lw) dL/d(upsampled disp)
+    const float* disp;   // (B, 1, hs, ws)
+    const float* img;    // (B, 3, hs, ws) target colour at this scale
+    const float* stats;  // [scale][B][4]
+    const float* grad_loss;
+    float smoothness;
+    float* out;          // (B, 1, hs, ws)
+};
+
+// weight of low-res index i in the upsample of full-res index y (factor 2^sh)
+__device__ __forceinline__ float up_weight(int y, int i, int n_in, float sc) {
+    const float sy = fmaxf(((float)y + 0.5f) * sc - 0.5f, 0.f);
+    const int y0 = min((int)sy, n_in - 1);
+    const int y1 = y0 + (y0 < n_in - 1 ? 1 : 0);
+    const float l1 = fminf(fmaxf(sy - (float)y0, 0.f), 1.f);
+    return (y0 == i ? 1.f - l1 : 0.f) + (y1 == i ? l1 : 0.f);
+}
+
+__global__ __launch_bounds__(kBlock) void disp_grad_kernel(DispGradArgs a) {
+    const int HWs = a.hs * a.ws;
+    const int idx = blockIdx.x * kBlock + threadIdx.x;
+    if (idx >= a.B * HWs) return;
+    const int b = idx / HWs, p = idx - b * HWs;
+    const int i = p / a.ws, j = p - i * a.ws;
+    const float* df = a.dfull + (size_t)b * a.lh * a.lw;
+    float acc = 0.f;
+    if (a.upsh == 0) {
+        acc = df[i * a.lw + j];
+    } else {
+        const int k = 1 << a.upsh, half = k >> 1;
+        const float sc = 1.0f / (float)k;
+        const int ylo = max(0, k * (i - 1) + half), yhi = min(a.lh, k * (i + 1) + half);
+        const int xlo = max(0, k * (j - 1) + half), xhi = min(a.lw, k * (j + 1) + half);
+        for (int y = ylo; y < yhi; ++y) {
+            const float wy = up_weight(y, i, a.hs, sc);
+            if (wy == 0.f) continue;
+            float row = 0.f;
+            for (int x = xlo; x < xhi; ++x) {
+                const float wx = up_weight(x, j, a.ws, sc);
+                row += wx * df[y * a.lw + x];
+            }
+            acc += wy * row;
+        }
+    }
+    // smoothness gradient on disp / (mean + 1e-7)
+    const int s = a.scale;
+    const float g = a.grad_loss[s] + a.grad_loss[a.num_scales] / (float)a.num_scales;
+    const float* st = a.stats + ((size_t)s * a.B + b) * 4;
+    const float m = st[0];
+    const float wsm = g * a.smoothness / (float)(1 << s);
+    const float ax = wsm / ((float)a.B * a.hs * (a.ws - 1)) / m;
+    const float ay = wsm / ((float)a.B * (a.hs - 1) * a.ws) / m;
+    const float* d = a.disp + (size_t)b * HWs;
+    const float* img = a.img + (size_t)b * 3 * HWs;
+    const float v = d[p];
+    float sg = 0.f;
+    if (j + 1 < a.ws) sg += ax * signf(v - d[p + 1]) * edge_weight(img, HWs, p, p + 1);
+    if (j > 0) sg -= ax * signf(d[p - 1] - v) * edge_weight(img, HWs, p - 1, p);
+    if (i + 1 < a.hs) sg += ay * signf(v - d[p + a.ws]) * edge_weight(img, HWs, p, p + a.ws);
+    if (i > 0) sg -= ay * signf(d[p - a.ws] - v) * edge_weight(img, HWs, p - a.ws, p);
+    sg -= (ax * st[1] + ay * st[2]) / (m * (float)HWs);
+    a.out[(size_t)b * HWs + p] = acc + sg;
+}
+
+// ----------------------------------------------------------------------------
+// dL/dT: fixed-order reduction of per-wave dL/dP partials, dT = K^T [dP; 0]
+// ----------------------------------------------------------------------------
+struct DTArgs {
+    int B, S, num_scales, per_scale;
+    int wpi[MD2_MAX_SCALES];
+    const float* dP_part[MD2_MAX_SCALES];   // [S][B*wpi][12]
+    const float* K[MD2_MAX_SCALES];         // K at each scale's loss resolution
+    float* grad_T;                          // (S,B,4,4) or (num_scales,S,B,4,4)
+};
+
+__global__ __launch_bounds__(kBlock) void grad_T_kernel(DTArgs a) {
+    // one block per (tscale, f, b)
+    const int nT = a.per_scale ? a.num_scales : 1;
+    int id = blockIdx.x;
+    const int b = id % a.B;
+    id /= a.B;
+    const int f = id % a.S;
+    const int ts = id / a.S;
+    __shared__ double red[kBlock];
+    __shared__ double dP[12];
+    double dT[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dT[j] = 0.0;
+    const int t = threadIdx.x;
+    for (int s = 0; s < a.num_scales; ++s) {
+        if (a.per_scale && s != ts) continue;
+        const int n = a.wpi[s];
+        const float* base = a.dP_part[s] + ((size_t)f * a.B * n + (size_t)b * n) * 12;
+        for (int j = 0; j < 12; ++j) {
+            double acc = 0.0;
+            for (int k = t; k < n; k += kBlock) acc += (double)base[(size_t)k * 12 + j];
+            red[t] = acc;
+            __syncthreads();
+            for (int o = kBlock / 2; o > 0; o >>= 1) {
+                if (t < o) red[t] += red[t + o];
+                __syncthreads();
+            }
+            if (t == 0) dP[j] = red[0];
+            __syncthreads();
+        }
+        const float* K = a.K[s] + b * 16;
+        for (int r = 0; r < 4; ++r)
+            for (int cidx = 0; cidx < 4; ++cidx)
+                dT[r * 4 + cidx] += (double)K[0 * 4 + r] * dP[0 * 4 + cidx] + (double)K[1 * 4 + r] * dP[1 * 4 + cidx] +
+                                    (double)K[2 * 4 + r] * dP[2 * 4 + cidx];
+        __syncthreads();
+    }
+    (void)nT;
+    if (t < 16) a.grad_T[(((size_t)ts * a.S + f) * a.B + b) * 16 + t] = (float)dT[t];
+}
+
+// ----------------------------------------------------------------------------
+// materialisation of generate_images_pred's outputs (logging / eval steps)
+// ----------------------------------------------------------------------------
+struct GenArgs {
+    PhotoArgs p;
+    int ls;
+    float* depth;    // (B,1,h,w) or null
+    float* sample[MD2_MAX_SRC];
+    float* color[MD2_MAX_SRC];
+};
+
+__global__ __launch_bounds__(kBlock) void generate_kernel(GenArgs g) {
+    const PhotoArgs& a = g.p;
+    const int HW = a.h * a.w;
+    const int idx = blockIdx.x * kBlock + threadIdx.x;
+    if (idx >= a.B * HW) return;
+    const int b = idx / HW, p = idx - b * HW;
+    const int y = p / a.w, x = p - y * a.w;
+    for (int f = 0; f < a.S; ++f) {
+        WarpCtx ctx;
+        make_ctx(a, g.ls, f, b, ctx);
+        Sample s;
+        project(ctx, y, x, s);
+        if (f == 0 && g.depth) g.depth[idx] = s.depth;
+        if (g.sample[f]) {
+            const float px = s.cam[0] / s.den, py = s.cam[1] / s.den;
+            g.sample[f][(size_t)idx * 2 + 0] = (px / (float)(a.w - 1) - 0.5f) * 2.f;
+            g.sample[f][(size_t)idx * 2 + 1] = (py / (float)(a.h - 1) - 0.5f) * 2.f;
+        }
+        if (g.color[f]) {
+            Corners v;
+            gather(ctx, s, v);
+            float o[3];
+            interp(s, v, o);
+            for (int ch = 0; ch < 3; ++ch) g.color[f][((size_t)b * 3 + ch) * HW + p] = o[ch];
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// host side
+// ----------------------------------------------------------------------------
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+struct Layout {
+    int nscales, S, B;
+    bool v1;
+    int lh[MD2_MAX_SCALES], lw[MD2_MAX_SCALES];      // loss resolution
+    int hs[MD2_MAX_SCALES], ws[MD2_MAX_SCALES];      // native resolution
+    int fstrips[MD2_MAX_SCALES], frows[MD2_MAX_SCALES], fwpi[MD2_MAX_SCALES];
+    int bstrips[MD2_MAX_SCALES], brows[MD2_MAX_SCALES], bwpi[MD2_MAX_SCALES];
+    int chunks[MD2_MAX_SCALES];
+    size_t photo_off[MD2_MAX_SCALES], dP_off[MD2_MAX_SCALES], smooth_off[MD2_MAX_SCALES];
+    size_t dfull_off[MD2_MAX_SCALES], stats_off, total;
+    size_t sel_off[MD2_MAX_SCALES], sel_total;
+    size_t noise_off[MD2_MAX_SCALES];
+};
+
+size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+int make_layout(const md2_desc* d, Layout& L) {
+    if (!d) return fail(MD2_ERR_ARG, "desc is NULL");
+    if (d->batch < 1) return fail(MD2_ERR_ARG, "batch must be >= 1 (got %d)", d->batch);
+    if (d->num_src < 1 || d->num_src > MD2_MAX_SRC)
+        return fail(MD2_ERR_ARG, "num_src must be 1..%d (got %d)", MD2_MAX_SRC, d->num_src);
+    if (d->num_scales < 1 || d->num_scales > MD2_MAX_SCALES)
+        return fail(MD2_ERR_ARG, "num_scales must be 1..%d (got %d)", MD2_MAX_SCALES, d->num_scales);
+    const int div = 1 << (d->num_scales - 1);
+    if (d->height % div || d->width % div)
+        return fail(MD2_ERR_ARG, "height/width (%d,%d) must be divisible by 2^(num_scales-1)=%d", d->height,
+                    d->width, div);
+    if ((d->height >> (d->num_scales - 1)) < 4 || (d->width >> (d->num_scales - 1)) < 4)
+        return fail(MD2_ERR_ARG, "coarsest scale must be at least 4x4");
+    if (!(d->min_depth > 0.f) || !(d->max_depth > d->min_depth))
+        return fail(MD2_ERR_ARG, "need 0 < min_depth < max_depth");
+    L.nscales = d->num_scales;
+    L.S = d->num_src;
+    L.B = d->batch;
+    L.v1 = (d->flags & MD2_V1_MULTISCALE) != 0;
+    size_t off = 0, soff = 0, noff = 0;
+    const int C = (d->flags & MD2_AVG_REPROJECTION) ? 1 : d->num_src;
+    for (int s = 0; s < L.nscales; ++s) {
+        L.hs[s] = d->height >> s;
+        L.ws[s] = d->width >> s;
+        L.lh[s] = L.v1 ? L.hs[s] : d->height;
+        L.lw[s] = L.v1 ? L.ws[s] : d->width;
+        L.fstrips[s] = (L.lw[s] + kFwdCols - 1) / kFwdCols;
+        L.frows[s] = (L.lh[s] + kRowsF - 1) / kRowsF;
+        L.fwpi[s] = L.fstrips[s] * L.frows[s];
+        L.bstrips[s] = (L.lw[s] + kBwdCols - 1) / kBwdCols;
+        L.brows[s] = (L.lh[s] + kRowsB - 1) / kRowsB;
+        L.bwpi[s] = L.bstrips[s] * L.brows[s];
+        L.chunks[s] = (L.hs[s] * L.ws[s] + kSmoothChunk - 1) / kSmoothChunk;
+        L.photo_off[s] = off;
+        off = align256(off + sizeof(float) * (size_t)L.B * L.fwpi[s]);
+        L.dP_off[s] = off;
+        off = align256(off + sizeof(float) * (size_t)L.S * L.B * L.bwpi[s] * 12);
+        L.smooth_off[s] = off;
+        off = align256(off + sizeof(float) * (size_t)L.B * L.chunks[s] * 3);
+        L.dfull_off[s] = off;
+        off = align256(off + sizeof(float) * (size_t)L.B * L.lh[s] * L.lw[s]);
+        L.sel_off[s] = soff;
+        soff += (size_t)L.B * L.lh[s] * L.lw[s];
+        L.noise_off[s] = noff;
+        noff += (size_t)L.B * C * L.lh[s] * L.lw[s];
+    }
+    L.stats_off = off;
+    off = align256(off + sizeof(float) * (size_t)L.nscales * L.B * 4);
+    L.total = off;
+    L.sel_total = soff;
+    return MD2_OK;
+}
+
+int check_tensors(const md2_desc* d, const md2_tensors* t, const Layout& L) {
+    if (!t) return fail(MD2_ERR_ARG, "tensors is NULL");
+    if (!t->T) return fail(MD2_ERR_ARG, "T is NULL");
+    for (int s = 0; s < L.nscales; ++s) {
+        if (!t->disp[s]) return fail(MD2_ERR_ARG, "disp[%d] is NULL", s);
+        if (!t->color[s][0]) return fail(MD2_ERR_ARG, "color[%d][0] (target) is NULL", s);
+        const int cs = L.v1 ? s : 0;
+        for (int f = 1; f <= L.S; ++f)
+            if (!t->color[cs][f]) return fail(MD2_ERR_ARG, "color[%d][%d] is NULL", cs, f);
+        if (!t->K[cs] || !t->inv_K[cs]) return fail(MD2_ERR_ARG, "K/inv_K[%d] is NULL", cs);
+    }
+    (void)d;
+    return MD2_OK;
+}
+
+int hip_check(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MD2_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    return MD2_OK;
+}
+
+// fill the PhotoArgs for the scale set [s_begin, s_end)
+void photo_args(const md2_desc* d, const md2_tensors* t, const Layout& L, int s_begin, int s_end, bool bwd,
+                uint8_t* ws, uint8_t* sel, PhotoArgs& a) {
+    memset(&a, 0, sizeof(a));
+    const int cs = L.v1 ? s_begin : 0;
+    a.B = L.B;
+    a.h = L.lh[s_begin];
+    a.w = L.lw[s_begin];
+    a.S = L.S;
+    a.nsc = s_end - s_begin;
+    a.strips = bwd ? L.bstrips[s_begin] : L.fstrips[s_begin];
+    a.rowblocks = bwd ? L.brows[s_begin] : L.frows[s_begin];
+    a.wpi = a.strips * a.rowblocks;
+    a.num_scales = L.nscales;
+    a.tgt = t->color[cs][0];
+    for (int f = 0; f < L.S; ++f) a.src[f] = t->color[cs][f + 1];
+    a.K = t->K[cs];
+    a.iK = t->inv_K[cs];
+    a.seed = d->seed;
+    a.min_disp = 1.0f / d->max_depth;
+    a.range = 1.0f / d->min_depth - 1.0f / d->max_depth;
+    a.flags = d->flags;
+    const size_t Tstride = (size_t)L.S * L.B * 16;
+    for (int s = s_begin; s < s_end; ++s) {
+        const int ls = s - s_begin;
+        a.gscale[ls] = s;
+        a.disp[ls] = t->disp[s];
+        a.dh[ls] = L.hs[s];
+        a.dw[ls] = L.ws[s];
+        a.upsh[ls] = L.v1 ? 0 : s;
+        a.T[ls] = t->T + ((d->flags & MD2_T_PER_SCALE) ? s * Tstride : 0);
+        a.noise[ls] = t->noise ? t->noise + L.noise_off[s] : nullptr;
+        a.photo_part[ls] = (float*)(ws + L.photo_off[s]);
+        a.sel[ls] = sel ? sel + L.sel_off[s] : nullptr;
+        a.dfull[ls] = (float*)(ws + L.dfull_off[s]);
+        a.dP_part[ls] = (float*)(ws + L.dP_off[s]);
+    }
+}
+
+template <int NS, bool SSIM>
+void launch_fwd_t(const PhotoArgs& a, hipStream_t st) {
+    const int waves = a.B * a.wpi;
+    const int blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL((photo_fwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, a);
+}
+template <int NS, bool SSIM>
+void launch_bwd_t(const PhotoArgs& a, hipStream_t st) {
+    const int waves = a.B * a.wpi;
+    const int blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL((photo_bwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, a);
+}
+
+void launch_photo(const PhotoArgs& a, bool bwd, hipStream_t st) {
+    const bool ssim = !(a.flags & MD2_NO_SSIM);
+#define MD2_DISPATCH(NS)                                          \
+    if (a.S == NS) {                                              \
+        if (bwd) {                                                \
+            if (ssim) launch_bwd_t<NS, true>(a, st);              \
+            else launch_bwd_t<NS, false>(a, st);                  \
+        } else {                                                  \
+            if (ssim) launch_fwd_t<NS, true>(a, st);              \
+            else launch_fwd_t<NS, false>(a, st);                  \
+        }                                                         \
+        return;                                                   \
+    }
+    MD2_DISPATCH(1)
+    MD2_DISPATCH(2)
+    MD2_DISPATCH(3)
+#undef MD2_DISPATCH
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int md2_abi_version(void) { return MD2_ABI_VERSION; }
+
+const char* md2_last_error(void) { return g_err; }
+
+size_t md2_workspace_bytes(const md2_desc* desc) {
+    Layout L;
+    if (make_layout(desc, L) != MD2_OK) return 0;
+    return L.total;
+}
+
+size_t md2_select_bytes(const md2_desc* desc) {
+    Layout L;
+    if (make_layout(desc, L) != MD2_OK) return 0;
+    return L.sel_total;
+}
+
+int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out, uint8_t* select_out,
+                        void* workspace, void* stream) {
+    Layout L;
+    int rc = make_layout(d, L);
+    if (rc) return rc;
+    if ((rc = check_tensors(d, t, L))) return rc;
+    if (!loss_out || !select_out || !workspace) return fail(MD2_ERR_ARG, "loss_out/select_out/workspace is NULL");
+    hipStream_t st = (hipStream_t)stream;
+    uint8_t* ws = (uint8_t*)workspace;
+    PhotoArgs a;
+    if (L.v1) {
+        for (int s = 0; s < L.nscales; ++s) {
+            photo_args(d, t, L, s, s + 1, false, ws, select_out, a);
+            launch_photo(a, false, st);
+        }
+    } else {
+        photo_args(d, t, L, 0, L.nscales, false, ws, select_out, a);
+        launch_photo(a, false, st);
+    }
+    if ((rc = hip_check("photo_fwd_kernel"))) return rc;
+
+    SmoothArgs sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.B = L.B;
+    sa.num_scales = L.nscales;
+    int blocks = 0;
+    for (int s = 0; s < L.nscales; ++s) {
+        sa.hs[s] = L.hs[s];
+        sa.ws[s] = L.ws[s];
+        sa.chunks[s] = L.chunks[s];
+        sa.block_base[s] = blocks;
+        blocks += L.B * L.chunks[s];
+        sa.disp[s] = t->disp[s];
+        sa.img[s] = t->color[s][0];
+        sa.part[s] = (float*)(ws + L.smooth_off[s]);
+    }
+    sa.block_base[L.nscales] = blocks;
+    hipLaunchKernelGGL(smooth_fwd_kernel, dim3(blocks), dim3(kBlock), 0, st, sa);
+    if ((rc = hip_check("smooth_fwd_kernel"))) return rc;
+
+    FinalArgs fa;
+    memset(&fa, 0, sizeof(fa));
+    fa.B = L.B;
+    fa.num_scales = L.nscales;
+    for (int s = 0; s < L.nscales; ++s) {
+        fa.lh[s] = L.lh[s];
+        fa.lw[s] = L.lw[s];
+        fa.hs[s] = L.hs[s];
+        fa.ws[s] = L.ws[s];
+        fa.chunks[s] = L.chunks[s];
+        fa.nphoto[s] = L.B * L.fwpi[s];
+        fa.photo_part[s] = (const float*)(ws + L.photo_off[s]);
+        fa.smooth_part[s] = (const float*)(ws + L.smooth_off[s]);
+    }
+    fa.stats = (float*)(ws + L.stats_off);
+    fa.smoothness = d->disparity_smoothness;
+    fa.loss_out = loss_out;
+    if (L.B > kBlock) return fail(MD2_ERR_ARG, "batch > %d not supported by the finalize kernel", kBlock);
+    hipLaunchKernelGGL(finalize_fwd_kernel, dim3(1), dim3(kBlock), 0, st, fa);
+    return hip_check("finalize_fwd_kernel");
+}
+
+int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* grad_loss, const uint8_t* select,
+                        float* const* grad_disp, float* grad_T, void* workspace, void* stream) {
+    Layout L;
+    int rc = make_layout(d, L);
+    if (rc) return rc;
+    if ((rc = check_tensors(d, t, L))) return rc;
+    if (!grad_loss || !select || !grad_disp || !grad_T || !workspace)
+        return fail(MD2_ERR_ARG, "grad_loss/select/grad_disp/grad_T/workspace is NULL");
+    for (int s = 0; s < L.nscales; ++s)
+        if (!grad_disp[s]) return fail(MD2_ERR_ARG, "grad_disp[%d] is NULL", s);
+    hipStream_t st = (hipStream_t)stream;
+    uint8_t* ws = (uint8_t*)workspace;
+    PhotoArgs a;
+    if (L.v1) {
+        for (int s = 0; s < L.nscales; ++s) {
+            photo_args(d, t, L, s, s + 1, true, ws, (uint8_t*)select, a);
+            a.grad_loss = grad_loss;
+            launch_photo(a, true, st);
+        }
+    } else {
+        photo_args(d, t, L, 0, L.nscales, true, ws, (uint8_t*)select, a);
+        a.grad_loss = grad_loss;
+        launch_photo(a, true, st);
+    }
+    if ((rc = hip_check("photo_bwd_kernel"))) return rc;
+
+    for (int s = 0; s < L.nscales; ++s) {
+        DispGradArgs g;
+        memset(&g, 0, sizeof(g));
+        g.B = L.B;
+        g.num_scales = L.nscales;
+        g.scale = s;
+        g.hs = L.hs[s];
+        g.ws = L.ws[s];
+        g.lh = L.lh[s];
+        g.lw = L.lw[s];
+        g.upsh = L.v1 ? 0 : s;
+        g.dfull = (const float*)(ws + L.dfull_off[s]);
+        g.disp = t->disp[s];
+        g.img = t->color[s][0];
+        g.stats = (const float*)(ws + L.stats_off);
+        g.grad_loss = grad_loss;
+        g.smoothness = d->disparity_smoothness;
+        g.out = grad_disp[s];
+        const int n = L.B * L.hs[s] * L.ws[s];
+        hipLaunchKernelGGL(disp_grad_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, g);
+    }
+    if ((rc = hip_check("disp_grad_kernel"))) return rc;
+
+    DTArgs ta;
+    memset(&ta, 0, sizeof(ta));
+    ta.B = L.B;
+    ta.S = L.S;
+    ta.num_scales = L.nscales;
+    ta.per_scale = (d->flags & MD2_T_PER_SCALE) ? 1 : 0;
+    for (int s = 0; s < L.nscales; ++s) {
+        ta.wpi[s] = L.B ? L.bwpi[s] : 0;
+        ta.dP_part[s] = (const float*)(ws + L.dP_off[s]);
+        ta.K[s] = t->K[L.v1 ? s : 0];
+    }
+    ta.grad_T = grad_T;
+    const int nT = ta.per_scale ? L.nscales : 1;
+    hipLaunchKernelGGL(grad_T_kernel, dim3(nT * L.S * L.B), dim3(kBlock), 0, st, ta);
+    return hip_check("grad_T_kernel");
+}
+
+int md2_generate_images(const md2_desc* d, const md2_tensors* t, float* const* depth_out, float* const* sample_out,
+                        float* const* color_out, void* stream) {
+    Layout L;
+    int rc = make_layout(d, L);
+    if (rc) return rc;
+    if ((rc = check_tensors(d, t, L))) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    for (int s = 0; s < L.nscales; ++s) {
+        GenArgs g;
+        memset(&g, 0, sizeof(g));
+        photo_args(d, t, L, L.v1 ? s : 0, L.v1 ? s + 1 : L.nscales, false, nullptr, nullptr, g.p);
+        g.ls = L.v1 ? 0 : s;
+        g.depth = depth_out ? depth_out[s] : nullptr;
+        for (int f = 0; f < L.S; ++f) {
+            g.sample[f] = sample_out ? sample_out[s * L.S + f] : nullptr;
+            g.color[f] = color_out ? color_out[s * L.S + f] : nullptr;
+        }
+        const int n = L.B * L.lh[s] * L.lw[s];
+        hipLaunchKernelGGL(generate_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, g);
+    }
+    return hip_check("generate_kernel");
+}
+
+}  // extern "C"

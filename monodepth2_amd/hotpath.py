@@ -1,0 +1,245 @@
+"""The fused photometric hot path as a torch.autograd.Function over the C ABI.
+
+`photometric_loss(...)` replaces, forward and backward, everything
+`Trainer.generate_images_pred` (trainer.py:341-391) and `Trainer.compute_losses`
+(trainer.py:407-496) compute: upsample -> depth -> back-project -> project ->
+border bilinear warp -> SSIM+L1 -> per-pixel min over identity/reprojection with
+tie-break noise -> mean, plus edge-aware smoothness, for every scale.
+
+Inputs are the reference's own tensors (no repacking): disparities per scale,
+colour pyramids, K / inv_K and the stacked cam_T_cam.  Gradients flow to the
+disparities and to T; colours, intrinsics and noise are constants (as in the
+reference, where they never require grad).
+
+There is no eager fallback: the library must be built and the tensors must be on
+a ROCm device, otherwise this raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from . import _lib
+
+
+@dataclass(frozen=True)
+class HotPathConfig:
+    """POD view of the `opt.*` fields the hot path reads (md2_desc)."""
+    batch: int
+    height: int
+    width: int
+    num_src: int
+    num_scales: int = 4
+    min_depth: float = 0.1
+    max_depth: float = 100.0
+    disparity_smoothness: float = 1e-3
+    no_ssim: bool = False
+    avg_reprojection: bool = False
+    disable_automasking: bool = False
+    v1_multiscale: bool = False
+    t_per_scale: bool = False
+
+    @property
+    def flags(self) -> int:
+        f = 0
+        f |= _lib.NO_SSIM if self.no_ssim else 0
+        f |= _lib.AVG_REPROJECTION if self.avg_reprojection else 0
+        f |= _lib.NO_AUTOMASK if self.disable_automasking else 0
+        f |= _lib.V1_MULTISCALE if self.v1_multiscale else 0
+        f |= _lib.T_PER_SCALE if self.t_per_scale else 0
+        return f
+
+    def desc(self, seed: int = 0) -> _lib.Desc:
+        return _lib.Desc(self.batch, self.height, self.width, self.num_src, self.num_scales, self.flags,
+                         self.min_depth, self.max_depth, self.disparity_smoothness, 0, seed & (2 ** 64 - 1))
+
+    def loss_res(self, s: int):
+        if self.v1_multiscale:
+            return self.height >> s, self.width >> s
+        return self.height, self.width
+
+    def noise_channels(self) -> int:
+        return 1 if self.avg_reprojection else self.num_src
+
+    def noise_shape(self, s: int):
+        h, w = self.loss_res(s)
+        return (self.batch, self.noise_channels(), h, w)
+
+
+def _stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _require(t: torch.Tensor, name: str, shape, device):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a tensor")
+    if t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
+    if t.dtype != torch.float32:
+        raise ValueError(f"{name} must be float32 (got {t.dtype})")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
+
+
+class Operands:
+    """The non-differentiable operands of one call, validated and made contiguous.
+
+    colors[s][fi]: (B,3,H>>s,W>>s) with fi=0 the target and fi=1..S the sources;
+    entries the configuration never reads may be None.  K / inv_K: per scale
+    (B,4,4) (only scale 0 unless v1_multiscale).
+    """
+
+    def __init__(self, cfg: HotPathConfig, colors: Sequence[Sequence[Optional[torch.Tensor]]],
+                 K: Sequence[Optional[torch.Tensor]], inv_K: Sequence[Optional[torch.Tensor]],
+                 noise: Optional[Dict[int, torch.Tensor]], device: torch.device):
+        B, H, W, S = cfg.batch, cfg.height, cfg.width, cfg.num_src
+        self.cfg = cfg
+        self.colors: List[List[Optional[torch.Tensor]]] = [[None] * (1 + S) for _ in range(cfg.num_scales)]
+        self.K: List[Optional[torch.Tensor]] = [None] * cfg.num_scales
+        self.inv_K: List[Optional[torch.Tensor]] = [None] * cfg.num_scales
+        for s in range(cfg.num_scales):
+            shp = (B, 3, H >> s, W >> s)
+            t = colors[s][0]
+            _require(t, f"color[{s}][target]", shp, device)
+            self.colors[s][0] = t.contiguous()
+            if cfg.v1_multiscale or s == 0:
+                for fi in range(1, S + 1):
+                    t = colors[s][fi]
+                    _require(t, f"color[{s}][{fi}]", shp, device)
+                    self.colors[s][fi] = t.contiguous()
+                _require(K[s], f"K[{s}]", (B, 4, 4), device)
+                _require(inv_K[s], f"inv_K[{s}]", (B, 4, 4), device)
+                self.K[s] = K[s].contiguous()
+                self.inv_K[s] = inv_K[s].contiguous()
+        self.noise = None
+        if noise is not None:
+            parts = []
+            for s in range(cfg.num_scales):
+                _require(noise[s], f"noise[{s}]", cfg.noise_shape(s), device)
+                parts.append(noise[s].reshape(-1))
+            self.noise = torch.cat(parts).contiguous()
+
+    def struct(self, disps: Sequence[torch.Tensor], T: torch.Tensor) -> _lib.Tensors:
+        st = _lib.Tensors()
+        for s, d in enumerate(disps):
+            st.disp[s] = d.data_ptr()
+        for s in range(self.cfg.num_scales):
+            for fi, c in enumerate(self.colors[s]):
+                if c is not None:
+                    st.color[s][fi] = c.data_ptr()
+            if self.K[s] is not None:
+                st.K[s] = self.K[s].data_ptr()
+                st.inv_K[s] = self.inv_K[s].data_ptr()
+        st.T = T.data_ptr()
+        st.noise = self.noise.data_ptr() if self.noise is not None else None
+        return st
+
+
+class _PhotometricLoss(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, cfg: HotPathConfig, ops: Operands, seed: int, T: torch.Tensor, *disps: torch.Tensor):
+        L = _lib.lib()
+        dev = T.device
+        desc = cfg.desc(seed)
+        st = ops.struct(disps, T)
+        ws = torch.empty(L.md2_workspace_bytes(ctypes.byref(desc)), dtype=torch.uint8, device=dev)
+        sel = torch.empty(L.md2_select_bytes(ctypes.byref(desc)), dtype=torch.uint8, device=dev)
+        loss = torch.empty(cfg.num_scales + 1, dtype=torch.float32, device=dev)
+        _lib.check(L.md2_photometric_fwd(ctypes.byref(desc), ctypes.byref(st), loss.data_ptr(), sel.data_ptr(),
+                                         ws.data_ptr(), _stream_ptr(dev)), "md2_photometric_fwd")
+        ctx.save_for_backward(T, *disps)
+        ctx.cfg, ctx.ops, ctx.seed, ctx.ws, ctx.sel = cfg, ops, seed, ws, sel
+        ctx.mark_non_differentiable(sel)
+        return loss, sel
+
+    @staticmethod
+    def backward(ctx, grad_loss, _grad_sel):
+        L = _lib.lib()
+        T, *disps = ctx.saved_tensors
+        cfg = ctx.cfg
+        dev = T.device
+        if grad_loss is None:
+            grad_loss = torch.zeros(cfg.num_scales + 1, dtype=torch.float32, device=dev)
+        grad_loss = grad_loss.contiguous().float()
+        desc = cfg.desc(ctx.seed)
+        st = ctx.ops.struct(disps, T)
+        gdisp = [torch.empty_like(d) for d in disps]
+        gT = torch.empty_like(T)
+        arr = (ctypes.c_void_p * _lib.MAX_SCALES)(*([g.data_ptr() for g in gdisp]
+                                                    + [None] * (_lib.MAX_SCALES - len(gdisp))))
+        _lib.check(L.md2_photometric_bwd(ctypes.byref(desc), ctypes.byref(st), grad_loss.data_ptr(),
+                                         ctx.sel.data_ptr(), arr, gT.data_ptr(), ctx.ws.data_ptr(),
+                                         _stream_ptr(dev)), "md2_photometric_bwd")
+        return (None, None, None, gT, *gdisp)
+
+
+def photometric_loss(cfg: HotPathConfig, disps: Sequence[torch.Tensor], colors, K, inv_K, T: torch.Tensor,
+                     noise: Optional[Dict[int, torch.Tensor]] = None, seed: int = 0):
+    """Fused hot path.  Returns (loss_vec, select).
+
+    loss_vec[s] = losses["loss/s"], loss_vec[num_scales] = losses["loss"];
+    select is the packed per-scale argmin map (uint8), see `selection_maps`.
+    T: (S,B,4,4) stacked cam_T_cam (or (num_scales,S,B,4,4) with t_per_scale).
+    noise: optional {scale: unit-normal (B,C,h,w)}; None draws it in-kernel from seed.
+    """
+    dev = T.device
+    if dev.type != "cuda":
+        raise RuntimeError("photometric_loss runs on the GPU only (HIP kernels); got device " + str(dev))
+    B, H, W, S = cfg.batch, cfg.height, cfg.width, cfg.num_src
+    if len(disps) != cfg.num_scales:
+        raise ValueError(f"expected {cfg.num_scales} disparity maps, got {len(disps)}")
+    disps = [d.contiguous() for d in disps]
+    for s, d in enumerate(disps):
+        _require(d, f"disp[{s}]", (B, 1, H >> s, W >> s), dev)
+    tshape = (cfg.num_scales, S, B, 4, 4) if cfg.t_per_scale else (S, B, 4, 4)
+    _require(T, "T", tshape, dev)
+    ops = Operands(cfg, colors, K, inv_K, noise, dev)
+    return _PhotometricLoss.apply(cfg, ops, int(seed), T.contiguous(), *disps)
+
+
+def selection_maps(cfg: HotPathConfig, select: torch.Tensor) -> Dict[int, torch.Tensor]:
+    """Unpack the argmin map into per-scale (B,h,w) index tensors."""
+    out, off = {}, 0
+    for s in range(cfg.num_scales):
+        h, w = cfg.loss_res(s)
+        n = cfg.batch * h * w
+        out[s] = select[off:off + n].view(cfg.batch, h, w)
+        off += n
+    return out
+
+
+def generate_images(cfg: HotPathConfig, disps, colors, K, inv_K, T, want_depth=True, want_sample=True,
+                    want_color=True):
+    """Materialise generate_images_pred's outputs (no autograd): returns
+    {"depth": {s: (B,1,h,w)}, "sample": {(f,s): (B,h,w,2)}, "color": {(f,s): (B,3,h,w)}}
+    with f the source index 0..S-1."""
+    L = _lib.lib()
+    dev = T.device
+    disps = [d.contiguous() for d in disps]
+    ops = Operands(cfg, colors, K, inv_K, None, dev)
+    st = ops.struct(disps, T.contiguous())
+    desc = cfg.desc()
+    S = cfg.num_src
+    depth, sample, color = {}, {}, {}
+    dptr = (ctypes.c_void_p * _lib.MAX_SCALES)()
+    sptr = (ctypes.c_void_p * (_lib.MAX_SCALES * _lib.MAX_SRC))()
+    cptr = (ctypes.c_void_p * (_lib.MAX_SCALES * _lib.MAX_SRC))()
+    for s in range(cfg.num_scales):
+        h, w = cfg.loss_res(s)
+        if want_depth:
+            depth[s] = torch.empty(cfg.batch, 1, h, w, device=dev)
+            dptr[s] = depth[s].data_ptr()
+        for f in range(S):
+            if want_sample:
+                sample[(f, s)] = torch.empty(cfg.batch, h, w, 2, device=dev)
+                sptr[s * S + f] = sample[(f, s)].data_ptr()
+            if want_color:
+                color[(f, s)] = torch.empty(cfg.batch, 3, h, w, device=dev)
+                cptr[s * S + f] = color[(f, s)].data_ptr()
+    _lib.check(L.md2_generate_images(ctypes.byref(desc), ctypes.byref(st), dptr, sptr, cptr, _stream_ptr(dev)),
+               "md2_generate_images")
+    return {"depth": depth, "sample": sample, "color": color}

@@ -119,13 +119,16 @@ def smooth_loss(disp, img):
 
 def hot_path(opt: HotPathOptions, disps: Dict[int, torch.Tensor], inputs: Dict,
              cam_T: Dict, noise: Optional[Dict[int, torch.Tensor]] = None,
-             keep_images: bool = True):
+             keep_images: bool = True, selection: Optional[Dict[int, torch.Tensor]] = None):
     """One forward of generate_images_pred + compute_losses.
 
     disps: {scale: (B,1,H/2^s,W/2^s)}; inputs: reference-keyed dict with
     ("color", f, s), ("K", s), ("inv_K", s); cam_T: {frame_id: (B,4,4)} (for "s"
     pass inputs["stereo_T"]); noise: {scale: unit-normal tensor shaped like the
     identity losses} (trainer.py:468-469 multiplies it by 1e-5).
+    selection: test-only {scale: (B,h,w) int64} pinning the per-pixel argmin of
+    trainer.py:478 to given indices, so that gradients of two fp32
+    implementations can be compared where rounding flips near-tied candidates.
 
     Returns (losses, outputs) with the reference's keys.
     """
@@ -176,6 +179,9 @@ def hot_path(opt: HotPathOptions, disps: Dict[int, torch.Tensor], inputs: Dict,
             combined = reproj
         if combined.shape[1] == 1:
             to_opt = combined
+        elif selection is not None:
+            idxs = selection[s].to(torch.int64)
+            to_opt = combined.gather(1, idxs.unsqueeze(1)).squeeze(1)
         else:
             to_opt, idxs = torch.min(combined, dim=1)
         if not opt.disable_automasking:

@@ -1,0 +1,85 @@
+"""Shared helpers: run a golden case through the HIP hot path and through the oracle."""
+from __future__ import annotations
+
+import torch
+
+from golden_io import Case
+from monodepth2_amd.hotpath import HotPathConfig, photometric_loss, selection_maps, generate_images
+from monodepth2_amd.layers import transformation_from_parameters
+
+
+def case_config(case: Case) -> HotPathConfig:
+    return HotPathConfig(batch=case.B, height=case.H, width=case.W, num_src=case.S, num_scales=4,
+                         no_ssim="no_ssim" in case.flags, avg_reprojection="avg_reprojection" in case.flags,
+                         disable_automasking="disable_automasking" in case.flags,
+                         v1_multiscale="v1_multiscale" in case.flags)
+
+
+def case_operands(case: Case, device):
+    frames = case.frame_ids[1:]
+    colors = [[None] * (1 + case.S) for _ in range(4)]
+    for s in range(4):
+        colors[s][0] = case.inputs[("color", 0, s)].to(device)
+        for fi, f in enumerate(frames):
+            key = ("color", f, s)
+            if key in case.inputs:
+                colors[s][fi + 1] = case.inputs[key].to(device)
+    K = [case.inputs[("K", s)].to(device) for s in range(4)]
+    inv_K = [case.inputs[("inv_K", s)].to(device) for s in range(4)]
+    noise = {s: n.to(device) for s, n in case.noise.items()} if case.noise else None
+    return colors, K, inv_K, noise
+
+
+def run_hip(case: Case, device="cuda"):
+    """Forward + backward on the GPU; returns dict of numpy results."""
+    cfg = case_config(case)
+    colors, K, inv_K, noise = case_operands(case, device)
+    disps = [case.disps[s].to(device).clone().requires_grad_(True) for s in range(4)]
+    axis = case.axisangle.to(device).clone().requires_grad_(True)
+    trans = case.translation.to(device).clone().requires_grad_(True)
+    Ts = []
+    ti = 0
+    for f in case.frame_ids[1:]:
+        if f == "s":
+            Ts.append(case.inputs["stereo_T"].to(device))
+        else:
+            Ts.append(transformation_from_parameters(axis[ti], trans[ti], invert=(f < 0)))
+            ti += 1
+    T = torch.stack(Ts, 0)
+    T.retain_grad()
+    loss, sel = photometric_loss(cfg, disps, colors, K, inv_K, T, noise=noise)
+    loss[cfg.num_scales].backward()
+    torch.cuda.synchronize()
+    out = {"loss": loss.detach().cpu().numpy(), "grad_disp": [d.grad.cpu().numpy() for d in disps],
+           "grad_axis": axis.grad.cpu().numpy(), "grad_trans": trans.grad.cpu().numpy(),
+           "grad_T": T.grad.cpu().numpy(), "select": {s: v.cpu().numpy() for s, v in selection_maps(cfg, sel).items()}}
+    with torch.no_grad():
+        T2 = T.detach()
+        out["gen"] = generate_images(cfg, [d.detach() for d in disps], colors, K, inv_K, T2)
+    return cfg, out
+
+
+def run_oracle(case: Case, selection=None):
+    """The CPU oracle on the case's inputs; selection optionally pins the argmin."""
+    from oracle.md2_oracle import HotPathOptions, hot_path
+    opt = HotPathOptions(height=case.H, width=case.W, frame_ids=case.frame_ids,
+                         v1_multiscale="v1_multiscale" in case.flags, no_ssim="no_ssim" in case.flags,
+                         avg_reprojection="avg_reprojection" in case.flags,
+                         disable_automasking="disable_automasking" in case.flags)
+    disps = {s: d.clone().requires_grad_(True) for s, d in case.disps.items()}
+    axis = case.axisangle.clone().requires_grad_(True)
+    trans = case.translation.clone().requires_grad_(True)
+    camT = {}
+    for i, f in enumerate(case.temporal):
+        camT[f] = transformation_from_parameters(axis[i], trans[i], invert=(f < 0))
+    if "s" in case.frame_ids:
+        camT["s"] = case.inputs["stereo_T"]
+    sel = None
+    if selection is not None:
+        sel = {s: torch.from_numpy(v).long() for s, v in selection.items()}
+    losses, outputs = hot_path(opt, disps, case.inputs, camT, noise=case.noise if case.noise else None,
+                               selection=sel)
+    losses["loss"].backward()
+    return {"loss": [float(losses[f"loss/{s}"]) for s in range(4)] + [float(losses["loss"])],
+            "grad_disp": [disps[s].grad.numpy() for s in range(4)],
+            "grad_axis": axis.grad.numpy(), "grad_trans": trans.grad.numpy(), "outputs": outputs}
