@@ -1,0 +1,263 @@
+"""Training throughput benchmark (BASELINE.json metric: training images/sec at
+640x192 mono, 1/2/4/8 GPUs; loss delta vs reference).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Workload (configs[1] of BASELINE.json): mono 640x192, ResNet-18 depth encoder +
+DepthDecoder + separate ResNet-18 pose encoder + PoseDecoder, frame_ids [0,-1,1],
+batch 12 per GPU, fp32, Adam step — one full `Trainer.train_step` per step, with
+the photometric hot path (warp + SSIM/L1 + min-reprojection + smoothness, fwd+bwd)
+in the fused HIP kernels.  Synthetic KITTI-shaped inputs resident in HBM, random
+init weights (no network for ImageNet weights).  Data parallel: one process per
+GPU, each with its own 12-image shard (weak scaling), DDP gradient all-reduce over
+RCCL.  Rank 0 prints ONE JSON line.
+
+Extra fields:
+  roofline      — the dominant HIP kernel (photo_bwd_kernel), HIP-event timed on
+                  its launch stream during the timed steps; algorithmic bytes per
+                  launch = B * 4*H*W*(3 + 3S + 1.328125 + 1 + 4);
+                  traffic from profiles/<round>/pmc_traffic.json when present.
+  cpu_baseline  — rank 0, N=1: the same training step on the host cores with the
+                  oracle hot path (oracle/md2_oracle.py, op-for-op restatement of
+                  the reference), a bounded sample of steps at batch 4 (configs[0]).
+  loss_delta_vs_oracle — |loss_GPU - loss_oracle| on identical inputs, weights and
+                  tie-break noise (first step).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+# MIOpen: heuristic (immediate-mode) solver choice instead of an exhaustive find that
+# compiles every candidate kernel on a fresh box (minutes with no kernel cache)
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "training images/sec at 640x192 mono, 1/2/4/8 GPUs; loss delta vs ref"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, HBM3E spec
+VALU_ISSUE_PEAK = 256 * 4 * 0.5 * 2.4e9   # wave-instructions/s: 256 CU x 4 SIMD x 1 per 2 clk x 2.4 GHz
+ROUND = "r01"
+
+
+def photo_bwd_bytes(B, H, W, S, nscales=4):
+    """Algorithmic HBM bytes of one photo_bwd_kernel launch: read target + S sources
+    (3 ch fp32), the disparity pyramid (fp32), the per-scale selection maps (u8);
+    write the per-scale full-resolution dL/ddisp (fp32)."""
+    N = H * W
+    pyr = sum(1.0 / 4 ** s for s in range(nscales))
+    return B * N * (4 * 3 * (1 + S) + 4 * pyr + 1 * nscales + 4 * nscales)
+
+
+def photo_fwd_bytes(B, H, W, S, nscales=4):
+    N = H * W
+    pyr = sum(1.0 / 4 ** s for s in range(nscales))
+    return B * N * (4 * 3 * (1 + S) + 4 * pyr + 1 * nscales)
+
+
+_T0 = time.perf_counter()
+
+
+def log(msg):
+    if int(os.environ.get("RANK", 0)) == 0:
+        print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=12, help="images per GPU")
+    ap.add_argument("--height", type=int, default=192)
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--num_layers", type=int, default=18)
+    ap.add_argument("--stereo", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen exhaustive find per conv shape")
+    return ap.parse_args()
+
+
+def make_trainer(args, device, rank, world):
+    from monodepth2_amd.options import default_options
+    from monodepth2_amd.trainer import Trainer
+    opt = default_options(batch_size=args.batch, height=args.height, width=args.width,
+                          num_layers=args.num_layers, weights_init="scratch", use_stereo=args.stereo,
+                          frame_ids=[0, -1, 1], log_dir="/tmp/md2_bench")
+    return Trainer(opt, device=device, rank=rank, world_size=world)
+
+
+def loss_delta_vs_oracle(trainer, batch):
+    """Same weights, inputs and noise: GPU fused hot path vs CPU oracle."""
+    from monodepth2_amd.hotpath import photometric_loss
+    from oracle.md2_oracle import HotPathOptions, hot_path
+    with torch.no_grad():
+        outputs = trainer.nets(trainer, batch)
+    hot = trainer.hot
+    gen = torch.Generator().manual_seed(1234)
+    noise = {s: torch.randn(*hot.noise_shape(s), generator=gen) for s in range(hot.num_scales)}
+    K, iK = trainer._intrinsics(batch)
+    T = trainer._stacked_T(batch, outputs).detach()
+    disps = [outputs[("disp", s)].detach() for s in range(hot.num_scales)]
+    loss, _ = photometric_loss(hot, disps, trainer._colors(batch), K, iK, T,
+                               noise={s: n.to(T.device) for s, n in noise.items()})
+    cpu_inputs = {k: v.detach().cpu() for k, v in batch.items()}
+    camT = {f: T[i].cpu() for i, f in enumerate(trainer.src_frames)}
+    opt = HotPathOptions(height=hot.height, width=hot.width, frame_ids=trainer.opt.frame_ids)
+    with torch.no_grad():
+        ref, _ = hot_path(opt, {s: d.cpu() for s, d in enumerate(disps)}, cpu_inputs, camT, noise=noise,
+                          keep_images=False)
+    return abs(float(loss[hot.num_scales]) - float(ref["loss"]))
+
+
+def cpu_baseline(args):
+    """The reference-equivalent training step on the host CPU (oracle hot path)."""
+    import torch.optim as optim
+    from monodepth2_amd import networks
+    from monodepth2_amd.data import synthetic_batch
+    from monodepth2_amd.layers import transformation_from_parameters
+    from oracle.md2_oracle import HotPathOptions, hot_path
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        cores = os.cpu_count()
+    cores = max(1, min(cores, 16))   # the GPU box's CPU share is 16 cores
+    torch.set_num_threads(cores)
+    B, H, W = 4, args.height, args.width          # configs[0]: batch 4 on the CPU
+    frame_ids = [0, -1, 1]
+    enc = networks.ResnetEncoder(args.num_layers, False)
+    dec = networks.DepthDecoder(enc.num_ch_enc, range(4))
+    penc = networks.ResnetEncoder(args.num_layers, False, num_input_images=2)
+    pdec = networks.PoseDecoder(penc.num_ch_enc, 1, 2)
+    params = [p for m in (enc, dec, penc, pdec) for p in m.parameters()]
+    adam = optim.Adam(params, 1e-4)
+    inputs = synthetic_batch(B, H, W, frame_ids, 4, seed=5)
+    opt = HotPathOptions(height=H, width=W, frame_ids=frame_ids)
+
+    def step():
+        outputs = dec(enc(inputs[("color_aug", 0, 0)]))
+        camT = {}
+        for f in frame_ids[1:]:
+            pair = [inputs[("color_aug", f, 0)], inputs[("color_aug", 0, 0)]] if f < 0 else \
+                [inputs[("color_aug", 0, 0)], inputs[("color_aug", f, 0)]]
+            a, t = pdec([penc(torch.cat(pair, 1))])
+            camT[f] = transformation_from_parameters(a[:, 0], t[:, 0], invert=(f < 0))
+        losses, _ = hot_path(opt, {s: outputs[("disp", s)] for s in range(4)}, inputs, camT, keep_images=False)
+        adam.zero_grad()
+        losses["loss"].backward()
+        adam.step()
+
+    step()  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or n >= 50:
+            break
+    return {"value": round(B * n / el, 4), "unit": "images/s", "cores": cores, "kind": "port",
+            "sample": f"{n} full training steps (R{args.num_layers} enc+dec+pose, oracle hot path, Adam) "
+                      f"at batch {B}, {W}x{H}, fp32, torch CPU {cores} threads, {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    from monodepth2_amd.distributed import init_process_group
+    from monodepth2_amd import _lib
+    from monodepth2_amd.data import synthetic_batch
+
+    rank, local_rank, world = init_process_group()
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    torch.backends.cudnn.benchmark = args.cudnn_benchmark
+    _lib.lib()
+    log(f"world={world} device={torch.cuda.get_device_name(device)}")
+
+    trainer = make_trainer(args, device, rank, world)
+    frame_ids = trainer.opt.frame_ids
+    batch = synthetic_batch(args.batch, args.height, args.width, frame_ids, 4, seed=100 + rank, device=device)
+    log("trainer + batch ready")
+
+    delta = None
+    if not args.no_parity and rank == 0:
+        delta = loss_delta_vs_oracle(trainer, batch)
+        log(f"loss delta vs oracle = {delta:.3e}")
+
+    trainer.set_train()
+    for i in range(args.warmup):
+        t = time.perf_counter()
+        trainer.train_step(batch)
+        torch.cuda.synchronize()
+        log(f"warmup step {i}: {1e3 * (time.perf_counter() - t):.1f} ms")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    with _lib.KernelTimer(max_launches=4 * args.steps + 8) as kt:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            _, losses = trainer.train_step(batch)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    final_loss = float(losses["loss"])
+
+    if rank == 0:
+        S = len(frame_ids) - 1
+        B, H, W = args.batch, args.height, args.width
+        bwd_ms = kt.bwd_ms / max(kt.n_bwd, 1)
+        fwd_ms = kt.fwd_ms / max(kt.n_fwd, 1)
+        alg = photo_bwd_bytes(B, H, W, S)
+        achieved = alg / (bwd_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", ROUND, "pmc_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("photo_bwd_kernel_bytes_per_launch")
+        roof = {"bound": "hbm", "kernel": "photo_bwd_kernel", "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": traffic, "algorithmic_bytes_per_launch": int(alg),
+                "avg_launch_ms": round(bwd_ms, 5), "launches": kt.n_bwd,
+                "fwd_kernel_avg_ms": round(fwd_ms, 5),
+                "fwd_kernel_gbs": round(photo_fwd_bytes(B, H, W, S) / (fwd_ms * 1e-3) / 1e9, 2)}
+        log(f"timed: {1e3 * dt / args.steps:.2f} ms/step, photo_bwd {bwd_ms:.3f} ms, photo_fwd {fwd_ms:.3f} ms")
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args)
+            log(f"cpu baseline: {cpu['value']} img/s")
+        value = world * B * args.steps / dt
+        line = {"metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic (KITTI-shaped smooth textures, random-init weights)",
+                "config": {"workload": f"{'mono+stereo' if args.stereo else 'mono'}_{W}x{H} ResNet-{args.num_layers}"
+                                       f" batch={B}/GPU full train step (configs[1])",
+                           "global_batch": B * world, "height": H, "width": W, "frame_ids": [str(f) for f in frame_ids],
+                           "parallelism": f"dp{world}"},
+                "roofline": roof, "cpu_baseline": cpu,
+                "loss_delta_vs_oracle": delta, "final_loss": round(final_loss, 6)}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

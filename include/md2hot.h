@@ -126,6 +126,17 @@ int md2_generate_images(const md2_desc* desc, const md2_tensors* t,
                         float* const* depth_out, float* const* sample_out,
                         float* const* color_out, void* stream);
 
+/*
+ * Optional kernel timing for benchmarks: between md2_timing_begin and
+ * md2_timing_end every launch of the two photometric kernels (the forward
+ * photo kernel and the backward photo kernel, which dominate the hot path) is
+ * bracketed by hipEvents recorded on the launch stream.  md2_timing_end waits
+ * for the last event and returns the summed durations (ms) and launch counts.
+ * Not for use under graph capture (events are recorded eagerly).
+ */
+int md2_timing_begin(int max_launches);
+int md2_timing_end(double* fwd_ms, int* n_fwd, double* bwd_ms, int* n_bwd);
+
 #ifdef __cplusplus
 }
 #endif

@@ -48,7 +48,8 @@ _lock = threading.Lock()
 _lib = None
 
 EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_select_bytes",
-           "md2_photometric_fwd", "md2_photometric_bwd", "md2_generate_images"]
+           "md2_photometric_fwd", "md2_photometric_bwd", "md2_generate_images",
+           "md2_timing_begin", "md2_timing_end"]
 
 
 def _declare(L):
@@ -68,6 +69,11 @@ def _declare(L):
     L.md2_generate_images.restype = ctypes.c_int
     L.md2_generate_images.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(Tensors),
                                       ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp]
+    L.md2_timing_begin.restype = ctypes.c_int
+    L.md2_timing_begin.argtypes = [ctypes.c_int]
+    L.md2_timing_end.restype = ctypes.c_int
+    L.md2_timing_end.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
 
 
 def lib():
@@ -94,3 +100,24 @@ def check(rc: int, what: str):
     if rc != 0:
         msg = lib().md2_last_error().decode(errors="replace")
         raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+class KernelTimer:
+    """Context manager around md2_timing_begin/end: average photo-kernel durations."""
+
+    def __init__(self, max_launches: int = 4096):
+        self.max_launches = max_launches
+        self.fwd_ms = self.bwd_ms = 0.0
+        self.n_fwd = self.n_bwd = 0
+
+    def __enter__(self):
+        check(lib().md2_timing_begin(self.max_launches), "md2_timing_begin")
+        return self
+
+    def __exit__(self, *exc):
+        f, b = ctypes.c_double(), ctypes.c_double()
+        nf, nb = ctypes.c_int(), ctypes.c_int()
+        check(lib().md2_timing_end(ctypes.byref(f), ctypes.byref(nf), ctypes.byref(b), ctypes.byref(nb)),
+              "md2_timing_end")
+        self.fwd_ms, self.n_fwd, self.bwd_ms, self.n_bwd = f.value, nf.value, b.value, nb.value
+        return False

@@ -31,6 +31,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <mutex>
+#include <vector>
+
 #include "md2hot.h"
 
 namespace {
@@ -948,6 +951,30 @@ __global__ __launch_bounds__(kBlock) void generate_kernel(GenArgs g) {
 // ----------------------------------------------------------------------------
 thread_local char g_err[512] = "";
 
+// optional benchmark timing of the photometric kernels (md2_timing_begin/end)
+struct Timing {
+    std::mutex mu;
+    bool on = false;
+    int cap = 0, used = 0;
+    std::vector<hipEvent_t> ev;   // pairs: [2*i] start, [2*i+1] stop
+    std::vector<int> kind;        // 0 fwd, 1 bwd
+};
+Timing g_timing;
+
+// returns the slot index or -1
+int timing_start(int kind, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(g_timing.mu);
+    if (!g_timing.on || g_timing.used >= g_timing.cap) return -1;
+    const int i = g_timing.used++;
+    g_timing.kind[i] = kind;
+    hipEventRecord(g_timing.ev[2 * i], st);
+    return i;
+}
+void timing_stop(int slot, hipStream_t st) {
+    if (slot < 0) return;
+    hipEventRecord(g_timing.ev[2 * slot + 1], st);
+}
+
 int fail(int code, const char* fmt, ...) {
     va_list ap;
     va_start(ap, fmt);
@@ -1150,6 +1177,7 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
     hipStream_t st = (hipStream_t)stream;
     uint8_t* ws = (uint8_t*)workspace;
     PhotoArgs a;
+    const int slot = timing_start(0, st);
     if (L.v1) {
         for (int s = 0; s < L.nscales; ++s) {
             photo_args(d, t, L, s, s + 1, false, ws, select_out, a);
@@ -1159,6 +1187,7 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
         photo_args(d, t, L, 0, L.nscales, false, ws, select_out, a);
         launch_photo(a, false, st);
     }
+    timing_stop(slot, st);
     if ((rc = hip_check("photo_fwd_kernel"))) return rc;
 
     SmoothArgs sa;
@@ -1215,6 +1244,7 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
     hipStream_t st = (hipStream_t)stream;
     uint8_t* ws = (uint8_t*)workspace;
     PhotoArgs a;
+    const int slot = timing_start(1, st);
     if (L.v1) {
         for (int s = 0; s < L.nscales; ++s) {
             photo_args(d, t, L, s, s + 1, true, ws, (uint8_t*)select, a);
@@ -1226,6 +1256,7 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
         a.grad_loss = grad_loss;
         launch_photo(a, true, st);
     }
+    timing_stop(slot, st);
     if ((rc = hip_check("photo_bwd_kernel"))) return rc;
 
     for (int s = 0; s < L.nscales; ++s) {
@@ -1289,6 +1320,42 @@ int md2_generate_images(const md2_desc* d, const md2_tensors* t, float* const* d
         hipLaunchKernelGGL(generate_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, g);
     }
     return hip_check("generate_kernel");
+}
+
+int md2_timing_begin(int max_launches) {
+    std::lock_guard<std::mutex> lk(g_timing.mu);
+    if (max_launches < 1) return fail(MD2_ERR_ARG, "max_launches must be >= 1");
+    for (hipEvent_t e : g_timing.ev) hipEventDestroy(e);
+    g_timing.ev.assign(2 * (size_t)max_launches, nullptr);
+    g_timing.kind.assign(max_launches, 0);
+    for (auto& e : g_timing.ev)
+        if (hipEventCreate(&e) != hipSuccess) return fail(MD2_ERR_HIP, "hipEventCreate failed");
+    g_timing.cap = max_launches;
+    g_timing.used = 0;
+    g_timing.on = true;
+    return MD2_OK;
+}
+
+int md2_timing_end(double* fwd_ms, int* n_fwd, double* bwd_ms, int* n_bwd) {
+    std::lock_guard<std::mutex> lk(g_timing.mu);
+    if (!g_timing.on) return fail(MD2_ERR_ARG, "md2_timing_begin was not called");
+    g_timing.on = false;
+    double tot[2] = {0.0, 0.0};
+    int cnt[2] = {0, 0};
+    for (int i = 0; i < g_timing.used; ++i) {
+        if (hipEventSynchronize(g_timing.ev[2 * i + 1]) != hipSuccess)
+            return fail(MD2_ERR_HIP, "hipEventSynchronize failed");
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, g_timing.ev[2 * i], g_timing.ev[2 * i + 1]) != hipSuccess)
+            return fail(MD2_ERR_HIP, "hipEventElapsedTime failed");
+        tot[g_timing.kind[i]] += ms;
+        cnt[g_timing.kind[i]] += 1;
+    }
+    if (fwd_ms) *fwd_ms = tot[0];
+    if (n_fwd) *n_fwd = cnt[0];
+    if (bwd_ms) *bwd_ms = tot[1];
+    if (n_bwd) *n_bwd = cnt[1];
+    return MD2_OK;
 }
 
 }  // extern "C"

@@ -1,0 +1,68 @@
+"""Single-node data parallelism: one process per GPU, RCCL over xGMI.
+
+The reference is single-GPU (README.md:147-155).  Every sample of the hot path is
+independent, so the batch shards over ranks with no collective on the data path;
+the only exchange is the gradient all-reduce (average) of the networks, done by
+DDP in buckets overlapped with the backward pass.
+On ROCm the "nccl" backend of torch.distributed is RCCL.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Tuple
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+# R18 depth+pose nets carry 26.8 M trainable fp32 parameters (107 MB of gradients);
+# 64 MB buckets give two all-reduces per step, each big enough to use every xGMI link
+BUCKET_CAP_MB = 64
+
+
+def env_world() -> Tuple[int, int, int]:
+    """(rank, local_rank, world_size) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def init_process_group(backend: str = None) -> Tuple[int, int, int]:
+    rank, local_rank, world = env_world()
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
+    return rank, local_rank, world
+
+
+def ignored_parameters(module: nn.Module):
+    """Parameters that never receive a gradient: the ImageNet classifier heads of the
+    ResNet encoders (`encoder.fc.*`, kept only for checkpoint key parity)."""
+    return [n for n, _ in module.named_parameters() if n.endswith("encoder.fc.weight")
+            or n.endswith("encoder.fc.bias")]
+
+
+def wrap_ddp(module: nn.Module, device: torch.device):
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    DDP._set_params_and_buffers_to_ignore_for_model(module, ignored_parameters(module))
+    kw = dict(broadcast_buffers=False, bucket_cap_mb=BUCKET_CAP_MB, gradient_as_bucket_view=True)
+    if device.type == "cuda":
+        kw.update(device_ids=[device.index], output_device=device.index)
+    return DDP(module, **kw)
+
+
+def shard(batch: Dict, rank: int, world: int) -> Dict:
+    """Contiguous B/world slice of every batched tensor of a reference-keyed batch."""
+    out = {}
+    for k, v in batch.items():
+        if k == "stereo_T" or (isinstance(k, tuple) and k[0] in ("color", "color_aug", "K", "inv_K")):
+            n = v.shape[0] // world
+            out[k] = v[rank * n:(rank + 1) * n]
+        else:
+            out[k] = v
+    return out

@@ -1,0 +1,108 @@
+"""Depth and pose decoders (PyTorch-ROCm modules; convolutions run on MIOpen).
+
+Restates `networks/depth_decoder.py:14-65`, `networks/pose_decoder.py:14-54` and
+`networks/pose_cnn.py:14-50` with identical constructor signatures, forward
+outputs and parameter names (`decoder.{i}.conv.conv.weight`, `net.{i}.weight`),
+so reference checkpoints load unchanged.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from ..layers import Conv3x3, ConvBlock, upsample
+
+
+class DepthDecoder(nn.Module):
+    """5-level skip decoder with sigmoid disparity heads (depth_decoder.py:14-65).
+
+    Module order inside `decoder` (state-dict indices): for i = 4..0 the pair
+    (upconv i 0, upconv i 1), then one dispconv per scale.
+    """
+
+    def __init__(self, num_ch_enc, scales=range(4), num_output_channels=1, use_skips=True):
+        super().__init__()
+        self.num_output_channels = num_output_channels
+        self.use_skips = use_skips
+        self.upsample_mode = "nearest"
+        self.scales = scales
+        self.num_ch_enc = num_ch_enc
+        self.num_ch_dec = np.array([16, 32, 64, 128, 256])
+        ch_enc, ch_dec = self.num_ch_enc, self.num_ch_dec
+        self.convs = {}
+        mods = []
+        for i in range(4, -1, -1):
+            cin = ch_enc[-1] if i == 4 else ch_dec[i + 1]
+            self.convs[("upconv", i, 0)] = ConvBlock(cin, ch_dec[i])
+            cin = ch_dec[i] + (ch_enc[i - 1] if (use_skips and i > 0) else 0)
+            self.convs[("upconv", i, 1)] = ConvBlock(cin, ch_dec[i])
+            mods += [self.convs[("upconv", i, 0)], self.convs[("upconv", i, 1)]]
+        for s in self.scales:
+            self.convs[("dispconv", s)] = Conv3x3(ch_dec[s], num_output_channels)
+            mods.append(self.convs[("dispconv", s)])
+        self.decoder = nn.ModuleList(mods)
+        self.sigmoid = nn.Sigmoid()
+
+    def forward(self, input_features):
+        self.outputs = {}
+        x = input_features[-1]
+        for i in range(4, -1, -1):
+            x = upsample(self.convs[("upconv", i, 0)](x))
+            if self.use_skips and i > 0:
+                x = torch.cat([x, input_features[i - 1]], 1)
+            x = self.convs[("upconv", i, 1)](x)
+            if i in self.scales:
+                self.outputs[("disp", i)] = self.sigmoid(self.convs[("dispconv", i)](x))
+        return self.outputs
+
+
+class PoseDecoder(nn.Module):
+    """Pose head: squeeze + 3 convs + spatial mean, scaled by 0.01 (pose_decoder.py:14-54)."""
+
+    def __init__(self, num_ch_enc, num_input_features, num_frames_to_predict_for=None, stride=1):
+        super().__init__()
+        self.num_ch_enc = num_ch_enc
+        self.num_input_features = num_input_features
+        if num_frames_to_predict_for is None:
+            num_frames_to_predict_for = num_input_features - 1
+        self.num_frames_to_predict_for = num_frames_to_predict_for
+        self.convs = {
+            "squeeze": nn.Conv2d(self.num_ch_enc[-1], 256, 1),
+            ("pose", 0): nn.Conv2d(num_input_features * 256, 256, 3, stride, 1),
+            ("pose", 1): nn.Conv2d(256, 256, 3, stride, 1),
+            ("pose", 2): nn.Conv2d(256, 6 * num_frames_to_predict_for, 1),
+        }
+        self.relu = nn.ReLU()
+        self.net = nn.ModuleList([self.convs["squeeze"], self.convs[("pose", 0)], self.convs[("pose", 1)],
+                                  self.convs[("pose", 2)]])
+
+    def forward(self, input_features):
+        x = torch.cat([self.relu(self.convs["squeeze"](f[-1])) for f in input_features], 1)
+        x = self.relu(self.convs[("pose", 0)](x))
+        x = self.relu(self.convs[("pose", 1)](x))
+        x = self.convs[("pose", 2)](x)
+        x = 0.01 * x.mean(3).mean(2).view(-1, self.num_frames_to_predict_for, 1, 6)
+        return x[..., :3], x[..., 3:]
+
+
+class PoseCNN(nn.Module):
+    """Stand-alone pose network of Zhou et al. (pose_cnn.py:14-50)."""
+
+    def __init__(self, num_input_frames):
+        super().__init__()
+        self.num_input_frames = num_input_frames
+        spec = [(3 * num_input_frames, 16, 7, 3), (16, 32, 5, 2), (32, 64, 3, 1), (64, 128, 3, 1),
+                (128, 256, 3, 1), (256, 256, 3, 1), (256, 256, 3, 1)]
+        self.convs = {i: nn.Conv2d(cin, cout, k, 2, p) for i, (cin, cout, k, p) in enumerate(spec)}
+        self.pose_conv = nn.Conv2d(256, 6 * (num_input_frames - 1), 1)
+        self.num_convs = len(self.convs)
+        self.relu = nn.ReLU(True)
+        self.net = nn.ModuleList([self.convs[i] for i in range(self.num_convs)])
+
+    def forward(self, out):
+        for i in range(self.num_convs):
+            out = self.relu(self.convs[i](out))
+        out = self.pose_conv(out).mean(3).mean(2)
+        out = 0.01 * out.view(-1, self.num_input_frames - 1, 1, 6)
+        return out[..., :3], out[..., 3:]

@@ -1,0 +1,353 @@
+"""Training step with the fused HIP photometric hot path.
+
+Counterpart of the reference `Trainer` (trainer.py:29-630) restricted to what a
+training step needs.  The networks stay PyTorch-ROCm modules (networks/*);
+`generate_images_pred` + `compute_losses` (trainer.py:341-496) run as ONE fused
+autograd op over hand-written HIP kernels (`monodepth2_amd.hotpath`).
+
+Differences from the reference, all deliberate:
+  * data comes from an iterable of reference-keyed batches (synthetic KITTI-shaped
+    tensors by default, `data.synthetic_batch`) instead of the JPEG loader;
+  * the tie-break noise of trainer.py:468 is drawn inside the kernel from a
+    counter-based generator (seed = noise_seed, step, rank) — no randn launches;
+  * `generate_images_pred` materialises warped colours / samples / depth only when
+    asked (logging, evaluation or `--materialize_images`), because the fused loss
+    does not need them;
+  * data parallelism: one process per GPU, DDP over RCCL (backend "nccl") with the
+    gradient all-reduce bucketed and overlapped with the backward pass.  The
+    reference is single-GPU (README.md:147-155).
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import Dict, Iterable, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+import torch.optim as optim
+
+from . import networks
+from .distributed import wrap_ddp
+from .hotpath import HotPathConfig, generate_images, photometric_loss, selection_maps
+from .layers import compute_depth_errors, disp_to_depth, transformation_from_parameters
+
+
+def _sec_to_hm_str(t):
+    t = int(t)
+    s = t % 60
+    t //= 60
+    m = t % 60
+    t //= 60
+    return "{:02d}h{:02d}m{:02d}s".format(t, m, s)
+
+
+class _Networks(nn.Module):
+    """All trainable networks behind one module so DDP sees a single graph."""
+
+    def __init__(self, models: Dict[str, nn.Module]):
+        super().__init__()
+        self.models = nn.ModuleDict(models)
+
+    def forward(self, trainer: "Trainer", inputs):
+        return trainer._run_networks(self.models, inputs)
+
+
+class Trainer:
+    def __init__(self, options, device: Optional[torch.device] = None, rank: int = 0, world_size: int = 1):
+        self.opt = options
+        self.log_path = os.path.join(self.opt.log_dir, self.opt.model_name)
+        assert self.opt.height % 32 == 0, "'height' must be a multiple of 32"
+        assert self.opt.width % 32 == 0, "'width' must be a multiple of 32"
+        if self.opt.no_cuda:
+            raise RuntimeError("the MI355X build has no CPU training path: the hot path is HIP-only")
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.rank, self.world_size = rank, world_size
+
+        self.num_scales = len(self.opt.scales)
+        if list(self.opt.scales) != list(range(self.num_scales)):
+            raise ValueError("scales must be 0..n-1 (got {})".format(self.opt.scales))
+        self.num_input_frames = len(self.opt.frame_ids)
+        self.num_pose_frames = 2 if self.opt.pose_model_input == "pairs" else self.num_input_frames
+        assert self.opt.frame_ids[0] == 0, "frame_ids must start with 0"
+        self.use_pose_net = not (self.opt.use_stereo and self.opt.frame_ids == [0])
+        if self.opt.use_stereo and "s" not in self.opt.frame_ids:
+            self.opt.frame_ids = list(self.opt.frame_ids) + ["s"]
+        if self.opt.predictive_mask:
+            assert self.opt.disable_automasking, \
+                "When using predictive_mask, please disable automasking with --disable_automasking"
+            raise NotImplementedError("--predictive_mask is not supported by the fused hot path yet")
+
+        pretrained = self.opt.weights_init == "pretrained"
+        self.models: Dict[str, nn.Module] = {}
+        self.models["encoder"] = networks.ResnetEncoder(self.opt.num_layers, pretrained)
+        self.models["depth"] = networks.DepthDecoder(self.models["encoder"].num_ch_enc, self.opt.scales)
+        if self.use_pose_net:
+            if self.opt.pose_model_type == "separate_resnet":
+                self.models["pose_encoder"] = networks.ResnetEncoder(
+                    self.opt.num_layers, pretrained, num_input_images=self.num_pose_frames)
+                self.models["pose"] = networks.PoseDecoder(self.models["pose_encoder"].num_ch_enc,
+                                                           num_input_features=1, num_frames_to_predict_for=2)
+            elif self.opt.pose_model_type == "shared":
+                self.models["pose"] = networks.PoseDecoder(self.models["encoder"].num_ch_enc, self.num_pose_frames)
+            elif self.opt.pose_model_type == "posecnn":
+                self.models["pose"] = networks.PoseCNN(
+                    self.num_input_frames if self.opt.pose_model_input == "all" else 2)
+        for m in self.models.values():
+            m.to(self.device)
+        self.nets = _Networks(self.models)
+        self.parameters_to_train = [p for m in self.models.values() for p in m.parameters()]
+
+        self.ddp = wrap_ddp(self.nets, self.device) if world_size > 1 else None
+
+        self.model_optimizer = optim.Adam(self.parameters_to_train, self.opt.learning_rate)
+        self.model_lr_scheduler = optim.lr_scheduler.StepLR(self.model_optimizer, self.opt.scheduler_step_size, 0.1)
+        if self.opt.load_weights_folder is not None:
+            self.load_model()
+
+        self.src_frames = list(self.opt.frame_ids[1:])
+        self.hot = HotPathConfig(
+            batch=self.opt.batch_size, height=self.opt.height, width=self.opt.width,
+            num_src=len(self.src_frames), num_scales=self.num_scales, min_depth=self.opt.min_depth,
+            max_depth=self.opt.max_depth, disparity_smoothness=self.opt.disparity_smoothness,
+            no_ssim=self.opt.no_ssim, avg_reprojection=self.opt.avg_reprojection,
+            disable_automasking=self.opt.disable_automasking, v1_multiscale=self.opt.v1_multiscale,
+            t_per_scale=self.opt.pose_model_type == "posecnn")
+        self.noise_override = None   # {scale: unit-normal noise}; tests pin the tie-break noise with it
+        self.depth_metric_names = ["de/abs_rel", "de/sq_rel", "de/rms", "de/log_rms", "da/a1", "da/a2", "da/a3"]
+        self.epoch = 0
+        self.step = 0
+
+    # ------------------------------------------------------------------ modes
+    def set_train(self):
+        for m in self.models.values():
+            m.train()
+
+    def set_eval(self):
+        for m in self.models.values():
+            m.eval()
+
+    # ------------------------------------------------------------- networks
+    def _run_networks(self, models, inputs):
+        """Encoder, depth decoder and pose networks (trainer.py:234-255)."""
+        if self.opt.pose_model_type == "shared":
+            all_color_aug = torch.cat([inputs[("color_aug", i, 0)] for i in self.opt.frame_ids])
+            all_features = models["encoder"](all_color_aug)
+            all_features = [torch.split(f, self.opt.batch_size) for f in all_features]
+            features = {k: [f[i] for f in all_features] for i, k in enumerate(self.opt.frame_ids)}
+            outputs = models["depth"](features[0])
+        else:
+            features = models["encoder"](inputs["color_aug", 0, 0])
+            outputs = models["depth"](features)
+        if self.use_pose_net:
+            outputs.update(self.predict_poses(inputs, features, models))
+        return outputs
+
+    def predict_poses(self, inputs, features, models=None):
+        """trainer.py:262-318."""
+        models = models if models is not None else self.models
+        outputs = {}
+        if self.num_pose_frames == 2:
+            if self.opt.pose_model_type == "shared":
+                pose_feats = {f_i: features[f_i] for f_i in self.opt.frame_ids}
+            else:
+                pose_feats = {f_i: inputs["color_aug", f_i, 0] for f_i in self.opt.frame_ids}
+            for f_i in self.opt.frame_ids[1:]:
+                if f_i == "s":
+                    continue
+                pair = [pose_feats[f_i], pose_feats[0]] if f_i < 0 else [pose_feats[0], pose_feats[f_i]]
+                if self.opt.pose_model_type == "separate_resnet":
+                    pair = [models["pose_encoder"](torch.cat(pair, 1))]
+                elif self.opt.pose_model_type == "posecnn":
+                    pair = torch.cat(pair, 1)
+                axisangle, translation = models["pose"](pair)
+                outputs[("axisangle", 0, f_i)] = axisangle
+                outputs[("translation", 0, f_i)] = translation
+                outputs[("cam_T_cam", 0, f_i)] = transformation_from_parameters(
+                    axisangle[:, 0], translation[:, 0], invert=(f_i < 0))
+        else:
+            if self.opt.pose_model_type in ["separate_resnet", "posecnn"]:
+                pose_inputs = torch.cat([inputs[("color_aug", i, 0)] for i in self.opt.frame_ids if i != "s"], 1)
+                if self.opt.pose_model_type == "separate_resnet":
+                    pose_inputs = [models["pose_encoder"](pose_inputs)]
+            else:
+                pose_inputs = [features[i] for i in self.opt.frame_ids if i != "s"]
+            axisangle, translation = models["pose"](pose_inputs)
+            for i, f_i in enumerate(self.opt.frame_ids[1:]):
+                if f_i != "s":
+                    outputs[("axisangle", 0, f_i)] = axisangle
+                    outputs[("translation", 0, f_i)] = translation
+                    outputs[("cam_T_cam", 0, f_i)] = transformation_from_parameters(
+                        axisangle[:, i], translation[:, i])
+        return outputs
+
+    # ------------------------------------------------------------- hot path
+    def _colors(self, inputs):
+        cols = []
+        for s in range(self.num_scales):
+            row = [inputs[("color", 0, s)]]
+            for f in self.src_frames:
+                row.append(inputs.get(("color", f, s)) if (self.opt.v1_multiscale or s == 0) else None)
+            cols.append(row)
+        return cols
+
+    def _intrinsics(self, inputs):
+        K = [inputs[("K", s)] for s in range(self.num_scales)]
+        inv_K = [inputs[("inv_K", s)] for s in range(self.num_scales)]
+        return K, inv_K
+
+    def _stacked_T(self, inputs, outputs):
+        """(S,B,4,4) cam_T_cam in frame order (trainer.py:360-363); posecnn: per scale
+        (num_scales,S,B,4,4) with the translation rescaled by mean inverse depth
+        (trainer.py:366-375)."""
+        if self.opt.pose_model_type != "posecnn":
+            Ts = [inputs["stereo_T"] if f == "s" else outputs[("cam_T_cam", 0, f)] for f in self.src_frames]
+            return torch.stack(Ts, 0)
+        per_scale = []
+        for s in range(self.num_scales):
+            disp = outputs[("disp", s)]
+            if not self.opt.v1_multiscale:
+                disp = F.interpolate(disp, [self.opt.height, self.opt.width], mode="bilinear", align_corners=False)
+            scaled, _ = disp_to_depth(disp, self.opt.min_depth, self.opt.max_depth)
+            mean_inv_depth = scaled.mean(3, True).mean(2, True)
+            Ts = []
+            for f in self.src_frames:
+                if f == "s":
+                    Ts.append(inputs["stereo_T"])
+                else:
+                    Ts.append(transformation_from_parameters(
+                        outputs[("axisangle", 0, f)][:, 0],
+                        outputs[("translation", 0, f)][:, 0] * mean_inv_depth[:, 0], f < 0))
+            per_scale.append(torch.stack(Ts, 0))
+        return torch.stack(per_scale, 0)
+
+    def generate_images_pred(self, inputs, outputs):
+        """Materialise what trainer.py:341-391 writes into `outputs` (no autograd)."""
+        K, inv_K = self._intrinsics(inputs)
+        with torch.no_grad():
+            T = self._stacked_T(inputs, outputs)
+            if self.hot.t_per_scale:
+                T = T[0]  # the materialised images use the scale-0 pose (logging only)
+                cfg = HotPathConfig(**{**self.hot.__dict__, "t_per_scale": False})
+            else:
+                cfg = self.hot
+            res = generate_images(cfg, [outputs[("disp", s)].detach() for s in range(self.num_scales)],
+                                  self._colors(inputs), K, inv_K, T.detach())
+        for s in range(self.num_scales):
+            outputs[("depth", 0, s)] = res["depth"][s]
+            src_s = s if self.opt.v1_multiscale else 0
+            for fi, f in enumerate(self.src_frames):
+                outputs[("sample", f, s)] = res["sample"][(fi, s)]
+                outputs[("color", f, s)] = res["color"][(fi, s)]
+                if not self.opt.disable_automasking:
+                    outputs[("color_identity", f, s)] = inputs[("color", f, src_s)]
+
+    def compute_losses(self, inputs, outputs):
+        """trainer.py:407-496 (+ the warp of 341-391) as one fused HIP op."""
+        K, inv_K = self._intrinsics(inputs)
+        T = self._stacked_T(inputs, outputs)
+        seed = (int(self.opt.noise_seed) * 1000003 + self.step) * 131 + self.rank
+        loss_vec, sel = photometric_loss(self.hot, [outputs[("disp", s)] for s in range(self.num_scales)],
+                                         self._colors(inputs), K, inv_K, T, noise=self.noise_override,
+                                         seed=seed)
+        losses = {"loss/{}".format(s): loss_vec[s] for s in range(self.num_scales)}
+        losses["loss"] = loss_vec[self.num_scales]
+        if not self.opt.disable_automasking:
+            C = self.hot.noise_channels()
+            for s, m in selection_maps(self.hot, sel).items():
+                outputs["identity_selection/{}".format(s)] = (m > C - 1).float()
+        return losses
+
+    def process_batch(self, inputs):
+        """trainer.py:228-260."""
+        for key, ipt in inputs.items():
+            if ipt.device != self.device:
+                inputs[key] = ipt.to(self.device, non_blocking=True)
+        nets = self.ddp if self.ddp is not None else self.nets
+        outputs = nets(self, inputs)
+        if self.opt.materialize_images:
+            self.generate_images_pred(inputs, outputs)
+        losses = self.compute_losses(inputs, outputs)
+        return outputs, losses
+
+    def train_step(self, inputs):
+        """One optimisation step (trainer.py:205-209)."""
+        outputs, losses = self.process_batch(inputs)
+        self.model_optimizer.zero_grad(set_to_none=True)
+        losses["loss"].backward()
+        self.model_optimizer.step()
+        self.step += 1
+        return outputs, losses
+
+    def run_epoch(self, batches: Iterable, log_every: int = 0):
+        self.set_train()
+        for batch_idx, inputs in enumerate(batches):
+            t0 = time.time()
+            outputs, losses = self.train_step(inputs)
+            if log_every and batch_idx % log_every == 0:
+                loss = float(losses["loss"])
+                self.log_time(batch_idx, time.time() - t0, loss)
+        self.model_lr_scheduler.step()
+        self.epoch += 1
+
+    def compute_depth_losses(self, inputs, outputs, losses):
+        """trainer.py:498-526 (monitoring only)."""
+        depth_pred = outputs[("depth", 0, 0)]
+        depth_pred = torch.clamp(F.interpolate(depth_pred, [375, 1242], mode="bilinear", align_corners=False),
+                                 1e-3, 80).detach()
+        depth_gt = inputs["depth_gt"]
+        mask = depth_gt > 0
+        crop = torch.zeros_like(mask)
+        crop[:, :, 153:371, 44:1197] = 1
+        mask = mask * crop
+        depth_gt = depth_gt[mask]
+        depth_pred = depth_pred[mask]
+        depth_pred *= torch.median(depth_gt) / torch.median(depth_pred)
+        depth_pred = torch.clamp(depth_pred, min=1e-3, max=80)
+        for name, v in zip(self.depth_metric_names, compute_depth_errors(depth_gt, depth_pred)):
+            losses[name] = np.array(v.cpu())
+
+    def log_time(self, batch_idx, duration, loss):
+        print("epoch {:>3} | batch {:>6} | examples/s: {:5.1f} | loss: {:.5f}".format(
+            self.epoch, batch_idx, self.opt.batch_size * self.world_size / max(duration, 1e-9), loss))
+
+    # -------------------------------------------------------- checkpoints
+    def save_opts(self):
+        models_dir = os.path.join(self.log_path, "models")
+        os.makedirs(models_dir, exist_ok=True)
+        with open(os.path.join(models_dir, "opt.json"), "w") as f:
+            json.dump(self.opt.__dict__.copy(), f, indent=2)
+
+    def save_model(self):
+        """trainer.py:585-603: weights_{epoch}/{model}.pth + adam.pth."""
+        folder = os.path.join(self.log_path, "models", "weights_{}".format(self.epoch))
+        os.makedirs(folder, exist_ok=True)
+        for name, model in self.models.items():
+            state = model.state_dict()
+            if name == "encoder":
+                state["height"] = self.opt.height
+                state["width"] = self.opt.width
+                state["use_stereo"] = self.opt.use_stereo
+            torch.save(state, os.path.join(folder, "{}.pth".format(name)))
+        torch.save(self.model_optimizer.state_dict(), os.path.join(folder, "adam.pth"))
+        return folder
+
+    def load_model(self):
+        """trainer.py:605-630 (safe loader: weights_only=True)."""
+        folder = os.path.expanduser(self.opt.load_weights_folder)
+        assert os.path.isdir(folder), "Cannot find folder {}".format(folder)
+        for n in self.opt.models_to_load:
+            if n not in self.models:
+                continue
+            model_dict = self.models[n].state_dict()
+            loaded = torch.load(os.path.join(folder, "{}.pth".format(n)), map_location=self.device,
+                                weights_only=True)
+            model_dict.update({k: v for k, v in loaded.items() if k in model_dict})
+            self.models[n].load_state_dict(model_dict)
+        adam = os.path.join(folder, "adam.pth")
+        if os.path.isfile(adam):
+            self.model_optimizer.load_state_dict(torch.load(adam, map_location=self.device, weights_only=True))
