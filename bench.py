@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen exhaustive find per conv shape")
+    ap.add_argument("--channels-last", type=int, default=0, help="NHWC convolutions (1/0)")
+    ap.add_argument("--graph", type=int, default=0, help="capture the whole step in a hipGraph (1/0)")
     return ap.parse_args()
 
 
@@ -93,7 +95,8 @@ def make_trainer(args, device, rank, world):
     from monodepth2_amd.trainer import Trainer
     opt = default_options(batch_size=args.batch, height=args.height, width=args.width,
                           num_layers=args.num_layers, weights_init="scratch", use_stereo=args.stereo,
-                          frame_ids=[0, -1, 1], log_dir="/tmp/md2_bench")
+                          frame_ids=[0, -1, 1], log_dir="/tmp/md2_bench",
+                          channels_last=bool(args.channels_last), hip_graph=bool(args.graph))
     return Trainer(opt, device=device, rank=rank, world_size=world)
 
 
@@ -118,6 +121,30 @@ def loss_delta_vs_oracle(trainer, batch):
         ref, _ = hot_path(opt, {s: d.cpu() for s, d in enumerate(disps)}, cpu_inputs, camT, noise=noise,
                           keep_images=False)
     return abs(float(loss[hot.num_scales]) - float(ref["loss"]))
+
+
+def time_hot_kernels(trainer, batch, n=10):
+    """Stand-alone fwd+bwd of the fused hot path on the step's own tensors, with the
+    photometric kernels HIP-event timed (used when the step runs as a hipGraph,
+    whose replays are not individually instrumented)."""
+    from monodepth2_amd import _lib
+    from monodepth2_amd.hotpath import photometric_loss
+    with torch.no_grad():
+        outputs = trainer.nets(trainer, batch)
+    hot = trainer.hot
+    K, iK = trainer._intrinsics(batch)
+    T = trainer._stacked_T(batch, outputs).detach().requires_grad_(True)
+    disps = [outputs[("disp", s)].detach().requires_grad_(True) for s in range(hot.num_scales)]
+    colors = trainer._colors(batch)
+    for _ in range(2):
+        loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=1)
+        loss[hot.num_scales].backward()
+    torch.cuda.synchronize()
+    with _lib.KernelTimer(max_launches=2 * n + 4) as kt:
+        for i in range(n):
+            loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=2 + i)
+            loss[hot.num_scales].backward()
+    return kt
 
 
 def cpu_baseline(args):
@@ -219,6 +246,9 @@ def main():
         dt = float(t)
     final_loss = float(losses["loss"])
 
+    if rank == 0 and kt.n_bwd == 0:
+        kt = time_hot_kernels(trainer, batch)
+        log("hot-path kernels timed stand-alone (graph mode)")
     if rank == 0:
         S = len(frame_ids) - 1
         B, H, W = args.batch, args.height, args.width

@@ -83,6 +83,9 @@ typedef struct md2_tensors {
      * back to back, scale s shaped (B, C, h_s, w_s) with C = S (or 1 with
      * AVG_REPROJECTION) at the loss resolution.  NULL: drawn in-kernel from seed. */
     const float* noise;
+    /* Optional device-side uint64 mixed into desc.seed at run time, so a captured
+     * hipGraph draws fresh noise on every replay (the caller increments it). */
+    const uint64_t* seed_ptr;
 } md2_tensors;
 
 int md2_abi_version(void);

@@ -41,7 +41,8 @@ class Tensors(ctypes.Structure):
                 ("K", _vp * MAX_SCALES),
                 ("inv_K", _vp * MAX_SCALES),
                 ("T", _vp),
-                ("noise", _vp)]
+                ("noise", _vp),
+                ("seed_ptr", _vp)]
 
 
 _lock = threading.Lock()

@@ -68,6 +68,16 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
+// Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, dispatch
+// placement; speed only, never correctness).  Give every XCD a contiguous range of
+// logical blocks so its private L2 streams a contiguous slice of the images instead
+// of all XCDs fetching every image.  Bijective for any n.
+__device__ __forceinline__ int xcd_contiguous_block(int bid, int n) {
+    const int q = n >> 3, r = n & 7;
+    const int xcd = bid & 7, idx = bid >> 3;
+    return xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
+}
+
 __device__ __forceinline__ float signf(float v) { return (v > 0.f) ? 1.f : ((v < 0.f) ? -1.f : 0.f); }
 
 // counter-based normal deviate for the tie-break noise (trainer.py:468)
@@ -277,6 +287,7 @@ struct PhotoArgs {
     const float* T[MD2_MAX_SCALES];         // per local scale (S,B,4,4)
     const float* noise[MD2_MAX_SCALES];     // per local scale (B,C,h,w) or null
     uint64_t seed;
+    const uint64_t* seed_ptr;               // optional device-side seed (graph replay)
     float min_disp, range;
     uint32_t flags;
     float* photo_part[MD2_MAX_SCALES];      // fwd: per local scale [B*wpi]
@@ -375,11 +386,13 @@ __global__ __launch_bounds__(kBlock, 2) void photo_fwd_kernel(PhotoArgs a) {
     __shared__ FwdState<NS> lds[kWavesPerBlock];
     const int lane = threadIdx.x & (kWave - 1);
     FwdState<NS>& L = lds[threadIdx.x >> 6];
-    const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int wv = __builtin_amdgcn_readfirstlane(blk * kWavesPerBlock + (threadIdx.x >> 6));
     if (wv >= a.B * a.wpi) return;
     const int b = wv / a.wpi, rem = wv - b * a.wpi;
     const int rb = rem / a.strips, st = rem - rb * a.strips;
     const int r0 = rb * kRowsF;
+    const uint64_t seed = a.seed_ptr ? (a.seed ^ (*a.seed_ptr * 0x9E3779B97F4A7C15ULL)) : a.seed;
     const int h = a.h, w = a.w, HW = h * w;
     const int c = st * kFwdCols - 1 + lane;
     const int cc = reflect_clamp(c, w);
@@ -419,7 +432,7 @@ __global__ __launch_bounds__(kBlock, 2) void photo_fwd_kernel(PhotoArgs a) {
                     }
                     const size_t nidx = (((size_t)b * C + ch) * h + r) * w + cc;
                     const float n = nz ? nz[nidx]
-                                       : hash_normal(a.seed, ((uint64_t)gsc << 56) ^ (uint64_t)nidx);
+                                       : hash_normal(seed, ((uint64_t)gsc << 56) ^ (uint64_t)nidx);
                     v = v + n * 1e-5f;
                     if (v < best) {
                         best = v;
@@ -498,7 +511,8 @@ __device__ __forceinline__ float frame_weight(int code, int f, bool automask, bo
 template <int NS, bool SSIM_ON>
 __global__ __launch_bounds__(kBlock, 2) void photo_bwd_kernel(PhotoArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
-    const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int wv = __builtin_amdgcn_readfirstlane(blk * kWavesPerBlock + (threadIdx.x >> 6));
     if (wv >= a.B * a.wpi) return;
     const int b = wv / a.wpi, rem = wv - b * a.wpi;
     const int rb = rem / a.strips, st = rem - rb * a.strips;
@@ -967,12 +981,12 @@ int timing_start(int kind, hipStream_t st) {
     if (!g_timing.on || g_timing.used >= g_timing.cap) return -1;
     const int i = g_timing.used++;
     g_timing.kind[i] = kind;
-    hipEventRecord(g_timing.ev[2 * i], st);
+    (void)hipEventRecord(g_timing.ev[2 * i], st);
     return i;
 }
 void timing_stop(int slot, hipStream_t st) {
     if (slot < 0) return;
-    hipEventRecord(g_timing.ev[2 * slot + 1], st);
+    (void)hipEventRecord(g_timing.ev[2 * slot + 1], st);
 }
 
 int fail(int code, const char* fmt, ...) {
@@ -1092,6 +1106,7 @@ void photo_args(const md2_desc* d, const md2_tensors* t, const Layout& L, int s_
     a.K = t->K[cs];
     a.iK = t->inv_K[cs];
     a.seed = d->seed;
+    a.seed_ptr = t->seed_ptr;
     a.min_disp = 1.0f / d->max_depth;
     a.range = 1.0f / d->min_depth - 1.0f / d->max_depth;
     a.flags = d->flags;
@@ -1325,7 +1340,7 @@ int md2_generate_images(const md2_desc* d, const md2_tensors* t, float* const* d
 int md2_timing_begin(int max_launches) {
     std::lock_guard<std::mutex> lk(g_timing.mu);
     if (max_launches < 1) return fail(MD2_ERR_ARG, "max_launches must be >= 1");
-    for (hipEvent_t e : g_timing.ev) hipEventDestroy(e);
+    for (hipEvent_t e : g_timing.ev) (void)hipEventDestroy(e);
     g_timing.ev.assign(2 * (size_t)max_launches, nullptr);
     g_timing.kind.assign(max_launches, 0);
     for (auto& e : g_timing.ev)

@@ -66,3 +66,49 @@ def shard(batch: Dict, rank: int, world: int) -> Dict:
         else:
             out[k] = v
     return out
+
+
+class FlatGradSync:
+    """Gradient averaging over flat buckets, graph-capturable.
+
+    Every trainable parameter's `.grad` is a view into one of a few flat fp32
+    buckets (BUCKET_CAP_MB each).  After the backward pass `sync()` issues one
+    all-reduce (ReduceOp.AVG on RCCL) per bucket; `zero()` clears the buckets
+    with one memset each.  Unlike DDP's autograd hooks this is plain stream
+    work, so it can sit inside a captured hipGraph of the whole training step.
+    Parameters that never get a gradient (the encoders' fc heads) are left out.
+    """
+
+    def __init__(self, named_params, world: int, group=None, bucket_cap_mb: int = BUCKET_CAP_MB):
+        self.world, self.group = world, group
+        params = [(n, p) for n, p in named_params if p.requires_grad and not (
+            n.endswith("encoder.fc.weight") or n.endswith("encoder.fc.bias"))]
+        cap = bucket_cap_mb * (1 << 20) // 4
+        self.buckets = []
+        cur, size = [], 0
+        for n, p in params:
+            if cur and size + p.numel() > cap:
+                self.buckets.append(cur)
+                cur, size = [], 0
+            cur.append(p)
+            size += p.numel()
+        if cur:
+            self.buckets.append(cur)
+        self.flat = []
+        for plist in self.buckets:
+            buf = torch.zeros(sum(p.numel() for p in plist), dtype=torch.float32, device=plist[0].device)
+            off = 0
+            for p in plist:
+                p.grad = buf[off:off + p.numel()].view_as(p)
+                off += p.numel()
+            self.flat.append(buf)
+
+    def zero(self):
+        for buf in self.flat:
+            buf.zero_()
+
+    def sync(self):
+        if self.world <= 1:
+            return
+        for buf in self.flat:
+            dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.group)

@@ -94,9 +94,14 @@ class Operands:
 
     def __init__(self, cfg: HotPathConfig, colors: Sequence[Sequence[Optional[torch.Tensor]]],
                  K: Sequence[Optional[torch.Tensor]], inv_K: Sequence[Optional[torch.Tensor]],
-                 noise: Optional[Dict[int, torch.Tensor]], device: torch.device):
+                 noise: Optional[Dict[int, torch.Tensor]], device: torch.device,
+                 seed_tensor: Optional[torch.Tensor] = None):
         B, H, W, S = cfg.batch, cfg.height, cfg.width, cfg.num_src
         self.cfg = cfg
+        if seed_tensor is not None and (seed_tensor.device != device or seed_tensor.dtype != torch.int64
+                                        or seed_tensor.numel() != 1):
+            raise ValueError("seed_tensor must be a 1-element int64 tensor on " + str(device))
+        self.seed_tensor = seed_tensor
         self.colors: List[List[Optional[torch.Tensor]]] = [[None] * (1 + S) for _ in range(cfg.num_scales)]
         self.K: List[Optional[torch.Tensor]] = [None] * cfg.num_scales
         self.inv_K: List[Optional[torch.Tensor]] = [None] * cfg.num_scales
@@ -135,6 +140,7 @@ class Operands:
                 st.inv_K[s] = self.inv_K[s].data_ptr()
         st.T = T.data_ptr()
         st.noise = self.noise.data_ptr() if self.noise is not None else None
+        st.seed_ptr = self.seed_tensor.data_ptr() if self.seed_tensor is not None else None
         return st
 
 
@@ -178,13 +184,16 @@ class _PhotometricLoss(torch.autograd.Function):
 
 
 def photometric_loss(cfg: HotPathConfig, disps: Sequence[torch.Tensor], colors, K, inv_K, T: torch.Tensor,
-                     noise: Optional[Dict[int, torch.Tensor]] = None, seed: int = 0):
+                     noise: Optional[Dict[int, torch.Tensor]] = None, seed: int = 0,
+                     seed_tensor: Optional[torch.Tensor] = None):
     """Fused hot path.  Returns (loss_vec, select).
 
     loss_vec[s] = losses["loss/s"], loss_vec[num_scales] = losses["loss"];
     select is the packed per-scale argmin map (uint8), see `selection_maps`.
     T: (S,B,4,4) stacked cam_T_cam (or (num_scales,S,B,4,4) with t_per_scale).
     noise: optional {scale: unit-normal (B,C,h,w)}; None draws it in-kernel from seed.
+    seed_tensor: optional 1-element int64 device tensor mixed into the seed at run
+    time (lets a captured hipGraph draw fresh noise per replay).
     """
     dev = T.device
     if dev.type != "cuda":
@@ -197,7 +206,7 @@ def photometric_loss(cfg: HotPathConfig, disps: Sequence[torch.Tensor], colors, 
         _require(d, f"disp[{s}]", (B, 1, H >> s, W >> s), dev)
     tshape = (cfg.num_scales, S, B, 4, 4) if cfg.t_per_scale else (S, B, 4, 4)
     _require(T, "T", tshape, dev)
-    ops = Operands(cfg, colors, K, inv_K, noise, dev)
+    ops = Operands(cfg, colors, K, inv_K, noise, dev, seed_tensor)
     return _PhotometricLoss.apply(cfg, ops, int(seed), T.contiguous(), *disps)
 
 

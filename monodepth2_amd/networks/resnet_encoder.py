@@ -130,6 +130,8 @@ class ResnetEncoder(nn.Module):
     def forward(self, input_image):
         e = self.encoder
         x = (input_image - 0.45) / 0.225
+        if e.conv1.weight.is_contiguous(memory_format=torch.channels_last):
+            x = x.contiguous(memory_format=torch.channels_last)
         f0 = e.relu(e.bn1(e.conv1(x)))
         f1 = e.layer1(e.maxpool(f0))
         f2 = e.layer2(f1)

@@ -32,7 +32,7 @@ import torch.nn.functional as F
 import torch.optim as optim
 
 from . import networks
-from .distributed import wrap_ddp
+from .distributed import FlatGradSync, wrap_ddp
 from .hotpath import HotPathConfig, generate_images, photometric_loss, selection_maps
 from .layers import compute_depth_errors, disp_to_depth, transformation_from_parameters
 
@@ -99,12 +99,27 @@ class Trainer:
                     self.num_input_frames if self.opt.pose_model_input == "all" else 2)
         for m in self.models.values():
             m.to(self.device)
+            if getattr(self.opt, "channels_last", False):
+                m.to(memory_format=torch.channels_last)
         self.nets = _Networks(self.models)
         self.parameters_to_train = [p for m in self.models.values() for p in m.parameters()]
 
-        self.ddp = wrap_ddp(self.nets, self.device) if world_size > 1 else None
+        # gradient averaging: DDP (hooks, overlapped with backward) for eager steps, flat
+        # buckets + one RCCL all-reduce each (graph-capturable) for --hip_graph
+        self.use_graph = bool(getattr(self.opt, "hip_graph", False))
+        sync = getattr(self.opt, "grad_sync", "auto")
+        if sync == "auto":
+            sync = "flat" if self.use_graph else "ddp"
+        if self.use_graph and sync == "ddp" and world_size > 1:
+            raise ValueError("--hip_graph needs --grad_sync flat (DDP hooks are not graph-capturable)")
+        self.ddp = wrap_ddp(self.nets, self.device) if (world_size > 1 and sync == "ddp") else None
+        self.flat_sync = FlatGradSync(self.nets.named_parameters(), world_size) \
+            if (sync == "flat" or self.use_graph) else None
+        self.graph = None
+        self.seed_tensor = None
 
-        self.model_optimizer = optim.Adam(self.parameters_to_train, self.opt.learning_rate)
+        self.model_optimizer = optim.Adam(self.parameters_to_train, self.opt.learning_rate,
+                                          capturable=self.use_graph)
         self.model_lr_scheduler = optim.lr_scheduler.StepLR(self.model_optimizer, self.opt.scheduler_step_size, 0.1)
         if self.opt.load_weights_folder is not None:
             self.load_model()
@@ -250,10 +265,13 @@ class Trainer:
         """trainer.py:407-496 (+ the warp of 341-391) as one fused HIP op."""
         K, inv_K = self._intrinsics(inputs)
         T = self._stacked_T(inputs, outputs)
-        seed = (int(self.opt.noise_seed) * 1000003 + self.step) * 131 + self.rank
+        if self.seed_tensor is not None:   # graph replay: the step counter lives on the device
+            seed = int(self.opt.noise_seed) * 1000003 * 131 + self.rank
+        else:
+            seed = (int(self.opt.noise_seed) * 1000003 + self.step) * 131 + self.rank
         loss_vec, sel = photometric_loss(self.hot, [outputs[("disp", s)] for s in range(self.num_scales)],
                                          self._colors(inputs), K, inv_K, T, noise=self.noise_override,
-                                         seed=seed)
+                                         seed=seed, seed_tensor=self.seed_tensor)
         losses = {"loss/{}".format(s): loss_vec[s] for s in range(self.num_scales)}
         losses["loss"] = loss_vec[self.num_scales]
         if not self.opt.disable_automasking:
@@ -274,14 +292,52 @@ class Trainer:
         losses = self.compute_losses(inputs, outputs)
         return outputs, losses
 
+    def _step_body(self, inputs):
+        """process_batch + backward + gradient averaging + Adam (trainer.py:205-209)."""
+        outputs, losses = self.process_batch(inputs)
+        if self.flat_sync is not None:
+            self.flat_sync.zero()
+        else:
+            self.model_optimizer.zero_grad(set_to_none=True)
+        losses["loss"].backward()
+        if self.flat_sync is not None:
+            self.flat_sync.sync()
+        self.model_optimizer.step()
+        if self.seed_tensor is not None:
+            self.seed_tensor.add_(1)
+        return outputs, losses
+
+    def _capture(self, inputs, warmup: int = 3):
+        """Capture one whole training step (networks, fused hot path, backward,
+        all-reduce, Adam) into a hipGraph; later steps replay it."""
+        self.static_inputs = {k: v.to(self.device).clone() for k, v in inputs.items()}
+        self.seed_tensor = torch.zeros(1, dtype=torch.int64, device=self.device)
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._step_body(self.static_inputs)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.static_outputs, self.static_losses = self._step_body(self.static_inputs)
+
     def train_step(self, inputs):
         """One optimisation step (trainer.py:205-209)."""
-        outputs, losses = self.process_batch(inputs)
-        self.model_optimizer.zero_grad(set_to_none=True)
-        losses["loss"].backward()
-        self.model_optimizer.step()
+        if not self.use_graph:
+            outputs, losses = self._step_body(inputs)
+            self.step += 1
+            return outputs, losses
+        if self.graph is None:
+            self._capture(inputs)
+        else:
+            for k, v in inputs.items():
+                dst = self.static_inputs[k]
+                if v.data_ptr() != dst.data_ptr():
+                    dst.copy_(v, non_blocking=True)
+        self.graph.replay()
         self.step += 1
-        return outputs, losses
+        return self.static_outputs, self.static_losses
 
     def run_epoch(self, batches: Iterable, log_every: int = 0):
         self.set_train()
