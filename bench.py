@@ -35,9 +35,11 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# MIOpen: heuristic (immediate-mode) solver choice instead of an exhaustive find that
-# compiles every candidate kernel on a fresh box (minutes with no kernel cache)
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+# MIOpen: FAST find mode = tuned find-db hits (monodepth2_amd/miopen_db) or the
+# immediate-mode heuristic, never an exhaustive search (see monodepth2_amd/__init__.py)
+if "--miopen-find" in sys.argv:
+    os.environ["MIOPEN_FIND_MODE"] = sys.argv[sys.argv.index("--miopen-find") + 1].upper()
+import monodepth2_amd  # noqa: E402,F401  (sets the MIOpen environment before torch loads MIOpen)
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -87,6 +89,7 @@ def parse():
     ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen exhaustive find per conv shape")
     ap.add_argument("--channels-last", type=int, default=0, help="NHWC convolutions (1/0)")
     ap.add_argument("--graph", type=int, default=0, help="capture the whole step in a hipGraph (1/0)")
+    ap.add_argument("--miopen-find", type=str, default="fast", help="MIOPEN_FIND_MODE (fast|normal|...)")
     return ap.parse_args()
 
 
@@ -221,12 +224,20 @@ def main():
         delta = loss_delta_vs_oracle(trainer, batch)
         log(f"loss delta vs oracle = {delta:.3e}")
 
+    import threading
+    stop_hb = threading.Event()
+
+    def heartbeat():
+        while not stop_hb.wait(30.0):
+            log("... still warming up (MIOpen solver search / kernel compilation)")
+    threading.Thread(target=heartbeat, daemon=True).start()
     trainer.set_train()
     for i in range(args.warmup):
         t = time.perf_counter()
         trainer.train_step(batch)
         torch.cuda.synchronize()
         log(f"warmup step {i}: {1e3 * (time.perf_counter() - t):.1f} ms")
+    stop_hb.set()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
