@@ -12,7 +12,10 @@ import threading
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
-from .build import LIB_PATH
+from .build import LIB_PATH as _BUILT_LIB
+
+# MD2_LIB overrides the library path (A/B runs of alternative builds)
+LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3

@@ -124,6 +124,7 @@ struct WarpCtx {
     int dh, dw, upsh;   // upsample factor 2^upsh to the loss resolution
     const float* src;   // (3, h, w) source colours at the loss resolution
     int h, w;
+    float sx, sy;       // W/(W-1), H/(H-1): pixel -> grid_sample source coordinate
     float min_disp, range;
     Cam cm;
 };
@@ -186,12 +187,59 @@ __device__ __forceinline__ void project(const WarpCtx& c, int y, int x, Sample& 
     s.ty = iyc - fy0;
 }
 
+__device__ __forceinline__ float rcpf(float v) { return __builtin_amdgcn_rcpf(v); }
+
+// Same projection as `project` with hardware reciprocals (v_rcp_f32, 1 ulp) in
+// place of IEEE divisions, and the normalise/unnormalise pair of layers.py:190-192
+// + grid_sample folded into one scale: ix = px * W/(W-1) - 0.5.  Differences to
+// the exact form are O(1 ulp) in the sampling position.
+struct FastSample {
+    float depth;
+    float ray[3];
+    float pt[3];
+    float cam[3];
+    float inv_den;
+    float px, py;
+    float gmx, gmy;  // 0 where grid_sample clips (border), else 1
+    int x0, y0;
+    float tx, ty;
+};
+
+__device__ __forceinline__ void project_fast(const WarpCtx& c, int y, int x, FastSample& s) {
+    const float d = disp_at(c, y, x);
+    s.depth = rcpf(c.min_disp + c.range * d);
+    const float fx = (float)x, fy = (float)y;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        s.ray[i] = c.cm.iK[i * 3 + 0] * fx + c.cm.iK[i * 3 + 1] * fy + c.cm.iK[i * 3 + 2];
+        s.pt[i] = s.depth * s.ray[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        s.cam[i] = c.cm.P[i * 4 + 0] * s.pt[0] + c.cm.P[i * 4 + 1] * s.pt[1] +
+                   c.cm.P[i * 4 + 2] * s.pt[2] + c.cm.P[i * 4 + 3];
+    s.inv_den = rcpf(s.cam[2] + 1e-7f);
+    s.px = s.cam[0] * s.inv_den;
+    s.py = s.cam[1] * s.inv_den;
+    const float ix = s.px * c.sx - 0.5f, iy = s.py * c.sy - 0.5f;
+    const float xmax = (float)(c.w - 1), ymax = (float)(c.h - 1);
+    const float ixc = fminf(fmaxf(ix, 0.f), xmax), iyc = fminf(fmaxf(iy, 0.f), ymax);
+    s.gmx = (ix > 0.f && ix < xmax) ? 1.f : 0.f;
+    s.gmy = (iy > 0.f && iy < ymax) ? 1.f : 0.f;
+    const float fx0 = floorf(ixc), fy0 = floorf(iyc);
+    s.x0 = (int)fx0;
+    s.y0 = (int)fy0;
+    s.tx = ixc - fx0;
+    s.ty = iyc - fy0;
+}
+
 // the four (masked) source corners of a sample for the 3 channels
 struct Corners {
     float nw[3], ne[3], sw[3], se[3];
 };
 
-__device__ __forceinline__ void gather(const WarpCtx& c, const Sample& s, Corners& v) {
+template <class SampleT>
+__device__ __forceinline__ void gather(const WarpCtx& c, const SampleT& s, Corners& v) {
     const bool vx1 = s.x0 + 1 < c.w, vy1 = s.y0 + 1 < c.h;
     const int x1 = vx1 ? s.x0 + 1 : s.x0, y1 = vy1 ? s.y0 + 1 : s.y0;
     const int HW = c.h * c.w;
@@ -206,7 +254,8 @@ __device__ __forceinline__ void gather(const WarpCtx& c, const Sample& s, Corner
     }
 }
 
-__device__ __forceinline__ void interp(const Sample& s, const Corners& v, float out[3]) {
+template <class SampleT>
+__device__ __forceinline__ void interp(const SampleT& s, const Corners& v, float out[3]) {
     const float e = 1.f - s.tx, so = 1.f - s.ty;
     const float wnw = so * e, wne = so * s.tx, wsw = s.ty * e, wse = s.ty * s.tx;
 #pragma unroll
@@ -214,8 +263,8 @@ __device__ __forceinline__ void interp(const Sample& s, const Corners& v, float 
 }
 
 __device__ __forceinline__ void warp_value(const WarpCtx& c, int y, int x, float out[3]) {
-    Sample s;
-    project(c, y, x, s);
+    FastSample s;
+    project_fast(c, y, x, s);
     Corners v;
     gather(c, s, v);
     interp(s, v, out);
@@ -247,7 +296,7 @@ __device__ __forceinline__ float ssim_from_sums(const H5& a, const H5& b, const 
     const float sxy = (a.xy + b.xy + c.xy) * kInv9 - mx * my;
     const float n = (2.f * mx * my + kC1) * (2.f * sxy + kC2);
     const float d = (mx * mx + my * my + kC1) * (sx + sy + kC2);
-    return fminf(fmaxf((1.f - n / d) * 0.5f, 0.f), 1.f);
+    return fminf(fmaxf((1.f - n * rcpf(d)) * 0.5f, 0.f), 1.f);
 }
 
 // dL/d(box mean of x), dL/d(box mean of x^2), dL/d(box mean of x*y) at one pixel,
@@ -261,10 +310,11 @@ __device__ __forceinline__ void ssim_adjoint(const H5& a, const H5& b, const H5&
     const float n1 = 2.f * mx * my + kC1, n2 = 2.f * sxy + kC2;
     const float d1 = mx * mx + my * my + kC1, d2 = sx + sy + kC2;
     const float n = n1 * n2, d = d1 * d2;
-    const float raw = (1.f - n / d) * 0.5f;
+    const float inv_d = rcpf(d);
+    const float raw = (1.f - n * inv_d) * 0.5f;
     const float g = (raw >= 0.f && raw <= 1.f) ? gS : 0.f;  // clamp passes [0,1] inclusive
-    const float dn = -0.5f * g / d;
-    const float dd = 0.5f * g * n / (d * d);
+    const float dn = -0.5f * g * inv_d;
+    const float dd = 0.5f * g * n * inv_d * inv_d;
     dA = dn * (2.f * my * (n2 - n1)) + dd * (2.f * mx * (d2 - d1));
     dB = dd * d1;
     dC = dn * 2.f * n1;
@@ -307,6 +357,8 @@ __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int 
     c.src = a.src[f] + (size_t)b * 3 * HW;
     c.h = a.h;
     c.w = a.w;
+    c.sx = (float)a.w / (float)(a.w - 1);
+    c.sy = (float)a.h / (float)(a.h - 1);
     c.min_disp = a.min_disp;
     c.range = a.range;
     load_cam(c.cm, a.K + b * 16, a.iK + b * 16, a.T[ls] + ((size_t)f * a.B + b) * 16);
@@ -508,14 +560,40 @@ __device__ __forceinline__ float frame_weight(int code, int f, bool automask, bo
     return code == (automask ? NS : 0) + f ? 1.f : 0.f;
 }
 
+// What the output row of the backward needs from its own forward sample, carried
+// two rows down the sliding window instead of re-projecting and re-gathering.
+struct Carry {
+    float jx[3], jy[3];  // d warp_c / d px, d warp_c / d py (bilinear slope x clip mask x W/(W-1))
+    float px, py, inv_den;
+    float pt[3];         // camera point = depth * ray
+    float u[3];          // P[:3,:3] @ ray  (d cam / d depth)
+    float dd;            // d depth / d disp = -range * depth^2
+};
+
+__device__ __forceinline__ void make_carry(const WarpCtx& c, const FastSample& s, const Corners& v, Carry& k) {
+    const float e = 1.f - s.tx, so = 1.f - s.ty;
+    const float mx = s.gmx * c.sx, my = s.gmy * c.sy;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        k.jx[ch] = ((v.ne[ch] - v.nw[ch]) * so + (v.se[ch] - v.sw[ch]) * s.ty) * mx;
+        k.jy[ch] = ((v.sw[ch] - v.nw[ch]) * e + (v.se[ch] - v.ne[ch]) * s.tx) * my;
+    }
+    k.px = s.px;
+    k.py = s.py;
+    k.inv_den = s.inv_den;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        k.pt[i] = s.pt[i];
+        k.u[i] = c.cm.P[i * 4 + 0] * s.ray[0] + c.cm.P[i * 4 + 1] * s.ray[1] + c.cm.P[i * 4 + 2] * s.ray[2];
+    }
+    k.dd = -c.range * s.depth * s.depth;
+}
+
+// One work item of the backward: (image b, local scale ls, strip st, row block rb),
+// all source frames.  Writes dL/d(upsampled disp) for its 60 x kRowsB pixels and one
+// 12-float dL/dP partial per frame.
 template <int NS, bool SSIM_ON>
-__global__ __launch_bounds__(kBlock, 2) void photo_bwd_kernel(PhotoArgs a) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
-    const int wv = __builtin_amdgcn_readfirstlane(blk * kWavesPerBlock + (threadIdx.x >> 6));
-    if (wv >= a.B * a.wpi) return;
-    const int b = wv / a.wpi, rem = wv - b * a.wpi;
-    const int rb = rem / a.strips, st = rem - rb * a.strips;
+__device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int st, int rb, int lane) {
     const int r0 = rb * kRowsB;
     const int h = a.h, w = a.w, HW = h * w;
     const int c = st * kBwdCols - 2 + lane;
@@ -527,139 +605,147 @@ __global__ __launch_bounds__(kBlock, 2) void photo_bwd_kernel(PhotoArgs a) {
     const bool automask = !(a.flags & MD2_NO_AUTOMASK);
     const bool avg = (a.flags & MD2_AVG_REPROJECTION) != 0;
     const float l1w = SSIM_ON ? 0.15f : 1.0f;
-    const float inv_count = 1.0f / ((float)a.B * (float)HW);
+    const int gsc = a.gscale[ls];
+    const float gscale = (a.grad_loss[gsc] + a.grad_loss[a.num_scales] / (float)a.num_scales) /
+                         ((float)a.B * (float)HW);
+    const uint8_t* sel = a.sel[ls] + (size_t)b * HW;
+    float* dfull = a.dfull[ls] + (size_t)b * HW;
+    const int item_in_scale = b * a.wpi + rb * a.strips + st;
 
-    for (int ls = 0; ls < a.nsc; ++ls) {
-        const int gsc = a.gscale[ls];
-        const float gscale = (a.grad_loss[gsc] + a.grad_loss[a.num_scales] / (float)a.num_scales) * inv_count;
-        const uint8_t* sel = a.sel[ls] + (size_t)b * HW;
-        float* dfull = a.dfull[ls] + (size_t)b * HW;
-        for (int f = 0; f < NS; ++f) {
-            WarpCtx ctx;
-            make_ctx(a, ls, f, b, ctx);
-            float dP[12];
+    for (int f = 0; f < NS; ++f) {
+        WarpCtx ctx;
+        make_ctx(a, ls, f, b, ctx);
+        float dP[12];
 #pragma unroll
-            for (int j = 0; j < 12; ++j) dP[j] = 0.f;
-            H5 hA[3], hB[3];
-            float x1[3] = {0.f, 0.f, 0.f}, y1[3] = {0.f, 0.f, 0.f};  // row r-1
-            float x2[3] = {0.f, 0.f, 0.f}, y2[3] = {0.f, 0.f, 0.f};  // row r-2
-            Coef cA, cB;
-            for (int k = 0; k < kRowsB + 4; ++k) {
-                const int r = r0 - 2 + k;
-                const int rr = reflect_clamp(r, h);
-                float x[3], y[3];
-                warp_value(ctx, rr, cc, x);
+        for (int j = 0; j < 12; ++j) dP[j] = 0.f;
+        H5 hA[3], hB[3];
+        float x1[3] = {0.f, 0.f, 0.f}, y1[3] = {0.f, 0.f, 0.f};  // row r-1
+        float x2[3] = {0.f, 0.f, 0.f}, y2[3] = {0.f, 0.f, 0.f};  // row r-2
+        Coef cA, cB;
+        Carry k1, k2;
+        for (int k = 0; k < kRowsB + 4; ++k) {
+            const int r = r0 - 2 + k;
+            const int rr = reflect_clamp(r, h);
+            FastSample sm;
+            project_fast(ctx, rr, cc, sm);
+            Corners v;
+            gather(ctx, sm, v);
+            float x[3], y[3];
+            interp(sm, v, x);
 #pragma unroll
-                for (int ch = 0; ch < 3; ++ch) y[ch] = tgt[ch * HW + rr * w + cc];
-                H5 hc[3];
+            for (int ch = 0; ch < 3; ++ch) y[ch] = tgt[ch * HW + rr * w + cc];
+            Carry kc;
+            if (k >= 2 && k < kRowsB + 2) make_carry(ctx, sm, v, kc);  // only output rows need it
+            H5 hc[3];
+            if (SSIM_ON) {
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) hc[ch] = hsum(x[ch], y[ch]);
+            }
+            if (k >= 2) {
+                // coefficient row p = r - 1
+                const int p = r - 1;
+                float gp = 0.f;
+                if (colreal && p >= 0 && p < h) gp = gscale * frame_weight<NS>(sel[p * w + c], f, automask, avg);
+                Coef cC;
+                cC.g = gp;
                 if (SSIM_ON) {
-#pragma unroll
-                    for (int ch = 0; ch < 3; ++ch) hc[ch] = hsum(x[ch], y[ch]);
-                }
-                if (k >= 2) {
-                    // coefficient row p = r - 1
-                    const int p = r - 1;
-                    float gp = 0.f;
-                    if (colreal && p >= 0 && p < h) gp = gscale * frame_weight<NS>(sel[p * w + c], f, automask, avg);
-                    Coef cC;
-                    cC.g = gp;
-                    if (SSIM_ON) {
-                        const float gS = gp * (0.85f / 3.f);
-#pragma unroll
-                        for (int ch = 0; ch < 3; ++ch) {
-                            float dA, dB, dC;
-                            ssim_adjoint(hA[ch], hB[ch], hc[ch], gS, dA, dB, dC);
-                            if (gp == 0.f) dA = dB = dC = 0.f;
-                            cC.A[ch] = pick(wl, shfl_prev(dA)) + dA + pick(wr, shfl_next(dA));
-                            cC.B[ch] = pick(wl, shfl_prev(dB)) + dB + pick(wr, shfl_next(dB));
-                            cC.C[ch] = pick(wl, shfl_prev(dC)) + dC + pick(wr, shfl_next(dC));
-                        }
-                    }
-                    if (k >= 4) {
-                        // output row q = r - 2 (coefficient rows q-1, q, q+1 = cA, cB, cC)
-                        const int q = r - 2;
-                        if (colok && q < h) {
-                            float gw[3];
-                            const float l1c = cB.g * (l1w / 3.f);
-#pragma unroll
-                            for (int ch = 0; ch < 3; ++ch) {
-                                float g = l1c * signf(x2[ch] - y2[ch]);
-                                if (SSIM_ON) {
-                                    const float wu = fold_lo(q), wd = fold_hi(q, h);
-                                    const float aA = pick(wu, cA.A[ch]) + cB.A[ch] + pick(wd, cC.A[ch]);
-                                    const float aB = pick(wu, cA.B[ch]) + cB.B[ch] + pick(wd, cC.B[ch]);
-                                    const float aC = pick(wu, cA.C[ch]) + cB.C[ch] + pick(wd, cC.C[ch]);
-                                    g += (aA + 2.f * x2[ch] * aB + y2[ch] * aC) * kInv9;
-                                }
-                                gw[ch] = g;
-                            }
-                            if (gw[0] != 0.f || gw[1] != 0.f || gw[2] != 0.f) {
-                                Sample sm;
-                                project(ctx, q, c, sm);
-                                Corners v;
-                                gather(ctx, sm, v);
-                                const float e = 1.f - sm.tx, so = 1.f - sm.ty;
-                                float gix = 0.f, giy = 0.f;
-#pragma unroll
-                                for (int ch = 0; ch < 3; ++ch) {
-                                    gix += ((v.ne[ch] - v.nw[ch]) * so + (v.se[ch] - v.sw[ch]) * sm.ty) * gw[ch];
-                                    giy += ((v.sw[ch] - v.nw[ch]) * e + (v.se[ch] - v.ne[ch]) * sm.tx) * gw[ch];
-                                }
-                                gix *= sm.gmx;
-                                giy *= sm.gmy;
-                                const float dpx = gix * 2.f / (float)(w - 1);
-                                const float dpy = giy * 2.f / (float)(h - 1);
-                                float dc[3];
-                                dc[0] = dpx / sm.den;
-                                dc[1] = dpy / sm.den;
-                                dc[2] = -(dpx * sm.cam[0]) / (sm.den * sm.den) - (dpy * sm.cam[1]) / (sm.den * sm.den);
-#pragma unroll
-                                for (int i = 0; i < 3; ++i) {
-#pragma unroll
-                                    for (int j = 0; j < 3; ++j) dP[i * 4 + j] += dc[i] * sm.pt[j];
-                                    dP[i * 4 + 3] += dc[i];
-                                }
-                                float ddepth = 0.f;
-#pragma unroll
-                                for (int j = 0; j < 3; ++j) {
-                                    const float dpt = ctx.cm.P[0 * 4 + j] * dc[0] + ctx.cm.P[1 * 4 + j] * dc[1] +
-                                                      ctx.cm.P[2 * 4 + j] * dc[2];
-                                    ddepth += dpt * sm.ray[j];
-                                }
-                                const float dd = -ddepth * (sm.depth * sm.depth) * ctx.range;
-                                if (f == 0) dfull[q * w + c] = dd;
-                                else dfull[q * w + c] += dd;
-                            } else {
-                                if (f == 0) dfull[q * w + c] = 0.f;
-                            }
-                        }
-                    }
-                    cA = cB;
-                    cB = cC;
-                }
-                if (SSIM_ON) {
+                    const float gS = gp * (0.85f / 3.f);
 #pragma unroll
                     for (int ch = 0; ch < 3; ++ch) {
-                        hA[ch] = hB[ch];
-                        hB[ch] = hc[ch];
+                        float dA, dB, dC;
+                        ssim_adjoint(hA[ch], hB[ch], hc[ch], gS, dA, dB, dC);
+                        if (gp == 0.f) dA = dB = dC = 0.f;
+                        cC.A[ch] = pick(wl, shfl_prev(dA)) + dA + pick(wr, shfl_next(dA));
+                        cC.B[ch] = pick(wl, shfl_prev(dB)) + dB + pick(wr, shfl_next(dB));
+                        cC.C[ch] = pick(wl, shfl_prev(dC)) + dC + pick(wr, shfl_next(dC));
                     }
                 }
+                if (k >= 4) {
+                    // output row q = r - 2 (coefficient rows q-1, q, q+1 = cA, cB, cC)
+                    const int q = r - 2;
+                    if (colok && q < h) {
+                        const float l1c = cB.g * (l1w / 3.f);
+                        float dpx = 0.f, dpy = 0.f;
+#pragma unroll
+                        for (int ch = 0; ch < 3; ++ch) {
+                            float g = l1c * signf(x2[ch] - y2[ch]);
+                            if (SSIM_ON) {
+                                const float wu = fold_lo(q), wd = fold_hi(q, h);
+                                const float aA = pick(wu, cA.A[ch]) + cB.A[ch] + pick(wd, cC.A[ch]);
+                                const float aB = pick(wu, cA.B[ch]) + cB.B[ch] + pick(wd, cC.B[ch]);
+                                const float aC = pick(wu, cA.C[ch]) + cB.C[ch] + pick(wd, cC.C[ch]);
+                                g += (aA + 2.f * x2[ch] * aB + y2[ch] * aC) * kInv9;
+                            }
+                            dpx += g * k2.jx[ch];
+                            dpy += g * k2.jy[ch];
+                        }
+                        float dc[3];
+                        dc[0] = dpx * k2.inv_den;
+                        dc[1] = dpy * k2.inv_den;
+                        dc[2] = -(dpx * k2.px + dpy * k2.py) * k2.inv_den;
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) {
+#pragma unroll
+                            for (int j = 0; j < 3; ++j) dP[i * 4 + j] += dc[i] * k2.pt[j];
+                            dP[i * 4 + 3] += dc[i];
+                        }
+                        const float dd = (dc[0] * k2.u[0] + dc[1] * k2.u[1] + dc[2] * k2.u[2]) * k2.dd;
+                        if (f == 0) dfull[q * w + c] = dd;
+                        else dfull[q * w + c] += dd;
+                    }
+                }
+                cA = cB;
+                cB = cC;
+            }
+            if (SSIM_ON) {
 #pragma unroll
                 for (int ch = 0; ch < 3; ++ch) {
-                    x2[ch] = x1[ch];
-                    y2[ch] = y1[ch];
-                    x1[ch] = x[ch];
-                    y1[ch] = y[ch];
+                    hA[ch] = hB[ch];
+                    hB[ch] = hc[ch];
                 }
             }
-            // one 12-float partial of dL/dP per (wave, frame)
-            float* dst = a.dP_part[ls] + ((size_t)f * a.B * a.wpi + wv) * 12;
 #pragma unroll
-            for (int j = 0; j < 12; ++j) {
-                const float t = wave_sum(dP[j]);
-                if (lane == 0) dst[j] = t;
+            for (int ch = 0; ch < 3; ++ch) {
+                x2[ch] = x1[ch];
+                y2[ch] = y1[ch];
+                x1[ch] = x[ch];
+                y1[ch] = y[ch];
             }
+            k2 = k1;
+            k1 = kc;
         }
+        // one 12-float partial of dL/dP per (item, frame)
+        float* dst = a.dP_part[ls] + ((size_t)f * a.B * a.wpi + item_in_scale) * 12;
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            const float t = wave_sum(dP[j]);
+            if (lane == 0) dst[j] = t;
+        }
+    }
+}
+
+// Resident waves walk the (image, row block, strip, scale) items; each XCD owns a
+// contiguous item range (its L2 streams a contiguous slice of the images).
+template <int NS, bool SSIM_ON>
+__global__ __launch_bounds__(kBlock, 2) void photo_bwd_kernel(PhotoArgs a) {
+    const int lane = threadIdx.x & (kWave - 1);
+    // G groups of blocks (the 8 XCDs under round-robin dispatch; fewer for tiny grids)
+    const int nb = gridDim.x, G = nb < 8 ? nb : 8, grp = blockIdx.x % G;
+    const int blks_here = nb / G + (grp < nb % G ? 1 : 0);
+    const int waves_here = blks_here * kWavesPerBlock;
+    const int wid = __builtin_amdgcn_readfirstlane((int)(blockIdx.x / G) * kWavesPerBlock + (threadIdx.x >> 6));
+    const int items = a.B * a.wpi * a.nsc;
+    const int i_begin = (int)((long long)items * grp / G), i_end = (int)((long long)items * (grp + 1) / G);
+    for (int it = i_begin + wid; it < i_end; it += waves_here) {
+        // item order: b, row block, strip, scale
+        int t = it;
+        const int ls = t % a.nsc;
+        t /= a.nsc;
+        const int st = t % a.strips;
+        t /= a.strips;
+        const int rb = t % a.rowblocks;
+        const int b = t / a.rowblocks;
+        bwd_item<NS, SSIM_ON>(a, b, ls, st, rb, lane);
     }
 }
 
@@ -1133,10 +1219,30 @@ void launch_fwd_t(const PhotoArgs& a, hipStream_t st) {
     const int blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     hipLaunchKernelGGL((photo_fwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, a);
 }
+// number of workgroups that can be resident at once for a kernel (cached per
+// kernel and device); the persistent-loop kernels launch exactly that many
+template <class K>
+int resident_blocks(K kernel) {
+    static std::mutex mu;
+    static int cache_dev = -1, cache_val = 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    if (dev != cache_dev) {
+        int cus = 0, per_cu = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0);
+        cache_val = max(1, cus) * max(1, per_cu);
+        cache_dev = dev;
+    }
+    return cache_val;
+}
+
 template <int NS, bool SSIM>
 void launch_bwd_t(const PhotoArgs& a, hipStream_t st) {
-    const int waves = a.B * a.wpi;
-    const int blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int items = a.B * a.wpi * a.nsc;
+    const int need = (items + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int blocks = min(need, resident_blocks(photo_bwd_kernel<NS, SSIM>));
     hipLaunchKernelGGL((photo_bwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, a);
 }
 
