@@ -43,8 +43,14 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kFwdCols = kWave - 2;  // output columns per forward strip
 constexpr int kBwdCols = kWave - 4;  // output columns per backward strip
-constexpr int kRowsF = 8;            // output rows per forward wave
-constexpr int kRowsB = 8;            // output rows per backward wave
+#ifndef MD2_ROWS_F
+#define MD2_ROWS_F 4
+#endif
+#ifndef MD2_ROWS_B
+#define MD2_ROWS_B 16
+#endif
+constexpr int kRowsF = MD2_ROWS_F;   // output rows per forward work item
+constexpr int kRowsB = MD2_ROWS_B;   // output rows per backward work item
 constexpr int kSmoothChunk = 2048;   // pixels per smoothness partial
 constexpr float kC1 = 0.0001f;       // 0.01 ** 2   layers.py:231
 constexpr float kC2 = 0.0009f;       // 0.03 ** 2   layers.py:232
