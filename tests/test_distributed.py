@@ -1,0 +1,146 @@
+"""Data parallelism on CPU with gloo, world size 2 (the GPU path uses RCCL).
+
+Each rank runs the real depth/pose networks on its own batch shard with the oracle
+hot-path loss (the HIP kernels need a GPU; the gradient-averaging logic under test
+does not depend on the loss implementation).  After the gradient sync every rank
+must hold the average of the per-shard gradients computed single-process, for both
+sync strategies: DDP (eager steps) and FlatGradSync (graph-capturable buckets).
+The classifier heads encoder.fc.* must be excluded from the sync.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from monodepth2_amd import networks
+from monodepth2_amd.data import synthetic_batch
+from monodepth2_amd.distributed import FlatGradSync, ignored_parameters, shard, wrap_ddp
+from monodepth2_amd.layers import transformation_from_parameters
+
+H, W, B_PER_RANK = 64, 64, 2
+FRAMES = [0, -1, 1]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class Nets(torch.nn.Module):
+    """Depth + pose networks behind one forward (as Trainer's _Networks), so DDP's
+    forward pre-hooks run."""
+
+    def __init__(self):
+        super().__init__()
+        enc = networks.ResnetEncoder(18, False)
+        self.models = torch.nn.ModuleDict({
+            "encoder": enc,
+            "depth": networks.DepthDecoder(enc.num_ch_enc, range(4)),
+            "pose_encoder": networks.ResnetEncoder(18, False, num_input_images=2),
+        })
+        self.models["pose"] = networks.PoseDecoder(self.models["pose_encoder"].num_ch_enc, 1, 2)
+
+    def forward(self, inputs):
+        m = self.models
+        outputs = m["depth"](m["encoder"](inputs[("color_aug", 0, 0)]))
+        for f in FRAMES[1:]:
+            pair = [inputs[("color_aug", f, 0)], inputs[("color_aug", 0, 0)]] if f < 0 else \
+                [inputs[("color_aug", 0, 0)], inputs[("color_aug", f, 0)]]
+            a, t = m["pose"]([m["pose_encoder"](torch.cat(pair, 1))])
+            outputs[("cam_T_cam", 0, f)] = transformation_from_parameters(a[:, 0], t[:, 0], invert=(f < 0))
+        return outputs
+
+
+def build_nets(seed=0):
+    torch.manual_seed(seed)
+    return Nets()
+
+
+def loss_fn(nets, inputs):
+    from oracle.md2_oracle import HotPathOptions, hot_path
+    outputs = nets(inputs)
+    camT = {f: outputs[("cam_T_cam", 0, f)] for f in FRAMES[1:]}
+    gen = torch.Generator().manual_seed(99)
+    noise = {s: torch.randn(inputs[("color", 0, 0)].shape[0], 2, H, W, generator=gen) for s in range(4)}
+    losses, _ = hot_path(HotPathOptions(height=H, width=W, frame_ids=FRAMES),
+                         {s: outputs[("disp", s)] for s in range(4)}, inputs, camT, noise=noise,
+                         keep_images=False)
+    return losses["loss"]
+
+
+def full_batch():
+    return synthetic_batch(2 * B_PER_RANK, H, W, FRAMES, 4, seed=7)
+
+
+def _worker(rank, world, port, mode, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    nets = build_nets()
+    inputs = shard(full_batch(), rank, world)
+    if mode == "ddp":
+        model = wrap_ddp(nets, torch.device("cpu"))
+        loss = loss_fn(model, inputs)
+        loss.backward()
+    else:
+        sync = FlatGradSync(nets.named_parameters(), world)
+        sync.zero()
+        loss = loss_fn(nets, inputs)
+        loss.backward()
+        sync.sync()
+    grads = {n: (p.grad.clone() if p.grad is not None else None) for n, p in nets.named_parameters()}
+    torch.save(grads, os.path.join(out_dir, f"{mode}_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _reference_grads():
+    """Average of the per-shard gradients, computed in one process."""
+    torch.set_num_threads(4)
+    batch = full_batch()
+    acc = None
+    for r in range(2):
+        nets = build_nets()
+        loss_fn(nets, shard(batch, r, 2)).backward()
+        g = {n: p.grad.clone() for n, p in nets.named_parameters() if p.grad is not None}
+        acc = g if acc is None else {n: acc[n] + g[n] for n in acc}
+    return {n: v / 2 for n, v in acc.items()}
+
+
+@pytest.fixture(scope="module")
+def ref_grads():
+    return _reference_grads()
+
+
+@pytest.mark.parametrize("mode", ["ddp", "flat"])
+def test_gradient_average_matches_single_process(mode, ref_grads, tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, mode, str(tmp_path)), nprocs=2, join=True)
+    g0 = torch.load(os.path.join(tmp_path, f"{mode}_0.pt"), weights_only=True)
+    g1 = torch.load(os.path.join(tmp_path, f"{mode}_1.pt"), weights_only=True)
+    ignored = set(ignored_parameters(build_nets()))
+    assert ignored and all(".encoder.fc." in n for n in ignored)
+    checked = 0
+    for n, ref in ref_grads.items():
+        assert n not in ignored
+        a, b = g0[n], g1[n]
+        assert torch.equal(a, b), f"ranks disagree on {n}"
+        torch.testing.assert_close(a, ref, rtol=1e-4, atol=1e-7)
+        checked += 1
+    assert checked > 100
+    for n in ignored:
+        assert g0[n] is None or float(g0[n].abs().sum()) == 0.0
+
+
+def test_shard_slices_batched_tensors():
+    batch = full_batch()
+    s1 = shard(batch, 1, 2)
+    assert torch.equal(s1[("color", 0, 0)], batch[("color", 0, 0)][B_PER_RANK:])
+    assert torch.equal(s1[("K", 2)], batch[("K", 2)][B_PER_RANK:])
+    assert s1[("color", -1, 3)].shape[0] == B_PER_RANK
