@@ -133,7 +133,9 @@ int md2_generate_images(const md2_desc* desc, const md2_tensors* t,
  * Optional kernel timing for benchmarks: between md2_timing_begin and
  * md2_timing_end every launch of the two photometric kernels (the forward
  * photo kernel and the backward photo kernel, which dominate the hot path) is
- * bracketed by hipEvents recorded on the launch stream.  md2_timing_end waits
+ * launched with hipExtLaunchKernelGGL, which stamps a start/stop hipEvent pair on
+ * the kernel dispatch itself (v1_multiscale's per-scale launches are not timed).
+ * md2_timing_end waits
  * for the last event and returns the summed durations (ms) and launch counts.
  * Not for use under graph capture (events are recorded eagerly).
  */

@@ -24,6 +24,7 @@
 // are reduced in a fixed order by single-block finalize kernels.
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <math.h>
 #include <stdarg.h>
@@ -1067,18 +1068,17 @@ struct Timing {
 };
 Timing g_timing;
 
-// returns the slot index or -1
-int timing_start(int kind, hipStream_t st) {
+// Reserve a timing slot (or -1).  The events are stamped by hipExtLaunchKernelGGL on
+// the kernel dispatch itself, so they measure the kernel, not the queue around it.
+int timing_slot(int kind, hipEvent_t* start, hipEvent_t* stop) {
     std::lock_guard<std::mutex> lk(g_timing.mu);
+    *start = *stop = nullptr;
     if (!g_timing.on || g_timing.used >= g_timing.cap) return -1;
     const int i = g_timing.used++;
     g_timing.kind[i] = kind;
-    (void)hipEventRecord(g_timing.ev[2 * i], st);
+    *start = g_timing.ev[2 * i];
+    *stop = g_timing.ev[2 * i + 1];
     return i;
-}
-void timing_stop(int slot, hipStream_t st) {
-    if (slot < 0) return;
-    (void)hipEventRecord(g_timing.ev[2 * slot + 1], st);
 }
 
 int fail(int code, const char* fmt, ...) {
@@ -1220,10 +1220,13 @@ void photo_args(const md2_desc* d, const md2_tensors* t, const Layout& L, int s_
 }
 
 template <int NS, bool SSIM>
-void launch_fwd_t(const PhotoArgs& a, hipStream_t st) {
+void launch_fwd_t(const PhotoArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
     const int waves = a.B * a.wpi;
     const int blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
-    hipLaunchKernelGGL((photo_fwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, a);
+    if (e0)
+        hipExtLaunchKernelGGL((photo_fwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, e0, e1, 0, a);
+    else
+        hipLaunchKernelGGL((photo_fwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, a);
 }
 // number of workgroups that can be resident at once for a kernel (cached per
 // kernel and device); the persistent-loop kernels launch exactly that many
@@ -1245,23 +1248,27 @@ int resident_blocks(K kernel) {
 }
 
 template <int NS, bool SSIM>
-void launch_bwd_t(const PhotoArgs& a, hipStream_t st) {
+void launch_bwd_t(const PhotoArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
     const int items = a.B * a.wpi * a.nsc;
     const int need = (items + kWavesPerBlock - 1) / kWavesPerBlock;
     const int blocks = min(need, resident_blocks(photo_bwd_kernel<NS, SSIM>));
-    hipLaunchKernelGGL((photo_bwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, a);
+    if (e0)
+        hipExtLaunchKernelGGL((photo_bwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, e0, e1, 0, a);
+    else
+        hipLaunchKernelGGL((photo_bwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, a);
 }
 
-void launch_photo(const PhotoArgs& a, bool bwd, hipStream_t st) {
+void launch_photo(const PhotoArgs& a, bool bwd, hipStream_t st, hipEvent_t e0 = nullptr,
+                  hipEvent_t e1 = nullptr) {
     const bool ssim = !(a.flags & MD2_NO_SSIM);
 #define MD2_DISPATCH(NS)                                          \
     if (a.S == NS) {                                              \
         if (bwd) {                                                \
-            if (ssim) launch_bwd_t<NS, true>(a, st);              \
-            else launch_bwd_t<NS, false>(a, st);                  \
+            if (ssim) launch_bwd_t<NS, true>(a, st, e0, e1);      \
+            else launch_bwd_t<NS, false>(a, st, e0, e1);          \
         } else {                                                  \
-            if (ssim) launch_fwd_t<NS, true>(a, st);              \
-            else launch_fwd_t<NS, false>(a, st);                  \
+            if (ssim) launch_fwd_t<NS, true>(a, st, e0, e1);      \
+            else launch_fwd_t<NS, false>(a, st, e0, e1);          \
         }                                                         \
         return;                                                   \
     }
@@ -1304,17 +1311,17 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
     hipStream_t st = (hipStream_t)stream;
     uint8_t* ws = (uint8_t*)workspace;
     PhotoArgs a;
-    const int slot = timing_start(0, st);
-    if (L.v1) {
+    if (L.v1) {  // one launch per scale (each at its own resolution); not timed
         for (int s = 0; s < L.nscales; ++s) {
             photo_args(d, t, L, s, s + 1, false, ws, select_out, a);
             launch_photo(a, false, st);
         }
     } else {
+        hipEvent_t e0, e1;
+        timing_slot(0, &e0, &e1);
         photo_args(d, t, L, 0, L.nscales, false, ws, select_out, a);
-        launch_photo(a, false, st);
+        launch_photo(a, false, st, e0, e1);
     }
-    timing_stop(slot, st);
     if ((rc = hip_check("photo_fwd_kernel"))) return rc;
 
     SmoothArgs sa;
@@ -1371,7 +1378,6 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
     hipStream_t st = (hipStream_t)stream;
     uint8_t* ws = (uint8_t*)workspace;
     PhotoArgs a;
-    const int slot = timing_start(1, st);
     if (L.v1) {
         for (int s = 0; s < L.nscales; ++s) {
             photo_args(d, t, L, s, s + 1, true, ws, (uint8_t*)select, a);
@@ -1379,11 +1385,12 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
             launch_photo(a, true, st);
         }
     } else {
+        hipEvent_t e0, e1;
+        timing_slot(1, &e0, &e1);
         photo_args(d, t, L, 0, L.nscales, true, ws, (uint8_t*)select, a);
         a.grad_loss = grad_loss;
-        launch_photo(a, true, st);
+        launch_photo(a, true, st, e0, e1);
     }
-    timing_stop(slot, st);
     if ((rc = hip_check("photo_bwd_kernel"))) return rc;
 
     for (int s = 0; s < L.nscales; ++s) {

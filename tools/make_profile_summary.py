@@ -1,0 +1,79 @@
+"""Turn gpurun_out/<round>/ rocprofv3 CSVs into the committed summaries under profiles/<round>/:
+  kernel_stats.csv       (copy of the --stats summary of the bench command)
+  hot_kernels.json       per hot-path kernel: calls, avg ns, PMC averages per dispatch
+  pmc_traffic.json       photo_bwd/photo_fwd HBM bytes per launch (bench.py reads it)
+
+HBM bytes per MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KB; on gfx950
+FETCH_SIZE reads 1/2 of the bytes of wide coalesced streaming reads, so the corrected
+read side is 2 x FETCH_SIZE (an upper estimate for 4-B-per-lane reads, which the guide
+leaves uncalibrated); traffic = 2 x FETCH + WRITE.
+    python tools/make_profile_summary.py r01
+"""
+import csv
+import collections
+import glob
+import json
+import os
+import re
+import shutil
+import sys
+
+VALU_ISSUE_PER_S = 256 * 4 * 0.5 * 2.4e9   # wave-instructions/s (SIMD32 issues a wave64 op per 2 clk)
+
+
+def short(n):
+    n = re.sub(r"\(anonymous namespace\)::", "", n)
+    return re.sub(r"^void ", "", n).split("(")[0]
+
+
+def main():
+    rnd = sys.argv[1]
+    src = os.path.join("gpurun_out", rnd)
+    dst = os.path.join("profiles", rnd)
+    os.makedirs(dst, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))[0]
+    shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
+    rows = list(csv.DictReader(open(stats)))
+    total = sum(float(r["TotalDurationNs"]) for r in rows)
+    res = {}
+    for r in rows:
+        k = short(r["Name"])
+        if any(t in k for t in ("photo_", "disp_grad", "smooth_fwd", "grad_T", "finalize_fwd")):
+            res.setdefault(k, {}).update(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
+                                         share_of_gpu_time=float(r["TotalDurationNs"]) / total)
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, cs in agg.items():
+        d = res.setdefault(k, {})
+        for c, v in cs.items():
+            d[c] = sum(v) / len(v)
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            d["hbm_read_bytes_corrected"] = 2 * d["FETCH_SIZE"] * 1024
+            d["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
+            d["hbm_traffic_bytes"] = d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]
+        if "SQ_INSTS_VALU" in d and "avg_ns" in d:
+            d["valu_issue_frac"] = d["SQ_INSTS_VALU"] / (d["avg_ns"] * 1e-9 * VALU_ISSUE_PER_S)
+        if "TCC_HIT_sum" in d:
+            d["l2_hit_rate"] = d["TCC_HIT_sum"] / max(1.0, d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
+    json.dump(res, open(os.path.join(dst, "hot_kernels.json"), "w"), indent=1, sort_keys=True)
+    bwd = next(v for k, v in res.items() if k.startswith("photo_bwd"))
+    fwd = next(v for k, v in res.items() if k.startswith("photo_fwd"))
+    traffic = {"photo_bwd_kernel_bytes_per_launch": bwd.get("hbm_traffic_bytes"),
+               "photo_fwd_kernel_bytes_per_launch": fwd.get("hbm_traffic_bytes"),
+               "photo_bwd_valu_issue_frac": bwd.get("valu_issue_frac"),
+               "photo_fwd_valu_issue_frac": fwd.get("valu_issue_frac"),
+               "photo_bwd_avg_ns_rocprof": bwd.get("avg_ns"),
+               "photo_fwd_avg_ns_rocprof": fwd.get("avg_ns"),
+               "note": "traffic = 2*FETCH_SIZE + WRITE_SIZE (KB->B) per launch, separate --pmc passes"}
+    json.dump(traffic, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps(traffic, indent=1))
+    for k, d in sorted(res.items()):
+        print(k, {c: round(v, 4) if isinstance(v, float) else v for c, v in d.items()
+                  if c in ("calls", "avg_ns", "share_of_gpu_time", "hbm_traffic_bytes", "valu_issue_frac",
+                           "l2_hit_rate")})
+
+
+if __name__ == "__main__":
+    main()
