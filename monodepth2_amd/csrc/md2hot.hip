@@ -834,22 +834,42 @@ struct FinalArgs {
     float* loss_out;
 };
 
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+// Fixed-order block sum of N doubles per thread: per-wave butterflies, then wave 0
+// adds the 4 wave totals in order.  Result valid in every thread.
+template <int N>
+__device__ __forceinline__ void block_sum_d(double (&v)[N]) {
+    __shared__ double red[N][kWavesPerBlock];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        v[j] = wave_sum_d(v[j]);
+        if (lane == 0) red[j][wid] = v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] = ((red[j][0] + red[j][1]) + red[j][2]) + red[j][3];
+    __syncthreads();
+}
+
+// one block; wave w < num_scales reduces scale w's photometric partials, thread t < B
+// of each scale the smoothness chunks of image t (both in a fixed order)
 __global__ __launch_bounds__(kBlock) void finalize_fwd_kernel(FinalArgs a) {
-    __shared__ double red[kBlock];
-    __shared__ double sm_loss[MD2_MAX_SCALES];
-    const int t = threadIdx.x;
-    for (int s = 0; s < a.num_scales; ++s) {
+    __shared__ double photo[MD2_MAX_SCALES];
+    __shared__ double smooth[MD2_MAX_SCALES][kBlock];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    if (wid < a.num_scales) {
         double acc = 0.0;
-        for (int i = t; i < a.nphoto[s]; i += kBlock) acc += (double)a.photo_part[s][i];
-        red[t] = acc;
-        __syncthreads();
-        for (int o = kBlock / 2; o > 0; o >>= 1) {
-            if (t < o) red[t] += red[t + o];
-            __syncthreads();
-        }
-        double photo = red[0];
-        __syncthreads();
-        // smoothness: per image, chunks in order
+        for (int i = lane; i < a.nphoto[wid]; i += kWave) acc += (double)a.photo_part[wid][i];
+        acc = wave_sum_d(acc);
+        if (lane == 0) photo[wid] = acc;
+    }
+    for (int s = 0; s < a.num_scales; ++s) {
         double sm = 0.0;
         const int hs = a.hs[s], ws = a.ws[s];
         if (t < a.B) {
@@ -868,23 +888,18 @@ __global__ __launch_bounds__(kBlock) void finalize_fwd_kernel(FinalArgs a) {
             st[2] = (float)sy;
             st[3] = 0.f;
         }
-        red[t] = sm;
-        __syncthreads();
-        for (int o = kBlock / 2; o > 0; o >>= 1) {
-            if (t < o) red[t] += red[t + o];
-            __syncthreads();
-        }
-        if (t == 0) {
-            const double photo_mean = photo / ((double)a.B * a.lh[s] * a.lw[s]);
-            sm_loss[s] = photo_mean + (double)a.smoothness * red[0] / (double)(1 << s);
-        }
-        __syncthreads();
+        smooth[s][t] = sm;
     }
+    __syncthreads();
     if (t == 0) {
         double total = 0.0;
         for (int s = 0; s < a.num_scales; ++s) {
-            a.loss_out[s] = (float)sm_loss[s];
-            total += sm_loss[s];
+            double sm = 0.0;
+            for (int b = 0; b < a.B; ++b) sm += smooth[s][b];
+            const double loss = photo[s] / ((double)a.B * a.lh[s] * a.lw[s]) +
+                                (double)a.smoothness * sm / (double)(1 << s);
+            a.loss_out[s] = (float)loss;
+            total += loss;
         }
         a.loss_out[a.num_scales] = (float)(total / a.num_scales);
     }
@@ -974,44 +989,43 @@ struct DTArgs {
 };
 
 __global__ __launch_bounds__(kBlock) void grad_T_kernel(DTArgs a) {
-    // one block per (tscale, f, b)
-    const int nT = a.per_scale ? a.num_scales : 1;
+    // one block per (tscale, f, b); every thread accumulates all 12 dP entries over
+    // a strided share of the partials, then one fixed-order block reduction
     int id = blockIdx.x;
     const int b = id % a.B;
     id /= a.B;
     const int f = id % a.S;
     const int ts = id / a.S;
-    __shared__ double red[kBlock];
-    __shared__ double dP[12];
+    const int t = threadIdx.x;
     double dT[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) dT[j] = 0.0;
-    const int t = threadIdx.x;
     for (int s = 0; s < a.num_scales; ++s) {
         if (a.per_scale && s != ts) continue;
         const int n = a.wpi[s];
         const float* base = a.dP_part[s] + ((size_t)f * a.B * n + (size_t)b * n) * 12;
-        for (int j = 0; j < 12; ++j) {
-            double acc = 0.0;
-            for (int k = t; k < n; k += kBlock) acc += (double)base[(size_t)k * 12 + j];
-            red[t] = acc;
-            __syncthreads();
-            for (int o = kBlock / 2; o > 0; o >>= 1) {
-                if (t < o) red[t] += red[t + o];
-                __syncthreads();
-            }
-            if (t == 0) dP[j] = red[0];
-            __syncthreads();
+        double dP[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) dP[j] = 0.0;
+        for (int k = t; k < n; k += kBlock) {
+#pragma unroll
+            for (int j = 0; j < 12; ++j) dP[j] += (double)base[(size_t)k * 12 + j];
         }
+        block_sum_d<12>(dP);
         const float* K = a.K[s] + b * 16;
+#pragma unroll
         for (int r = 0; r < 4; ++r)
-            for (int cidx = 0; cidx < 4; ++cidx)
-                dT[r * 4 + cidx] += (double)K[0 * 4 + r] * dP[0 * 4 + cidx] + (double)K[1 * 4 + r] * dP[1 * 4 + cidx] +
-                                    (double)K[2 * 4 + r] * dP[2 * 4 + cidx];
-        __syncthreads();
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                dT[r * 4 + c] += (double)K[0 * 4 + r] * dP[0 * 4 + c] + (double)K[1 * 4 + r] * dP[1 * 4 + c] +
+                                 (double)K[2 * 4 + r] * dP[2 * 4 + c];
     }
-    (void)nT;
-    if (t < 16) a.grad_T[(((size_t)ts * a.S + f) * a.B + b) * 16 + t] = (float)dT[t];
+    if (t < 16) {
+        double v = 0.0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v = (j == t) ? dT[j] : v;
+        a.grad_T[(((size_t)ts * a.S + f) * a.B + b) * 16 + t] = (float)v;
+    }
 }
 
 // ----------------------------------------------------------------------------
