@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 1
+#define MD2_ABI_VERSION 2
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -49,6 +49,7 @@ extern "C" {
 #define MD2_NO_AUTOMASK      (1u << 2) /* --disable_automasking trainer.py:432,466,480  */
 #define MD2_V1_MULTISCALE    (1u << 3) /* --v1_multiscale       trainer.py:347-352,417  */
 #define MD2_T_PER_SCALE      (1u << 4) /* a cam_T_cam per scale (posecnn, trainer.py:366-375) */
+#define MD2_PREDICTIVE_MASK  (1u << 5) /* --predictive_mask     trainer.py:447-459 (needs NO_AUTOMASK) */
 
 typedef struct md2_desc {
     int32_t batch;               /* B: images per rank (opt.batch_size)                  */
@@ -86,6 +87,10 @@ typedef struct md2_tensors {
     /* Optional device-side uint64 mixed into desc.seed at run time, so a captured
      * hipGraph draws fresh noise on every replay (the caller increments it). */
     const uint64_t* seed_ptr;
+    /* MD2_PREDICTIVE_MASK: outputs["predictive_mask"][("disp", s)] upsampled to the
+     * loss resolution (trainer.py:449-453), per scale packed back to back, scale s
+     * shaped (B, S, h_s, w_s).  Multiplies each frame's reprojection loss. */
+    const float* mask;
 } md2_tensors;
 
 int md2_abi_version(void);
@@ -111,11 +116,13 @@ int md2_photometric_fwd(const md2_desc* desc, const md2_tensors* t,
 /*
  * Backward.  grad_loss: device (num_scales+1) upstream gradients of loss_out.
  * Writes (overwrites) grad_disp[s] shaped like disp[s], and grad_T shaped like
- * T.  select and workspace must come from the matching forward.
+ * T, and with MD2_PREDICTIVE_MASK grad_mask shaped like tensors.mask (dL/dmask
+ * through trainer.py:455; the BCE term of 457-459 is the caller's).  select and
+ * workspace must come from the matching forward.
  */
 int md2_photometric_bwd(const md2_desc* desc, const md2_tensors* t,
                         const float* grad_loss, const uint8_t* select,
-                        float* const* grad_disp, float* grad_T,
+                        float* const* grad_disp, float* grad_T, float* grad_mask,
                         void* workspace, void* stream);
 
 /*

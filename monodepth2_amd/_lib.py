@@ -19,13 +19,14 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
 NO_AUTOMASK = 1 << 2
 V1_MULTISCALE = 1 << 3
 T_PER_SCALE = 1 << 4
+PREDICTIVE_MASK = 1 << 5
 
 _vp = ctypes.c_void_p
 
@@ -45,7 +46,8 @@ class Tensors(ctypes.Structure):
                 ("inv_K", _vp * MAX_SCALES),
                 ("T", _vp),
                 ("noise", _vp),
-                ("seed_ptr", _vp)]
+                ("seed_ptr", _vp),
+                ("mask", _vp)]
 
 
 _lock = threading.Lock()
@@ -69,7 +71,7 @@ def _declare(L):
     L.md2_photometric_fwd.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(Tensors), _vp, _vp, _vp, _vp]
     L.md2_photometric_bwd.restype = ctypes.c_int
     L.md2_photometric_bwd.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(Tensors), _vp, _vp,
-                                      ctypes.POINTER(_vp), _vp, _vp, _vp]
+                                      ctypes.POINTER(_vp), _vp, _vp, _vp, _vp]
     L.md2_generate_images.restype = ctypes.c_int
     L.md2_generate_images.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(Tensors),
                                       ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp]

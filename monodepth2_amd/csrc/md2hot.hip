@@ -353,6 +353,9 @@ struct PhotoArgs {
     const float* grad_loss;                 // (num_scales + 1)
     float* dfull[MD2_MAX_SCALES];           // per local scale (B,h,w)
     float* dP_part[MD2_MAX_SCALES];         // per local scale [S][B*wpi][12]
+    // predictive mask (MD2_PREDICTIVE_MASK): per local scale (B,S,h,w)
+    const float* mask[MD2_MAX_SCALES];
+    float* gmask[MD2_MAX_SCALES];
 };
 
 __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int b, WarpCtx& c) {
@@ -503,11 +506,13 @@ __global__ __launch_bounds__(kBlock, 2) void photo_fwd_kernel(PhotoArgs a) {
             L.code[i][lane] = code;
             L.accum[i][lane] = 0.f;
         }
+        const float* pmask = (a.flags & MD2_PREDICTIVE_MASK) ? a.mask[ls] : nullptr;
         for (int f = 0; f < NS; ++f) {
             WarpCtx ctx;
             make_ctx(a, ls, f, b, ctx);
             const int cand = (automask ? NS : 0) + f;
             reproj_rows<SSIM_ON, true>(ctx, tgt, r0, cc, [&](int i, float v) {
+                if (pmask) v *= pmask[(((size_t)b * NS + f) * h + min(r0 + i, h - 1)) * w + cc];  // trainer.py:455
                 if (avg) {
                     L.accum[i][lane] += v;
                 } else if (v < L.best[i][lane]) {
@@ -618,6 +623,8 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
     const uint8_t* sel = a.sel[ls] + (size_t)b * HW;
     float* dfull = a.dfull[ls] + (size_t)b * HW;
     const int item_in_scale = b * a.wpi + rb * a.strips + st;
+    const float* pmask = (a.flags & MD2_PREDICTIVE_MASK) ? a.mask[ls] : nullptr;
+    float* pgmask = pmask ? a.gmask[ls] : nullptr;
 
     for (int f = 0; f < NS; ++f) {
         WarpCtx ctx;
@@ -652,7 +659,23 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
                 // coefficient row p = r - 1
                 const int p = r - 1;
                 float gp = 0.f;
-                if (colreal && p >= 0 && p < h) gp = gscale * frame_weight<NS>(sel[p * w + c], f, automask, avg);
+                const bool own = colreal && p >= 0 && p < h;
+                if (own) gp = gscale * frame_weight<NS>(sel[p * w + c], f, automask, avg);
+                if (pmask) {
+                    // masked = reproj * mask (trainer.py:455): d/dreproj = g*mask, d/dmask = g*reproj
+                    const size_t mi = (((size_t)b * NS + f) * h + (own ? p : 0)) * w + (own ? c : 0);
+                    if (pgmask && colok && p >= r0 && p < r0 + kRowsB && p < h) {
+                        float ss = 0.f, l1 = 0.f;
+#pragma unroll
+                        for (int ch = 0; ch < 3; ++ch) {
+                            if (SSIM_ON) ss += ssim_from_sums(hA[ch], hB[ch], hc[ch]);
+                            l1 += fabsf(y1[ch] - x1[ch]);
+                        }
+                        const float rep = SSIM_ON ? 0.85f * (ss / 3.f) + 0.15f * (l1 / 3.f) : l1 / 3.f;
+                        pgmask[mi] = gp * rep;
+                    }
+                    gp *= own ? pmask[mi] : 0.f;
+                }
                 Coef cC;
                 cC.g = gp;
                 if (SSIM_ON) {
@@ -1115,6 +1138,7 @@ struct Layout {
     size_t dfull_off[MD2_MAX_SCALES], stats_off, total;
     size_t sel_off[MD2_MAX_SCALES], sel_total;
     size_t noise_off[MD2_MAX_SCALES];
+    size_t mask_off[MD2_MAX_SCALES];
 };
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -1138,7 +1162,7 @@ int make_layout(const md2_desc* d, Layout& L) {
     L.S = d->num_src;
     L.B = d->batch;
     L.v1 = (d->flags & MD2_V1_MULTISCALE) != 0;
-    size_t off = 0, soff = 0, noff = 0;
+    size_t off = 0, soff = 0, noff = 0, moff = 0;
     const int C = (d->flags & MD2_AVG_REPROJECTION) ? 1 : d->num_src;
     for (int s = 0; s < L.nscales; ++s) {
         L.hs[s] = d->height >> s;
@@ -1164,6 +1188,8 @@ int make_layout(const md2_desc* d, Layout& L) {
         soff += (size_t)L.B * L.lh[s] * L.lw[s];
         L.noise_off[s] = noff;
         noff += (size_t)L.B * C * L.lh[s] * L.lw[s];
+        L.mask_off[s] = moff;
+        moff += (size_t)L.B * L.S * L.lh[s] * L.lw[s];
     }
     L.stats_off = off;
     off = align256(off + sizeof(float) * (size_t)L.nscales * L.B * 4);
@@ -1174,6 +1200,11 @@ int make_layout(const md2_desc* d, Layout& L) {
 
 int check_tensors(const md2_desc* d, const md2_tensors* t, const Layout& L) {
     if (!t) return fail(MD2_ERR_ARG, "tensors is NULL");
+    if (d->flags & MD2_PREDICTIVE_MASK) {
+        if (!(d->flags & MD2_NO_AUTOMASK))
+            return fail(MD2_ERR_ARG, "MD2_PREDICTIVE_MASK requires MD2_NO_AUTOMASK (trainer.py:91-92)");
+        if (!t->mask) return fail(MD2_ERR_ARG, "MD2_PREDICTIVE_MASK set but mask is NULL");
+    }
     if (!t->T) return fail(MD2_ERR_ARG, "T is NULL");
     for (int s = 0; s < L.nscales; ++s) {
         if (!t->disp[s]) return fail(MD2_ERR_ARG, "disp[%d] is NULL", s);
@@ -1195,7 +1226,7 @@ int hip_check(const char* what) {
 
 // fill the PhotoArgs for the scale set [s_begin, s_end)
 void photo_args(const md2_desc* d, const md2_tensors* t, const Layout& L, int s_begin, int s_end, bool bwd,
-                uint8_t* ws, uint8_t* sel, PhotoArgs& a) {
+                uint8_t* ws, uint8_t* sel, PhotoArgs& a, float* grad_mask = nullptr) {
     memset(&a, 0, sizeof(a));
     const int cs = L.v1 ? s_begin : 0;
     a.B = L.B;
@@ -1230,6 +1261,8 @@ void photo_args(const md2_desc* d, const md2_tensors* t, const Layout& L, int s_
         a.sel[ls] = sel ? sel + L.sel_off[s] : nullptr;
         a.dfull[ls] = (float*)(ws + L.dfull_off[s]);
         a.dP_part[ls] = (float*)(ws + L.dP_off[s]);
+        a.mask[ls] = t->mask ? t->mask + L.mask_off[s] : nullptr;
+        a.gmask[ls] = grad_mask ? grad_mask + L.mask_off[s] : nullptr;
     }
 }
 
@@ -1380,13 +1413,15 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
 }
 
 int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* grad_loss, const uint8_t* select,
-                        float* const* grad_disp, float* grad_T, void* workspace, void* stream) {
+                        float* const* grad_disp, float* grad_T, float* grad_mask, void* workspace, void* stream) {
     Layout L;
     int rc = make_layout(d, L);
     if (rc) return rc;
     if ((rc = check_tensors(d, t, L))) return rc;
     if (!grad_loss || !select || !grad_disp || !grad_T || !workspace)
         return fail(MD2_ERR_ARG, "grad_loss/select/grad_disp/grad_T/workspace is NULL");
+    if ((d->flags & MD2_PREDICTIVE_MASK) && !grad_mask)
+        return fail(MD2_ERR_ARG, "MD2_PREDICTIVE_MASK needs grad_mask");
     for (int s = 0; s < L.nscales; ++s)
         if (!grad_disp[s]) return fail(MD2_ERR_ARG, "grad_disp[%d] is NULL", s);
     hipStream_t st = (hipStream_t)stream;
@@ -1394,14 +1429,14 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
     PhotoArgs a;
     if (L.v1) {
         for (int s = 0; s < L.nscales; ++s) {
-            photo_args(d, t, L, s, s + 1, true, ws, (uint8_t*)select, a);
+            photo_args(d, t, L, s, s + 1, true, ws, (uint8_t*)select, a, grad_mask);
             a.grad_loss = grad_loss;
             launch_photo(a, true, st);
         }
     } else {
         hipEvent_t e0, e1;
         timing_slot(1, &e0, &e1);
-        photo_args(d, t, L, 0, L.nscales, true, ws, (uint8_t*)select, a);
+        photo_args(d, t, L, 0, L.nscales, true, ws, (uint8_t*)select, a, grad_mask);
         a.grad_loss = grad_loss;
         launch_photo(a, true, st, e0, e1);
     }

@@ -41,6 +41,7 @@ class HotPathConfig:
     disable_automasking: bool = False
     v1_multiscale: bool = False
     t_per_scale: bool = False
+    predictive_mask: bool = False
 
     @property
     def flags(self) -> int:
@@ -50,6 +51,7 @@ class HotPathConfig:
         f |= _lib.NO_AUTOMASK if self.disable_automasking else 0
         f |= _lib.V1_MULTISCALE if self.v1_multiscale else 0
         f |= _lib.T_PER_SCALE if self.t_per_scale else 0
+        f |= _lib.PREDICTIVE_MASK if self.predictive_mask else 0
         return f
 
     def desc(self, seed: int = 0) -> _lib.Desc:
@@ -127,7 +129,8 @@ class Operands:
                 parts.append(noise[s].reshape(-1))
             self.noise = torch.cat(parts).contiguous()
 
-    def struct(self, disps: Sequence[torch.Tensor], T: torch.Tensor) -> _lib.Tensors:
+    def struct(self, disps: Sequence[torch.Tensor], T: torch.Tensor,
+               mask: Optional[torch.Tensor] = None) -> _lib.Tensors:
         st = _lib.Tensors()
         for s, d in enumerate(disps):
             st.disp[s] = d.data_ptr()
@@ -141,23 +144,25 @@ class Operands:
         st.T = T.data_ptr()
         st.noise = self.noise.data_ptr() if self.noise is not None else None
         st.seed_ptr = self.seed_tensor.data_ptr() if self.seed_tensor is not None else None
+        st.mask = mask.data_ptr() if mask is not None else None
         return st
 
 
 class _PhotometricLoss(torch.autograd.Function):
 
     @staticmethod
-    def forward(ctx, cfg: HotPathConfig, ops: Operands, seed: int, T: torch.Tensor, *disps: torch.Tensor):
+    def forward(ctx, cfg: HotPathConfig, ops: Operands, seed: int, T: torch.Tensor, mask, *disps: torch.Tensor):
         L = _lib.lib()
         dev = T.device
         desc = cfg.desc(seed)
-        st = ops.struct(disps, T)
+        st = ops.struct(disps, T, mask)
         ws = torch.empty(L.md2_workspace_bytes(ctypes.byref(desc)), dtype=torch.uint8, device=dev)
         sel = torch.empty(L.md2_select_bytes(ctypes.byref(desc)), dtype=torch.uint8, device=dev)
         loss = torch.empty(cfg.num_scales + 1, dtype=torch.float32, device=dev)
         _lib.check(L.md2_photometric_fwd(ctypes.byref(desc), ctypes.byref(st), loss.data_ptr(), sel.data_ptr(),
                                          ws.data_ptr(), _stream_ptr(dev)), "md2_photometric_fwd")
-        ctx.save_for_backward(T, *disps)
+        ctx.has_mask = mask is not None
+        ctx.save_for_backward(T, *(([mask] if mask is not None else []) + list(disps)))
         ctx.cfg, ctx.ops, ctx.seed, ctx.ws, ctx.sel = cfg, ops, seed, ws, sel
         ctx.mark_non_differentiable(sel)
         return loss, sel
@@ -165,27 +170,32 @@ class _PhotometricLoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_loss, _grad_sel):
         L = _lib.lib()
-        T, *disps = ctx.saved_tensors
+        T, *rest = ctx.saved_tensors
+        mask = rest[0] if ctx.has_mask else None
+        disps = rest[1:] if ctx.has_mask else rest
         cfg = ctx.cfg
         dev = T.device
         if grad_loss is None:
             grad_loss = torch.zeros(cfg.num_scales + 1, dtype=torch.float32, device=dev)
         grad_loss = grad_loss.contiguous().float()
         desc = cfg.desc(ctx.seed)
-        st = ctx.ops.struct(disps, T)
+        st = ctx.ops.struct(disps, T, mask)
         gdisp = [torch.empty_like(d) for d in disps]
         gT = torch.empty_like(T)
+        gmask = torch.empty_like(mask) if mask is not None else None
         arr = (ctypes.c_void_p * _lib.MAX_SCALES)(*([g.data_ptr() for g in gdisp]
                                                     + [None] * (_lib.MAX_SCALES - len(gdisp))))
         _lib.check(L.md2_photometric_bwd(ctypes.byref(desc), ctypes.byref(st), grad_loss.data_ptr(),
-                                         ctx.sel.data_ptr(), arr, gT.data_ptr(), ctx.ws.data_ptr(),
+                                         ctx.sel.data_ptr(), arr, gT.data_ptr(),
+                                         gmask.data_ptr() if gmask is not None else None, ctx.ws.data_ptr(),
                                          _stream_ptr(dev)), "md2_photometric_bwd")
-        return (None, None, None, gT, *gdisp)
+        return (None, None, None, gT, gmask, *gdisp)
 
 
 def photometric_loss(cfg: HotPathConfig, disps: Sequence[torch.Tensor], colors, K, inv_K, T: torch.Tensor,
                      noise: Optional[Dict[int, torch.Tensor]] = None, seed: int = 0,
-                     seed_tensor: Optional[torch.Tensor] = None):
+                     seed_tensor: Optional[torch.Tensor] = None,
+                     mask: Optional[Dict[int, torch.Tensor]] = None):
     """Fused hot path.  Returns (loss_vec, select).
 
     loss_vec[s] = losses["loss/s"], loss_vec[num_scales] = losses["loss"];
@@ -194,6 +204,9 @@ def photometric_loss(cfg: HotPathConfig, disps: Sequence[torch.Tensor], colors, 
     noise: optional {scale: unit-normal (B,C,h,w)}; None draws it in-kernel from seed.
     seed_tensor: optional 1-element int64 device tensor mixed into the seed at run
     time (lets a captured hipGraph draw fresh noise per replay).
+    mask: with cfg.predictive_mask, {scale: (B,S,h,w)} predictive masks already
+    upsampled to the loss resolution (trainer.py:449-455); differentiable.  The
+    BCE weighting term (trainer.py:457-459) is the caller's.
     """
     dev = T.device
     if dev.type != "cuda":
@@ -207,7 +220,34 @@ def photometric_loss(cfg: HotPathConfig, disps: Sequence[torch.Tensor], colors, 
     tshape = (cfg.num_scales, S, B, 4, 4) if cfg.t_per_scale else (S, B, 4, 4)
     _require(T, "T", tshape, dev)
     ops = Operands(cfg, colors, K, inv_K, noise, dev, seed_tensor)
-    return _PhotometricLoss.apply(cfg, ops, int(seed), T.contiguous(), *disps)
+    packed = None
+    if cfg.predictive_mask:
+        if mask is None:
+            raise ValueError("cfg.predictive_mask needs mask={scale: (B,S,h,w)}")
+        if not cfg.disable_automasking:
+            raise ValueError("predictive_mask requires disable_automasking (trainer.py:91-92)")
+        for s in range(cfg.num_scales):
+            h, w = cfg.loss_res(s)
+            _require(mask[s], f"mask[{s}]", (B, S, h, w), dev)
+        packed = torch.cat([mask[s].reshape(-1) for s in range(cfg.num_scales)]).contiguous()
+    elif mask is not None:
+        raise ValueError("mask given but cfg.predictive_mask is False")
+    return _PhotometricLoss.apply(cfg, ops, int(seed), T.contiguous(), packed, *disps)
+
+
+def predictive_mask_inputs(cfg: HotPathConfig, masks: Dict[int, torch.Tensor]):
+    """trainer.py:449-459: upsample the mask decoder's outputs to the loss
+    resolution (bilinear, align_corners=False) and form the BCE weighting terms
+    0.2 * BCE(mask, 1).  Returns ({scale: upsampled mask}, (num_scales,) BCE)."""
+    import torch.nn.functional as F
+    up, bce = {}, []
+    for s in range(cfg.num_scales):
+        m = masks[s]
+        if not cfg.v1_multiscale:
+            m = F.interpolate(m, [cfg.height, cfg.width], mode="bilinear", align_corners=False)
+        up[s] = m
+        bce.append(0.2 * F.binary_cross_entropy(m, torch.ones_like(m)))
+    return up, torch.stack(bce)
 
 
 def selection_maps(cfg: HotPathConfig, select: torch.Tensor) -> Dict[int, torch.Tensor]:

@@ -33,7 +33,7 @@ import torch.optim as optim
 
 from . import networks
 from .distributed import FlatGradSync, wrap_ddp
-from .hotpath import HotPathConfig, generate_images, photometric_loss, selection_maps
+from .hotpath import HotPathConfig, generate_images, photometric_loss, predictive_mask_inputs, selection_maps
 from .layers import compute_depth_errors, disp_to_depth, transformation_from_parameters
 
 
@@ -80,7 +80,6 @@ class Trainer:
         if self.opt.predictive_mask:
             assert self.opt.disable_automasking, \
                 "When using predictive_mask, please disable automasking with --disable_automasking"
-            raise NotImplementedError("--predictive_mask is not supported by the fused hot path yet")
 
         pretrained = self.opt.weights_init == "pretrained"
         self.models: Dict[str, nn.Module] = {}
@@ -97,6 +96,11 @@ class Trainer:
             elif self.opt.pose_model_type == "posecnn":
                 self.models["pose"] = networks.PoseCNN(
                     self.num_input_frames if self.opt.pose_model_input == "all" else 2)
+        if self.opt.predictive_mask:
+            # same architecture as the depth decoder, one mask per source frame (trainer.py:94-100)
+            self.models["predictive_mask"] = networks.DepthDecoder(
+                self.models["encoder"].num_ch_enc, self.opt.scales,
+                num_output_channels=(len(self.opt.frame_ids) - 1))
         for m in self.models.values():
             m.to(self.device)
             if getattr(self.opt, "channels_last", False):
@@ -131,7 +135,7 @@ class Trainer:
             max_depth=self.opt.max_depth, disparity_smoothness=self.opt.disparity_smoothness,
             no_ssim=self.opt.no_ssim, avg_reprojection=self.opt.avg_reprojection,
             disable_automasking=self.opt.disable_automasking, v1_multiscale=self.opt.v1_multiscale,
-            t_per_scale=self.opt.pose_model_type == "posecnn")
+            t_per_scale=self.opt.pose_model_type == "posecnn", predictive_mask=bool(self.opt.predictive_mask))
         self.noise_override = None   # {scale: unit-normal noise}; tests pin the tie-break noise with it
         self.depth_metric_names = ["de/abs_rel", "de/sq_rel", "de/rms", "de/log_rms", "da/a1", "da/a2", "da/a3"]
         self.epoch = 0
@@ -158,6 +162,9 @@ class Trainer:
         else:
             features = models["encoder"](inputs["color_aug", 0, 0])
             outputs = models["depth"](features)
+        if self.opt.predictive_mask:
+            outputs["predictive_mask"] = models["predictive_mask"](
+                features[0] if isinstance(features, dict) else features)
         if self.use_pose_net:
             outputs.update(self.predict_poses(inputs, features, models))
         return outputs
@@ -269,9 +276,15 @@ class Trainer:
             seed = int(self.opt.noise_seed) * 1000003 * 131 + self.rank
         else:
             seed = (int(self.opt.noise_seed) * 1000003 + self.step) * 131 + self.rank
+        mask, bce = None, None
+        if self.hot.predictive_mask:
+            mask, bce = predictive_mask_inputs(self.hot, {s: outputs["predictive_mask"][("disp", s)]
+                                                          for s in range(self.num_scales)})
         loss_vec, sel = photometric_loss(self.hot, [outputs[("disp", s)] for s in range(self.num_scales)],
                                          self._colors(inputs), K, inv_K, T, noise=self.noise_override,
-                                         seed=seed, seed_tensor=self.seed_tensor)
+                                         seed=seed, seed_tensor=self.seed_tensor, mask=mask)
+        if bce is not None:   # trainer.py:457-459: loss/s += 0.2 * BCE(mask, 1)
+            loss_vec = loss_vec + torch.cat([bce, bce.mean().view(1)])
         losses = {"loss/{}".format(s): loss_vec[s] for s in range(self.num_scales)}
         losses["loss"] = loss_vec[self.num_scales]
         if not self.opt.disable_automasking:

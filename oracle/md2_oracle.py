@@ -50,6 +50,7 @@ class HotPathOptions:
     no_ssim: bool = False
     avg_reprojection: bool = False
     disable_automasking: bool = False
+    predictive_mask: bool = False
     align_corners: Optional[bool] = None     # None = torch default (False)
 
 
@@ -119,7 +120,8 @@ def smooth_loss(disp, img):
 
 def hot_path(opt: HotPathOptions, disps: Dict[int, torch.Tensor], inputs: Dict,
              cam_T: Dict, noise: Optional[Dict[int, torch.Tensor]] = None,
-             keep_images: bool = True, selection: Optional[Dict[int, torch.Tensor]] = None):
+             keep_images: bool = True, selection: Optional[Dict[int, torch.Tensor]] = None,
+             masks: Optional[Dict[int, torch.Tensor]] = None):
     """One forward of generate_images_pred + compute_losses.
 
     disps: {scale: (B,1,H/2^s,W/2^s)}; inputs: reference-keyed dict with
@@ -129,6 +131,8 @@ def hot_path(opt: HotPathOptions, disps: Dict[int, torch.Tensor], inputs: Dict,
     selection: test-only {scale: (B,h,w) int64} pinning the per-pixel argmin of
     trainer.py:478 to given indices, so that gradients of two fp32
     implementations can be compared where rounding flips near-tied candidates.
+    masks: with opt.predictive_mask, outputs["predictive_mask"][("disp", s)] at
+    the native scale (trainer.py:449).
 
     Returns (losses, outputs) with the reference's keys.
     """
@@ -160,6 +164,7 @@ def hot_path(opt: HotPathOptions, disps: Dict[int, torch.Tensor], inputs: Dict,
     losses: Dict = {}
     total = 0
     for s in opt.scales:
+        loss = 0
         src_s = s if opt.v1_multiscale else 0
         target = inputs[("color", 0, src_s)]
         reproj = torch.cat([reprojection_loss(outputs[("color", f, s)], target, opt.no_ssim)
@@ -169,6 +174,13 @@ def hot_path(opt: HotPathOptions, disps: Dict[int, torch.Tensor], inputs: Dict,
                                for f in frames], 1)
             if opt.avg_reprojection:
                 ident = ident.mean(1, keepdim=True)
+        elif opt.predictive_mask:
+            # trainer.py:447-459
+            mask = masks[s]
+            if not opt.v1_multiscale:
+                mask = F.interpolate(mask, [H, W], mode="bilinear", align_corners=False)
+            reproj = reproj * mask
+            loss = loss + (0.2 * F.binary_cross_entropy(mask, torch.ones(mask.shape))).mean()
         if opt.avg_reprojection:
             reproj = reproj.mean(1, keepdim=True)
         if not opt.disable_automasking:
@@ -187,7 +199,7 @@ def hot_path(opt: HotPathOptions, disps: Dict[int, torch.Tensor], inputs: Dict,
         if not opt.disable_automasking:
             outputs["identity_selection/{}".format(s)] = (idxs > ident.shape[1] - 1).float()
             outputs["argmin/{}".format(s)] = idxs
-        loss = to_opt.mean()
+        loss = loss + to_opt.mean()
         loss = loss + opt.disparity_smoothness * smooth_loss(disps[s], inputs[("color", 0, s)]) / (2 ** s)
         total = total + loss
         losses["loss/{}".format(s)] = loss

@@ -52,6 +52,8 @@ CASES = {
                                  {"disable_automasking": True, "avg_reprojection": True}, 0.05, True),
     "v1_multiscale_b2_64x128": (2, 64, 128, [0, -1, 1], {"v1_multiscale": True}, 0.05, True),
     "full_mono_b2_192x640": (2, 192, 640, [0, -1, 1], {}, 0.01, False),
+    "predictive_mask_b2_32x64": (2, 32, 64, [0, -1, 1],
+                                 {"disable_automasking": True, "predictive_mask": True}, 0.05, True),
 }
 
 
@@ -100,7 +102,7 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
         v1_multiscale=flags.get("v1_multiscale", False), min_depth=0.1, max_depth=100.0,
         pose_model_type="separate_resnet", disable_automasking=flags.get("disable_automasking", False),
         no_ssim=flags.get("no_ssim", False), avg_reprojection=flags.get("avg_reprojection", False),
-        predictive_mask=False, disparity_smoothness=1e-3, batch_size=B)
+        predictive_mask=flags.get("predictive_mask", False), disparity_smoothness=1e-3, batch_size=B)
     self = types.SimpleNamespace(opt=opt, device=torch.device("cpu"), num_scales=len(scales))
     self.ssim = ref_layers.SSIM()
     self.backproject_depth, self.project_3d = {}, {}
@@ -112,6 +114,14 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
         ref_trainer.Trainer.compute_reprojection_loss, self)
 
     outputs = {("disp", s): disps[s] for s in scales}
+    masks = {}
+    if flags.get("predictive_mask"):
+        # the mask decoder's sigmoid outputs (B, S, h_s, w_s) (trainer.py:96-98, 252)
+        mgen = torch.Generator().manual_seed(seed + 777)
+        for s in scales:
+            h, w = H // 2 ** s, W // 2 ** s
+            masks[s] = torch.sigmoid(torch.randn(B, S, h, w, generator=mgen)).requires_grad_(True)
+        outputs["predictive_mask"] = {("disp", s): masks[s] for s in scales}
     camT = {}
     for i, f in enumerate(temporal):
         T = ref_layers.transformation_from_parameters(axis[i], trans[i], invert=(f < 0))
@@ -130,11 +140,14 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
         return n
 
     ref_trainer.torch.randn = fake_randn
+    real_cuda = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda t, *a, **k: t     # trainer.py:458 calls .cuda(); CPU-only here
     try:
         ref_trainer.Trainer.generate_images_pred(self, inputs, outputs)
         losses = ref_trainer.Trainer.compute_losses(self, inputs, outputs)
     finally:
         ref_trainer.torch.randn = real_randn
+        torch.Tensor.cuda = real_cuda
     losses["loss"].backward()
 
     rec = {"B": B, "H": H, "W": W, "S": S, "seed": seed, "pose_scale": pose_scale,
@@ -146,6 +159,9 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
     rec["loss"] = losses["loss"].detach().numpy()
     rec["grad_axisangle"] = axis.grad.numpy()
     rec["grad_translation"] = trans.grad.numpy()
+    for s, m in masks.items():
+        rec[f"mask_{s}"] = m.detach().numpy()
+        rec[f"grad_mask_{s}"] = m.grad.numpy()
     for f in temporal:
         rec[f"grad_T_{f}"] = camT[f].grad.numpy()
         rec[f"T_{f}"] = camT[f].detach().numpy()

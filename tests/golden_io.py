@@ -55,6 +55,7 @@ class Case:
         self.translation = torch.from_numpy(z["translation"])
         self.noise = {s: torch.from_numpy(z[f"noise_{i}"]) for i, s in enumerate(self.scales)
                       if f"noise_{i}" in z.files}
+        self.masks = {s: torch.from_numpy(z[f"mask_{s}"]) for s in self.scales if f"mask_{s}" in z.files}
 
     def _regenerate(self):
         z = self.z
@@ -64,6 +65,7 @@ class Case:
                                pose_scale=float(z["pose_scale"]))
         self.disps = {s: hp["disps"][s] for s in self.scales}
         nt = len(self.temporal)
+        self.masks = {}
         self.axisangle = hp["axisangle"][:nt].clone()
         self.translation = hp["translation"][:nt].clone()
         gen = torch.Generator().manual_seed(int(z["noise_seed"]))

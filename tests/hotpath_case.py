@@ -4,7 +4,8 @@ from __future__ import annotations
 import torch
 
 from golden_io import Case
-from monodepth2_amd.hotpath import HotPathConfig, photometric_loss, selection_maps, generate_images
+from monodepth2_amd.hotpath import (HotPathConfig, generate_images, photometric_loss, predictive_mask_inputs,
+                                    selection_maps)
 from monodepth2_amd.layers import transformation_from_parameters
 
 
@@ -12,7 +13,8 @@ def case_config(case: Case) -> HotPathConfig:
     return HotPathConfig(batch=case.B, height=case.H, width=case.W, num_src=case.S, num_scales=4,
                          no_ssim="no_ssim" in case.flags, avg_reprojection="avg_reprojection" in case.flags,
                          disable_automasking="disable_automasking" in case.flags,
-                         v1_multiscale="v1_multiscale" in case.flags)
+                         v1_multiscale="v1_multiscale" in case.flags,
+                         predictive_mask="predictive_mask" in case.flags)
 
 
 def case_operands(case: Case, device):
@@ -47,12 +49,21 @@ def run_hip(case: Case, device="cuda"):
             ti += 1
     T = torch.stack(Ts, 0)
     T.retain_grad()
-    loss, sel = photometric_loss(cfg, disps, colors, K, inv_K, T, noise=noise)
+    masks, bce = None, None
+    if cfg.predictive_mask:
+        masks = {s: m.to(device).clone().requires_grad_(True) for s, m in case.masks.items()}
+        up, bce = predictive_mask_inputs(cfg, masks)
+        loss, sel = photometric_loss(cfg, disps, colors, K, inv_K, T, noise=noise, mask=up)
+        loss = loss + torch.cat([bce, bce.mean().view(1)])   # losses["loss/s"] += BCE_s; total += mean
+    else:
+        loss, sel = photometric_loss(cfg, disps, colors, K, inv_K, T, noise=noise)
     loss[cfg.num_scales].backward()
     torch.cuda.synchronize()
     out = {"loss": loss.detach().cpu().numpy(), "grad_disp": [d.grad.cpu().numpy() for d in disps],
            "grad_axis": axis.grad.cpu().numpy(), "grad_trans": trans.grad.cpu().numpy(),
            "grad_T": T.grad.cpu().numpy(), "select": {s: v.cpu().numpy() for s, v in selection_maps(cfg, sel).items()}}
+    if masks is not None:
+        out["grad_mask"] = {s: m.grad.cpu().numpy() for s, m in masks.items()}
     with torch.no_grad():
         T2 = T.detach()
         out["gen"] = generate_images(cfg, [d.detach() for d in disps], colors, K, inv_K, T2)
@@ -65,7 +76,9 @@ def run_oracle(case: Case, selection=None):
     opt = HotPathOptions(height=case.H, width=case.W, frame_ids=case.frame_ids,
                          v1_multiscale="v1_multiscale" in case.flags, no_ssim="no_ssim" in case.flags,
                          avg_reprojection="avg_reprojection" in case.flags,
-                         disable_automasking="disable_automasking" in case.flags)
+                         disable_automasking="disable_automasking" in case.flags,
+                         predictive_mask="predictive_mask" in case.flags)
+    masks = {s: m.clone().requires_grad_(True) for s, m in case.masks.items()} if case.masks else None
     disps = {s: d.clone().requires_grad_(True) for s, d in case.disps.items()}
     axis = case.axisangle.clone().requires_grad_(True)
     trans = case.translation.clone().requires_grad_(True)
@@ -78,8 +91,11 @@ def run_oracle(case: Case, selection=None):
     if selection is not None:
         sel = {s: torch.from_numpy(v).long() for s, v in selection.items()}
     losses, outputs = hot_path(opt, disps, case.inputs, camT, noise=case.noise if case.noise else None,
-                               selection=sel)
+                               selection=sel, masks=masks)
     losses["loss"].backward()
-    return {"loss": [float(losses[f"loss/{s}"]) for s in range(4)] + [float(losses["loss"])],
-            "grad_disp": [disps[s].grad.numpy() for s in range(4)],
-            "grad_axis": axis.grad.numpy(), "grad_trans": trans.grad.numpy(), "outputs": outputs}
+    res = {"loss": [float(losses[f"loss/{s}"]) for s in range(4)] + [float(losses["loss"])],
+           "grad_disp": [disps[s].grad.numpy() for s in range(4)],
+           "grad_axis": axis.grad.numpy(), "grad_trans": trans.grad.numpy(), "outputs": outputs}
+    if masks:
+        res["grad_mask"] = {s: m.grad.numpy() for s, m in masks.items()}
+    return res

@@ -37,7 +37,7 @@ def test_abi_version(L):
 
 def test_struct_sizes():
     assert ctypes.sizeof(_lib.Desc) == 48
-    assert ctypes.sizeof(_lib.Tensors) == 8 * (4 + 16 + 4 + 4 + 3)
+    assert ctypes.sizeof(_lib.Tensors) == 8 * (4 + 16 + 4 + 4 + 4)
 
 
 @pytest.mark.parametrize("B,H,W,S", [(12, 192, 640, 2), (8, 320, 1024, 2), (12, 192, 640, 3), (1, 32, 32, 1)])

@@ -76,6 +76,8 @@ def test_hip_matches_reference(name):
     assert rel_l2(out["grad_trans"], case.expected("grad_translation")) <= 2e-2
     for i, f in enumerate(case.temporal):
         assert rel_l2(out["grad_T"][case.frame_ids[1:].index(f)], case.expected(f"grad_T_{f}")) <= 2e-2
+    for s, g in out.get("grad_mask", {}).items():
+        assert rel_l2(g, case.expected(f"grad_mask_{s}")) <= 2e-2, (s, rel_l2(g, case.expected(f"grad_mask_{s}")))
 
 
 @pytest.mark.parametrize("name", case_names())
@@ -92,6 +94,8 @@ def test_hip_gradients_match_oracle_pinned_selection(name):
         assert rel_l2(g, r) <= 1e-2, (s, rel_l2(g, r))
     assert rel_l2(out["grad_axis"], ref["grad_axis"]) <= 1e-2
     assert rel_l2(out["grad_trans"], ref["grad_trans"]) <= 1e-2
+    for s, g in out.get("grad_mask", {}).items():
+        assert rel_l2(g, ref["grad_mask"][s]) <= 1e-2, s
 
 
 def test_hip_deterministic():

@@ -20,7 +20,9 @@ def run_oracle(case: Case, keep_images=True):
                          v1_multiscale="v1_multiscale" in case.flags,
                          no_ssim="no_ssim" in case.flags,
                          avg_reprojection="avg_reprojection" in case.flags,
-                         disable_automasking="disable_automasking" in case.flags)
+                         disable_automasking="disable_automasking" in case.flags,
+                         predictive_mask="predictive_mask" in case.flags)
+    masks = {s: m.clone().requires_grad_(True) for s, m in case.masks.items()} if case.masks else None
     disps = {s: d.clone().requires_grad_(True) for s, d in case.disps.items()}
     axis = case.axisangle.clone().requires_grad_(True)
     trans = case.translation.clone().requires_grad_(True)
@@ -32,8 +34,9 @@ def run_oracle(case: Case, keep_images=True):
     if "s" in case.frame_ids:
         camT["s"] = case.inputs["stereo_T"]
     losses, outputs = hot_path(opt, disps, case.inputs, camT,
-                               noise=case.noise if case.noise else None, keep_images=keep_images)
+                               noise=case.noise if case.noise else None, keep_images=keep_images, masks=masks)
     losses["loss"].backward()
+    outputs["_masks"] = masks
     return losses, outputs, disps, axis, trans, camT
 
 
@@ -54,6 +57,9 @@ def test_oracle_matches_reference(name):
     for f in case.temporal:
         np.testing.assert_allclose(camT[f].detach().numpy(), case.expected(f"T_{f}"), atol=1e-7)
         np.testing.assert_allclose(camT[f].grad.numpy(), case.expected(f"grad_T_{f}"), rtol=1e-4, atol=1e-8)
+    if outputs["_masks"]:
+        for s, m in outputs["_masks"].items():
+            np.testing.assert_allclose(m.grad.numpy(), case.expected(f"grad_mask_{s}"), rtol=1e-4, atol=1e-9)
     if case.full:
         for s in case.scales:
             np.testing.assert_allclose(outputs[("depth", 0, s)].detach().numpy(),
