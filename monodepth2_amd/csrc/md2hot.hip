@@ -1198,9 +1198,9 @@ int make_layout(const md2_desc* d, Layout& L) {
     return MD2_OK;
 }
 
-int check_tensors(const md2_desc* d, const md2_tensors* t, const Layout& L) {
+int check_tensors(const md2_desc* d, const md2_tensors* t, const Layout& L, bool need_mask = true) {
     if (!t) return fail(MD2_ERR_ARG, "tensors is NULL");
-    if (d->flags & MD2_PREDICTIVE_MASK) {
+    if (need_mask && (d->flags & MD2_PREDICTIVE_MASK)) {
         if (!(d->flags & MD2_NO_AUTOMASK))
             return fail(MD2_ERR_ARG, "MD2_PREDICTIVE_MASK requires MD2_NO_AUTOMASK (trainer.py:91-92)");
         if (!t->mask) return fail(MD2_ERR_ARG, "MD2_PREDICTIVE_MASK set but mask is NULL");
@@ -1487,7 +1487,7 @@ int md2_generate_images(const md2_desc* d, const md2_tensors* t, float* const* d
     Layout L;
     int rc = make_layout(d, L);
     if (rc) return rc;
-    if ((rc = check_tensors(d, t, L))) return rc;
+    if ((rc = check_tensors(d, t, L, false))) return rc;
     hipStream_t st = (hipStream_t)stream;
     for (int s = 0; s < L.nscales; ++s) {
         GenArgs g;
