@@ -149,6 +149,29 @@ int md2_generate_images(const md2_desc* desc, const md2_tensors* t,
 int md2_timing_begin(int max_launches);
 int md2_timing_end(double* fwd_ms, int* n_fwd, double* bwd_ms, int* n_bwd);
 
+/*
+ * DepthDecoder block fusion: the input of every decoder
+ * conv — ReflectionPad2d(1) (layers.py:127-135) of [ELU(previous conv output)
+ * (layers.py:113-118), nearest x2 upsampled (layers.py:196-199), concatenated with
+ * the encoder skip feature (networks/depth_decoder.py:55-58)] — in one pass, and its
+ * adjoint in one pass.  x: (B,C,h,w); skip: (B,Cs,H,W) with (H,W) = (2h,2w) if
+ * MD2_PAD_UPSAMPLE else (h,w); out: (B,C+Cs,H+2,W+2).  With MD2_PAD_ELU x is the
+ * pre-activation and the backward needs it again.  Returns MD2_OK / MD2_ERR_*.
+ */
+#define MD2_PAD_ELU      (1u << 0)
+#define MD2_PAD_UPSAMPLE (1u << 1)
+
+typedef struct md2_pad_desc {
+    int32_t batch, channels, height, width; /* of x */
+    int32_t skip_channels;                  /* 0: no skip tensor */
+    uint32_t flags;                         /* MD2_PAD_* */
+} md2_pad_desc;
+
+int md2_decoder_pad_fwd(const md2_pad_desc* desc, const float* x, const float* skip, float* out,
+                        void* stream);
+int md2_decoder_pad_bwd(const md2_pad_desc* desc, const float* x, const float* grad_out, float* grad_x,
+                        float* grad_skip, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -55,7 +55,15 @@ _lib = None
 
 EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_select_bytes",
            "md2_photometric_fwd", "md2_photometric_bwd", "md2_generate_images",
-           "md2_timing_begin", "md2_timing_end"]
+           "md2_timing_begin", "md2_timing_end", "md2_decoder_pad_fwd", "md2_decoder_pad_bwd"]
+
+PAD_ELU = 1 << 0
+PAD_UPSAMPLE = 1 << 1
+
+
+class PadDesc(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("channels", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("width", ctypes.c_int32), ("skip_channels", ctypes.c_int32), ("flags", ctypes.c_uint32)]
 
 
 def _declare(L):
@@ -75,6 +83,10 @@ def _declare(L):
     L.md2_generate_images.restype = ctypes.c_int
     L.md2_generate_images.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(Tensors),
                                       ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp]
+    L.md2_decoder_pad_fwd.restype = ctypes.c_int
+    L.md2_decoder_pad_fwd.argtypes = [ctypes.POINTER(PadDesc), _vp, _vp, _vp, _vp]
+    L.md2_decoder_pad_bwd.restype = ctypes.c_int
+    L.md2_decoder_pad_bwd.argtypes = [ctypes.POINTER(PadDesc), _vp, _vp, _vp, _vp, _vp]
     L.md2_timing_begin.restype = ctypes.c_int
     L.md2_timing_begin.argtypes = [ctypes.c_int]
     L.md2_timing_end.restype = ctypes.c_int

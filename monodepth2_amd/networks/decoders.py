@@ -43,8 +43,28 @@ class DepthDecoder(nn.Module):
             mods.append(self.convs[("dispconv", s)])
         self.decoder = nn.ModuleList(mods)
         self.sigmoid = nn.Sigmoid()
+        self.fused = True   # GPU: build each conv input with the fused HIP pass
+
+    def _forward_fused(self, input_features):
+        """Same graph with each conv input built by one HIP pass (decoder_ops):
+        pad(x) -> conv -> [ELU -> up x2 -> cat skip -> pad] -> conv -> [ELU -> pad] ->
+        (dispconv -> sigmoid) and the next level's first conv."""
+        from ..decoder_ops import conv_input
+        self.outputs = {}
+        P = conv_input(input_features[-1])                       # ReflectionPad2d only
+        for i in range(4, -1, -1):
+            y0 = self.convs[("upconv", i, 0)].conv.conv(P)
+            skip = input_features[i - 1] if (self.use_skips and i > 0) else None
+            P = conv_input(y0, skip, elu=True, upsample=True)
+            y1 = self.convs[("upconv", i, 1)].conv.conv(P)
+            P = conv_input(y1, None, elu=True, upsample=False)   # shared by dispconv and the next level
+            if i in self.scales:
+                self.outputs[("disp", i)] = self.sigmoid(self.convs[("dispconv", i)].conv(P))
+        return self.outputs
 
     def forward(self, input_features):
+        if input_features[-1].is_cuda and self.fused and self.num_output_channels >= 1:
+            return self._forward_fused(input_features)
         self.outputs = {}
         x = input_features[-1]
         for i in range(4, -1, -1):
