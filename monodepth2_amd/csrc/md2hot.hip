@@ -443,7 +443,7 @@ struct FwdState {
     int code[kRowsF][kWave];
 };
 
-template <int NS, bool SSIM_ON>
+template <int NS, bool SSIM_ON, bool MASK>
 __global__ __launch_bounds__(kBlock, 2) void photo_fwd_kernel(PhotoArgs a) {
     __shared__ FwdState<NS> lds[kWavesPerBlock];
     const int lane = threadIdx.x & (kWave - 1);
@@ -506,13 +506,13 @@ __global__ __launch_bounds__(kBlock, 2) void photo_fwd_kernel(PhotoArgs a) {
             L.code[i][lane] = code;
             L.accum[i][lane] = 0.f;
         }
-        const float* pmask = (a.flags & MD2_PREDICTIVE_MASK) ? a.mask[ls] : nullptr;
+        const float* pmask = MASK ? a.mask[ls] : nullptr;
         for (int f = 0; f < NS; ++f) {
             WarpCtx ctx;
             make_ctx(a, ls, f, b, ctx);
             const int cand = (automask ? NS : 0) + f;
             reproj_rows<SSIM_ON, true>(ctx, tgt, r0, cc, [&](int i, float v) {
-                if (pmask) v *= pmask[(((size_t)b * NS + f) * h + min(r0 + i, h - 1)) * w + cc];  // trainer.py:455
+                if (MASK) v *= pmask[(((size_t)b * NS + f) * h + min(r0 + i, h - 1)) * w + cc];  // trainer.py:455
                 if (avg) {
                     L.accum[i][lane] += v;
                 } else if (v < L.best[i][lane]) {
@@ -604,7 +604,7 @@ __device__ __forceinline__ void make_carry(const WarpCtx& c, const FastSample& s
 // One work item of the backward: (image b, local scale ls, strip st, row block rb),
 // all source frames.  Writes dL/d(upsampled disp) for its 60 x kRowsB pixels and one
 // 12-float dL/dP partial per frame.
-template <int NS, bool SSIM_ON>
+template <int NS, bool SSIM_ON, bool MASK>
 __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int st, int rb, int lane) {
     const int r0 = rb * kRowsB;
     const int h = a.h, w = a.w, HW = h * w;
@@ -623,8 +623,8 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
     const uint8_t* sel = a.sel[ls] + (size_t)b * HW;
     float* dfull = a.dfull[ls] + (size_t)b * HW;
     const int item_in_scale = b * a.wpi + rb * a.strips + st;
-    const float* pmask = (a.flags & MD2_PREDICTIVE_MASK) ? a.mask[ls] : nullptr;
-    float* pgmask = pmask ? a.gmask[ls] : nullptr;
+    const float* pmask = MASK ? a.mask[ls] : nullptr;
+    float* pgmask = MASK ? a.gmask[ls] : nullptr;
 
     for (int f = 0; f < NS; ++f) {
         WarpCtx ctx;
@@ -637,6 +637,7 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
         float x2[3] = {0.f, 0.f, 0.f}, y2[3] = {0.f, 0.f, 0.f};  // row r-2
         Coef cA, cB;
         Carry k1, k2;
+#pragma unroll 2
         for (int k = 0; k < kRowsB + 4; ++k) {
             const int r = r0 - 2 + k;
             const int rr = reflect_clamp(r, h);
@@ -661,7 +662,7 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
                 float gp = 0.f;
                 const bool own = colreal && p >= 0 && p < h;
                 if (own) gp = gscale * frame_weight<NS>(sel[p * w + c], f, automask, avg);
-                if (pmask) {
+                if (MASK) {
                     // masked = reproj * mask (trainer.py:455): d/dreproj = g*mask, d/dmask = g*reproj
                     const size_t mi = (((size_t)b * NS + f) * h + (own ? p : 0)) * w + (own ? c : 0);
                     if (pgmask && colok && p >= r0 && p < r0 + kRowsB && p < h) {
@@ -756,7 +757,7 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
 
 // Resident waves walk the (image, row block, strip, scale) items; each XCD owns a
 // contiguous item range (its L2 streams a contiguous slice of the images).
-template <int NS, bool SSIM_ON>
+template <int NS, bool SSIM_ON, bool MASK>
 __global__ __launch_bounds__(kBlock, 2) void photo_bwd_kernel(PhotoArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
     // G groups of blocks (the 8 XCDs under round-robin dispatch; fewer for tiny grids)
@@ -775,7 +776,7 @@ __global__ __launch_bounds__(kBlock, 2) void photo_bwd_kernel(PhotoArgs a) {
         t /= a.strips;
         const int rb = t % a.rowblocks;
         const int b = t / a.rowblocks;
-        bwd_item<NS, SSIM_ON>(a, b, ls, st, rb, lane);
+        bwd_item<NS, SSIM_ON, MASK>(a, b, ls, st, rb, lane);
     }
 }
 
@@ -1266,14 +1267,14 @@ void photo_args(const md2_desc* d, const md2_tensors* t, const Layout& L, int s_
     }
 }
 
-template <int NS, bool SSIM>
+template <int NS, bool SSIM, bool MASK>
 void launch_fwd_t(const PhotoArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
     const int waves = a.B * a.wpi;
     const int blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (e0)
-        hipExtLaunchKernelGGL((photo_fwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, e0, e1, 0, a);
+        hipExtLaunchKernelGGL((photo_fwd_kernel<NS, SSIM, MASK>), dim3(blocks), dim3(kBlock), 0, st, e0, e1, 0, a);
     else
-        hipLaunchKernelGGL((photo_fwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, a);
+        hipLaunchKernelGGL((photo_fwd_kernel<NS, SSIM, MASK>), dim3(blocks), dim3(kBlock), 0, st, a);
 }
 // number of workgroups that can be resident at once for a kernel (cached per
 // kernel and device); the persistent-loop kernels launch exactly that many
@@ -1294,35 +1295,39 @@ int resident_blocks(K kernel) {
     return cache_val;
 }
 
-template <int NS, bool SSIM>
+template <int NS, bool SSIM, bool MASK>
 void launch_bwd_t(const PhotoArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
     const int items = a.B * a.wpi * a.nsc;
     const int need = (items + kWavesPerBlock - 1) / kWavesPerBlock;
-    const int blocks = min(need, resident_blocks(photo_bwd_kernel<NS, SSIM>));
+    const int blocks = min(need, resident_blocks(photo_bwd_kernel<NS, SSIM, MASK>));
     if (e0)
-        hipExtLaunchKernelGGL((photo_bwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, e0, e1, 0, a);
+        hipExtLaunchKernelGGL((photo_bwd_kernel<NS, SSIM, MASK>), dim3(blocks), dim3(kBlock), 0, st, e0, e1, 0, a);
     else
-        hipLaunchKernelGGL((photo_bwd_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, a);
+        hipLaunchKernelGGL((photo_bwd_kernel<NS, SSIM, MASK>), dim3(blocks), dim3(kBlock), 0, st, a);
 }
 
-void launch_photo(const PhotoArgs& a, bool bwd, hipStream_t st, hipEvent_t e0 = nullptr,
-                  hipEvent_t e1 = nullptr) {
-    const bool ssim = !(a.flags & MD2_NO_SSIM);
-#define MD2_DISPATCH(NS)                                          \
-    if (a.S == NS) {                                              \
-        if (bwd) {                                                \
-            if (ssim) launch_bwd_t<NS, true>(a, st, e0, e1);      \
-            else launch_bwd_t<NS, false>(a, st, e0, e1);          \
-        } else {                                                  \
-            if (ssim) launch_fwd_t<NS, true>(a, st, e0, e1);      \
-            else launch_fwd_t<NS, false>(a, st, e0, e1);          \
-        }                                                         \
-        return;                                                   \
+template <int NS, bool SSIM, bool MASK>
+void launch_one(const PhotoArgs& a, bool bwd, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+    if (bwd) launch_bwd_t<NS, SSIM, MASK>(a, st, e0, e1);
+    else launch_fwd_t<NS, SSIM, MASK>(a, st, e0, e1);
+}
+
+template <int NS>
+void launch_ns(const PhotoArgs& a, bool bwd, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+    const bool ssim = !(a.flags & MD2_NO_SSIM), mask = (a.flags & MD2_PREDICTIVE_MASK) != 0;
+    if (ssim) {
+        if (mask) launch_one<NS, true, true>(a, bwd, st, e0, e1);
+        else launch_one<NS, true, false>(a, bwd, st, e0, e1);
+    } else {
+        if (mask) launch_one<NS, false, true>(a, bwd, st, e0, e1);
+        else launch_one<NS, false, false>(a, bwd, st, e0, e1);
     }
-    MD2_DISPATCH(1)
-    MD2_DISPATCH(2)
-    MD2_DISPATCH(3)
-#undef MD2_DISPATCH
+}
+
+void launch_photo(const PhotoArgs& a, bool bwd, hipStream_t st, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+    if (a.S == 1) launch_ns<1>(a, bwd, st, e0, e1);
+    else if (a.S == 2) launch_ns<2>(a, bwd, st, e0, e1);
+    else launch_ns<3>(a, bwd, st, e0, e1);
 }
 
 }  // namespace
