@@ -66,8 +66,16 @@ __device__ __forceinline__ int reflect_clamp(int i, int n) {
     return min(max(i, 0), n - 1);
 }
 
-__device__ __forceinline__ float shfl_prev(float v) { return __shfl_up(v, 1, kWave); }
-__device__ __forceinline__ float shfl_next(float v) { return __shfl_down(v, 1, kWave); }
+// Neighbour-lane reads as DPP wave shifts (one VALU op, no LDS round trip, unlike the
+// ds_bpermute that __shfl_up/down lower to).  wave_shr:1 gives lane i the value of
+// lane i-1, wave_shl:1 of lane i+1 (checked on MI355X); lanes 0 / 63 receive 0,
+// they are halo lanes whose results are never used.
+__device__ __forceinline__ float shfl_prev(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float shfl_next(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
