@@ -239,6 +239,14 @@ def main():
         log(f"warmup step {i}: {1e3 * (time.perf_counter() - t):.1f} ms")
     stop_hb.set()
     torch.cuda.synchronize()
+    # host enqueue rate: how long the CPU takes to issue 3 steps right after a sync
+    # (<< 3 x ms_per_step means the GPU, not the launch path, bounds the step)
+    t = time.perf_counter()
+    for _ in range(3):
+        trainer.train_step(batch)
+    host_ms = 1e3 * (time.perf_counter() - t) / 3
+    torch.cuda.synchronize()
+    log(f"host enqueue time: {host_ms:.2f} ms/step")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -293,7 +301,8 @@ def main():
                            "global_batch": B * world, "height": H, "width": W, "frame_ids": [str(f) for f in frame_ids],
                            "parallelism": f"dp{world}"},
                 "roofline": roof, "cpu_baseline": cpu,
-                "loss_delta_vs_oracle": delta, "final_loss": round(final_loss, 6)}
+                "loss_delta_vs_oracle": delta, "final_loss": round(final_loss, 6),
+                "host_enqueue_ms_per_step": round(host_ms, 3)}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

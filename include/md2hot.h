@@ -172,6 +172,19 @@ int md2_decoder_pad_fwd(const md2_pad_desc* desc, const float* x, const float* s
 int md2_decoder_pad_bwd(const md2_pad_desc* desc, const float* x, const float* grad_out, float* grad_x,
                         float* grad_skip, void* stream);
 
+/*
+ * Fused pose producer: transformation_from_parameters
+ * (layers.py:28-45, with rot_from_axisangle 64-103 and get_translation_matrix
+ * 48-61) for every (frame, image) of a step in one launch, and its adjoint.
+ * axisangle, translation: (frames, batch, 3); T / grad_T: (frames, batch, 4, 4);
+ * bit f of invert_mask selects invert=True for frame f (trainer.py:294-295).
+ */
+int md2_pose_fwd(int32_t frames, int32_t batch, uint32_t invert_mask, const float* axisangle,
+                 const float* translation, float* T, void* stream);
+int md2_pose_bwd(int32_t frames, int32_t batch, uint32_t invert_mask, const float* axisangle,
+                 const float* translation, const float* grad_T, float* grad_axisangle,
+                 float* grad_translation, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

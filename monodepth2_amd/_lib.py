@@ -55,7 +55,8 @@ _lib = None
 
 EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_select_bytes",
            "md2_photometric_fwd", "md2_photometric_bwd", "md2_generate_images",
-           "md2_timing_begin", "md2_timing_end", "md2_decoder_pad_fwd", "md2_decoder_pad_bwd"]
+           "md2_timing_begin", "md2_timing_end", "md2_decoder_pad_fwd", "md2_decoder_pad_bwd",
+           "md2_pose_fwd", "md2_pose_bwd"]
 
 PAD_ELU = 1 << 0
 PAD_UPSAMPLE = 1 << 1
@@ -87,6 +88,10 @@ def _declare(L):
     L.md2_decoder_pad_fwd.argtypes = [ctypes.POINTER(PadDesc), _vp, _vp, _vp, _vp]
     L.md2_decoder_pad_bwd.restype = ctypes.c_int
     L.md2_decoder_pad_bwd.argtypes = [ctypes.POINTER(PadDesc), _vp, _vp, _vp, _vp, _vp]
+    L.md2_pose_fwd.restype = ctypes.c_int
+    L.md2_pose_fwd.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _vp, _vp, _vp, _vp]
+    L.md2_pose_bwd.restype = ctypes.c_int
+    L.md2_pose_bwd.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp]
     L.md2_timing_begin.restype = ctypes.c_int
     L.md2_timing_begin.argtypes = [ctypes.c_int]
     L.md2_timing_end.restype = ctypes.c_int

@@ -34,7 +34,8 @@ import torch.optim as optim
 from . import networks
 from .distributed import FlatGradSync, wrap_ddp
 from .hotpath import HotPathConfig, generate_images, photometric_loss, predictive_mask_inputs, selection_maps
-from .layers import compute_depth_errors, disp_to_depth, transformation_from_parameters
+from .layers import compute_depth_errors, disp_to_depth
+from .pose_ops import poses_to_transforms
 
 
 def _sec_to_hm_str(t):
@@ -170,9 +171,12 @@ class Trainer:
         return outputs
 
     def predict_poses(self, inputs, features, models=None):
-        """trainer.py:262-318."""
+        """trainer.py:262-318; all cam_T_cam of the step come from one fused launch
+        (pose_ops.poses_to_transforms, the transformation_from_parameters of
+        trainer.py:294-295 / 315-316)."""
         models = models if models is not None else self.models
         outputs = {}
+        aas, trs, invs, fids = [], [], [], []
         if self.num_pose_frames == 2:
             if self.opt.pose_model_type == "shared":
                 pose_feats = {f_i: features[f_i] for f_i in self.opt.frame_ids}
@@ -189,8 +193,10 @@ class Trainer:
                 axisangle, translation = models["pose"](pair)
                 outputs[("axisangle", 0, f_i)] = axisangle
                 outputs[("translation", 0, f_i)] = translation
-                outputs[("cam_T_cam", 0, f_i)] = transformation_from_parameters(
-                    axisangle[:, 0], translation[:, 0], invert=(f_i < 0))
+                aas.append(axisangle[:, 0, 0])
+                trs.append(translation[:, 0, 0])
+                invs.append(f_i < 0)
+                fids.append(f_i)
         else:
             if self.opt.pose_model_type in ["separate_resnet", "posecnn"]:
                 pose_inputs = torch.cat([inputs[("color_aug", i, 0)] for i in self.opt.frame_ids if i != "s"], 1)
@@ -203,8 +209,14 @@ class Trainer:
                 if f_i != "s":
                     outputs[("axisangle", 0, f_i)] = axisangle
                     outputs[("translation", 0, f_i)] = translation
-                    outputs[("cam_T_cam", 0, f_i)] = transformation_from_parameters(
-                        axisangle[:, i], translation[:, i])
+                    aas.append(axisangle[:, i, 0])
+                    trs.append(translation[:, i, 0])
+                    invs.append(False)
+                    fids.append(f_i)
+        if fids:
+            T = poses_to_transforms(torch.stack(aas), torch.stack(trs), invs)
+            for i, f_i in enumerate(fids):
+                outputs[("cam_T_cam", 0, f_i)] = T[i]
         return outputs
 
     # ------------------------------------------------------------- hot path
@@ -235,15 +247,20 @@ class Trainer:
             if not self.opt.v1_multiscale:
                 disp = F.interpolate(disp, [self.opt.height, self.opt.width], mode="bilinear", align_corners=False)
             scaled, _ = disp_to_depth(disp, self.opt.min_depth, self.opt.max_depth)
-            mean_inv_depth = scaled.mean(3, True).mean(2, True)
-            Ts = []
+            mean_inv_depth = scaled.mean(3, True).mean(2, True)          # (B,1,1,1)
+            temporal = [f for f in self.src_frames if f != "s"]
+            Tt = poses_to_transforms(
+                torch.stack([outputs[("axisangle", 0, f)][:, 0, 0] for f in temporal]),
+                torch.stack([outputs[("translation", 0, f)][:, 0, 0] * mean_inv_depth[:, 0, 0]
+                             for f in temporal]),
+                [f < 0 for f in temporal])
+            Ts, ti = [], 0
             for f in self.src_frames:
                 if f == "s":
                     Ts.append(inputs["stereo_T"])
                 else:
-                    Ts.append(transformation_from_parameters(
-                        outputs[("axisangle", 0, f)][:, 0],
-                        outputs[("translation", 0, f)][:, 0] * mean_inv_depth[:, 0], f < 0))
+                    Ts.append(Tt[ti])
+                    ti += 1
             per_scale.append(torch.stack(Ts, 0))
         return torch.stack(per_scale, 0)
 

@@ -54,3 +54,26 @@ def test_fused_decoder_matches_eager(num_layers, H, W):
         torch.testing.assert_close(out_f[("disp", s)], out_e[("disp", s)], rtol=1e-5, atol=1e-6)
     for a, b in zip(g_f, g_e):
         torch.testing.assert_close(a, b, rtol=2e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("inv", [[True, False], [False, False, True]])
+def test_fused_pose_matches_eager(inv):
+    """pose_ops (HIP) vs layers.transformation_from_parameters (pinned by the golden
+    axisangle/translation gradients) — values and gradients, incl. a zero rotation."""
+    from monodepth2_amd.layers import transformation_from_parameters
+    from monodepth2_amd.pose_ops import poses_to_transforms
+    torch.manual_seed(1)
+    F_, B = len(inv), 5
+    aa = (0.1 * torch.randn(F_, B, 3, device="cuda")).requires_grad_(True)
+    with torch.no_grad():
+        aa[0, 0] = 0.0
+    tr = torch.randn(F_, B, 3, device="cuda", requires_grad=True)
+    T = poses_to_transforms(aa, tr, inv)
+    Tr = torch.stack([transformation_from_parameters(aa[i].unsqueeze(1), tr[i].unsqueeze(1), invert=v)
+                      for i, v in enumerate(inv)])
+    torch.testing.assert_close(T, Tr, rtol=1e-5, atol=1e-6)
+    g = torch.randn_like(T)
+    ga, gt = torch.autograd.grad(T, (aa, tr), g, retain_graph=True)
+    gar, gtr = torch.autograd.grad(Tr, (aa, tr), g)
+    torch.testing.assert_close(ga, gar, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(gt, gtr, rtol=1e-5, atol=1e-6)
