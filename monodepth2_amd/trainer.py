@@ -108,6 +108,16 @@ class Trainer:
                 m.to(memory_format=torch.channels_last)
         self.nets = _Networks(self.models)
         self.parameters_to_train = [p for m in self.models.values() for p in m.parameters()]
+        # BatchNorm's num_batches_tracked only matters with momentum=None (never used
+        # here or in the reference), yet costs one tiny launch per BN layer per step:
+        # keep one step counter instead and write it back into checkpoints.
+        self._bn_layers = []
+        for name, m in self.nets.named_modules():
+            if isinstance(m, nn.modules.batchnorm._BatchNorm) and m.momentum is not None \
+                    and m.num_batches_tracked is not None:
+                self._bn_layers.append(m)
+                m.num_batches_tracked = None
+        self._bn_steps = 0
 
         # gradient averaging: DDP (hooks, overlapped with backward) for eager steps, flat
         # buckets + one RCCL all-reduce each (graph-capturable) for --hip_graph
@@ -123,8 +133,9 @@ class Trainer:
         self.graph = None
         self.seed_tensor = None
 
+        # one fused multi-tensor Adam kernel per step (not the foreach chain)
         self.model_optimizer = optim.Adam(self.parameters_to_train, self.opt.learning_rate,
-                                          capturable=self.use_graph)
+                                          capturable=self.use_graph, fused=not self.use_graph)
         self.model_lr_scheduler = optim.lr_scheduler.StepLR(self.model_optimizer, self.opt.scheduler_step_size, 0.1)
         if self.opt.load_weights_folder is not None:
             self.load_model()
@@ -352,8 +363,18 @@ class Trainer:
         with torch.cuda.graph(self.graph):
             self.static_outputs, self.static_losses = self._step_body(self.static_inputs)
 
+    def _bn_state(self):
+        """Restore the folded BatchNorm counters (checkpoint key parity)."""
+        for m in self._bn_layers:
+            m.num_batches_tracked = torch.tensor(self._bn_steps, dtype=torch.long, device=self.device)
+
+    def _bn_fold(self):
+        for m in self._bn_layers:
+            m.num_batches_tracked = None
+
     def train_step(self, inputs):
         """One optimisation step (trainer.py:205-209)."""
+        self._bn_steps += 1
         if not self.use_graph:
             outputs, losses = self._step_body(inputs)
             self.step += 1
@@ -412,6 +433,7 @@ class Trainer:
         """trainer.py:585-603: weights_{epoch}/{model}.pth + adam.pth."""
         folder = os.path.join(self.log_path, "models", "weights_{}".format(self.epoch))
         os.makedirs(folder, exist_ok=True)
+        self._bn_state()
         for name, model in self.models.items():
             state = model.state_dict()
             if name == "encoder":
@@ -420,12 +442,14 @@ class Trainer:
                 state["use_stereo"] = self.opt.use_stereo
             torch.save(state, os.path.join(folder, "{}.pth".format(name)))
         torch.save(self.model_optimizer.state_dict(), os.path.join(folder, "adam.pth"))
+        self._bn_fold()
         return folder
 
     def load_model(self):
         """trainer.py:605-630 (safe loader: weights_only=True)."""
         folder = os.path.expanduser(self.opt.load_weights_folder)
         assert os.path.isdir(folder), "Cannot find folder {}".format(folder)
+        self._bn_state()
         for n in self.opt.models_to_load:
             if n not in self.models:
                 continue
@@ -434,6 +458,9 @@ class Trainer:
                                 weights_only=True)
             model_dict.update({k: v for k, v in loaded.items() if k in model_dict})
             self.models[n].load_state_dict(model_dict)
+        if self._bn_layers:
+            self._bn_steps = int(self._bn_layers[0].num_batches_tracked)
+        self._bn_fold()
         adam = os.path.join(folder, "adam.pth")
         if os.path.isfile(adam):
             self.model_optimizer.load_state_dict(torch.load(adam, map_location=self.device, weights_only=True))

@@ -115,6 +115,7 @@ def test_checkpoint_roundtrip(tmp_path):
     assert sorted(os.listdir(folder)) == ["adam.pth", "depth.pth", "encoder.pth", "pose.pth", "pose_encoder.pth"]
     enc = torch.load(os.path.join(folder, "encoder.pth"), weights_only=True)
     assert enc["height"] == H and enc["width"] == W and "encoder.conv1.weight" in enc
+    assert int(enc["encoder.bn1.num_batches_tracked"]) == 1   # folded BN counter written back
     tr2, _ = make("mono", log_dir=str(tmp_path), load_weights_folder=folder)
     for (n, p), (n2, p2) in zip(tr.nets.named_parameters(), tr2.nets.named_parameters()):
         assert n == n2 and torch.equal(p, p2)
