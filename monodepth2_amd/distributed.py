@@ -21,14 +21,20 @@ BUCKET_CAP_MB = 64
 
 
 def env_world() -> Tuple[int, int, int]:
-    """(rank, local_rank, world_size) from the torch.distributed.run environment."""
-    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
-            int(os.environ.get("WORLD_SIZE", 1)))
+    """(rank, local_rank, world_size) from the torch.distributed.run environment.
+    MD2_DEVICE_INDEX pins every rank to one device (one-GPU rehearsals with gloo)."""
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if "MD2_DEVICE_INDEX" in os.environ:
+        local = int(os.environ["MD2_DEVICE_INDEX"])
+    return int(os.environ.get("RANK", 0)), local, int(os.environ.get("WORLD_SIZE", 1))
 
 
 def init_process_group(backend: str = None) -> Tuple[int, int, int]:
+    """Initialise from the torch.distributed.run environment.  MD2_DIST_BACKEND
+    overrides the backend (e.g. "gloo" to rehearse several ranks on one GPU)."""
     rank, local_rank, world = env_world()
     if world > 1 and not dist.is_initialized():
+        backend = os.environ.get("MD2_DIST_BACKEND", backend)
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
