@@ -185,6 +185,54 @@ int md2_pose_bwd(int32_t frames, int32_t batch, uint32_t invert_mask, const floa
                  const float* translation, const float* grad_T, float* grad_axisangle,
                  float* grad_translation, void* stream);
 
+/*
+ * GPU input pipeline: what MonoDataset.__getitem__ does to
+ * the decoded frames of a batch (datasets/mono_dataset.py:136-200 with
+ * kitti_dataset.py:58-63) — horizontal flip, the cascaded Resize(ANTIALIAS) pyramid
+ * (mono_dataset.py:80-84, 96-101), ToTensor and the per-item ColorJitter
+ * (mono_dataset.py:66-78, 175-181, 103-108) — bit-exact with the PIL arithmetic the
+ * reference runs on the CPU workers.  The per-item random decisions are drawn by the
+ * caller (same draws, same order as the reference) and passed in `items`.
+ */
+typedef struct md2_aug_desc {
+    int32_t items;                 /* batch size B */
+    int32_t frames;                /* frames per item F (frame_ids, incl. "s") */
+    int32_t in_height, in_width;   /* decoded frame size (scale -1) */
+    int32_t height, width;         /* scale-0 size; scale s is (height>>s, width>>s) */
+    int32_t num_scales;            /* 1..4 */
+    int32_t reserved;
+} md2_aug_desc;
+
+#define MD2_AUG_BRIGHTNESS 0
+#define MD2_AUG_CONTRAST   1
+#define MD2_AUG_SATURATION 2
+#define MD2_AUG_HUE        3
+
+typedef struct md2_aug_item {
+    uint8_t flip;        /* do_flip (mono_dataset.py:137): frames flipped left-right */
+    uint8_t color_aug;   /* do_color_aug (mono_dataset.py:136) */
+    uint8_t hue_shift;   /* np.uint8(hue_factor * 255), wrapped as numpy 1.x does */
+    uint8_t reserved;
+    uint8_t order[4];    /* MD2_AUG_* in application order (ColorJitter's shuffle) */
+    float brightness, contrast, saturation;   /* the get_params factors */
+} md2_aug_item;
+
+typedef struct md2_aug_plan md2_aug_plan;
+
+/* Builds the LANCZOS tables (host, double, as PIL) and allocates the uint8 pyramid
+ * scratch on the current device.  NULL on error (see md2_last_error). */
+md2_aug_plan* md2_aug_plan_create(const md2_aug_desc* desc);
+void md2_aug_plan_destroy(md2_aug_plan* plan);
+
+/*
+ * frames: device uint8 (F, B, in_height, in_width, 3), frame-major (frame f of item b
+ * at index f*B + b); items: device md2_aug_item[B];
+ * color[s] / color_aug[s]: device float32 (F, B, 3, height>>s, width>>s), i.e.
+ * inputs[("color", frame_ids[f], s)][b] and inputs[("color_aug", ...)][b].
+ */
+int md2_aug_run(md2_aug_plan* plan, const uint8_t* frames, const md2_aug_item* items,
+                float* const* color, float* const* color_aug, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -56,7 +56,7 @@ _lib = None
 EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_select_bytes",
            "md2_photometric_fwd", "md2_photometric_bwd", "md2_generate_images",
            "md2_timing_begin", "md2_timing_end", "md2_decoder_pad_fwd", "md2_decoder_pad_bwd",
-           "md2_pose_fwd", "md2_pose_bwd"]
+           "md2_pose_fwd", "md2_pose_bwd", "md2_aug_plan_create", "md2_aug_plan_destroy", "md2_aug_run"]
 
 PAD_ELU = 1 << 0
 PAD_UPSAMPLE = 1 << 1
@@ -65,6 +65,18 @@ PAD_UPSAMPLE = 1 << 1
 class PadDesc(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int32), ("channels", ctypes.c_int32), ("height", ctypes.c_int32),
                 ("width", ctypes.c_int32), ("skip_channels", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
+class AugDesc(ctypes.Structure):
+    _fields_ = [("items", ctypes.c_int32), ("frames", ctypes.c_int32), ("in_height", ctypes.c_int32),
+                ("in_width", ctypes.c_int32), ("height", ctypes.c_int32), ("width", ctypes.c_int32),
+                ("num_scales", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class AugItem(ctypes.Structure):
+    _fields_ = [("flip", ctypes.c_uint8), ("color_aug", ctypes.c_uint8), ("hue_shift", ctypes.c_uint8),
+                ("reserved", ctypes.c_uint8), ("order", ctypes.c_uint8 * 4), ("brightness", ctypes.c_float),
+                ("contrast", ctypes.c_float), ("saturation", ctypes.c_float)]
 
 
 def _declare(L):
@@ -92,6 +104,12 @@ def _declare(L):
     L.md2_pose_fwd.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _vp, _vp, _vp, _vp]
     L.md2_pose_bwd.restype = ctypes.c_int
     L.md2_pose_bwd.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.md2_aug_plan_create.restype = _vp
+    L.md2_aug_plan_create.argtypes = [ctypes.POINTER(AugDesc)]
+    L.md2_aug_plan_destroy.restype = None
+    L.md2_aug_plan_destroy.argtypes = [_vp]
+    L.md2_aug_run.restype = ctypes.c_int
+    L.md2_aug_run.argtypes = [_vp, _vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp]
     L.md2_timing_begin.restype = ctypes.c_int
     L.md2_timing_begin.argtypes = [ctypes.c_int]
     L.md2_timing_end.restype = ctypes.c_int

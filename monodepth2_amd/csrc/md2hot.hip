@@ -1340,6 +1340,11 @@ void launch_photo(const PhotoArgs& a, bool bwd, hipStream_t st, hipEvent_t e0 = 
 
 }  // namespace
 
+// md2_last_error() for the library's other translation units (not exported).
+__attribute__((visibility("hidden"))) int md2_report_error(int code, const char* msg) {
+    return fail(code, "%s", msg);
+}
+
 // ============================================================================
 // C ABI
 // ============================================================================

@@ -1,0 +1,113 @@
+"""GPU input pipeline (csrc/augment.hip via md2_aug_run) vs the PIL-pinned oracle
+(oracle/augment_oracle.py, itself bit-exact with Pillow: test_augment_oracle.py).
+The bar is bit-exact: every float32 of every ("color"/"color_aug", f, s) output."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import augment_oracle as A
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(rng, F, B, h, w):
+    """Textured uint8 frames (smooth + noise, like camera images)."""
+    yy, xx = np.mgrid[0:h, 0:w]
+    out = np.empty((F, B, h, w, 3), np.uint8)
+    for f in range(F):
+        for b in range(B):
+            base = np.zeros((h, w, 3))
+            for _ in range(6):
+                k = rng.uniform(0.005, 0.05, 2)
+                base += rng.uniform(20, 60) * np.sin(k[0] * xx + k[1] * yy + rng.uniform(0, 6.3))[..., None] \
+                    * rng.uniform(0.3, 1.0, 3)
+            base += 128 + rng.normal(0, 12, base.shape)
+            out[f, b] = np.clip(base, 0, 255).astype(np.uint8)
+    return out
+
+
+def _check(aug, frames_np, draws, h, w, S):
+    frames = torch.from_numpy(frames_np).cuda()
+    inputs = aug(frames, draws)
+    torch.cuda.synchronize()
+    for fi, fid in enumerate(aug.frame_ids):
+        for b, d in enumerate(draws):
+            jit = (d.order, d.brightness, d.contrast, d.saturation, d.hue) if d.do_color_aug else None
+            color, caug = A.preprocess(frames_np[fi, b], h, w, S, flip=d.do_flip, jitter=jit)
+            for s in range(S):
+                got = inputs[("color", fid, s)][b].cpu().numpy()
+                gaug = inputs[("color_aug", fid, s)][b].cpu().numpy()
+                assert np.array_equal(got, color[s]), (fid, b, s, int((got != color[s]).sum()))
+                assert np.array_equal(gaug, caug[s]), (fid, b, s, d, int((gaug != caug[s]).sum()))
+    return inputs
+
+
+def test_kitti_pyramid_bit_exact():
+    """375x1242 decoded KITTI frames -> the 4-level 192x640 pyramid, mixed draws."""
+    from monodepth2_amd.augment import GpuAugment, ItemDraw, draw_item
+    rng = np.random.default_rng(0)
+    F, B = 3, 5
+    draws = [ItemDraw(True, True, 1.15, 0.83, 1.07, -0.09, [1, 3, 0, 2]),   # contrast first
+             ItemDraw(True, False, 0.81, 1.19, 0.92, 0.06, [3, 2, 1, 0]),   # contrast after hue+sat
+             ItemDraw(False, True), ItemDraw(False, False), draw_item(random.Random(5))]
+    aug = GpuAugment(192, 640, 375, 1242, [0, -1, 1], B)
+    inputs = _check(aug, _frames(rng, F, B, 375, 1242), draws, 192, 640, 4)
+    K = inputs[("K", 2)]
+    assert K.shape == (B, 4, 4) and float(K[0, 0, 0]) == pytest.approx(0.58 * 160)
+
+
+def test_upsampling_and_stereo_keys():
+    from monodepth2_amd.augment import GpuAugment, ItemDraw
+    rng = np.random.default_rng(1)
+    draws = [ItemDraw(True, True, 1.2, 1.2, 0.8, 0.1, [0, 1, 2, 3]), ItemDraw(False, False)]
+    aug = GpuAugment(128, 416, 100, 300, [0, "s"], 2)
+    inputs = _check(aug, _frames(rng, 2, 2, 100, 300), draws, 128, 416, 4)
+    T = inputs["stereo_T"].cpu()
+    assert float(T[0, 0, 3]) == pytest.approx(0.1) and float(T[1, 0, 3]) == pytest.approx(-0.1)
+
+
+@pytest.mark.parametrize("op", ["hue", "brightness", "contrast", "saturation"])
+def test_jitter_ops_exhaustive_colours(op):
+    """Every RGB colour through each op at level 0 (equal in/out size: identity
+    resample), against the oracle's op (exhaustively pinned to Pillow)."""
+    from monodepth2_amd.augment import GpuAugment, ItemDraw
+    g = np.arange(256, dtype=np.uint8)
+    img = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(4096, 4096, 3)
+    aug = GpuAugment(4096, 4096, 4096, 4096, [0], 1, num_scales=1)
+    frames = torch.from_numpy(img).view(1, 1, 4096, 4096, 3).cuda()
+    params = {"hue": [(1, 1, 1, h) for h in (-0.1, -0.037, 0.052, 0.1)],
+              "brightness": [(f, 1, 1, 0) for f in (0.8, 0.93, 1.17)],
+              "contrast": [(1, f, 1, 0) for f in (0.81, 1.2)],
+              "saturation": [(1, 1, f, 0) for f in (0.85, 1.11)]}[op]
+    for b, c, s, h in params:
+        d = ItemDraw(True, False, b, c, s, h, [3, 0, 1, 2])
+        out = aug(frames, [d])[("color_aug", 0, 0)][0]
+        got = torch.round(out * 255).to(torch.uint8).permute(1, 2, 0).cpu().numpy()
+        want = A.color_jitter(img, d.order, b, c, s, h)
+        bad = int((got != want).any(-1).sum())
+        assert bad == 0, (op, b, c, s, h, bad)
+        del out
+
+
+def test_deterministic_and_stream_safe():
+    from monodepth2_amd.augment import GpuAugment, draw_item
+    rng = np.random.default_rng(2)
+    r = random.Random(3)
+    draws = [draw_item(r) for _ in range(4)]
+    aug = GpuAugment(96, 320, 188, 621, [0, -1, 1], 4)
+    frames = torch.from_numpy(_frames(rng, 3, 4, 188, 621)).cuda()
+    a = aug(frames, draws)
+    b = aug(frames, draws)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
+def test_bad_shapes_raise():
+    from monodepth2_amd.augment import GpuAugment, ItemDraw
+    aug = GpuAugment(64, 128, 80, 160, [0], 1, num_scales=2)
+    with pytest.raises(ValueError):
+        aug(torch.zeros(1, 1, 80, 161, 3, dtype=torch.uint8, device="cuda"), [ItemDraw()])
+    with pytest.raises(ValueError):
+        aug(torch.zeros(1, 1, 80, 160, 3, dtype=torch.float32, device="cuda"), [ItemDraw()])
