@@ -90,6 +90,9 @@ def parse():
     ap.add_argument("--channels-last", type=int, default=0, help="NHWC convolutions (1/0)")
     ap.add_argument("--graph", type=int, default=0, help="capture the whole step in a hipGraph (1/0)")
     ap.add_argument("--miopen-find", type=str, default="fast", help="MIOPEN_FIND_MODE (fast|normal|...)")
+    ap.add_argument("--gpu-augment", type=int, default=0,
+                    help="1: every step also runs the input pipeline (flip + LANCZOS pyramid + jitter, "
+                         "md2_aug_run) from resident 375x1242 uint8 frames")
     return ap.parse_args()
 
 
@@ -201,6 +204,22 @@ def cpu_baseline(args):
                       f"at batch {B}, {W}x{H}, fp32, torch CPU {cores} threads, {el:.1f} s"}
 
 
+def make_augmenting_source(args, frame_ids, device, rank):
+    """Per step: host draws (mono_dataset.py:136-179 order) + md2_aug_run over resident
+    decoded frames, i.e. the reference DataLoader's per-item work on the GPU."""
+    import random
+    from monodepth2_amd.augment import GpuAugment, draw_item
+    from monodepth2_amd.data import synthetic_batch
+    Hn, Wn = 375, 1242
+    nat = synthetic_batch(args.batch, Hn, Wn, frame_ids, 1, seed=300 + rank, device=device)
+    frames = torch.stack([(nat[("color", f, 0)] * 255).round().to(torch.uint8).permute(0, 2, 3, 1)
+                          for f in frame_ids]).contiguous()
+    del nat
+    aug = GpuAugment(args.height, args.width, Hn, Wn, frame_ids, args.batch, device=device)
+    rng = random.Random(1000 + rank)
+    return lambda: aug(frames, [draw_item(rng) for _ in range(args.batch)])
+
+
 def main():
     args = parse()
     from monodepth2_amd.distributed import init_process_group
@@ -217,6 +236,9 @@ def main():
     trainer = make_trainer(args, device, rank, world)
     frame_ids = trainer.opt.frame_ids
     batch = synthetic_batch(args.batch, args.height, args.width, frame_ids, 4, seed=100 + rank, device=device)
+    next_batch = lambda: batch   # noqa: E731
+    if args.gpu_augment:
+        next_batch = make_augmenting_source(args, frame_ids, device, rank)
     log("trainer + batch ready")
 
     delta = None
@@ -234,7 +256,7 @@ def main():
     trainer.set_train()
     for i in range(args.warmup):
         t = time.perf_counter()
-        trainer.train_step(batch)
+        trainer.train_step(next_batch())
         torch.cuda.synchronize()
         log(f"warmup step {i}: {1e3 * (time.perf_counter() - t):.1f} ms")
     stop_hb.set()
@@ -243,7 +265,7 @@ def main():
     # (<< 3 x ms_per_step means the GPU, not the launch path, bounds the step)
     t = time.perf_counter()
     for _ in range(3):
-        trainer.train_step(batch)
+        trainer.train_step(next_batch())
     host_ms = 1e3 * (time.perf_counter() - t) / 3
     torch.cuda.synchronize()
     log(f"host enqueue time: {host_ms:.2f} ms/step")
@@ -253,7 +275,7 @@ def main():
     with _lib.KernelTimer(max_launches=4 * args.steps + 8) as kt:
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            _, losses = trainer.train_step(batch)
+            _, losses = trainer.train_step(next_batch())
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -297,7 +319,8 @@ def main():
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
                 "data": "synthetic (KITTI-shaped smooth textures, random-init weights)",
                 "config": {"workload": f"{'mono+stereo' if args.stereo else 'mono'}_{W}x{H} ResNet-{args.num_layers}"
-                                       f" batch={B}/GPU full train step (configs[1])",
+                                       f" batch={B}/GPU full train step (configs[1])"
+                                       + (" + GPU input pipeline from 375x1242 uint8" if args.gpu_augment else ""),
                            "global_batch": B * world, "height": H, "width": W, "frame_ids": [str(f) for f in frame_ids],
                            "parallelism": f"dp{world}"},
                 "roofline": roof, "cpu_baseline": cpu,

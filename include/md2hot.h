@@ -16,11 +16,13 @@
  *
  * Conventions
  *  - Every tensor is fp32, contiguous NCHW, device memory owned by the caller
- *    (PyTorch's caching allocator).  The library never allocates: scratch
- *    lives in `workspace` (md2_workspace_bytes) and must be the SAME buffer for
- *    a forward and its backward (the forward leaves per-image statistics there).
+ *    (PyTorch's caching allocator).  The library never allocates outside
+ *    md2_aug_plan_create: scratch lives in `workspace` (md2_workspace_bytes) and
+ *    must be the SAME buffer for a forward and its backward (the forward leaves
+ *    per-image statistics there).
  *  - Work is enqueued on `stream` (a hipStream_t); no host synchronisation, no
- *    device malloc, so every call is hipGraph-capturable.
+ *    device malloc, so every call except md2_aug_run (host-staged parameters) is
+ *    hipGraph-capturable.
  *  - Return 0 on success, a negative code otherwise; md2_last_error() then
  *    describes the failure (thread-local).  Nothing in the library aborts.
  *  - Results are deterministic: every reduction is a fixed-order tree.
@@ -226,7 +228,9 @@ void md2_aug_plan_destroy(md2_aug_plan* plan);
 
 /*
  * frames: device uint8 (F, B, in_height, in_width, 3), frame-major (frame f of item b
- * at index f*B + b); items: device md2_aug_item[B];
+ * at index f*B + b); items: HOST md2_aug_item[B], staged through a pinned ring owned by
+ * the plan and uploaded on `stream` (the call does not wait for the GPU; a plan is not
+ * thread-safe);
  * color[s] / color_aug[s]: device float32 (F, B, 3, height>>s, width>>s), i.e.
  * inputs[("color", frame_ids[f], s)][b] and inputs[("color_aug", ...)][b].
  */

@@ -63,8 +63,8 @@ def hue_shift(hue_factor: float) -> int:
     return int(math.trunc(hue_factor * 255)) % 256
 
 
-def pack_items(draws: Sequence[ItemDraw]) -> torch.Tensor:
-    """md2_aug_item[B] as a uint8 CPU tensor."""
+def pack_items(draws: Sequence[ItemDraw]):
+    """md2_aug_item[B] (host ctypes array; md2_aug_run stages it through pinned memory)."""
     arr = (_lib.AugItem * len(draws))()
     for a, d in zip(arr, draws):
         a.flip = int(d.do_flip)
@@ -73,7 +73,7 @@ def pack_items(draws: Sequence[ItemDraw]) -> torch.Tensor:
         for k in range(4):
             a.order[k] = d.order[k]
         a.brightness, a.contrast, a.saturation = d.brightness, d.contrast, d.saturation
-    return torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+    return arr
 
 
 class GpuAugment:
@@ -117,15 +117,16 @@ class GpuAugment:
                 pass
             self._plan = None
 
-    def run(self, frames: torch.Tensor, items_dev: torch.Tensor):
-        """Raw call: returns (color[s], color_aug[s]) tensors shaped (F,B,3,h,w)."""
+    def run(self, frames: torch.Tensor, items):
+        """Raw call (items = pack_items(...)): returns (color[s], color_aug[s]) tensors
+        shaped (F,B,3,h,w)."""
         F, B = len(self.frame_ids), self.batch_size
         want = (F, B, self.in_height, self.in_width, 3)
         if tuple(frames.shape) != want or frames.dtype != torch.uint8 or not frames.is_contiguous():
             raise ValueError(f"frames must be contiguous uint8 {want}, got {tuple(frames.shape)} {frames.dtype}")
-        if frames.device != self.device or items_dev.device != self.device:
-            raise ValueError("frames/items must live on the plan's device")
-        if items_dev.numel() != B * ctypes.sizeof(_lib.AugItem):
+        if frames.device != self.device:
+            raise ValueError("frames must live on the plan's device")
+        if len(items) != B:
             raise ValueError("items must hold one md2_aug_item per batch item")
         color, color_aug = [], []
         for s in range(self.num_scales):
@@ -135,14 +136,13 @@ class GpuAugment:
         cp = (ctypes.c_void_p * self.num_scales)(*[t.data_ptr() for t in color])
         ap = (ctypes.c_void_p * self.num_scales)(*[t.data_ptr() for t in color_aug])
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        _lib.check(_lib.lib().md2_aug_run(self._plan, frames.data_ptr(), items_dev.data_ptr(), cp, ap, stream),
+        _lib.check(_lib.lib().md2_aug_run(self._plan, frames.data_ptr(), ctypes.byref(items), cp, ap, stream),
                    "md2_aug_run")
         return color, color_aug
 
     def __call__(self, frames: torch.Tensor, draws: Sequence[ItemDraw], sides: Optional[Sequence[str]] = None
                  ) -> Dict:
-        items = pack_items(draws).to(self.device, non_blocking=True)
-        color, color_aug = self.run(frames, items)
+        color, color_aug = self.run(frames, pack_items(draws))
         inputs = {}
         for s in range(self.num_scales):
             for i, f in enumerate(self.frame_ids):

@@ -42,6 +42,7 @@ namespace {
 
 constexpr int kPrecisionBits = 32 - 8 - 2;   // Resample.c PRECISION_BITS
 constexpr int kThreads = 256;
+constexpr int kRing = 4;   // pinned item-staging slots per plan
 
 struct Rgb {
     int r, g, b;
@@ -312,6 +313,10 @@ struct md2_aug_plan {
     uint8_t* pyr[MD2_MAX_SCALES];
     uint8_t* mid = nullptr;
     unsigned long long* sums = nullptr;
+    md2_aug_item* dev_items = nullptr;    // kRing slots of d.items on the device
+    md2_aug_item* host_items = nullptr;   // pinned staging, same shape
+    hipEvent_t staged[kRing] = {};        // slot reusable once its upload has run
+    int slot = 0;
     void* block = nullptr;
 };
 
@@ -356,6 +361,9 @@ md2_aug_plan* md2_aug_plan_create(const md2_aug_desc* d) {
     off = align256(off + mid);
     const size_t o_sums = off;
     off = align256(off + (size_t)P->N * d->num_scales * sizeof(unsigned long long));
+    const size_t o_items = off;
+    const size_t item_bytes = (size_t)kRing * d->items * sizeof(md2_aug_item);
+    off = align256(off + item_bytes);
     if (hipMalloc(&P->block, off) != hipSuccess) {
         delete P;
         return md2_report_error(MD2_ERR_HIP, "aug: hipMalloc of the pyramid scratch failed"), nullptr;
@@ -382,24 +390,55 @@ md2_aug_plan* md2_aug_plan_create(const md2_aug_desc* d) {
     }
     P->mid = (uint8_t*)(base + o_mid);
     P->sums = (unsigned long long*)(base + o_sums);
+    P->dev_items = (md2_aug_item*)(base + o_items);
+    bool ok = hipHostMalloc((void**)&P->host_items, item_bytes, hipHostMallocDefault) == hipSuccess;
+    for (int r = 0; ok && r < kRing; ++r)
+        ok = hipEventCreateWithFlags(&P->staged[r], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        md2_aug_plan_destroy(P);
+        return md2_report_error(MD2_ERR_HIP, "aug: pinned staging / events allocation failed"), nullptr;
+    }
     return P;
 }
 
 void md2_aug_plan_destroy(md2_aug_plan* P) {
     if (!P) return;
+    for (int r = 0; r < kRing; ++r)
+        if (P->staged[r]) {
+            (void)hipEventSynchronize(P->staged[r]);
+            (void)hipEventDestroy(P->staged[r]);
+        }
+    if (P->host_items) (void)hipHostFree(P->host_items);
     if (P->block) (void)hipFree(P->block);
     delete P;
 }
 
-int md2_aug_run(md2_aug_plan* P, const uint8_t* frames, const md2_aug_item* items, float* const* color,
+int md2_aug_run(md2_aug_plan* P, const uint8_t* frames, const md2_aug_item* host_items, float* const* color,
                 float* const* color_aug, void* stream) {
-    if (!P || !frames || !items || !color || !color_aug)
+    if (!P || !frames || !host_items || !color || !color_aug)
         return md2_report_error(MD2_ERR_ARG, "aug: plan/frames/items/color/color_aug is NULL");
     const md2_aug_desc& d = P->d;
     for (int s = 0; s < d.num_scales; ++s)
         if (!color[s] || !color_aug[s]) return md2_report_error(MD2_ERR_ARG, "aug: color[s]/color_aug[s] is NULL");
+    for (int b = 0; b < d.items; ++b) {
+        const md2_aug_item& it = host_items[b];
+        unsigned seen = 0;
+        for (int k = 0; k < 4; ++k) seen |= it.order[k] < 4 ? 1u << it.order[k] : 16u;
+        if (seen != 15u) return md2_report_error(MD2_ERR_ARG, "aug: items[b].order must be a permutation of 0..3");
+    }
     hipStream_t st = (hipStream_t)stream;
     const int N = P->N, B = d.items;
+    // stage the item parameters: pinned slot -> device slot, asynchronously on `st`
+    const int r = P->slot;
+    P->slot = (P->slot + 1) % kRing;
+    if (hipEventSynchronize(P->staged[r]) != hipSuccess)
+        return md2_report_error(MD2_ERR_HIP, "aug: waiting for a staging slot failed");
+    memcpy(P->host_items + (size_t)r * B, host_items, (size_t)B * sizeof(md2_aug_item));
+    const md2_aug_item* items = P->dev_items + (size_t)r * B;
+    if (hipMemcpyAsync((void*)items, P->host_items + (size_t)r * B, (size_t)B * sizeof(md2_aug_item),
+                       hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipEventRecord(P->staged[r], st) != hipSuccess)
+        return md2_report_error(MD2_ERR_HIP, "aug: staging the item parameters failed");
     if (hipMemsetAsync(P->sums, 0, (size_t)N * d.num_scales * sizeof(unsigned long long), st) != hipSuccess)
         return md2_report_error(MD2_ERR_HIP, "aug: hipMemsetAsync failed");
     for (int s = 0; s < d.num_scales; ++s) {

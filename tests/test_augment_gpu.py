@@ -111,3 +111,5 @@ def test_bad_shapes_raise():
         aug(torch.zeros(1, 1, 80, 161, 3, dtype=torch.uint8, device="cuda"), [ItemDraw()])
     with pytest.raises(ValueError):
         aug(torch.zeros(1, 1, 80, 160, 3, dtype=torch.float32, device="cuda"), [ItemDraw()])
+    with pytest.raises(RuntimeError, match="permutation"):
+        aug(torch.zeros(1, 1, 80, 160, 3, dtype=torch.uint8, device="cuda"), [ItemDraw(order=[0, 0, 1, 2])])

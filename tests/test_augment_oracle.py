@@ -103,6 +103,6 @@ def test_item_struct_layout():
     from monodepth2_amd.augment import ItemDraw, pack_items
     assert ctypes.sizeof(_lib.AugItem) == 20 and ctypes.sizeof(_lib.AugDesc) == 32
     t = pack_items([ItemDraw(True, True, 1.1, 0.9, 1.0, -0.1, [3, 2, 1, 0])])
-    raw = bytes(t.numpy())
+    raw = bytes(t)
     assert raw[:8] == bytes([1, 1, 231, 0, 3, 2, 1, 0])
     assert np.frombuffer(raw[8:], np.float32).tolist() == [np.float32(1.1), np.float32(0.9), 1.0]
