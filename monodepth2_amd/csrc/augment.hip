@@ -18,9 +18,9 @@
 //            adjust_hue = RGB->HSV (Convert.c), uint8 hue add, HSV->RGB.
 //   to_tensor  float(u8) / 255 for color and color_aug.
 //
-// Launches per batch: 2 per pyramid level (h, v), one memset + one mean pass + one
-// apply pass per level.  All passes are thread-per-output-pixel gathers; integer
-// atomics only (the contrast sums), so results are deterministic.
+// Launches per batch: a memset, one fused (h+v, LDS-tiled, contrast-mean summing)
+// resize per pyramid level, then one jitter/to_tensor pass over all levels.
+// Integer atomics only (the contrast sums), so results are deterministic.
 
 #include <hip/hip_runtime.h>
 
@@ -28,6 +28,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <new>
 #include <vector>
 
@@ -87,7 +88,8 @@ __global__ void __launch_bounds__(kThreads) resize_h_kernel(const uint8_t* __res
 __global__ void __launch_bounds__(kThreads) resize_v_kernel(const uint8_t* __restrict__ src,
                                                             uint8_t* __restrict__ dst, int N, int sh, int dh,
                                                             int w, const int2* __restrict__ bounds,
-                                                            const int* __restrict__ kk, int ksize) {
+                                                            const int* __restrict__ kk, int ksize,
+                                                            float* __restrict__ color) {
     const size_t total = (size_t)N * dh * w;
     const size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x;
     if (i >= total) return;
@@ -109,6 +111,160 @@ __global__ void __launch_bounds__(kThreads) resize_v_kernel(const uint8_t* __res
     o[0] = clip8(a0);
     o[1] = clip8(a1);
     o[2] = clip8(a2);
+    const size_t hw = (size_t)dh * w;
+    float* c = color + n * 3 * hw + (i - n * hw);
+    c[0] = (float)o[0] / 255.f;
+    c[hw] = (float)o[1] / 255.f;
+    c[2 * hw] = (float)o[2] / 255.f;
+}
+
+// Both LANCZOS passes of one pyramid level for a TW x TH output tile, through LDS:
+// the tile's input rows are staged once by LDS-DMA (global_load_lds_dword, every row
+// in flight at once); the horizontal pass reads each lane's whole KX-tap window as
+// aligned dwords, realigns them with v_alignbyte and takes the bytes at compile-time
+// positions (sub-dword LDS reads at odd addresses run at a fraction of the rate);
+// taps past a clipped window carry zero weight.  The uint8 intermediate is one
+// aligned RGBx dword per pixel; the vertical pass writes the level (uint8, for the
+// next level and the jitter) and its to_tensor (color), and adds the tile's share of
+// the contrast degenerate sum (see mean_kernel).  A flipped item reads its staged
+// rows mirrored (the flip is a column permutation of the source).  One wave per row,
+// lane = output column.  Weights are < 2^23 in magnitude: 24-bit multiplies.
+constexpr int kTileW = 64;
+constexpr int kTileH = 16;
+constexpr int kPatchPad = 64;   // bytes before / after the staged rows (clipped windows)
+
+struct FusedLds {
+    int patch, inter;   // byte offsets (patch includes kPatchPad in front)
+    int cin_max, rin_max;
+    int pitch;          // bytes per staged row (multiple of 4, >= cin_max*3 + 3)
+    int bytes;
+};
+
+__device__ __forceinline__ int gray(const Rgb& p);
+__device__ __forceinline__ int contrast_pos(const md2_aug_item& it);
+__device__ int contrast_gray(int r, int g, int b, uint32_t order, float fb, float fc, float fs, int hue, int stop);
+
+// Accumulate KX taps from the realigned window e[] (byte 3p+c = pixel p, channel c);
+// tap t reads pixel t, or KX-1-t for a flipped row.
+template <int KX, int ND, bool FLIP>
+__device__ __forceinline__ void window_taps(const uint32_t (&e)[ND - 1], const int (&wx)[KX], int& a0, int& a1,
+                                            int& a2) {
+#pragma unroll
+    for (int t = 0; t < KX; ++t) {
+        const int o = 3 * (FLIP ? KX - 1 - t : t);
+        const int w = wx[t];
+        a0 += __mul24((int)((e[o >> 2] >> (8 * (o & 3))) & 255), w);
+        a1 += __mul24((int)((e[(o + 1) >> 2] >> (8 * ((o + 1) & 3))) & 255), w);
+        a2 += __mul24((int)((e[(o + 2) >> 2] >> (8 * ((o + 2) & 3))) & 255), w);
+    }
+}
+
+template <int KX, int KY>
+__global__ void __launch_bounds__(kThreads) resize_fused_kernel(
+    const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, float* __restrict__ color, int sh, int sw, int dh,
+    int dw, const int2* __restrict__ bx, const int* __restrict__ kx, const int2* __restrict__ by,
+    const int* __restrict__ ky, FusedLds L, const md2_aug_item* __restrict__ items, int B, int flip_level,
+    unsigned long long* __restrict__ sums) {
+    extern __shared__ __align__(16) uint8_t lds[];
+    uint8_t* patch = lds + L.patch;
+    uint32_t* inter = (uint32_t*)(lds + L.inter);
+    const int n = blockIdx.z;
+    const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * kTileH;
+    const int tw = min(kTileW, dw - x0), th = min(kTileH, dh - y0);
+    const int c0 = bx[x0].x, c1 = bx[x0 + tw - 1].x + bx[x0 + tw - 1].y;
+    const int r0 = by[y0].x, r1 = by[y0 + th - 1].x + by[y0 + th - 1].y;
+    const int cin3 = (c1 - c0) * 3, rin = r1 - r0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const md2_aug_item it = items[n % B];
+    const bool flip = flip_level && it.flip;
+    const int pc0 = flip ? sw - c1 : c0;   // first source column of the staged segment
+    // stage: row r's segment [pc0, pc0 + (c1-c0)) from its 4-byte-aligned start
+    for (int r = wave; r < rin; r += kThreads / 64) {
+        const uint8_t* g = src + (((size_t)n * sh + r0 + r) * sw + pc0) * 3;
+        const uint32_t* ga = (const uint32_t*)((uintptr_t)g & ~(uintptr_t)3);
+        const int nd = ((int)((uintptr_t)g & 3) + cin3 + 3) >> 2;
+        for (int j0 = 0; j0 < nd; j0 += 64)
+            if (j0 + lane < nd)
+                __builtin_amdgcn_global_load_lds(ga + j0 + lane, (uint32_t*)(patch + r * L.pitch) + j0, 4, 0, 0);
+    }
+    // this lane's horizontal weights, in registers for every row
+    int wx[KX];
+    const int xo = min(x0 + lane, dw - 1);
+    const int2 b = bx[xo];
+#pragma unroll
+    for (int t = 0; t < KX; ++t) wx[t] = kx[(size_t)xo * KX + t];
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    // horizontal pass -> RGBx intermediate (rin rows x tw columns)
+    constexpr int ND = (3 * KX + 3 + 3) / 4 + 1;   // dwords covering a window at any byte offset
+    if (lane < tw) {
+        // first staged pixel of the window: tap t sits at pixel (first + t), or (first + KX-1-t) flipped
+        const int first = flip ? (c1 - 1 - b.x) - (KX - 1) : (b.x - c0);
+        for (int r = wave; r < rin; r += kThreads / 64) {
+            const int shift = (int)((uintptr_t)(src + (((size_t)n * sh + r0 + r) * sw + pc0) * 3) & 3);
+            const int byte0 = r * L.pitch + shift + first * 3;   // may be < 0 (pad) when clipped
+            const uint32_t* q = (const uint32_t*)(patch + (byte0 & ~3));
+            const int off = byte0 & 3;
+            uint32_t d[ND];
+#pragma unroll
+            for (int k = 0; k < ND; ++k) d[k] = q[k];
+            uint32_t e[ND - 1];
+#pragma unroll
+            for (int k = 0; k < ND - 1; ++k) e[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], off);
+            int a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
+            if (flip)   // block-uniform; two unrolled bodies keep e[] indices compile-time
+                window_taps<KX, ND, true>(e, wx, a0, a1, a2);
+            else
+                window_taps<KX, ND, false>(e, wx, a0, a1, a2);
+            inter[r * kTileW + lane] = (uint32_t)clip8(a0) | ((uint32_t)clip8(a1) << 8) | ((uint32_t)clip8(a2) << 16);
+        }
+    }
+    __syncthreads();
+    // vertical pass -> level output + to_tensor (+ contrast-mean share)
+    unsigned long long msum = 0;
+    if (lane < tw) {
+        const size_t hw = (size_t)dh * dw;
+        const int stop = it.color_aug ? contrast_pos(it) : 0;
+        const uint32_t order = (uint32_t)it.order[0] | ((uint32_t)it.order[1] << 8) | ((uint32_t)it.order[2] << 16) |
+                               ((uint32_t)it.order[3] << 24);
+        for (int y = wave; y < th; y += kThreads / 64) {
+            const int2 bb = by[y0 + y];
+            const int* k = ky + (size_t)(y0 + y) * KY;
+            const uint32_t* p = inter + (bb.x - r0) * kTileW + lane;
+            int a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
+#pragma unroll
+            for (int t = 0; t < KY; ++t) {
+                if (t < bb.y) {   // wave-uniform; rows past a clipped window are not staged
+                    const int w = k[t];
+                    const uint32_t v = p[t * kTileW];
+                    a0 += __mul24((int)(v & 255), w);
+                    a1 += __mul24((int)((v >> 8) & 255), w);
+                    a2 += __mul24((int)((v >> 16) & 255), w);
+                }
+            }
+            const size_t pix = (size_t)(y0 + y) * dw + x0 + lane;
+            uint8_t* o = dst + ((size_t)n * hw + pix) * 3;
+            const uint8_t v0 = clip8(a0), v1 = clip8(a1), v2 = clip8(a2);
+            o[0] = v0;
+            o[1] = v1;
+            o[2] = v2;
+            float* c = color + (size_t)n * 3 * hw + pix;
+            c[0] = (float)v0 / 255.f;
+            c[hw] = (float)v1 / 255.f;
+            c[2 * hw] = (float)v2 / 255.f;
+            if (it.color_aug)
+                msum += (unsigned long long)contrast_gray(v0, v1, v2, order, it.brightness, it.contrast,
+                                                          it.saturation, it.hue_shift, stop);
+        }
+    }
+    if (it.color_aug) {   // block-uniform
+        for (int off = 32; off > 0; off >>= 1) msum += __shfl_down(msum, off, 64);
+        __shared__ unsigned long long part[kThreads / 64];
+        if (lane == 0) part[wave] = msum;
+        __syncthreads();
+        if (threadIdx.x == 0) atomicAdd(sums + n, part[0] + part[1] + part[2] + part[3]);
+    }
 }
 
 // ---- the ColorJitter ops, in Pillow's C arithmetic ---------------------------------
@@ -155,7 +311,8 @@ __device__ Rgb hue_op(const Rgb& p, int shift) {
             h = (float)(2.0 + (double)rc - (double)bc);
         else
             h = (float)(4.0 + (double)gc - (double)rc);
-        h = (float)fmod((double)h / 6.0 + 1.0, 1.0);
+        const double y = (double)h / 6.0 + 1.0;   // in [5/6, 11/6): fmod(y, 1) is y or y - 1, exact
+        h = (float)(y >= 1.0 ? y - 1.0 : y);
         uh = clip8i((int)((double)h * 255.0));
         us = clip8i((int)((double)s * 255.0));
     }
@@ -197,20 +354,56 @@ __device__ __forceinline__ int contrast_pos(const md2_aug_item& it) {
     return 4;
 }
 
+// gray() of the pixel after the ops that precede contrast (its degenerate's input).
+// (Out of line and by value: it is called once per pixel, from every resize instance.)
+__device__ __noinline__ int contrast_gray(int r, int g, int b, uint32_t order, float fb, float fc, float fs, int hue,
+                                          int stop) {
+    md2_aug_item it{};
+    it.brightness = fb;
+    it.contrast = fc;
+    it.saturation = fs;
+    it.hue_shift = (uint8_t)hue;
+    Rgb v{r, g, b};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (k < stop) v = apply_op((int)((order >> (8 * k)) & 255u), v, it, 0);
+    return gray(v);
+}
+
+// The pyramid levels of one batch, for the all-level mean / apply launches.
+struct Levels {
+    const uint8_t* img[MD2_MAX_SCALES];   // nullptr: level skipped (mean_kernel)
+    float* aug[MD2_MAX_SCALES];
+    int hw[MD2_MAX_SCALES];
+    int first[MD2_MAX_SCALES + 1];   // first block of each level along gridDim.x
+    int nlev, N;
+};
+
+__device__ __forceinline__ int level_of(const Levels& L, int bx) {
+    int s = 0;
+    while (s + 1 < L.nlev && bx >= L.first[s + 1]) ++s;
+    return s;
+}
+
 // Contrast degenerate: sum of L over the image as it stands when contrast runs
-// (ImageEnhance.Contrast, ImageStat mean).  Exact integer sums per image.
-__global__ void __launch_bounds__(kThreads) mean_kernel(const uint8_t* __restrict__ img, int hw, int B,
-                                                        const md2_aug_item* __restrict__ items,
+// (ImageEnhance.Contrast, ImageStat mean).  Exact integer sums per (level, image).
+__global__ void __launch_bounds__(kThreads) mean_kernel(Levels L, int B, const md2_aug_item* __restrict__ items,
                                                         unsigned long long* __restrict__ sums) {
     const int n = blockIdx.y;
     const md2_aug_item it = items[n % B];
     if (!it.color_aug) return;
+    const int s = level_of(L, blockIdx.x);
+    if (!L.img[s]) return;   // fused level: summed inside resize_fused_kernel
+    const int hw = L.hw[s], nb = L.first[s + 1] - L.first[s];
     const int stop = contrast_pos(it);
+    const uint8_t* img = L.img[s] + (size_t)n * hw * 3;
     unsigned long long acc = 0;
-    for (int p = blockIdx.x * kThreads + threadIdx.x; p < hw; p += gridDim.x * kThreads) {
-        const uint8_t* s = img + ((size_t)n * hw + p) * 3;
-        Rgb v{s[0], s[1], s[2]};
-        for (int k = 0; k < stop; ++k) v = apply_op(it.order[k], v, it, 0);
+    for (int p = (blockIdx.x - L.first[s]) * kThreads + threadIdx.x; p < hw; p += nb * kThreads) {
+        const uint8_t* q = img + (size_t)p * 3;
+        Rgb v{q[0], q[1], q[2]};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < stop) v = apply_op(it.order[k], v, it, 0);
         acc += (unsigned long long)gray(v);
     }
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
@@ -220,30 +413,26 @@ __global__ void __launch_bounds__(kThreads) mean_kernel(const uint8_t* __restric
     if (threadIdx.x == 0) {
         unsigned long long t = 0;
         for (int w = 0; w < kThreads / 64; ++w) t += part[w];
-        atomicAdd(sums + n, t);
+        atomicAdd(sums + (size_t)s * L.N + n, t);
     }
 }
 
-// to_tensor(img) -> color, to_tensor(color_aug(img)) -> color_aug (planar float).
-__global__ void __launch_bounds__(kThreads) apply_kernel(const uint8_t* __restrict__ img, int hw, int B,
-                                                         const md2_aug_item* __restrict__ items,
-                                                         const unsigned long long* __restrict__ sums,
-                                                         float* __restrict__ color, float* __restrict__ color_aug) {
+// to_tensor(color_aug(img)) -> color_aug (planar float), every level in one launch.
+__global__ void __launch_bounds__(kThreads) apply_kernel(Levels L, int B, const md2_aug_item* __restrict__ items,
+                                                         const unsigned long long* __restrict__ sums) {
     const int n = blockIdx.y;
-    const int p = blockIdx.x * kThreads + threadIdx.x;
+    const int s = level_of(L, blockIdx.x);
+    const int hw = L.hw[s];
+    const int p = (blockIdx.x - L.first[s]) * kThreads + threadIdx.x;
     if (p >= hw) return;
     const md2_aug_item it = items[n % B];
-    const uint8_t* s = img + ((size_t)n * hw + p) * 3;
-    Rgb v{s[0], s[1], s[2]};
-    float* c = color + (size_t)n * 3 * hw + p;
-    c[0] = (float)v.r / 255.f;
-    c[hw] = (float)v.g / 255.f;
-    c[2 * hw] = (float)v.b / 255.f;
+    const uint8_t* q = L.img[s] + ((size_t)n * hw + p) * 3;
+    Rgb v{q[0], q[1], q[2]};
     if (it.color_aug) {
-        const int mean = (int)((double)sums[n] / (double)hw + 0.5);
+        const int mean = (int)((double)sums[(size_t)s * L.N + n] / (double)hw + 0.5);
         for (int k = 0; k < 4; ++k) v = apply_op(it.order[k], v, it, mean);
     }
-    float* a = color_aug + (size_t)n * 3 * hw + p;
+    float* a = L.aug[s] + (size_t)n * 3 * hw + p;
     a[0] = (float)v.r / 255.f;
     a[hw] = (float)v.g / 255.f;
     a[2 * hw] = (float)v.b / 255.f;
@@ -296,6 +485,52 @@ void lanczos_tables(int in_size, int out_size, std::vector<int2>& bounds, std::v
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// resize_fused_kernel instantiation for the two window sizes (2*ceil(3*max(scale,1))+1:
+// 7 up-scaling, 9/11/13 down to 2x), nullptr for wider windows (two-pass kernels).
+using FusedFn = void (*)(const uint8_t*, uint8_t*, float*, int, int, int, int, const int2*, const int*,
+                         const int2*, const int*, FusedLds, const md2_aug_item*, int, int, unsigned long long*);
+
+template <int KX>
+FusedFn fused_for_ky(int ky) {
+    switch (ky) {
+        case 7: return resize_fused_kernel<KX, 7>;
+        case 9: return resize_fused_kernel<KX, 9>;
+        case 11: return resize_fused_kernel<KX, 11>;
+        case 13: return resize_fused_kernel<KX, 13>;
+        default: return nullptr;
+    }
+}
+
+FusedFn fused_kernel(int kx, int ky) {
+    switch (kx) {
+        case 7: return fused_for_ky<7>(ky);
+        case 9: return fused_for_ky<9>(ky);
+        case 11: return fused_for_ky<11>(ky);
+        case 13: return fused_for_ky<13>(ky);
+        default: return nullptr;
+    }
+}
+
+// LDS layout of resize_fused_kernel for one level: the widest input patch over all
+// tiles.  bytes > 64 KB (extreme down-scaling) selects the two-pass kernels instead.
+FusedLds fused_layout(const std::vector<int2>& bx, const std::vector<int2>& by) {
+    FusedLds L{};
+    const int dw = (int)bx.size(), dh = (int)by.size();
+    for (int x0 = 0; x0 < dw; x0 += kTileW) {
+        const int xl = std::min(x0 + kTileW, dw) - 1;
+        L.cin_max = std::max(L.cin_max, bx[xl].x + bx[xl].y - bx[x0].x);
+    }
+    for (int y0 = 0; y0 < dh; y0 += kTileH) {
+        const int yl = std::min(y0 + kTileH, dh) - 1;
+        L.rin_max = std::max(L.rin_max, by[yl].x + by[yl].y - by[y0].x);
+    }
+    L.pitch = (L.cin_max * 3 + 3 + 3) & ~3;
+    L.patch = kPatchPad;
+    L.inter = (kPatchPad + L.rin_max * L.pitch + kPatchPad + 15) & ~15;
+    L.bytes = L.inter + L.rin_max * kTileW * 4;
+    return L;
+}
+
 unsigned blocks_for(size_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
 
 }  // namespace
@@ -311,7 +546,9 @@ struct md2_aug_plan {
     int* wx[MD2_MAX_SCALES];
     int* wy[MD2_MAX_SCALES];
     uint8_t* pyr[MD2_MAX_SCALES];
-    uint8_t* mid = nullptr;
+    FusedLds lds[MD2_MAX_SCALES];
+    bool fused[MD2_MAX_SCALES];
+    uint8_t* mid = nullptr;   // two-pass intermediate (levels that are not fused)
     unsigned long long* sums = nullptr;
     md2_aug_item* dev_items = nullptr;    // kRing slots of d.items on the device
     md2_aug_item* host_items = nullptr;   // pinned staging, same shape
@@ -354,8 +591,10 @@ md2_aug_plan* md2_aug_plan_create(const md2_aug_desc* d) {
         o_wx[s] = off; off = align256(off + wxh[s].size() * sizeof(int));
         o_wy[s] = off; off = align256(off + wyh[s].size() * sizeof(int));
         o_pyr[s] = off; off = align256(off + (size_t)P->N * P->h[s] * P->w[s] * 3);
+        P->lds[s] = fused_layout(bxh[s], byh[s]);
+        P->fused[s] = P->lds[s].bytes <= 64 * 1024 && fused_kernel(P->kx[s], P->ky[s]) != nullptr;
         const size_t m = (size_t)P->N * P->sh[s] * P->w[s] * 3;
-        if (m > mid) mid = m;
+        if (!P->fused[s] && m > mid) mid = m;
     }
     const size_t o_mid = off;
     off = align256(off + mid);
@@ -443,21 +682,38 @@ int md2_aug_run(md2_aug_plan* P, const uint8_t* frames, const md2_aug_item* host
         return md2_report_error(MD2_ERR_HIP, "aug: hipMemsetAsync failed");
     for (int s = 0; s < d.num_scales; ++s) {
         const uint8_t* src = s ? P->pyr[s - 1] : frames;
-        hipLaunchKernelGGL(resize_h_kernel, dim3(blocks_for((size_t)N * P->sh[s] * P->w[s])), dim3(kThreads), 0, st,
-                           src, P->mid, N, P->sh[s], P->sw[s], P->w[s], P->bx[s], P->wx[s], P->kx[s],
-                           s ? nullptr : items, B);
-        hipLaunchKernelGGL(resize_v_kernel, dim3(blocks_for((size_t)N * P->h[s] * P->w[s])), dim3(kThreads), 0, st,
-                           P->mid, P->pyr[s], N, P->sh[s], P->h[s], P->w[s], P->by[s], P->wy[s], P->ky[s]);
+        const md2_aug_item* flip = s ? nullptr : items;
+        if (P->fused[s]) {
+            const dim3 grid((P->w[s] + kTileW - 1) / kTileW, (P->h[s] + kTileH - 1) / kTileH, N);
+            hipLaunchKernelGGL(fused_kernel(P->kx[s], P->ky[s]), grid, dim3(kThreads), P->lds[s].bytes, st, src,
+                               P->pyr[s], color[s], P->sh[s], P->sw[s], P->h[s], P->w[s], P->bx[s], P->wx[s],
+                               P->by[s], P->wy[s], P->lds[s], items, B, s == 0 ? 1 : 0, P->sums + (size_t)s * N);
+        } else {
+            hipLaunchKernelGGL(resize_h_kernel, dim3(blocks_for((size_t)N * P->sh[s] * P->w[s])), dim3(kThreads), 0,
+                               st, src, P->mid, N, P->sh[s], P->sw[s], P->w[s], P->bx[s], P->wx[s], P->kx[s], flip, B);
+            hipLaunchKernelGGL(resize_v_kernel, dim3(blocks_for((size_t)N * P->h[s] * P->w[s])), dim3(kThreads), 0,
+                               st, P->mid, P->pyr[s], N, P->sh[s], P->h[s], P->w[s], P->by[s], P->wy[s], P->ky[s],
+                               color[s]);
+        }
     }
+    Levels L{};
+    L.nlev = d.num_scales;
+    L.N = N;
+    Levels M = L;   // the mean pass caps blocks per image at 64 per level
+    bool any_two_pass = false;
     for (int s = 0; s < d.num_scales; ++s) {
-        const int hw = P->h[s] * P->w[s];
-        const unsigned gx = blocks_for(hw);
-        unsigned long long* sums = P->sums + (size_t)s * N;
-        hipLaunchKernelGGL(mean_kernel, dim3(gx < 64 ? gx : 64, N), dim3(kThreads), 0, st, P->pyr[s], hw, B, items,
-                           sums);
-        hipLaunchKernelGGL(apply_kernel, dim3(gx, N), dim3(kThreads), 0, st, P->pyr[s], hw, B, items, sums,
-                           color[s], color_aug[s]);
+        any_two_pass |= !P->fused[s];
+        L.img[s] = P->pyr[s];
+        M.img[s] = P->fused[s] ? nullptr : P->pyr[s];
+        L.aug[s] = M.aug[s] = color_aug[s];
+        L.hw[s] = M.hw[s] = P->h[s] * P->w[s];
+        const int nb = (int)blocks_for(L.hw[s]);
+        L.first[s + 1] = L.first[s] + nb;
+        M.first[s + 1] = M.first[s] + std::min(nb, 64);
     }
+    if (any_two_pass)
+        hipLaunchKernelGGL(mean_kernel, dim3(M.first[d.num_scales], N), dim3(kThreads), 0, st, M, B, items, P->sums);
+    hipLaunchKernelGGL(apply_kernel, dim3(L.first[d.num_scales], N), dim3(kThreads), 0, st, L, B, items, P->sums);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }

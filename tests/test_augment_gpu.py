@@ -91,6 +91,16 @@ def test_jitter_ops_exhaustive_colours(op):
         del out
 
 
+def test_extreme_downscale_two_pass_path():
+    """A 52x down-scale needs a 313-tap window: the LDS tile would not fit, so this
+    level takes the two-pass (global-memory) kernels; same bit-exact bar."""
+    from monodepth2_amd.augment import GpuAugment, ItemDraw
+    rng = np.random.default_rng(4)
+    draws = [ItemDraw(True, True, 0.9, 1.1, 1.2, -0.02, [2, 1, 3, 0]), ItemDraw(False, True)]
+    aug = GpuAugment(24, 48, 600, 2500, [0], 2, num_scales=2)
+    _check(aug, _frames(rng, 1, 2, 600, 2500), draws, 24, 48, 2)
+
+
 def test_deterministic_and_stream_safe():
     from monodepth2_amd.augment import GpuAugment, draw_item
     rng = np.random.default_rng(2)
