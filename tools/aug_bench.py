@@ -48,8 +48,23 @@ def main():
     out_bytes = sum(F * B * 3 * (H >> s) * (W >> s) * 4 * 2 for s in range(4))
     in_bytes = F * B * Hn * Wn * 3
 
-    from oracle import augment_oracle as A   # CPU leg: Pillow itself (the reference's arithmetic)
-    from PIL import Image
+    from PIL import Image, ImageEnhance   # CPU leg: Pillow itself, as the reference's loader runs it
+
+    def pil_jitter(arr, order, b, c, s, h):
+        # torchvision 0.2.1 adjust_* on PIL (not installed here): the same Pillow calls
+        pim = Image.fromarray(arr)
+        for o in order:
+            if o == 0:
+                pim = ImageEnhance.Brightness(pim).enhance(b)
+            elif o == 1:
+                pim = ImageEnhance.Contrast(pim).enhance(c)
+            elif o == 2:
+                pim = ImageEnhance.Color(pim).enhance(s)
+            else:
+                hh, ss, vv = pim.convert("HSV").split()
+                np_h = ((np.array(hh, dtype=np.int32) + int(h * 255)) % 256).astype(np.uint8)
+                pim = Image.merge("HSV", (Image.fromarray(np_h, "L"), ss, vv)).convert("RGB")
+        return np.asarray(pim)
     t0 = time.perf_counter()
     for b in range(a.cpu_items):
         d = draws[b]
@@ -61,7 +76,7 @@ def main():
                 img = img.resize((W >> s, H >> s), Image.Resampling.LANCZOS)
                 arr = np.asarray(img)
                 _ = arr.transpose(2, 0, 1).astype(np.float32) / 255
-                j = A.pil_jitter(arr, d.order, d.brightness, d.contrast, d.saturation, d.hue) if d.do_color_aug \
+                j = pil_jitter(arr, d.order, d.brightness, d.contrast, d.saturation, d.hue) if d.do_color_aug \
                     else arr
                 _ = j.transpose(2, 0, 1).astype(np.float32) / 255
     cpu_item_ms = (time.perf_counter() - t0) * 1000 / a.cpu_items
