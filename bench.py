@@ -87,7 +87,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen exhaustive find per conv shape")
-    ap.add_argument("--channels-last", type=int, default=0, help="NHWC convolutions (1/0)")
+    ap.add_argument("--channels-last", type=int, default=1, help="NHWC convolutions (1/0)")
     ap.add_argument("--graph", type=int, default=0, help="capture the whole step in a hipGraph (1/0)")
     ap.add_argument("--miopen-find", type=str, default="fast", help="MIOPEN_FIND_MODE (fast|normal|...)")
     ap.add_argument("--gpu-augment", type=int, default=0,

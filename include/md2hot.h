@@ -162,6 +162,7 @@ int md2_timing_end(double* fwd_ms, int* n_fwd, double* bwd_ms, int* n_bwd);
  */
 #define MD2_PAD_ELU      (1u << 0)
 #define MD2_PAD_UPSAMPLE (1u << 1)
+#define MD2_PAD_NHWC     (1u << 2)   /* x, skip, out (and their grads) channels_last */
 
 typedef struct md2_pad_desc {
     int32_t batch, channels, height, width; /* of x */

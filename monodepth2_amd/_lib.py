@@ -60,6 +60,7 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
 
 PAD_ELU = 1 << 0
 PAD_UPSAMPLE = 1 << 1
+PAD_NHWC = 1 << 2
 
 
 class PadDesc(ctypes.Structure):

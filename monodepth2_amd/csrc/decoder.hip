@@ -10,9 +10,12 @@
 // derivative x upsample fold x reflection fold; the skip gradient falls out of the
 // same sweep).  The convolutions themselves stay MIOpen's.
 //
-// Layouts: NCHW fp32 contiguous.  x: (B, C, h, w) pre-activation (or the raw
+// Layouts: fp32, all three tensors NCHW contiguous, or all NHWC (channels_last,
+// MD2_PAD_NHWC: what MIOpen's NHWC convolutions read and write, so no layout copy
+// sits between them and this pass).  x: (B, C, h, w) pre-activation (or the raw
 // feature when ELU is off); skip: (B, Cs, H, W) with (H, W) = (2h, 2w) when
-// upsampling else (h, w); out: (B, C + Cs, H + 2, W + 2).
+// upsampling else (h, w); out: (B, C + Cs, H + 2, W + 2).  In NHWC the channel is
+// the fastest index of every loop, so loads and stores stay coalesced.
 
 #include <hip/hip_runtime.h>
 
@@ -42,87 +45,140 @@ struct PadArgs {
     float* gskip;
 };
 
-template <bool ELU, bool UP>
+// element (b, c, y, x) of a (B, C, Hh, Ww) tensor
+template <bool NHWC>
+__device__ __forceinline__ size_t at(int b, int c, int y, int x, int C, int Hh, int Ww) {
+    return NHWC ? (((size_t)b * Hh + y) * Ww + x) * C + c : (((size_t)b * C + c) * Hh + y) * Ww + x;
+}
+
+template <bool ELU, bool UP, bool NHWC>
 __global__ __launch_bounds__(kThreads) void pad_fwd_kernel(PadArgs a) {
-    const int Hp = a.H + 2, Wp = a.W + 2;
-    const long long total = (long long)a.B * (a.C + a.Cs) * Hp * Wp;
+    const int Hp = a.H + 2, Wp = a.W + 2, Ct = a.C + a.Cs;
+    const long long total = (long long)a.B * Ct * Hp * Wp;
     for (long long idx = (long long)blockIdx.x * kThreads + threadIdx.x; idx < total;
          idx += (long long)gridDim.x * kThreads) {
-        const int px = (int)(idx % Wp);
-        long long t = idx / Wp;
-        const int py = (int)(t % Hp);
-        t /= Hp;
-        const int c = (int)(t % (a.C + a.Cs));
-        const int b = (int)(t / (a.C + a.Cs));
+        int px, py, c, b;
+        long long t;
+        if (NHWC) {
+            c = (int)(idx % Ct);
+            t = idx / Ct;
+            px = (int)(t % Wp);
+            t /= Wp;
+            py = (int)(t % Hp);
+            b = (int)(t / Hp);
+        } else {
+            px = (int)(idx % Wp);
+            t = idx / Wp;
+            py = (int)(t % Hp);
+            t /= Hp;
+            c = (int)(t % Ct);
+            b = (int)(t / Ct);
+        }
         const int yy = reflect1(py - 1, a.H), xx = reflect1(px - 1, a.W);
         float v;
         if (c < a.C) {
             const int sy = UP ? (yy >> 1) : yy, sx = UP ? (xx >> 1) : xx;
-            v = a.x[(((size_t)b * a.C + c) * a.h + sy) * a.w + sx];
+            v = a.x[at<NHWC>(b, c, sy, sx, a.C, a.h, a.w)];
             if (ELU) v = elu(v);
         } else {
-            v = a.skip[(((size_t)b * a.Cs + (c - a.C)) * a.H + yy) * a.W + xx];
+            v = a.skip[at<NHWC>(b, c - a.C, yy, xx, a.Cs, a.H, a.W)];
         }
         a.out[idx] = v;
     }
 }
 
-// sum of the padded gradient over every padded position that reads source (yy, xx)
-__device__ __forceinline__ float fold(const float* g, int Wp, int H, int W, int yy, int xx) {
-    float s = g[(yy + 1) * Wp + (xx + 1)];
+// sum of the padded gradient over every padded position that reads source (yy, xx);
+// g points at (b, c, 0, 0) of the padded gradient, es = element stride of a pixel
+// (1 in NCHW, C + Cs in NHWC).
+__device__ __forceinline__ float fold(const float* g, int Wp, int H, int W, int yy, int xx, int es) {
+    auto G = [&](int y, int x) { return g[((size_t)y * Wp + x) * es]; };
+    float s = G(yy + 1, xx + 1);
     const bool ry = (yy == 1), ry2 = (yy == H - 2), rx = (xx == 1), rx2 = (xx == W - 2);
-    if (rx) s += g[(yy + 1) * Wp + 0];
-    if (rx2) s += g[(yy + 1) * Wp + (W + 1)];
+    if (rx) s += G(yy + 1, 0);
+    if (rx2) s += G(yy + 1, W + 1);
     if (ry) {
-        s += g[0 * Wp + (xx + 1)];
-        if (rx) s += g[0];
-        if (rx2) s += g[W + 1];
+        s += G(0, xx + 1);
+        if (rx) s += G(0, 0);
+        if (rx2) s += G(0, W + 1);
     }
     if (ry2) {
-        const float* r = g + (size_t)(H + 1) * Wp;
-        s += r[xx + 1];
-        if (rx) s += r[0];
-        if (rx2) s += r[W + 1];
+        s += G(H + 1, xx + 1);
+        if (rx) s += G(H + 1, 0);
+        if (rx2) s += G(H + 1, W + 1);
     }
     return s;
 }
 
-template <bool ELU, bool UP>
+// (b, c, y, x) of flat index k over a (B, C, Hh, Ww) tensor in the given layout
+template <bool NHWC>
+__device__ __forceinline__ void coords(long long k, int C, int Hh, int Ww, int& b, int& c, int& y, int& x) {
+    if (NHWC) {
+        c = (int)(k % C);
+        k /= C;
+        x = (int)(k % Ww);
+        k /= Ww;
+        y = (int)(k % Hh);
+        b = (int)(k / Hh);
+    } else {
+        x = (int)(k % Ww);
+        k /= Ww;
+        y = (int)(k % Hh);
+        k /= Hh;
+        c = (int)(k % C);
+        b = (int)(k / C);
+    }
+}
+
+template <bool ELU, bool UP, bool NHWC>
 __global__ __launch_bounds__(kThreads) void pad_bwd_kernel(PadArgs a) {
-    const int Hp = a.H + 2, Wp = a.W + 2;
+    const int Hp = a.H + 2, Wp = a.W + 2, Ct = a.C + a.Cs;
+    const int es = NHWC ? Ct : 1;
     const long long nx = (long long)a.B * a.C * a.h * a.w;
     const long long ns = (long long)a.B * a.Cs * a.H * a.W;
     for (long long idx = (long long)blockIdx.x * kThreads + threadIdx.x; idx < nx + ns;
          idx += (long long)gridDim.x * kThreads) {
+        int b, c, i, j;
         if (idx < nx) {
-            const int j = (int)(idx % a.w);
-            long long t = idx / a.w;
-            const int i = (int)(t % a.h);
-            t /= a.h;
-            const int c = (int)(t % a.C);
-            const int b = (int)(t / a.C);
-            const float* g = a.gout + (((size_t)b * (a.C + a.Cs) + c) * Hp) * Wp;
+            coords<NHWC>(idx, a.C, a.h, a.w, b, c, i, j);
+            const float* g = a.gout + at<NHWC>(b, c, 0, 0, Ct, Hp, Wp);
             float s;
             if (UP) {
-                s = fold(g, Wp, a.H, a.W, 2 * i, 2 * j) + fold(g, Wp, a.H, a.W, 2 * i, 2 * j + 1) +
-                    fold(g, Wp, a.H, a.W, 2 * i + 1, 2 * j) + fold(g, Wp, a.H, a.W, 2 * i + 1, 2 * j + 1);
+                s = fold(g, Wp, a.H, a.W, 2 * i, 2 * j, es) + fold(g, Wp, a.H, a.W, 2 * i, 2 * j + 1, es) +
+                    fold(g, Wp, a.H, a.W, 2 * i + 1, 2 * j, es) + fold(g, Wp, a.H, a.W, 2 * i + 1, 2 * j + 1, es);
             } else {
-                s = fold(g, Wp, a.H, a.W, i, j);
+                s = fold(g, Wp, a.H, a.W, i, j, es);
             }
             if (ELU) s *= elu_grad(a.x[idx]);
             a.gx[idx] = s;
         } else {
             const long long k = idx - nx;
-            const int xx = (int)(k % a.W);
-            long long t = k / a.W;
-            const int yy = (int)(t % a.H);
-            t /= a.H;
-            const int c = (int)(t % a.Cs);
-            const int b = (int)(t / a.Cs);
-            const float* g = a.gout + (((size_t)b * (a.C + a.Cs) + a.C + c) * Hp) * Wp;
-            a.gskip[k] = fold(g, Wp, a.H, a.W, yy, xx);
+            coords<NHWC>(k, a.Cs, a.H, a.W, b, c, i, j);
+            a.gskip[k] = fold(a.gout + at<NHWC>(b, a.C + c, 0, 0, Ct, Hp, Wp), Wp, a.H, a.W, i, j, es);
         }
     }
+}
+
+using PadFn = void (*)(PadArgs);
+
+template <bool E, bool U, bool N>
+PadFn fwd_of() { return pad_fwd_kernel<E, U, N>; }
+template <bool E, bool U, bool N>
+PadFn bwd_of() { return pad_bwd_kernel<E, U, N>; }
+
+// the kernel instance for MD2_PAD_* flags (ELU, UPSAMPLE, NHWC)
+PadFn fwd_kernel(uint32_t f) {
+    static const PadFn t[8] = {fwd_of<false, false, false>(), fwd_of<true, false, false>(),
+                               fwd_of<false, true, false>(),  fwd_of<true, true, false>(),
+                               fwd_of<false, false, true>(),  fwd_of<true, false, true>(),
+                               fwd_of<false, true, true>(),   fwd_of<true, true, true>()};
+    return t[f & 7u];
+}
+PadFn bwd_kernel(uint32_t f) {
+    static const PadFn t[8] = {bwd_of<false, false, false>(), bwd_of<true, false, false>(),
+                               bwd_of<false, true, false>(),  bwd_of<true, true, false>(),
+                               bwd_of<false, false, true>(),  bwd_of<true, false, true>(),
+                               bwd_of<false, true, true>(),   bwd_of<true, true, true>()};
+    return t[f & 7u];
 }
 
 int grid_for(long long n) {
@@ -154,12 +210,7 @@ int md2_decoder_pad_fwd(const md2_pad_desc* d, const float* x, const float* skip
     a.skip = skip;
     a.out = out;
     const long long n = (long long)a.B * (a.C + a.Cs) * (a.H + 2) * (a.W + 2);
-    hipStream_t st = (hipStream_t)stream;
-    const bool elu = d->flags & MD2_PAD_ELU, up = d->flags & MD2_PAD_UPSAMPLE;
-    if (elu && up) hipLaunchKernelGGL((pad_fwd_kernel<true, true>), dim3(grid_for(n)), dim3(kThreads), 0, st, a);
-    else if (elu) hipLaunchKernelGGL((pad_fwd_kernel<true, false>), dim3(grid_for(n)), dim3(kThreads), 0, st, a);
-    else if (up) hipLaunchKernelGGL((pad_fwd_kernel<false, true>), dim3(grid_for(n)), dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL((pad_fwd_kernel<false, false>), dim3(grid_for(n)), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(fwd_kernel(d->flags), dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
 }
 
@@ -173,12 +224,9 @@ int md2_decoder_pad_bwd(const md2_pad_desc* d, const float* x, const float* grad
     a.gout = grad_out;
     a.gx = grad_x;
     a.gskip = grad_skip;
+    (void)up;
     const long long n = (long long)a.B * a.C * a.h * a.w + (long long)a.B * a.Cs * a.H * a.W;
-    hipStream_t st = (hipStream_t)stream;
-    if (elu && up) hipLaunchKernelGGL((pad_bwd_kernel<true, true>), dim3(grid_for(n)), dim3(kThreads), 0, st, a);
-    else if (elu) hipLaunchKernelGGL((pad_bwd_kernel<true, false>), dim3(grid_for(n)), dim3(kThreads), 0, st, a);
-    else if (up) hipLaunchKernelGGL((pad_bwd_kernel<false, true>), dim3(grid_for(n)), dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL((pad_bwd_kernel<false, false>), dim3(grid_for(n)), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(bwd_kernel(d->flags), dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
 }
 

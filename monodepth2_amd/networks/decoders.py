@@ -51,13 +51,15 @@ class DepthDecoder(nn.Module):
         (dispconv -> sigmoid) and the next level's first conv."""
         from ..decoder_ops import conv_input
         self.outputs = {}
-        P = conv_input(input_features[-1])                       # ReflectionPad2d only
+        # NHWC convolutions (channels_last weights): keep every conv input NHWC too
+        cl = self.convs[("upconv", 4, 0)].conv.conv.weight.is_contiguous(memory_format=torch.channels_last)
+        P = conv_input(input_features[-1], nhwc=cl)               # ReflectionPad2d only
         for i in range(4, -1, -1):
             y0 = self.convs[("upconv", i, 0)].conv.conv(P)
             skip = input_features[i - 1] if (self.use_skips and i > 0) else None
-            P = conv_input(y0, skip, elu=True, upsample=True)
+            P = conv_input(y0, skip, elu=True, upsample=True, nhwc=cl)
             y1 = self.convs[("upconv", i, 1)].conv.conv(P)
-            P = conv_input(y1, None, elu=True, upsample=False)   # shared by dispconv and the next level
+            P = conv_input(y1, None, elu=True, upsample=False, nhwc=cl)   # shared by dispconv and the next level
             if i in self.scales:
                 self.outputs[("disp", i)] = self.sigmoid(self.convs[("dispconv", i)].conv(P))
         return self.outputs

@@ -74,7 +74,8 @@ _FLAGS = [
     ("--materialize_images", dict(action="store_true",
                                   help="build: also materialise warped colours/samples/depth every step")),
     ("--noise_seed", dict(type=int, default=0, help="build: seed of the in-kernel tie-break noise")),
-    ("--channels_last", dict(action="store_true", help="build: NHWC activations/weights for the convolutions")),
+    ("--channels_last", dict(type=int, default=1,
+                             help="build: 1 (default) NHWC activations/weights for the convolutions, 0 NCHW")),
     ("--hip_graph", dict(action="store_true", help="build: capture the whole training step in one hipGraph")),
     ("--grad_sync", dict(type=str, default="auto", choices=["auto", "ddp", "flat"],
                          help="build: gradient averaging for >1 GPU (auto: flat with --hip_graph, else ddp)")),

@@ -10,14 +10,18 @@ from monodepth2_amd.decoder_ops import conv_input
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("nhwc", [False, True])
 @pytest.mark.parametrize("elu,up,skip_ch", [(False, False, 0), (True, True, 0), (True, True, 64),
                                             (True, False, 0), (False, True, 32)])
-def test_conv_input_matches_eager(elu, up, skip_ch):
+def test_conv_input_matches_eager(elu, up, skip_ch, nhwc):
     torch.manual_seed(0)
-    x = torch.randn(3, 8, 6, 10, device="cuda", requires_grad=True)
+    fmt = torch.channels_last if nhwc else torch.contiguous_format
+    x = torch.randn(3, 8, 6, 10, device="cuda").contiguous(memory_format=fmt).requires_grad_(True)
     H, W = (12, 20) if up else (6, 10)
-    skip = torch.randn(3, skip_ch, H, W, device="cuda", requires_grad=True) if skip_ch else None
-    out = conv_input(x, skip, elu=elu, upsample=up)
+    skip = (torch.randn(3, skip_ch, H, W, device="cuda").contiguous(memory_format=fmt).requires_grad_(True)
+            if skip_ch else None)
+    out = conv_input(x, skip, elu=elu, upsample=up, nhwc=nhwc)
+    assert out.is_contiguous(memory_format=fmt)
     y = torch.nn.functional.elu(x) if elu else x
     if up:
         y = torch.nn.functional.interpolate(y, scale_factor=2, mode="nearest")
@@ -26,8 +30,9 @@ def test_conv_input_matches_eager(elu, up, skip_ch):
     ref = torch.nn.functional.pad(y, (1, 1, 1, 1), mode="reflect")
     assert torch.equal(out, ref)
     g = torch.randn_like(ref)
-    gx, = torch.autograd.grad(out, x, g, retain_graph=True)
+    gx, = torch.autograd.grad(out, x, g.contiguous(memory_format=fmt), retain_graph=True)
     gxr, = torch.autograd.grad(ref, x, g, retain_graph=True)
+    assert gx.is_contiguous(memory_format=fmt)
     torch.testing.assert_close(gx, gxr, rtol=1e-5, atol=1e-6)
     if skip is not None:
         gs, = torch.autograd.grad(out, skip, g, retain_graph=True)
@@ -35,11 +40,14 @@ def test_conv_input_matches_eager(elu, up, skip_ch):
         torch.testing.assert_close(gs, gsr, rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("num_layers,H,W", [(18, 64, 128), (18, 192, 640), (50, 64, 96)])
-def test_fused_decoder_matches_eager(num_layers, H, W):
+@pytest.mark.parametrize("num_layers,H,W,cl", [(18, 64, 128, False), (18, 192, 640, False), (50, 64, 96, False),
+                                               (18, 64, 128, True)])
+def test_fused_decoder_matches_eager(num_layers, H, W, cl):
     torch.manual_seed(0)
     enc = networks.ResnetEncoder(num_layers, False).cuda()
     dec = networks.DepthDecoder(enc.num_ch_enc, range(4)).cuda()
+    if cl:   # channels_last build (--channels_last): NHWC convs and fused conv inputs
+        enc, dec = enc.to(memory_format=torch.channels_last), dec.to(memory_format=torch.channels_last)
     img = torch.rand(2, 3, H, W, device="cuda")
     feats = [f.detach().requires_grad_(True) for f in enc(img)]
     dec.fused = True

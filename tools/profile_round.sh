@@ -13,7 +13,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench --outp
 echo "trace ok"
 i=0
 for p in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "TCC_HIT_sum TCC_MISS_sum"; do
-    timeout -k 10 300 rocprofv3 --pmc $p --kernel-include-regex "photo_|disp_grad|smooth_fwd|grad_T|finalize" \
+    timeout -k 10 300 rocprofv3 --pmc $p --kernel-include-regex "photo_|disp_grad|smooth_fwd|grad_T|finalize|pad_fwd|pad_bwd|pose_" \
         -d $OUT/pmc$i -o pmc --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-parity \
         > $OUT/pmc$i.log 2>&1 || exit 1
     echo "pmc pass $i ($p) ok"
