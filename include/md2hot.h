@@ -238,6 +238,38 @@ void md2_aug_plan_destroy(md2_aug_plan* plan);
 int md2_aug_run(md2_aug_plan* plan, const uint8_t* frames, const md2_aug_item* items,
                 float* const* color, float* const* color_aug, void* stream);
 
+/*
+ * Training-mode BatchNorm2d (+ residual add) (+ ReLU) on channels_last activations:
+ * relu(bn(x)) and relu(bn(x) + identity) of the ResNet encoders' blocks
+ * (torchvision BasicBlock / Bottleneck behind networks/resnet_encoder.py:62-98).
+ * x, y, residual and their gradients: (pixels = N*H*W, channels) fp32 (NHWC);
+ * channels a multiple of 4 with channels/4 dividing, or a multiple of, 256.
+ * Forward writes y, the batch mean and 1/sqrt(var + eps) (save_*), and updates the
+ * running statistics when running_mean/var are given (momentum, unbiased variance,
+ * as nn.BatchNorm2d).  workspace: md2_bn_workspace_bytes, no initialisation needed;
+ * a backward must not share its workspace with another call in flight.  Three
+ * launches each way; deterministic.
+ */
+#define MD2_BN_RELU     (1u << 0)
+#define MD2_BN_RESIDUAL (1u << 1)
+
+typedef struct md2_bn_desc {
+    int64_t pixels;
+    int32_t channels;
+    uint32_t flags;   /* MD2_BN_* */
+    float eps, momentum;
+} md2_bn_desc;
+
+size_t md2_bn_workspace_bytes(const md2_bn_desc* desc);
+int md2_bn_fwd(const md2_bn_desc* desc, const float* x, const float* gamma, const float* beta,
+               const float* residual, float* running_mean, float* running_var, float* y,
+               float* save_mean, float* save_invstd, void* workspace, void* stream);
+/* grad_residual = d(loss)/d(residual) (with MD2_BN_RESIDUAL); y is needed with MD2_BN_RELU. */
+int md2_bn_bwd(const md2_bn_desc* desc, const float* x, const float* y, const float* grad_y,
+               const float* gamma, const float* save_mean, const float* save_invstd,
+               float* grad_x, float* grad_residual, float* grad_gamma, float* grad_beta,
+               void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

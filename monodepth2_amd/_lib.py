@@ -56,7 +56,8 @@ _lib = None
 EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_select_bytes",
            "md2_photometric_fwd", "md2_photometric_bwd", "md2_generate_images",
            "md2_timing_begin", "md2_timing_end", "md2_decoder_pad_fwd", "md2_decoder_pad_bwd",
-           "md2_pose_fwd", "md2_pose_bwd", "md2_aug_plan_create", "md2_aug_plan_destroy", "md2_aug_run"]
+           "md2_pose_fwd", "md2_pose_bwd", "md2_aug_plan_create", "md2_aug_plan_destroy", "md2_aug_run",
+           "md2_bn_workspace_bytes", "md2_bn_fwd", "md2_bn_bwd"]
 
 PAD_ELU = 1 << 0
 PAD_UPSAMPLE = 1 << 1
@@ -78,6 +79,15 @@ class AugItem(ctypes.Structure):
     _fields_ = [("flip", ctypes.c_uint8), ("color_aug", ctypes.c_uint8), ("hue_shift", ctypes.c_uint8),
                 ("reserved", ctypes.c_uint8), ("order", ctypes.c_uint8 * 4), ("brightness", ctypes.c_float),
                 ("contrast", ctypes.c_float), ("saturation", ctypes.c_float)]
+
+
+BN_RELU = 1 << 0
+BN_RESIDUAL = 1 << 1
+
+
+class BnDesc(ctypes.Structure):
+    _fields_ = [("pixels", ctypes.c_int64), ("channels", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("eps", ctypes.c_float), ("momentum", ctypes.c_float)]
 
 
 def _declare(L):
@@ -111,6 +121,12 @@ def _declare(L):
     L.md2_aug_plan_destroy.argtypes = [_vp]
     L.md2_aug_run.restype = ctypes.c_int
     L.md2_aug_run.argtypes = [_vp, _vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp]
+    L.md2_bn_workspace_bytes.restype = ctypes.c_size_t
+    L.md2_bn_workspace_bytes.argtypes = [ctypes.POINTER(BnDesc)]
+    L.md2_bn_fwd.restype = ctypes.c_int
+    L.md2_bn_fwd.argtypes = [ctypes.POINTER(BnDesc)] + [_vp] * 11
+    L.md2_bn_bwd.restype = ctypes.c_int
+    L.md2_bn_bwd.argtypes = [ctypes.POINTER(BnDesc)] + [_vp] * 12
     L.md2_timing_begin.restype = ctypes.c_int
     L.md2_timing_begin.argtypes = [ctypes.c_int]
     L.md2_timing_end.restype = ctypes.c_int

@@ -1,0 +1,102 @@
+"""Fused training-mode BatchNorm2d (+ residual add) (+ ReLU) for the ResNet encoders
+(csrc/bnorm.hip, ABI `md2_bn_*`).
+
+`bn_act(bn, x, residual, relu)` computes relu(bn(x) [+ residual]) for an
+`nn.BatchNorm2d` module with its own parameters and buffers (so the torchvision
+state-dict keys of networks/resnet_encoder.py are unchanged): two HIP launches
+forward, two backward, instead of MIOpen's three-kernel BatchNorm each way plus the
+separate ReLU / add passes.  It takes the channels_last (NHWC) activations of the
+default build; other layouts, eval mode, momentum=None and the CPU run
+`nn.BatchNorm2d` itself.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+ENABLED = True   # tests flip this to compare with nn.BatchNorm2d on the same module
+
+_CL = torch.channels_last
+_workspaces: Dict[torch.device, torch.Tensor] = {}
+
+
+def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+    """Per-device scratch (partial sums + backward coefficients), reused by every
+    call on the device's stream."""
+    ws = _workspaces.get(device)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _workspaces[device] = ws
+    return ws
+
+
+def _supported(C: int) -> bool:
+    Q = C // 4
+    return C % 4 == 0 and Q > 0 and (Q % 256 == 0 if Q >= 256 else 256 % Q == 0)
+
+
+class _BNAct(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu: bool, eps: float,
+                momentum: float):
+        B, C, H, W = x.shape
+        flags = (_lib.BN_RELU if relu else 0) | (_lib.BN_RESIDUAL if residual is not None else 0)
+        d = _lib.BnDesc(B * H * W, C, flags, eps, momentum)
+        L = _lib.lib()
+        ws = _workspace(x.device, L.md2_bn_workspace_bytes(ctypes.byref(d)))
+        y = torch.empty_like(x, memory_format=_CL)
+        mean = torch.empty(C, device=x.device)
+        invstd = torch.empty(C, device=x.device)
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        rc = L.md2_bn_fwd(ctypes.byref(d), x.data_ptr(), weight.data_ptr(), bias.data_ptr(),
+                          residual.data_ptr() if residual is not None else None,
+                          running_mean.data_ptr() if running_mean is not None else None,
+                          running_var.data_ptr() if running_var is not None else None,
+                          y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ws.data_ptr(), stream)
+        _lib.check(rc, "md2_bn_fwd")
+        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        ctx.desc = (B * H * W, C, flags, eps, momentum)
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, y, weight, mean, invstd = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=_CL)
+        d = _lib.BnDesc(*ctx.desc)
+        L = _lib.lib()
+        ws = _workspace(x.device, L.md2_bn_workspace_bytes(ctypes.byref(d)))
+        gx = torch.empty_like(x, memory_format=_CL)
+        gr = torch.empty_like(x, memory_format=_CL) if ctx.has_res else None
+        gw = torch.empty_like(weight)
+        gb = torch.empty_like(weight)
+        rc = L.md2_bn_bwd(ctypes.byref(d), x.data_ptr(), y.data_ptr() if y is not None else None, gy.data_ptr(),
+                          weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gx.data_ptr(),
+                          gr.data_ptr() if gr is not None else None, gw.data_ptr(), gb.data_ptr(), ws.data_ptr(),
+                          torch.cuda.current_stream(x.device).cuda_stream)
+        _lib.check(rc, "md2_bn_bwd")
+        return gx, gw, gb, None, None, gr, None, None, None
+
+
+def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+           relu: bool = True) -> torch.Tensor:
+    """relu(bn(x) + residual) (ReLU / residual optional) for a training-mode BatchNorm2d."""
+    if (ENABLED and bn.training and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and bn.affine and bn.track_running_stats and bn.momentum is not None and _supported(x.shape[1])
+            and x.is_contiguous(memory_format=_CL) and x.shape[1] > 1
+            and (residual is None or residual.is_contiguous(memory_format=_CL))):
+        if bn.num_batches_tracked is not None:   # nn.BatchNorm2d counts training batches
+            bn.num_batches_tracked.add_(1)
+        return _BNAct.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual, relu, bn.eps,
+                            bn.momentum)
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y

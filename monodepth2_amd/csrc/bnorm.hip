@@ -1,0 +1,357 @@
+// bnorm.hip — training-mode BatchNorm2d (+ residual add) (+ ReLU) for NHWC
+// activations on gfx950.
+//
+// The ResNet encoders (networks/resnet_encoder.py -> torchvision BasicBlock /
+// Bottleneck) run relu(bn(conv(x))) and relu(bn(conv(x)) + identity) about 60 times
+// per training step (three encoders).  MIOpen's BatchNorm is three kernels each way,
+// and the ReLU / residual add are separate passes over the same activation.  Here:
+//
+//   forward   bn_stats_kernel        per-block partial Σx, Σx² (float4 along C)
+//             bn_stats_final_kernel  one block per channel: fixed-order double sums of
+//                                    the partials -> saved mean / invstd, running
+//                                    statistics (momentum, unbiased var, as nn.BatchNorm2d)
+//             bn_apply_kernel        y = relu((x - mean)·invstd·γ + β [+ r])
+//   backward  bn_bwd_reduce_kernel   g' = g·[y > 0]; partial Σg', Σg'·(x - mean)
+//             bn_bwd_final_kernel    dγ, dβ and the dx coefficients, per channel
+//             bn_bwd_apply_kernel    dx = γ·invstd·(g' - Σg'/N - x̂·Σg'x̂/N), d(residual) = g'
+//
+// Three launches each way, as MIOpen's BatchNorm, with the ReLU and the residual add
+// folded into the passes.  (A single-pass "last block finalises" variant measured
+// ~15 µs per layer on this chip: device-scope fences + ticket atomic + the finalising
+// block's reads of the partials from memory form a serial chain.)
+//
+// Layout: x, y, r, g, dx, dr (N·H·W, C) fp32 — a channels_last NCHW tensor; C a
+// multiple of 4 (every ResNet width is).  Deterministic: fixed-order reductions, no
+// atomics.
+
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "md2hot.h"
+
+int md2_report_error(int code, const char* msg);
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxBlocks = 1024;   // partial rows per channel (the finalise reads them in parallel)
+
+// thread -> (channel quad, pixel lane) mapping for C channels
+struct Map {
+    int Q;     // quads per pixel (C/4)
+    int QPT;   // quads per thread (Q > 256 only)
+    int PPB;   // pixels per block iteration
+};
+
+__host__ __device__ inline Map make_map(int C) {
+    Map m;
+    m.Q = C / 4;
+    m.QPT = m.Q > kThreads ? m.Q / kThreads : 1;
+    m.PPB = m.Q >= kThreads ? 1 : kThreads / m.Q;
+    return m;
+}
+
+// workspace layout (floats): partial[2][G][C] | coef[3][C]
+struct Work {
+    float* part;
+    float* coef;
+};
+
+__host__ __device__ __forceinline__ Work work(void* ws, int G, int C) {
+    Work w;
+    w.part = (float*)ws;
+    w.coef = w.part + 2 * (size_t)G * C;
+    return w;
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *(const float4*)p; }
+__device__ __forceinline__ void st4(float* p, float4 v) { *(float4*)p = v; }
+
+// Reduce the per-thread float4 pair over the PPB pixel lanes of the block (LDS tree)
+// into the block's partial rows.  Ends with a barrier (LDS reused by the caller).
+__device__ void block_partials(float4 a, float4 b, int q, int pl, const Map& m, int C, int G, Work w,
+                               float4 (*lds)[kThreads]) {
+    lds[0][threadIdx.x] = a;
+    lds[1][threadIdx.x] = b;
+    __syncthreads();
+    for (int half = m.PPB / 2; half > 0; half /= 2) {   // PPB is a power of 2
+        if (pl < half) {
+            const int o = threadIdx.x + half * m.Q;
+            const float4 u = lds[0][o], v = lds[1][o];
+            a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+            b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+            lds[0][threadIdx.x] = a;
+            lds[1][threadIdx.x] = b;
+        }
+        __syncthreads();
+    }
+    if (pl == 0) {
+        st4(w.part + (size_t)blockIdx.x * C + 4 * q, a);
+        st4(w.part + ((size_t)G + blockIdx.x) * C + 4 * q, b);
+    }
+    __syncthreads();
+}
+
+// Per-channel Σx and Σx² partials of this block's pixels.
+__global__ void __launch_bounds__(kThreads) bn_stats_kernel(const float* __restrict__ x, long long P, int C, int G,
+                                                            void* ws) {
+    const Map m = make_map(C);
+    const Work w = work(ws, G, C);
+    __shared__ float4 lds[2][kThreads];
+    for (int qq = 0; qq < m.QPT; ++qq) {
+        const int q = (threadIdx.x % m.Q) + qq * kThreads, pl = threadIdx.x / m.Q;
+        float4 s = {0.f, 0.f, 0.f, 0.f}, ss = {0.f, 0.f, 0.f, 0.f};
+        auto acc = [&](const float4 v) {
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            ss.x += v.x * v.x; ss.y += v.y * v.y; ss.z += v.z * v.z; ss.w += v.w * v.w;
+        };
+        const long long stride = (long long)G * m.PPB;
+        const float* xq = x + 4 * q;
+        long long p = (long long)blockIdx.x * m.PPB + pl;
+        for (; p + 3 * stride < P; p += 4 * stride) {   // four loads in flight per lane
+            const float4 v0 = ld4(xq + p * C), v1 = ld4(xq + (p + stride) * C), v2 = ld4(xq + (p + 2 * stride) * C),
+                         v3 = ld4(xq + (p + 3 * stride) * C);
+            acc(v0); acc(v1); acc(v2); acc(v3);
+        }
+        for (; p < P; p += stride) acc(ld4(xq + p * C));
+        block_partials(s, ss, q, pl, m, C, G, w, lds);
+    }
+}
+
+// One block per channel: fixed-order double sums of its G partial pairs (strided
+// over the block, then an LDS tree).  Returns the sums in thread 0.
+__device__ bool channel_sums(Work w, int G, int C, int c, double& a, double& b) {
+    __shared__ double red[2][kThreads];
+    a = 0.0;
+    b = 0.0;
+    for (int g = threadIdx.x; g < G; g += kThreads) {
+        a += w.part[(size_t)g * C + c];
+        b += w.part[((size_t)G + g) * C + c];
+    }
+    red[0][threadIdx.x] = a;
+    red[1][threadIdx.x] = b;
+    __syncthreads();
+    for (int half = kThreads / 2; half > 0; half /= 2) {
+        if (threadIdx.x < half) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + half];
+            red[1][threadIdx.x] += red[1][threadIdx.x + half];
+        }
+        __syncthreads();
+    }
+    a = red[0][0];
+    b = red[1][0];
+    return threadIdx.x == 0;
+}
+
+// mean, 1/sqrt(var + eps), running statistics (nn.BatchNorm2d: momentum, unbiased var)
+__global__ void __launch_bounds__(kThreads) bn_stats_final_kernel(long long P, int C, int G, float eps,
+                                                                  float momentum, float* __restrict__ rmean,
+                                                                  float* __restrict__ rvar,
+                                                                  float* __restrict__ smean,
+                                                                  float* __restrict__ sinvstd, void* ws) {
+    const int c = blockIdx.x;
+    double a, b;
+    if (!channel_sums(work(ws, G, C), G, C, c, a, b)) return;
+    const double mean = a / (double)P;
+    double var = b / (double)P - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    smean[c] = (float)mean;
+    sinvstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (rmean) {
+        rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+        rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * (double)P / (double)(P - 1));
+    }
+}
+
+template <bool RELU, bool RES>
+__global__ void __launch_bounds__(kThreads) bn_apply_kernel(const float* __restrict__ x, const float* __restrict__ r,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta,
+                                                            const float* __restrict__ smean,
+                                                            const float* __restrict__ sinvstd, float* __restrict__ y,
+                                                            long long n4, int Q) {
+    for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long long)gridDim.x * kThreads) {
+        const int c = 4 * (int)(i % Q);
+        const float4 v = ld4(x + 4 * i), mu = ld4(smean + c), is = ld4(sinvstd + c), ga = ld4(gamma + c),
+                     be = ld4(beta + c);
+        float4 o;
+        o.x = (v.x - mu.x) * is.x * ga.x + be.x;
+        o.y = (v.y - mu.y) * is.y * ga.y + be.y;
+        o.z = (v.z - mu.z) * is.z * ga.z + be.z;
+        o.w = (v.w - mu.w) * is.w * ga.w + be.w;
+        if (RES) {
+            const float4 rv = ld4(r + 4 * i);
+            o.x += rv.x; o.y += rv.y; o.z += rv.z; o.w += rv.w;
+        }
+        if (RELU) {
+            o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+        }
+        st4(y + 4 * i, o);
+    }
+}
+
+template <bool RELU>
+__global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ y,
+                                                                 const float* __restrict__ g, long long P, int C,
+                                                                 int G, const float* __restrict__ smean, void* ws) {
+    const Map m = make_map(C);
+    const Work w = work(ws, G, C);
+    __shared__ float4 lds[2][kThreads];
+    for (int qq = 0; qq < m.QPT; ++qq) {
+        const int q = (threadIdx.x % m.Q) + qq * kThreads, pl = threadIdx.x / m.Q;
+        const float4 mu = ld4(smean + 4 * q);
+        float4 s = {0.f, 0.f, 0.f, 0.f}, sx = {0.f, 0.f, 0.f, 0.f};
+        auto acc = [&](float4 gv, const float4 yv, const float4 v) {
+            if (RELU) {
+                gv.x = yv.x > 0.f ? gv.x : 0.f; gv.y = yv.y > 0.f ? gv.y : 0.f;
+                gv.z = yv.z > 0.f ? gv.z : 0.f; gv.w = yv.w > 0.f ? gv.w : 0.f;
+            }
+            s.x += gv.x; s.y += gv.y; s.z += gv.z; s.w += gv.w;
+            sx.x += gv.x * (v.x - mu.x); sx.y += gv.y * (v.y - mu.y);
+            sx.z += gv.z * (v.z - mu.z); sx.w += gv.w * (v.w - mu.w);
+        };
+        const long long stride = (long long)G * m.PPB;
+        const float4 zero = {0.f, 0.f, 0.f, 0.f};
+        long long p = (long long)blockIdx.x * m.PPB + pl;
+        for (; p + stride < P; p += 2 * stride) {   // two pixels (up to six loads) in flight per lane
+            const size_t o0 = p * C + 4 * q, o1 = (p + stride) * C + 4 * q;
+            const float4 g0 = ld4(g + o0), g1 = ld4(g + o1);
+            const float4 y0 = RELU ? ld4(y + o0) : zero, y1 = RELU ? ld4(y + o1) : zero;
+            const float4 v0 = ld4(x + o0), v1 = ld4(x + o1);
+            acc(g0, y0, v0);
+            acc(g1, y1, v1);
+        }
+        for (; p < P; p += stride) {
+            const size_t o = p * C + 4 * q;
+            acc(ld4(g + o), RELU ? ld4(y + o) : zero, ld4(x + o));
+        }
+        block_partials(s, sx, q, pl, m, C, G, w, lds);
+    }
+}
+
+// dγ = Σg'x̂, dβ = Σg' and the dx coefficients, one block per channel
+__global__ void __launch_bounds__(kThreads) bn_bwd_final_kernel(long long P, int C, int G,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ sinvstd,
+                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                                void* ws) {
+    const int c = blockIdx.x;
+    const Work w = work(ws, G, C);
+    double a, b;
+    if (!channel_sums(w, G, C, c, a, b)) return;
+    const double is = sinvstd[c];
+    const double dg = b * is;   // Σ g'·x̂
+    dgamma[c] = (float)dg;
+    dbeta[c] = (float)a;
+    w.coef[c] = (float)((double)gamma[c] * is);          // γ·invstd
+    w.coef[C + c] = (float)(a / (double)P);              // Σg'/N
+    w.coef[2 * C + c] = (float)(dg * is / (double)P);    // Σg'x̂/N · invstd
+}
+
+template <bool RELU, bool RES>
+__global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const float* __restrict__ x,
+                                                                const float* __restrict__ y,
+                                                                const float* __restrict__ g,
+                                                                const float* __restrict__ smean, const float* coef,
+                                                                float* __restrict__ dx, float* __restrict__ dr,
+                                                                long long n4, int Q, int C) {
+    for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long long)gridDim.x * kThreads) {
+        const int c = 4 * (int)(i % Q);
+        float4 gv = ld4(g + 4 * i);
+        if (RELU) {
+            const float4 yv = ld4(y + 4 * i);
+            gv.x = yv.x > 0.f ? gv.x : 0.f; gv.y = yv.y > 0.f ? gv.y : 0.f;
+            gv.z = yv.z > 0.f ? gv.z : 0.f; gv.w = yv.w > 0.f ? gv.w : 0.f;
+        }
+        const float4 v = ld4(x + 4 * i), mu = ld4(smean + c), k1 = ld4(coef + c), k2 = ld4(coef + C + c),
+                     k3 = ld4(coef + 2 * C + c);
+        float4 o;
+        o.x = k1.x * (gv.x - k2.x - (v.x - mu.x) * k3.x);
+        o.y = k1.y * (gv.y - k2.y - (v.y - mu.y) * k3.y);
+        o.z = k1.z * (gv.z - k2.z - (v.z - mu.z) * k3.z);
+        o.w = k1.w * (gv.w - k2.w - (v.w - mu.w) * k3.w);
+        st4(dx + 4 * i, o);
+        if (RES) st4(dr + 4 * i, gv);
+    }
+}
+
+int blocks_for_stats(long long P, int C) {
+    const Map m = make_map(C);
+    const long long rows = (P + m.PPB - 1) / m.PPB;
+    const long long g = (rows + 7) / 8;   // about 8 pixel steps per lane
+    return (int)(g < 1 ? 1 : (g > kMaxBlocks ? kMaxBlocks : g));
+}
+
+int grid_elem(long long n4) {
+    const long long g = (n4 + kThreads - 1) / kThreads;
+    return (int)(g < 4096 ? g : 4096);
+}
+
+bool valid(const md2_bn_desc* d) {
+    if (!d || d->pixels < 2 || d->channels < 4 || d->channels % 4) return false;
+    const int Q = d->channels / 4;
+    return Q >= kThreads ? (Q % kThreads == 0) : (kThreads % Q == 0);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t md2_bn_workspace_bytes(const md2_bn_desc* d) {
+    if (!valid(d)) return 0;
+    const int G = blocks_for_stats(d->pixels, d->channels);
+    return (2 * (size_t)G * d->channels + 3 * (size_t)d->channels) * sizeof(float);
+}
+
+int md2_bn_fwd(const md2_bn_desc* d, const float* x, const float* gamma, const float* beta, const float* residual,
+               float* running_mean, float* running_var, float* y, float* save_mean, float* save_invstd,
+               void* workspace, void* stream) {
+    if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "bn: need pixels >= 2 and channels a multiple of 4 "
+                                                        "with channels/4 dividing (or a multiple of) 256");
+    if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !workspace ||
+        ((d->flags & MD2_BN_RESIDUAL) && !residual) || (!running_mean != !running_var))
+        return md2_report_error(MD2_ERR_ARG, "bn_fwd: NULL operand");
+    const long long P = d->pixels;
+    const int C = d->channels, G = blocks_for_stats(P, C);
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(G), dim3(kThreads), 0, st, x, P, C, G, workspace);
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, d->eps, d->momentum,
+                       running_mean, running_var, save_mean, save_invstd, workspace);
+    const long long n4 = P * C / 4;
+    const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
+    auto k = relu ? (res ? bn_apply_kernel<true, true> : bn_apply_kernel<true, false>)
+                  : (res ? bn_apply_kernel<false, true> : bn_apply_kernel<false, false>);
+    hipLaunchKernelGGL(k, dim3(grid_elem(n4)), dim3(kThreads), 0, st, x, residual, gamma, beta, save_mean,
+                       save_invstd, y, n4, C / 4);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
+int md2_bn_bwd(const md2_bn_desc* d, const float* x, const float* y, const float* grad_y, const float* gamma,
+               const float* save_mean, const float* save_invstd, float* grad_x, float* grad_residual,
+               float* grad_gamma, float* grad_beta, void* workspace, void* stream) {
+    if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "bn: unsupported shape");
+    const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
+    if (!x || !grad_y || !gamma || !save_mean || !save_invstd || !grad_x || !grad_gamma || !grad_beta ||
+        !workspace || (relu && !y) || (res && !grad_residual))
+        return md2_report_error(MD2_ERR_ARG, "bn_bwd: NULL operand");
+    const long long P = d->pixels;
+    const int C = d->channels, G = blocks_for_stats(P, C);
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(relu ? bn_bwd_reduce_kernel<true> : bn_bwd_reduce_kernel<false>, dim3(G), dim3(kThreads), 0,
+                       st, x, y, grad_y, P, C, G, save_mean, workspace);
+    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, gamma, save_invstd, grad_gamma,
+                       grad_beta, workspace);
+    const long long n4 = P * C / 4;
+    const float* coef = work(workspace, G, C).coef;
+    auto k = relu ? (res ? bn_bwd_apply_kernel<true, true> : bn_bwd_apply_kernel<true, false>)
+                  : (res ? bn_bwd_apply_kernel<false, true> : bn_bwd_apply_kernel<false, false>);
+    hipLaunchKernelGGL(k, dim3(grid_elem(n4)), dim3(kThreads), 0, st, x, y, grad_y, save_mean, coef, grad_x,
+                       grad_residual, n4, C / 4, C);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
+}  // extern "C"

@@ -19,6 +19,8 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from ..bn_ops import bn_act
+
 
 def _conv3x3(cin, cout, stride=1):
     return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
@@ -42,10 +44,15 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + identity)
+        # relu(bn(conv)) and relu(bn(conv) + identity), fused on the GPU (bn_ops)
+        identity = x if self.downsample is None else _downsample(self.downsample, x)
+        out = bn_act(self.bn1, self.conv1(x))
+        return bn_act(self.bn2, self.conv2(out), residual=identity)
+
+
+def _downsample(down: nn.Sequential, x):
+    """The (conv1x1, BatchNorm2d) shortcut: BN without ReLU."""
+    return bn_act(down[1], down[0](x), relu=False)
 
 
 class Bottleneck(nn.Module):
@@ -64,11 +71,10 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        return self.relu(out + identity)
+        identity = x if self.downsample is None else _downsample(self.downsample, x)
+        out = bn_act(self.bn1, self.conv1(x))
+        out = bn_act(self.bn2, self.conv2(out))
+        return bn_act(self.bn3, self.conv3(out), residual=identity)
 
 
 _SPECS = {18: (BasicBlock, [2, 2, 2, 2]), 34: (BasicBlock, [3, 4, 6, 3]), 50: (Bottleneck, [3, 4, 6, 3]),
@@ -132,7 +138,7 @@ class ResnetEncoder(nn.Module):
         x = (input_image - 0.45) / 0.225
         if e.conv1.weight.is_contiguous(memory_format=torch.channels_last):
             x = x.contiguous(memory_format=torch.channels_last)
-        f0 = e.relu(e.bn1(e.conv1(x)))
+        f0 = bn_act(e.bn1, e.conv1(x))
         f1 = e.layer1(e.maxpool(f0))
         f2 = e.layer2(f1)
         f3 = e.layer3(f2)
