@@ -158,6 +158,98 @@ __global__ __launch_bounds__(kThreads) void pad_bwd_kernel(PadArgs a) {
     }
 }
 
+// NHWC with C and Cs multiples of 4 (every decoder width): the same passes on float4
+// channel quads (a quad never straddles the x / skip boundary).
+__device__ __forceinline__ float4 ld4(const float* p) { return *(const float4*)p; }
+__device__ __forceinline__ void st4(float* p, float4 v) { *(float4*)p = v; }
+__device__ __forceinline__ float4 add4(float4 a, float4 b) { return {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
+
+template <bool ELU, bool UP>
+__global__ __launch_bounds__(kThreads) void pad_fwd_v4_kernel(PadArgs a) {
+    const int Hp = a.H + 2, Wp = a.W + 2, Ct4 = (a.C + a.Cs) / 4;
+    const long long total = (long long)a.B * Hp * Wp * Ct4;
+    for (long long idx = (long long)blockIdx.x * kThreads + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * kThreads) {
+        const int c = 4 * (int)(idx % Ct4);
+        long long t = idx / Ct4;
+        const int px = (int)(t % Wp);
+        t /= Wp;
+        const int py = (int)(t % Hp);
+        const int b = (int)(t / Hp);
+        const int yy = reflect1(py - 1, a.H), xx = reflect1(px - 1, a.W);
+        float4 v;
+        if (c < a.C) {
+            const int sy = UP ? (yy >> 1) : yy, sx = UP ? (xx >> 1) : xx;
+            v = ld4(a.x + (((size_t)b * a.h + sy) * a.w + sx) * a.C + c);
+            if (ELU) v = {elu(v.x), elu(v.y), elu(v.z), elu(v.w)};
+        } else {
+            v = ld4(a.skip + (((size_t)b * a.H + yy) * a.W + xx) * a.Cs + (c - a.C));
+        }
+        st4(a.out + 4 * idx, v);
+    }
+}
+
+// fold() on quads: g points at (b, 0, 0, c) of the NHWC padded gradient
+__device__ __forceinline__ float4 fold4(const float* g, int Wp, int H, int W, int yy, int xx, int Ct) {
+    auto G = [&](int y, int x) { return ld4(g + ((size_t)y * Wp + x) * Ct); };
+    float4 s = G(yy + 1, xx + 1);
+    const bool ry = (yy == 1), ry2 = (yy == H - 2), rx = (xx == 1), rx2 = (xx == W - 2);
+    if (rx) s = add4(s, G(yy + 1, 0));
+    if (rx2) s = add4(s, G(yy + 1, W + 1));
+    if (ry) {
+        s = add4(s, G(0, xx + 1));
+        if (rx) s = add4(s, G(0, 0));
+        if (rx2) s = add4(s, G(0, W + 1));
+    }
+    if (ry2) {
+        s = add4(s, G(H + 1, xx + 1));
+        if (rx) s = add4(s, G(H + 1, 0));
+        if (rx2) s = add4(s, G(H + 1, W + 1));
+    }
+    return s;
+}
+
+template <bool ELU, bool UP>
+__global__ __launch_bounds__(kThreads) void pad_bwd_v4_kernel(PadArgs a) {
+    const int Hp = a.H + 2, Wp = a.W + 2, Ct = a.C + a.Cs, C4 = a.C / 4, Cs4 = a.Cs / 4;
+    const long long nx = (long long)a.B * a.h * a.w * C4;
+    const long long ns = (long long)a.B * a.H * a.W * Cs4;
+    for (long long idx = (long long)blockIdx.x * kThreads + threadIdx.x; idx < nx + ns;
+         idx += (long long)gridDim.x * kThreads) {
+        if (idx < nx) {
+            const int c = 4 * (int)(idx % C4);
+            long long t = idx / C4;
+            const int j = (int)(t % a.w);
+            t /= a.w;
+            const int i = (int)(t % a.h);
+            const int b = (int)(t / a.h);
+            const float* g = a.gout + (size_t)b * Hp * Wp * Ct + c;
+            float4 s;
+            if (UP) {
+                s = add4(add4(fold4(g, Wp, a.H, a.W, 2 * i, 2 * j, Ct), fold4(g, Wp, a.H, a.W, 2 * i, 2 * j + 1, Ct)),
+                         add4(fold4(g, Wp, a.H, a.W, 2 * i + 1, 2 * j, Ct),
+                              fold4(g, Wp, a.H, a.W, 2 * i + 1, 2 * j + 1, Ct)));
+            } else {
+                s = fold4(g, Wp, a.H, a.W, i, j, Ct);
+            }
+            if (ELU) {
+                const float4 xv = ld4(a.x + 4 * idx);
+                s = {s.x * elu_grad(xv.x), s.y * elu_grad(xv.y), s.z * elu_grad(xv.z), s.w * elu_grad(xv.w)};
+            }
+            st4(a.gx + 4 * idx, s);
+        } else {
+            const long long k = idx - nx;
+            const int c = 4 * (int)(k % Cs4);
+            long long t = k / Cs4;
+            const int xx = (int)(t % a.W);
+            t /= a.W;
+            const int yy = (int)(t % a.H);
+            const int b = (int)(t / a.H);
+            st4(a.gskip + 4 * k, fold4(a.gout + (size_t)b * Hp * Wp * Ct + a.C + c, Wp, a.H, a.W, yy, xx, Ct));
+        }
+    }
+}
+
 using PadFn = void (*)(PadArgs);
 
 template <bool E, bool U, bool N>
@@ -186,6 +278,11 @@ int grid_for(long long n) {
     return (int)(g < 8192 ? g : 8192);   // grid-stride beyond 8192 blocks (32 per CU)
 }
 
+// float4 channel-quad kernels: NHWC with both channel counts multiples of 4
+bool vec4(const md2_pad_desc* d) {
+    return (d->flags & MD2_PAD_NHWC) && d->channels % 4 == 0 && d->skip_channels % 4 == 0;
+}
+
 bool make_args(const md2_pad_desc* d, PadArgs& a) {
     if (!d || d->batch < 1 || d->channels < 1 || d->skip_channels < 0 || d->height < 2 || d->width < 2) return false;
     const bool up = (d->flags & MD2_PAD_UPSAMPLE) != 0;
@@ -210,6 +307,13 @@ int md2_decoder_pad_fwd(const md2_pad_desc* d, const float* x, const float* skip
     a.skip = skip;
     a.out = out;
     const long long n = (long long)a.B * (a.C + a.Cs) * (a.H + 2) * (a.W + 2);
+    if (vec4(d)) {
+        const bool elu = d->flags & MD2_PAD_ELU, up = d->flags & MD2_PAD_UPSAMPLE;
+        PadFn k = elu ? (up ? pad_fwd_v4_kernel<true, true> : pad_fwd_v4_kernel<true, false>)
+                      : (up ? pad_fwd_v4_kernel<false, true> : pad_fwd_v4_kernel<false, false>);
+        hipLaunchKernelGGL(k, dim3(grid_for(n / 4)), dim3(kThreads), 0, (hipStream_t)stream, a);
+        return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
+    }
     hipLaunchKernelGGL(fwd_kernel(d->flags), dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
 }
@@ -224,8 +328,13 @@ int md2_decoder_pad_bwd(const md2_pad_desc* d, const float* x, const float* grad
     a.gout = grad_out;
     a.gx = grad_x;
     a.gskip = grad_skip;
-    (void)up;
     const long long n = (long long)a.B * a.C * a.h * a.w + (long long)a.B * a.Cs * a.H * a.W;
+    if (vec4(d)) {
+        PadFn k = elu ? (up ? pad_bwd_v4_kernel<true, true> : pad_bwd_v4_kernel<true, false>)
+                      : (up ? pad_bwd_v4_kernel<false, true> : pad_bwd_v4_kernel<false, false>);
+        hipLaunchKernelGGL(k, dim3(grid_for(n / 4)), dim3(kThreads), 0, (hipStream_t)stream, a);
+        return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
+    }
     hipLaunchKernelGGL(bwd_kernel(d->flags), dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
 }

@@ -10,13 +10,13 @@ from monodepth2_amd.decoder_ops import conv_input
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("nhwc", [False, True])
+@pytest.mark.parametrize("nhwc,C", [(False, 8), (True, 8), (True, 6)])   # NHWC C=8: float4 kernels, C=6: scalar
 @pytest.mark.parametrize("elu,up,skip_ch", [(False, False, 0), (True, True, 0), (True, True, 64),
                                             (True, False, 0), (False, True, 32)])
-def test_conv_input_matches_eager(elu, up, skip_ch, nhwc):
+def test_conv_input_matches_eager(elu, up, skip_ch, nhwc, C):
     torch.manual_seed(0)
     fmt = torch.channels_last if nhwc else torch.contiguous_format
-    x = torch.randn(3, 8, 6, 10, device="cuda").contiguous(memory_format=fmt).requires_grad_(True)
+    x = torch.randn(3, C, 6, 10, device="cuda").contiguous(memory_format=fmt).requires_grad_(True)
     H, W = (12, 20) if up else (6, 10)
     skip = (torch.randn(3, skip_ch, H, W, device="cuda").contiguous(memory_format=fmt).requires_grad_(True)
             if skip_ch else None)
