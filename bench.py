@@ -90,6 +90,8 @@ def parse():
     ap.add_argument("--channels-last", type=int, default=1, help="NHWC convolutions (1/0)")
     ap.add_argument("--graph", type=int, default=0, help="capture the whole step in a hipGraph (1/0)")
     ap.add_argument("--miopen-find", type=str, default="fast", help="MIOPEN_FIND_MODE (fast|normal|...)")
+    ap.add_argument("--amp", type=str, default="none", choices=["none", "bf16"],
+                    help="bf16 autocast for the networks (config C5); the photometric loss stays fp32")
     ap.add_argument("--gpu-augment", type=int, default=0,
                     help="1: every step also runs the input pipeline (flip + LANCZOS pyramid + jitter, "
                          "md2_aug_run) from resident 375x1242 uint8 frames")
@@ -102,7 +104,7 @@ def make_trainer(args, device, rank, world):
     opt = default_options(batch_size=args.batch, height=args.height, width=args.width,
                           num_layers=args.num_layers, weights_init="scratch", use_stereo=args.stereo,
                           frame_ids=[0, -1, 1], log_dir="/tmp/md2_bench",
-                          channels_last=bool(args.channels_last), hip_graph=bool(args.graph))
+                          channels_last=bool(args.channels_last), hip_graph=bool(args.graph), amp=args.amp)
     return Trainer(opt, device=device, rank=rank, world_size=world)
 
 
@@ -316,7 +318,8 @@ def main():
         value = world * B * args.steps / dt
         line = {"metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": "f32" if args.amp == "none" else "bf16 networks (autocast) + f32 photometric loss",
                 "data": "synthetic (KITTI-shaped smooth textures, random-init weights)",
                 "config": {"workload": f"{'mono+stereo' if args.stereo else 'mono'}_{W}x{H} ResNet-{args.num_layers}"
                                        f" batch={B}/GPU full train step (configs[1])"

@@ -65,7 +65,8 @@ class DepthDecoder(nn.Module):
         return self.outputs
 
     def forward(self, input_features):
-        if input_features[-1].is_cuda and self.fused and self.num_output_channels >= 1:
+        if (input_features[-1].is_cuda and self.fused and self.num_output_channels >= 1
+                and input_features[-1].dtype == torch.float32):   # bf16 autocast: eager chain
             return self._forward_fused(input_features)
         self.outputs = {}
         x = input_features[-1]

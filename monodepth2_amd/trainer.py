@@ -47,6 +47,15 @@ def _sec_to_hm_str(t):
     return "{:02d}h{:02d}m{:02d}s".format(t, m, s)
 
 
+def _to_fp32(outputs):
+    """Network outputs (nested dicts of tensors) as fp32 (--amp bf16)."""
+    if isinstance(outputs, dict):
+        return {k: _to_fp32(v) for k, v in outputs.items()}
+    if torch.is_tensor(outputs) and outputs.is_floating_point() and outputs.dtype != torch.float32:
+        return outputs.float()
+    return outputs
+
+
 class _Networks(nn.Module):
     """All trainable networks behind one module so DDP sees a single graph."""
 
@@ -164,7 +173,17 @@ class Trainer:
 
     # ------------------------------------------------------------- networks
     def _run_networks(self, models, inputs):
-        """Encoder, depth decoder and pose networks (trainer.py:234-255)."""
+        """Encoder, depth decoder and pose networks (trainer.py:234-255).  With
+        --amp bf16 they run under bf16 autocast and their outputs are cast back to
+        fp32 for the (fp32) photometric loss."""
+        amp = getattr(self.opt, "amp", "none") == "bf16"
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp and self.device.type == "cuda"):
+            outputs = self._networks_body(models, inputs)
+        if amp:
+            outputs = _to_fp32(outputs)
+        return outputs
+
+    def _networks_body(self, models, inputs):
         if self.opt.pose_model_type == "shared":
             all_color_aug = torch.cat([inputs[("color_aug", i, 0)] for i in self.opt.frame_ids])
             all_features = models["encoder"](all_color_aug)
@@ -225,7 +244,7 @@ class Trainer:
                     invs.append(False)
                     fids.append(f_i)
         if fids:
-            T = poses_to_transforms(torch.stack(aas), torch.stack(trs), invs)
+            T = poses_to_transforms(torch.stack(aas).float(), torch.stack(trs).float(), invs)
             for i, f_i in enumerate(fids):
                 outputs[("cam_T_cam", 0, f_i)] = T[i]
         return outputs

@@ -28,6 +28,7 @@ CONFIGS = {
     "pose_all": {"pose_model_input": "all"},
     "resnet50": {"num_layers": 50},
     "mono_nchw": {"channels_last": 0},
+    "amp_bf16": {"amp": "bf16"},
 }
 
 
@@ -58,7 +59,7 @@ def test_train_step_runs_and_updates(name):
 
 
 @pytest.mark.parametrize("name", ["mono", "stereo", "no_ssim", "avg_reprojection", "no_automask",
-                                  "predictive_mask", "v1_multiscale", "posecnn", "mono_nchw"])
+                                  "predictive_mask", "v1_multiscale", "posecnn", "mono_nchw", "amp_bf16"])
 def test_losses_match_oracle_on_same_outputs(name):
     """compute_losses (fused HIP) vs the oracle on identical network outputs + noise."""
     from oracle.md2_oracle import HotPathOptions, hot_path
