@@ -163,6 +163,7 @@ int md2_timing_end(double* fwd_ms, int* n_fwd, double* bwd_ms, int* n_bwd);
 #define MD2_PAD_ELU      (1u << 0)
 #define MD2_PAD_UPSAMPLE (1u << 1)
 #define MD2_PAD_NHWC     (1u << 2)   /* x, skip, out (and their grads) channels_last */
+#define MD2_PAD_BF16     (1u << 3)   /* bf16 tensors (needs NHWC, channels multiples of 4) */
 
 typedef struct md2_pad_desc {
     int32_t batch, channels, height, width; /* of x */
@@ -242,7 +243,8 @@ int md2_aug_run(md2_aug_plan* plan, const uint8_t* frames, const md2_aug_item* i
  * Training-mode BatchNorm2d (+ residual add) (+ ReLU) on channels_last activations:
  * relu(bn(x)) and relu(bn(x) + identity) of the ResNet encoders' blocks
  * (torchvision BasicBlock / Bottleneck behind networks/resnet_encoder.py:62-98).
- * x, y, residual and their gradients: (pixels = N*H*W, channels) fp32 (NHWC);
+ * x, y, residual and their gradients: (pixels = N*H*W, channels) fp32, or bf16 with
+ * MD2_BN_BF16 (NHWC; fp32 arithmetic and statistics);
  * channels a multiple of 4 with channels/4 dividing, or a multiple of, 256.
  * Forward writes y, the batch mean and 1/sqrt(var + eps) (save_*), and updates the
  * running statistics when running_mean/var are given (momentum, unbiased variance,
@@ -252,6 +254,7 @@ int md2_aug_run(md2_aug_plan* plan, const uint8_t* frames, const md2_aug_item* i
  */
 #define MD2_BN_RELU     (1u << 0)
 #define MD2_BN_RESIDUAL (1u << 1)
+#define MD2_BN_BF16     (1u << 2)   /* x, residual, y and their gradients are bf16 (params, stats fp32) */
 
 typedef struct md2_bn_desc {
     int64_t pixels;
@@ -261,13 +264,13 @@ typedef struct md2_bn_desc {
 } md2_bn_desc;
 
 size_t md2_bn_workspace_bytes(const md2_bn_desc* desc);
-int md2_bn_fwd(const md2_bn_desc* desc, const float* x, const float* gamma, const float* beta,
-               const float* residual, float* running_mean, float* running_var, float* y,
+int md2_bn_fwd(const md2_bn_desc* desc, const void* x, const float* gamma, const float* beta,
+               const void* residual, float* running_mean, float* running_var, void* y,
                float* save_mean, float* save_invstd, void* workspace, void* stream);
 /* grad_residual = d(loss)/d(residual) (with MD2_BN_RESIDUAL); y is needed with MD2_BN_RELU. */
-int md2_bn_bwd(const md2_bn_desc* desc, const float* x, const float* y, const float* grad_y,
+int md2_bn_bwd(const md2_bn_desc* desc, const void* x, const void* y, const void* grad_y,
                const float* gamma, const float* save_mean, const float* save_invstd,
-               float* grad_x, float* grad_residual, float* grad_gamma, float* grad_beta,
+               void* grad_x, void* grad_residual, float* grad_gamma, float* grad_beta,
                void* workspace, void* stream);
 
 #ifdef __cplusplus

@@ -62,6 +62,7 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
 PAD_ELU = 1 << 0
 PAD_UPSAMPLE = 1 << 1
 PAD_NHWC = 1 << 2
+PAD_BF16 = 1 << 3
 
 
 class PadDesc(ctypes.Structure):
@@ -83,6 +84,7 @@ class AugItem(ctypes.Structure):
 
 BN_RELU = 1 << 0
 BN_RESIDUAL = 1 << 1
+BN_BF16 = 1 << 2
 
 
 class BnDesc(ctypes.Structure):

@@ -6,7 +6,8 @@
 state-dict keys of networks/resnet_encoder.py are unchanged): two HIP launches
 forward, two backward, instead of MIOpen's three-kernel BatchNorm each way plus the
 separate ReLU / add passes.  It takes the channels_last (NHWC) activations of the
-default build; other layouts, eval mode, momentum=None and the CPU run
+default build, fp32 or bf16 (--amp bf16: bf16 storage, fp32 arithmetic and
+statistics); other layouts, eval mode, momentum=None and the CPU run
 `nn.BatchNorm2d` itself.
 """
 from __future__ import annotations
@@ -47,7 +48,8 @@ class _BNAct(torch.autograd.Function):
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu: bool, eps: float,
                 momentum: float):
         B, C, H, W = x.shape
-        flags = (_lib.BN_RELU if relu else 0) | (_lib.BN_RESIDUAL if residual is not None else 0)
+        flags = ((_lib.BN_RELU if relu else 0) | (_lib.BN_RESIDUAL if residual is not None else 0)
+                 | (_lib.BN_BF16 if x.dtype == torch.bfloat16 else 0))
         d = _lib.BnDesc(B * H * W, C, flags, eps, momentum)
         L = _lib.lib()
         ws = _workspace(x.device, L.md2_bn_workspace_bytes(ctypes.byref(d)))
@@ -69,7 +71,7 @@ class _BNAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, y, weight, mean, invstd = ctx.saved_tensors
-        gy = gy.contiguous(memory_format=_CL)
+        gy = gy.to(x.dtype).contiguous(memory_format=_CL)
         d = _lib.BnDesc(*ctx.desc)
         L = _lib.lib()
         ws = _workspace(x.device, L.md2_bn_workspace_bytes(ctypes.byref(d)))
@@ -88,10 +90,12 @@ class _BNAct(torch.autograd.Function):
 def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
            relu: bool = True) -> torch.Tensor:
     """relu(bn(x) + residual) (ReLU / residual optional) for a training-mode BatchNorm2d."""
-    if (ENABLED and bn.training and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+    if (ENABLED and bn.training and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.dim() == 4
             and bn.affine and bn.track_running_stats and bn.momentum is not None and _supported(x.shape[1])
             and x.is_contiguous(memory_format=_CL) and x.shape[1] > 1
             and (residual is None or residual.is_contiguous(memory_format=_CL))):
+        if residual is not None and residual.dtype != x.dtype:
+            residual = residual.to(x.dtype)
         if bn.num_batches_tracked is not None:   # nn.BatchNorm2d counts training batches
             bn.num_batches_tracked.add_(1)
         return _BNAct.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual, relu, bn.eps,

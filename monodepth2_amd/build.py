@@ -31,7 +31,8 @@ def needs_build() -> bool:
     if not os.path.exists(LIB_PATH):
         return True
     t = os.path.getmtime(LIB_PATH)
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(INCLUDE, "md2hot.h")]
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(INCLUDE, "md2hot.h"),
+                                                       os.path.join(CSRC, "md2_bf16.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 

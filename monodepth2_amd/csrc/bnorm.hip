@@ -28,6 +28,7 @@
 
 #include <stdint.h>
 
+#include "md2_bf16.h"
 #include "md2hot.h"
 
 int md2_report_error(int code, const char* msg);
@@ -68,6 +69,12 @@ __host__ __device__ __forceinline__ Work work(void* ws, int G, int C) {
 __device__ __forceinline__ float4 ld4(const float* p) { return *(const float4*)p; }
 __device__ __forceinline__ void st4(float* p, float4 v) { *(float4*)p = v; }
 
+// Activation storage (fp32 or bf16): md2_bf16.h
+template <typename T>
+__device__ __forceinline__ float4 ldT(const void* p, size_t off) { return md2::ld4T<T>(p, off); }
+template <typename T>
+__device__ __forceinline__ void stT(void* p, size_t off, float4 v) { md2::st4T<T>(p, off, v); }
+
 // Reduce the per-thread float4 pair over the PPB pixel lanes of the block (LDS tree)
 // into the block's partial rows.  Ends with a barrier (LDS reused by the caller).
 __device__ void block_partials(float4 a, float4 b, int q, int pl, const Map& m, int C, int G, Work w,
@@ -94,7 +101,8 @@ __device__ void block_partials(float4 a, float4 b, int q, int pl, const Map& m, 
 }
 
 // Per-channel Σx and Σx² partials of this block's pixels.
-__global__ void __launch_bounds__(kThreads) bn_stats_kernel(const float* __restrict__ x, long long P, int C, int G,
+template <typename T>
+__global__ void __launch_bounds__(kThreads) bn_stats_kernel(const void* __restrict__ x, long long P, int C, int G,
                                                             void* ws) {
     const Map m = make_map(C);
     const Work w = work(ws, G, C);
@@ -107,14 +115,13 @@ __global__ void __launch_bounds__(kThreads) bn_stats_kernel(const float* __restr
             ss.x += v.x * v.x; ss.y += v.y * v.y; ss.z += v.z * v.z; ss.w += v.w * v.w;
         };
         const long long stride = (long long)G * m.PPB;
-        const float* xq = x + 4 * q;
         long long p = (long long)blockIdx.x * m.PPB + pl;
         for (; p + 3 * stride < P; p += 4 * stride) {   // four loads in flight per lane
-            const float4 v0 = ld4(xq + p * C), v1 = ld4(xq + (p + stride) * C), v2 = ld4(xq + (p + 2 * stride) * C),
-                         v3 = ld4(xq + (p + 3 * stride) * C);
+            const float4 v0 = ldT<T>(x, p * C + 4 * q), v1 = ldT<T>(x, (p + stride) * C + 4 * q),
+                         v2 = ldT<T>(x, (p + 2 * stride) * C + 4 * q), v3 = ldT<T>(x, (p + 3 * stride) * C + 4 * q);
             acc(v0); acc(v1); acc(v2); acc(v3);
         }
-        for (; p < P; p += stride) acc(ld4(xq + p * C));
+        for (; p < P; p += stride) acc(ldT<T>(x, p * C + 4 * q));
         block_partials(s, ss, q, pl, m, C, G, w, lds);
     }
 }
@@ -164,16 +171,16 @@ __global__ void __launch_bounds__(kThreads) bn_stats_final_kernel(long long P, i
     }
 }
 
-template <bool RELU, bool RES>
-__global__ void __launch_bounds__(kThreads) bn_apply_kernel(const float* __restrict__ x, const float* __restrict__ r,
+template <typename T, bool RELU, bool RES>
+__global__ void __launch_bounds__(kThreads) bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ r,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta,
                                                             const float* __restrict__ smean,
-                                                            const float* __restrict__ sinvstd, float* __restrict__ y,
+                                                            const float* __restrict__ sinvstd, void* __restrict__ y,
                                                             long long n4, int Q) {
     for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long long)gridDim.x * kThreads) {
         const int c = 4 * (int)(i % Q);
-        const float4 v = ld4(x + 4 * i), mu = ld4(smean + c), is = ld4(sinvstd + c), ga = ld4(gamma + c),
+        const float4 v = ldT<T>(x, 4 * i), mu = ld4(smean + c), is = ld4(sinvstd + c), ga = ld4(gamma + c),
                      be = ld4(beta + c);
         float4 o;
         o.x = (v.x - mu.x) * is.x * ga.x + be.x;
@@ -181,20 +188,20 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const float* __restr
         o.z = (v.z - mu.z) * is.z * ga.z + be.z;
         o.w = (v.w - mu.w) * is.w * ga.w + be.w;
         if (RES) {
-            const float4 rv = ld4(r + 4 * i);
+            const float4 rv = ldT<T>(r, 4 * i);
             o.x += rv.x; o.y += rv.y; o.z += rv.z; o.w += rv.w;
         }
         if (RELU) {
             o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
         }
-        st4(y + 4 * i, o);
+        stT<T>(y, 4 * i, o);
     }
 }
 
-template <bool RELU>
-__global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const float* __restrict__ x,
-                                                                 const float* __restrict__ y,
-                                                                 const float* __restrict__ g, long long P, int C,
+template <typename T, bool RELU>
+__global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const void* __restrict__ x,
+                                                                 const void* __restrict__ y,
+                                                                 const void* __restrict__ g, long long P, int C,
                                                                  int G, const float* __restrict__ smean, void* ws) {
     const Map m = make_map(C);
     const Work w = work(ws, G, C);
@@ -217,15 +224,15 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const float* __
         long long p = (long long)blockIdx.x * m.PPB + pl;
         for (; p + stride < P; p += 2 * stride) {   // two pixels (up to six loads) in flight per lane
             const size_t o0 = p * C + 4 * q, o1 = (p + stride) * C + 4 * q;
-            const float4 g0 = ld4(g + o0), g1 = ld4(g + o1);
-            const float4 y0 = RELU ? ld4(y + o0) : zero, y1 = RELU ? ld4(y + o1) : zero;
-            const float4 v0 = ld4(x + o0), v1 = ld4(x + o1);
+            const float4 g0 = ldT<T>(g, o0), g1 = ldT<T>(g, o1);
+            const float4 y0 = RELU ? ldT<T>(y, o0) : zero, y1 = RELU ? ldT<T>(y, o1) : zero;
+            const float4 v0 = ldT<T>(x, o0), v1 = ldT<T>(x, o1);
             acc(g0, y0, v0);
             acc(g1, y1, v1);
         }
         for (; p < P; p += stride) {
             const size_t o = p * C + 4 * q;
-            acc(ld4(g + o), RELU ? ld4(y + o) : zero, ld4(x + o));
+            acc(ldT<T>(g, o), RELU ? ldT<T>(y, o) : zero, ldT<T>(x, o));
         }
         block_partials(s, sx, q, pl, m, C, G, w, lds);
     }
@@ -250,30 +257,30 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_final_kernel(long long P, int
     w.coef[2 * C + c] = (float)(dg * is / (double)P);    // Σg'x̂/N · invstd
 }
 
-template <bool RELU, bool RES>
-__global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const float* __restrict__ x,
-                                                                const float* __restrict__ y,
-                                                                const float* __restrict__ g,
+template <typename T, bool RELU, bool RES>
+__global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const void* __restrict__ x,
+                                                                const void* __restrict__ y,
+                                                                const void* __restrict__ g,
                                                                 const float* __restrict__ smean, const float* coef,
-                                                                float* __restrict__ dx, float* __restrict__ dr,
+                                                                void* __restrict__ dx, void* __restrict__ dr,
                                                                 long long n4, int Q, int C) {
     for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long long)gridDim.x * kThreads) {
         const int c = 4 * (int)(i % Q);
-        float4 gv = ld4(g + 4 * i);
+        float4 gv = ldT<T>(g, 4 * i);
         if (RELU) {
-            const float4 yv = ld4(y + 4 * i);
+            const float4 yv = ldT<T>(y, 4 * i);
             gv.x = yv.x > 0.f ? gv.x : 0.f; gv.y = yv.y > 0.f ? gv.y : 0.f;
             gv.z = yv.z > 0.f ? gv.z : 0.f; gv.w = yv.w > 0.f ? gv.w : 0.f;
         }
-        const float4 v = ld4(x + 4 * i), mu = ld4(smean + c), k1 = ld4(coef + c), k2 = ld4(coef + C + c),
+        const float4 v = ldT<T>(x, 4 * i), mu = ld4(smean + c), k1 = ld4(coef + c), k2 = ld4(coef + C + c),
                      k3 = ld4(coef + 2 * C + c);
         float4 o;
         o.x = k1.x * (gv.x - k2.x - (v.x - mu.x) * k3.x);
         o.y = k1.y * (gv.y - k2.y - (v.y - mu.y) * k3.y);
         o.z = k1.z * (gv.z - k2.z - (v.z - mu.z) * k3.z);
         o.w = k1.w * (gv.w - k2.w - (v.w - mu.w) * k3.w);
-        st4(dx + 4 * i, o);
-        if (RES) st4(dr + 4 * i, gv);
+        stT<T>(dx, 4 * i, o);
+        if (RES) stT<T>(dr, 4 * i, gv);
     }
 }
 
@@ -295,6 +302,42 @@ bool valid(const md2_bn_desc* d) {
     return Q >= kThreads ? (Q % kThreads == 0) : (kThreads % Q == 0);
 }
 
+template <typename T>
+void launch_fwd(const md2_bn_desc* d, const void* x, const float* gamma, const float* beta, const void* residual,
+                float* running_mean, float* running_var, void* y, float* save_mean, float* save_invstd,
+                void* workspace, hipStream_t st) {
+    const long long P = d->pixels;
+    const int C = d->channels, G = blocks_for_stats(P, C);
+    hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(G), dim3(kThreads), 0, st, x, P, C, G, workspace);
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, d->eps, d->momentum,
+                       running_mean, running_var, save_mean, save_invstd, workspace);
+    const long long n4 = P * C / 4;
+    const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
+    auto k = relu ? (res ? bn_apply_kernel<T, true, true> : bn_apply_kernel<T, true, false>)
+                  : (res ? bn_apply_kernel<T, false, true> : bn_apply_kernel<T, false, false>);
+    hipLaunchKernelGGL(k, dim3(grid_elem(n4)), dim3(kThreads), 0, st, x, residual, gamma, beta, save_mean,
+                       save_invstd, y, n4, C / 4);
+}
+
+template <typename T>
+void launch_bwd(const md2_bn_desc* d, const void* x, const void* y, const void* grad_y, const float* gamma,
+                const float* save_mean, const float* save_invstd, void* grad_x, void* grad_residual,
+                float* grad_gamma, float* grad_beta, void* workspace, hipStream_t st) {
+    const long long P = d->pixels;
+    const int C = d->channels, G = blocks_for_stats(P, C);
+    const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
+    auto red = relu ? bn_bwd_reduce_kernel<T, true> : bn_bwd_reduce_kernel<T, false>;
+    hipLaunchKernelGGL(red, dim3(G), dim3(kThreads), 0, st, x, y, grad_y, P, C, G, save_mean, workspace);
+    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, gamma, save_invstd, grad_gamma,
+                       grad_beta, workspace);
+    const long long n4 = P * C / 4;
+    const float* coef = work(workspace, G, C).coef;
+    auto k = relu ? (res ? bn_bwd_apply_kernel<T, true, true> : bn_bwd_apply_kernel<T, true, false>)
+                  : (res ? bn_bwd_apply_kernel<T, false, true> : bn_bwd_apply_kernel<T, false, false>);
+    hipLaunchKernelGGL(k, dim3(grid_elem(n4)), dim3(kThreads), 0, st, x, y, grad_y, save_mean, coef, grad_x,
+                       grad_residual, n4, C / 4, C);
+}
+
 }  // namespace
 
 extern "C" {
@@ -305,51 +348,38 @@ size_t md2_bn_workspace_bytes(const md2_bn_desc* d) {
     return (2 * (size_t)G * d->channels + 3 * (size_t)d->channels) * sizeof(float);
 }
 
-int md2_bn_fwd(const md2_bn_desc* d, const float* x, const float* gamma, const float* beta, const float* residual,
-               float* running_mean, float* running_var, float* y, float* save_mean, float* save_invstd,
+int md2_bn_fwd(const md2_bn_desc* d, const void* x, const float* gamma, const float* beta, const void* residual,
+               float* running_mean, float* running_var, void* y, float* save_mean, float* save_invstd,
                void* workspace, void* stream) {
     if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "bn: need pixels >= 2 and channels a multiple of 4 "
                                                         "with channels/4 dividing (or a multiple of) 256");
     if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !workspace ||
         ((d->flags & MD2_BN_RESIDUAL) && !residual) || (!running_mean != !running_var))
         return md2_report_error(MD2_ERR_ARG, "bn_fwd: NULL operand");
-    const long long P = d->pixels;
-    const int C = d->channels, G = blocks_for_stats(P, C);
-    hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(bn_stats_kernel, dim3(G), dim3(kThreads), 0, st, x, P, C, G, workspace);
-    hipLaunchKernelGGL(bn_stats_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, d->eps, d->momentum,
-                       running_mean, running_var, save_mean, save_invstd, workspace);
-    const long long n4 = P * C / 4;
-    const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
-    auto k = relu ? (res ? bn_apply_kernel<true, true> : bn_apply_kernel<true, false>)
-                  : (res ? bn_apply_kernel<false, true> : bn_apply_kernel<false, false>);
-    hipLaunchKernelGGL(k, dim3(grid_elem(n4)), dim3(kThreads), 0, st, x, residual, gamma, beta, save_mean,
-                       save_invstd, y, n4, C / 4);
+    if (d->flags & MD2_BN_BF16)
+        launch_fwd<uint16_t>(d, x, gamma, beta, residual, running_mean, running_var, y, save_mean, save_invstd,
+                             workspace, (hipStream_t)stream);
+    else
+        launch_fwd<float>(d, x, gamma, beta, residual, running_mean, running_var, y, save_mean, save_invstd,
+                          workspace, (hipStream_t)stream);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }
 
-int md2_bn_bwd(const md2_bn_desc* d, const float* x, const float* y, const float* grad_y, const float* gamma,
-               const float* save_mean, const float* save_invstd, float* grad_x, float* grad_residual,
+int md2_bn_bwd(const md2_bn_desc* d, const void* x, const void* y, const void* grad_y, const float* gamma,
+               const float* save_mean, const float* save_invstd, void* grad_x, void* grad_residual,
                float* grad_gamma, float* grad_beta, void* workspace, void* stream) {
     if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "bn: unsupported shape");
     const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
     if (!x || !grad_y || !gamma || !save_mean || !save_invstd || !grad_x || !grad_gamma || !grad_beta ||
         !workspace || (relu && !y) || (res && !grad_residual))
         return md2_report_error(MD2_ERR_ARG, "bn_bwd: NULL operand");
-    const long long P = d->pixels;
-    const int C = d->channels, G = blocks_for_stats(P, C);
-    hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(relu ? bn_bwd_reduce_kernel<true> : bn_bwd_reduce_kernel<false>, dim3(G), dim3(kThreads), 0,
-                       st, x, y, grad_y, P, C, G, save_mean, workspace);
-    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, gamma, save_invstd, grad_gamma,
-                       grad_beta, workspace);
-    const long long n4 = P * C / 4;
-    const float* coef = work(workspace, G, C).coef;
-    auto k = relu ? (res ? bn_bwd_apply_kernel<true, true> : bn_bwd_apply_kernel<true, false>)
-                  : (res ? bn_bwd_apply_kernel<false, true> : bn_bwd_apply_kernel<false, false>);
-    hipLaunchKernelGGL(k, dim3(grid_elem(n4)), dim3(kThreads), 0, st, x, y, grad_y, save_mean, coef, grad_x,
-                       grad_residual, n4, C / 4, C);
+    if (d->flags & MD2_BN_BF16)
+        launch_bwd<uint16_t>(d, x, y, grad_y, gamma, save_mean, save_invstd, grad_x, grad_residual, grad_gamma,
+                             grad_beta, workspace, (hipStream_t)stream);
+    else
+        launch_bwd<float>(d, x, y, grad_y, gamma, save_mean, save_invstd, grad_x, grad_residual, grad_gamma,
+                          grad_beta, workspace, (hipStream_t)stream);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }

@@ -21,6 +21,7 @@
 
 #include <stdint.h>
 
+#include "md2_bf16.h"
 #include "md2hot.h"
 
 namespace {
@@ -164,7 +165,7 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *(const float4*)p
 __device__ __forceinline__ void st4(float* p, float4 v) { *(float4*)p = v; }
 __device__ __forceinline__ float4 add4(float4 a, float4 b) { return {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
 
-template <bool ELU, bool UP>
+template <typename T, bool ELU, bool UP>
 __global__ __launch_bounds__(kThreads) void pad_fwd_v4_kernel(PadArgs a) {
     const int Hp = a.H + 2, Wp = a.W + 2, Ct4 = (a.C + a.Cs) / 4;
     const long long total = (long long)a.B * Hp * Wp * Ct4;
@@ -180,18 +181,19 @@ __global__ __launch_bounds__(kThreads) void pad_fwd_v4_kernel(PadArgs a) {
         float4 v;
         if (c < a.C) {
             const int sy = UP ? (yy >> 1) : yy, sx = UP ? (xx >> 1) : xx;
-            v = ld4(a.x + (((size_t)b * a.h + sy) * a.w + sx) * a.C + c);
+            v = md2::ld4T<T>(a.x, (((size_t)b * a.h + sy) * a.w + sx) * a.C + c);
             if (ELU) v = {elu(v.x), elu(v.y), elu(v.z), elu(v.w)};
         } else {
-            v = ld4(a.skip + (((size_t)b * a.H + yy) * a.W + xx) * a.Cs + (c - a.C));
+            v = md2::ld4T<T>(a.skip, (((size_t)b * a.H + yy) * a.W + xx) * a.Cs + (c - a.C));
         }
-        st4(a.out + 4 * idx, v);
+        md2::st4T<T>(a.out, 4 * idx, v);
     }
 }
 
-// fold() on quads: g points at (b, 0, 0, c) of the NHWC padded gradient
-__device__ __forceinline__ float4 fold4(const float* g, int Wp, int H, int W, int yy, int xx, int Ct) {
-    auto G = [&](int y, int x) { return ld4(g + ((size_t)y * Wp + x) * Ct); };
+// fold() on quads: element offset g0 = (b, 0, 0, c) of the NHWC padded gradient
+template <typename T>
+__device__ __forceinline__ float4 fold4(const float* gout, size_t g0, int Wp, int H, int W, int yy, int xx, int Ct) {
+    auto G = [&](int y, int x) { return md2::ld4T<T>(gout, g0 + ((size_t)y * Wp + x) * Ct); };
     float4 s = G(yy + 1, xx + 1);
     const bool ry = (yy == 1), ry2 = (yy == H - 2), rx = (xx == 1), rx2 = (xx == W - 2);
     if (rx) s = add4(s, G(yy + 1, 0));
@@ -209,7 +211,7 @@ __device__ __forceinline__ float4 fold4(const float* g, int Wp, int H, int W, in
     return s;
 }
 
-template <bool ELU, bool UP>
+template <typename T, bool ELU, bool UP>
 __global__ __launch_bounds__(kThreads) void pad_bwd_v4_kernel(PadArgs a) {
     const int Hp = a.H + 2, Wp = a.W + 2, Ct = a.C + a.Cs, C4 = a.C / 4, Cs4 = a.Cs / 4;
     const long long nx = (long long)a.B * a.h * a.w * C4;
@@ -223,20 +225,21 @@ __global__ __launch_bounds__(kThreads) void pad_bwd_v4_kernel(PadArgs a) {
             t /= a.w;
             const int i = (int)(t % a.h);
             const int b = (int)(t / a.h);
-            const float* g = a.gout + (size_t)b * Hp * Wp * Ct + c;
+            const size_t g = (size_t)b * Hp * Wp * Ct + c;
             float4 s;
             if (UP) {
-                s = add4(add4(fold4(g, Wp, a.H, a.W, 2 * i, 2 * j, Ct), fold4(g, Wp, a.H, a.W, 2 * i, 2 * j + 1, Ct)),
-                         add4(fold4(g, Wp, a.H, a.W, 2 * i + 1, 2 * j, Ct),
-                              fold4(g, Wp, a.H, a.W, 2 * i + 1, 2 * j + 1, Ct)));
+                s = add4(add4(fold4<T>(a.gout, g, Wp, a.H, a.W, 2 * i, 2 * j, Ct),
+                              fold4<T>(a.gout, g, Wp, a.H, a.W, 2 * i, 2 * j + 1, Ct)),
+                         add4(fold4<T>(a.gout, g, Wp, a.H, a.W, 2 * i + 1, 2 * j, Ct),
+                              fold4<T>(a.gout, g, Wp, a.H, a.W, 2 * i + 1, 2 * j + 1, Ct)));
             } else {
-                s = fold4(g, Wp, a.H, a.W, i, j, Ct);
+                s = fold4<T>(a.gout, g, Wp, a.H, a.W, i, j, Ct);
             }
             if (ELU) {
-                const float4 xv = ld4(a.x + 4 * idx);
+                const float4 xv = md2::ld4T<T>(a.x, 4 * idx);
                 s = {s.x * elu_grad(xv.x), s.y * elu_grad(xv.y), s.z * elu_grad(xv.z), s.w * elu_grad(xv.w)};
             }
-            st4(a.gx + 4 * idx, s);
+            md2::st4T<T>(a.gx, 4 * idx, s);
         } else {
             const long long k = idx - nx;
             const int c = 4 * (int)(k % Cs4);
@@ -245,7 +248,7 @@ __global__ __launch_bounds__(kThreads) void pad_bwd_v4_kernel(PadArgs a) {
             t /= a.W;
             const int yy = (int)(t % a.H);
             const int b = (int)(t / a.H);
-            st4(a.gskip + 4 * k, fold4(a.gout + (size_t)b * Hp * Wp * Ct + a.C + c, Wp, a.H, a.W, yy, xx, Ct));
+            md2::st4T<T>(a.gskip, 4 * k, fold4<T>(a.gout, (size_t)b * Hp * Wp * Ct + a.C + c, Wp, a.H, a.W, yy, xx, Ct));
         }
     }
 }
@@ -283,8 +286,20 @@ bool vec4(const md2_pad_desc* d) {
     return (d->flags & MD2_PAD_NHWC) && d->channels % 4 == 0 && d->skip_channels % 4 == 0;
 }
 
+template <typename T>
+PadFn v4_fwd(bool elu, bool up) {
+    return elu ? (up ? pad_fwd_v4_kernel<T, true, true> : pad_fwd_v4_kernel<T, true, false>)
+               : (up ? pad_fwd_v4_kernel<T, false, true> : pad_fwd_v4_kernel<T, false, false>);
+}
+template <typename T>
+PadFn v4_bwd(bool elu, bool up) {
+    return elu ? (up ? pad_bwd_v4_kernel<T, true, true> : pad_bwd_v4_kernel<T, true, false>)
+               : (up ? pad_bwd_v4_kernel<T, false, true> : pad_bwd_v4_kernel<T, false, false>);
+}
+
 bool make_args(const md2_pad_desc* d, PadArgs& a) {
     if (!d || d->batch < 1 || d->channels < 1 || d->skip_channels < 0 || d->height < 2 || d->width < 2) return false;
+    if ((d->flags & MD2_PAD_BF16) && !vec4(d)) return false;   // bf16: NHWC, channels multiples of 4
     const bool up = (d->flags & MD2_PAD_UPSAMPLE) != 0;
     a.B = d->batch;
     a.C = d->channels;
@@ -309,8 +324,7 @@ int md2_decoder_pad_fwd(const md2_pad_desc* d, const float* x, const float* skip
     const long long n = (long long)a.B * (a.C + a.Cs) * (a.H + 2) * (a.W + 2);
     if (vec4(d)) {
         const bool elu = d->flags & MD2_PAD_ELU, up = d->flags & MD2_PAD_UPSAMPLE;
-        PadFn k = elu ? (up ? pad_fwd_v4_kernel<true, true> : pad_fwd_v4_kernel<true, false>)
-                      : (up ? pad_fwd_v4_kernel<false, true> : pad_fwd_v4_kernel<false, false>);
+        PadFn k = (d->flags & MD2_PAD_BF16) ? v4_fwd<uint16_t>(elu, up) : v4_fwd<float>(elu, up);
         hipLaunchKernelGGL(k, dim3(grid_for(n / 4)), dim3(kThreads), 0, (hipStream_t)stream, a);
         return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
     }
@@ -330,8 +344,7 @@ int md2_decoder_pad_bwd(const md2_pad_desc* d, const float* x, const float* grad
     a.gskip = grad_skip;
     const long long n = (long long)a.B * a.C * a.h * a.w + (long long)a.B * a.Cs * a.H * a.W;
     if (vec4(d)) {
-        PadFn k = elu ? (up ? pad_bwd_v4_kernel<true, true> : pad_bwd_v4_kernel<true, false>)
-                      : (up ? pad_bwd_v4_kernel<false, true> : pad_bwd_v4_kernel<false, false>);
+        PadFn k = (d->flags & MD2_PAD_BF16) ? v4_bwd<uint16_t>(elu, up) : v4_bwd<float>(elu, up);
         hipLaunchKernelGGL(k, dim3(grid_for(n / 4)), dim3(kThreads), 0, (hipStream_t)stream, a);
         return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
     }

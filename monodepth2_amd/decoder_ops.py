@@ -19,8 +19,9 @@ from . import _lib
 _CL = torch.channels_last
 
 
-def _flags(elu: bool, upsample: bool, nhwc: bool) -> int:
-    return (_lib.PAD_ELU if elu else 0) | (_lib.PAD_UPSAMPLE if upsample else 0) | (_lib.PAD_NHWC if nhwc else 0)
+def _flags(elu: bool, upsample: bool, nhwc: bool, bf16: bool = False) -> int:
+    return ((_lib.PAD_ELU if elu else 0) | (_lib.PAD_UPSAMPLE if upsample else 0) | (_lib.PAD_NHWC if nhwc else 0)
+            | (_lib.PAD_BF16 if bf16 else 0))
 
 
 class _ConvInput(torch.autograd.Function):
@@ -36,12 +37,15 @@ class _ConvInput(torch.autograd.Function):
             raise ValueError(f"skip shape {tuple(skip.shape)} does not match {(B, '*', H, W)}")
         Cs = 0 if skip is None else skip.shape[1]
         out = torch.empty(B, C + Cs, H + 2, W + 2, device=x.device, dtype=x.dtype, memory_format=fmt)
-        d = _lib.PadDesc(B, C, h, w, Cs, _flags(elu, upsample, nhwc))
+        bf16 = x.dtype == torch.bfloat16
+        if skip is not None and skip.dtype != x.dtype:
+            skip = skip.to(x.dtype)
+        d = _lib.PadDesc(B, C, h, w, Cs, _flags(elu, upsample, nhwc, bf16))
         rc = _lib.lib().md2_decoder_pad_fwd(ctypes.byref(d), x.data_ptr(),
                                             skip.data_ptr() if skip is not None else None, out.data_ptr(),
                                             torch.cuda.current_stream(x.device).cuda_stream)
         _lib.check(rc, "md2_decoder_pad_fwd")
-        ctx.elu, ctx.upsample, ctx.has_skip, ctx.nhwc = elu, upsample, skip is not None, nhwc
+        ctx.elu, ctx.upsample, ctx.has_skip, ctx.nhwc, ctx.bf16 = elu, upsample, skip is not None, nhwc, bf16
         ctx.skip_shape = None if skip is None else skip.shape
         ctx.save_for_backward(x if elu else None)
         ctx.x_shape = x.shape
@@ -51,13 +55,13 @@ class _ConvInput(torch.autograd.Function):
     def backward(ctx, gout):
         (x,) = ctx.saved_tensors
         fmt = _CL if ctx.nhwc else torch.contiguous_format
-        gout = gout.contiguous(memory_format=fmt)
+        gout = gout.to(torch.bfloat16 if ctx.bf16 else torch.float32).contiguous(memory_format=fmt)
         B, C, h, w = ctx.x_shape
         gx = torch.empty(ctx.x_shape, device=gout.device, dtype=gout.dtype, memory_format=fmt)
         gskip = (torch.empty(ctx.skip_shape, device=gout.device, dtype=gout.dtype, memory_format=fmt)
                  if ctx.has_skip else None)
         d = _lib.PadDesc(B, C, h, w, 0 if gskip is None else ctx.skip_shape[1],
-                         _flags(ctx.elu, ctx.upsample, ctx.nhwc))
+                         _flags(ctx.elu, ctx.upsample, ctx.nhwc, ctx.bf16))
         rc = _lib.lib().md2_decoder_pad_bwd(ctypes.byref(d), x.data_ptr() if x is not None else None,
                                             gout.data_ptr(), gx.data_ptr(),
                                             gskip.data_ptr() if gskip is not None else None,
@@ -66,12 +70,16 @@ class _ConvInput(torch.autograd.Function):
         return gx, gskip, None, None, None
 
 
+def supports_bf16(x: torch.Tensor, skip: Optional[torch.Tensor], nhwc: bool) -> bool:
+    return nhwc and x.shape[1] % 4 == 0 and (skip is None or skip.shape[1] % 4 == 0)
+
+
 def conv_input(x: torch.Tensor, skip: Optional[torch.Tensor] = None, elu: bool = False,
                upsample: bool = False, nhwc: bool = False) -> torch.Tensor:
     """ReflectionPad2d(1)(cat([upsample?(elu?(x)), skip], 1)) in one fused pass.
     nhwc: tensors in (and out) channels_last, as the NHWC convolutions around it."""
     if x.device.type != "cuda":
         raise RuntimeError("conv_input is a HIP kernel; use the eager chain on the CPU")
-    if x.dtype != torch.float32:
-        raise ValueError("conv_input supports float32")
+    if x.dtype != torch.float32 and not (x.dtype == torch.bfloat16 and supports_bf16(x, skip, nhwc)):
+        raise ValueError("conv_input supports float32, and bfloat16 in NHWC with channel counts multiple of 4")
     return _ConvInput.apply(x, skip, elu, upsample, nhwc)

@@ -65,8 +65,10 @@ class DepthDecoder(nn.Module):
         return self.outputs
 
     def forward(self, input_features):
-        if (input_features[-1].is_cuda and self.fused and self.num_output_channels >= 1
-                and input_features[-1].dtype == torch.float32):   # bf16 autocast: eager chain
+        f = input_features[-1]
+        cl = self.convs[("upconv", 4, 0)].conv.conv.weight.is_contiguous(memory_format=torch.channels_last)
+        if (f.is_cuda and self.fused and self.num_output_channels >= 1
+                and (f.dtype == torch.float32 or (f.dtype == torch.bfloat16 and cl))):   # bf16: NHWC kernels
             return self._forward_fused(input_features)
         self.outputs = {}
         x = input_features[-1]

@@ -56,6 +56,32 @@ def test_bn_act_matches_batchnorm(C, shape, relu, res):
         assert float((a - b).abs().max()) <= 2e-4 * scale + 1e-6, name
 
 
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
+def test_bn_act_bf16_matches_batchnorm_fp32(relu, res):
+    """bf16 storage (--amp bf16): vs nn.BatchNorm2d in fp32 on the same bf16 values,
+    within bf16 rounding of the outputs / gradients."""
+    torch.manual_seed(2)
+    C, B, H, W = 128, 2, 24, 80
+    bn = nn.BatchNorm2d(C).cuda()
+    ref_bn = copy.deepcopy(bn)
+    xb = (torch.randn(B, C, H, W, device="cuda") * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=CL)
+    rb = torch.randn(B, C, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL) if res else None
+    x = xb.clone().requires_grad_(True)
+    r = rb.clone().requires_grad_(True) if res else None
+    xr = xb.float().requires_grad_(True)
+    rr = rb.float().requires_grad_(True) if res else None
+    y = bn_ops.bn_act(bn, x, r, relu)
+    yr = _eager(ref_bn, xr, rr, relu)
+    assert y.dtype == torch.bfloat16
+    torch.testing.assert_close(y.float(), yr, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(bn.running_var, ref_bn.running_var, rtol=1e-4, atol=1e-5)
+    g = torch.randn_like(yr)
+    got = torch.autograd.grad(y, [x, bn.weight, bn.bias], g.to(torch.bfloat16).contiguous(memory_format=CL))
+    ref = torch.autograd.grad(yr, [xr, ref_bn.weight, ref_bn.bias], g.to(torch.bfloat16).float())
+    for a, b in zip(got, ref):
+        assert float((a.float() - b).norm() / b.norm()) < 1e-2
+
+
 def test_bn_act_deterministic():
     torch.manual_seed(1)
     bn = nn.BatchNorm2d(64).cuda()

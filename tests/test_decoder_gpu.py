@@ -40,6 +40,26 @@ def test_conv_input_matches_eager(elu, up, skip_ch, nhwc, C):
         torch.testing.assert_close(gs, gsr, rtol=1e-6, atol=1e-6)
 
 
+def test_conv_input_bf16_matches_eager():
+    """bf16 NHWC (--amp bf16): copies are exact, ELU rounded once to bf16."""
+    torch.manual_seed(3)
+    CL = torch.channels_last
+    x = torch.randn(2, 16, 6, 10, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    skip = torch.randn(2, 32, 12, 20, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    skip.requires_grad_(True)
+    out = conv_input(x, skip, elu=True, upsample=True, nhwc=True)
+    y = torch.cat([torch.nn.functional.interpolate(torch.nn.functional.elu(x.float()), scale_factor=2,
+                                                   mode="nearest"), skip.float()], 1)
+    ref = torch.nn.functional.pad(y, (1, 1, 1, 1), mode="reflect")
+    assert out.dtype == torch.bfloat16 and out.is_contiguous(memory_format=CL)
+    assert torch.equal(out.float(), ref.to(torch.bfloat16).float())
+    g = torch.randn_like(ref).to(torch.bfloat16)
+    gx, gs = torch.autograd.grad(out, (x, skip), g.contiguous(memory_format=CL))
+    gxr, gsr = torch.autograd.grad(ref, (x, skip), g.float())
+    torch.testing.assert_close(gx.float(), gxr.float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(gs.float(), gsr.float(), rtol=1e-2, atol=1e-2)
+
+
 @pytest.mark.parametrize("num_layers,H,W,cl", [(18, 64, 128, False), (18, 192, 640, False), (50, 64, 96, False),
                                                (18, 64, 128, True)])
 def test_fused_decoder_matches_eager(num_layers, H, W, cl):
