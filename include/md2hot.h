@@ -257,10 +257,16 @@ int md2_aug_run(md2_aug_plan* plan, const uint8_t* frames, const md2_aug_item* i
 #define MD2_BN_BF16     (1u << 2)   /* x, residual, y and their gradients are bf16 (params, stats fp32) */
 
 typedef struct md2_bn_desc {
-    int64_t pixels;
+    int64_t pixels;   /* N*H*W over all groups */
     int32_t channels;
     uint32_t flags;   /* MD2_BN_* */
     float eps, momentum;
+    /* groups > 1: the N images form `groups` equal consecutive chunks, each normalised
+     * with its own batch statistics, running statistics updated chunk by chunk in
+     * order — exactly `groups` separate BatchNorm calls (the pose encoder runs both
+     * frame pairs as one batch this way).  save_mean / save_invstd: (groups, C). */
+    int32_t groups;
+    int32_t reserved;
 } md2_bn_desc;
 
 size_t md2_bn_workspace_bytes(const md2_bn_desc* desc);

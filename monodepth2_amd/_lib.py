@@ -89,7 +89,8 @@ BN_BF16 = 1 << 2
 
 class BnDesc(ctypes.Structure):
     _fields_ = [("pixels", ctypes.c_int64), ("channels", ctypes.c_int32), ("flags", ctypes.c_uint32),
-                ("eps", ctypes.c_float), ("momentum", ctypes.c_float)]
+                ("eps", ctypes.c_float), ("momentum", ctypes.c_float), ("groups", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 def _declare(L):

@@ -12,6 +12,7 @@ statistics); other layouts, eval mode, momentum=None and the CPU run
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from typing import Dict, Optional
 
@@ -22,6 +23,21 @@ import torch.nn.functional as F
 from . import _lib
 
 ENABLED = True   # tests flip this to compare with nn.BatchNorm2d on the same module
+_GROUPS = 1      # bn_groups(): the batch holds this many independently normalised chunks
+
+
+@contextlib.contextmanager
+def bn_groups(n: int):
+    """Inside, every bn_act treats its batch as n equal consecutive chunks with their
+    own batch statistics — identical to running the network on each chunk separately
+    (convolutions, pooling and activations are per-image anyway).  The trainer runs
+    the pose encoder once over both frame pairs this way."""
+    global _GROUPS
+    prev, _GROUPS = _GROUPS, int(n)
+    try:
+        yield
+    finally:
+        _GROUPS = prev
 
 _CL = torch.channels_last
 _workspaces: Dict[torch.device, torch.Tensor] = {}
@@ -46,16 +62,16 @@ class _BNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu: bool, eps: float,
-                momentum: float):
+                momentum: float, groups: int):
         B, C, H, W = x.shape
         flags = ((_lib.BN_RELU if relu else 0) | (_lib.BN_RESIDUAL if residual is not None else 0)
                  | (_lib.BN_BF16 if x.dtype == torch.bfloat16 else 0))
-        d = _lib.BnDesc(B * H * W, C, flags, eps, momentum)
+        d = _lib.BnDesc(B * H * W, C, flags, eps, momentum, groups, 0)
         L = _lib.lib()
         ws = _workspace(x.device, L.md2_bn_workspace_bytes(ctypes.byref(d)))
         y = torch.empty_like(x, memory_format=_CL)
-        mean = torch.empty(C, device=x.device)
-        invstd = torch.empty(C, device=x.device)
+        mean = torch.empty(groups, C, device=x.device)
+        invstd = torch.empty(groups, C, device=x.device)
         stream = torch.cuda.current_stream(x.device).cuda_stream
         rc = L.md2_bn_fwd(ctypes.byref(d), x.data_ptr(), weight.data_ptr(), bias.data_ptr(),
                           residual.data_ptr() if residual is not None else None,
@@ -64,7 +80,7 @@ class _BNAct(torch.autograd.Function):
                           y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ws.data_ptr(), stream)
         _lib.check(rc, "md2_bn_fwd")
         ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
-        ctx.desc = (B * H * W, C, flags, eps, momentum)
+        ctx.desc = (B * H * W, C, flags, eps, momentum, groups, 0)
         ctx.has_res = residual is not None
         return y
 
@@ -84,12 +100,16 @@ class _BNAct(torch.autograd.Function):
                           gr.data_ptr() if gr is not None else None, gw.data_ptr(), gb.data_ptr(), ws.data_ptr(),
                           torch.cuda.current_stream(x.device).cuda_stream)
         _lib.check(rc, "md2_bn_bwd")
-        return gx, gw, gb, None, None, gr, None, None, None
+        return gx, gw, gb, None, None, gr, None, None, None, None
 
 
 def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
            relu: bool = True) -> torch.Tensor:
-    """relu(bn(x) + residual) (ReLU / residual optional) for a training-mode BatchNorm2d."""
+    """relu(bn(x) + residual) (ReLU / residual optional) for a training-mode BatchNorm2d
+    (per chunk inside bn_groups)."""
+    groups = _GROUPS if bn.training else 1
+    if groups > 1 and x.shape[0] % groups:
+        raise ValueError(f"batch {x.shape[0]} does not split into {groups} BatchNorm groups")
     if (ENABLED and bn.training and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.dim() == 4
             and bn.affine and bn.track_running_stats and bn.momentum is not None and _supported(x.shape[1])
             and x.is_contiguous(memory_format=_CL) and x.shape[1] > 1
@@ -97,10 +117,10 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, residual: Optional[torch.Tensor]
         if residual is not None and residual.dtype != x.dtype:
             residual = residual.to(x.dtype)
         if bn.num_batches_tracked is not None:   # nn.BatchNorm2d counts training batches
-            bn.num_batches_tracked.add_(1)
+            bn.num_batches_tracked.add_(groups)
         return _BNAct.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual, relu, bn.eps,
-                            bn.momentum)
-    y = bn(x)
+                            bn.momentum, groups)
+    y = bn(x) if groups == 1 else torch.cat([bn(xc) for xc in x.chunk(groups)], 0)
     if residual is not None:
         y = y + residual
     return F.relu(y) if relu else y

@@ -53,16 +53,16 @@ __host__ __device__ inline Map make_map(int C) {
     return m;
 }
 
-// workspace layout (floats): partial[2][G][C] | coef[3][C]
+// workspace layout (floats): partial[2][NG*G][C] (row = group*G + block) | coef[3][NG][C]
 struct Work {
     float* part;
     float* coef;
 };
 
-__host__ __device__ __forceinline__ Work work(void* ws, int G, int C) {
+__host__ __device__ __forceinline__ Work work(void* ws, int G, int C, int NG) {
     Work w;
     w.part = (float*)ws;
-    w.coef = w.part + 2 * (size_t)G * C;
+    w.coef = w.part + 2 * (size_t)NG * G * C;
     return w;
 }
 
@@ -77,7 +77,7 @@ __device__ __forceinline__ void stT(void* p, size_t off, float4 v) { md2::st4T<T
 
 // Reduce the per-thread float4 pair over the PPB pixel lanes of the block (LDS tree)
 // into the block's partial rows.  Ends with a barrier (LDS reused by the caller).
-__device__ void block_partials(float4 a, float4 b, int q, int pl, const Map& m, int C, int G, Work w,
+__device__ void block_partials(float4 a, float4 b, int q, int pl, const Map& m, int C, int rows, int row, Work w,
                                float4 (*lds)[kThreads]) {
     lds[0][threadIdx.x] = a;
     lds[1][threadIdx.x] = b;
@@ -94,18 +94,23 @@ __device__ void block_partials(float4 a, float4 b, int q, int pl, const Map& m, 
         __syncthreads();
     }
     if (pl == 0) {
-        st4(w.part + (size_t)blockIdx.x * C + 4 * q, a);
-        st4(w.part + ((size_t)G + blockIdx.x) * C + 4 * q, b);
+        st4(w.part + (size_t)row * C + 4 * q, a);
+        st4(w.part + ((size_t)rows + row) * C + 4 * q, b);
     }
     __syncthreads();
 }
 
 // Per-channel Σx and Σx² partials of this block's pixels.
+// Grouped BatchNorm (NG > 1): the pixels are NG equal contiguous groups (batch
+// chunks), each normalised with its own statistics — what NG separate BatchNorm calls
+// on the chunks compute.  P is the pixel count of one group; blockIdx.y the group.
 template <typename T>
 __global__ void __launch_bounds__(kThreads) bn_stats_kernel(const void* __restrict__ x, long long P, int C, int G,
                                                             void* ws) {
     const Map m = make_map(C);
-    const Work w = work(ws, G, C);
+    const int NG = gridDim.y, grp = blockIdx.y;
+    const Work w = work(ws, G, C, NG);
+    x = (const char*)x + (size_t)grp * P * C * sizeof(T);
     __shared__ float4 lds[2][kThreads];
     for (int qq = 0; qq < m.QPT; ++qq) {
         const int q = (threadIdx.x % m.Q) + qq * kThreads, pl = threadIdx.x / m.Q;
@@ -122,19 +127,19 @@ __global__ void __launch_bounds__(kThreads) bn_stats_kernel(const void* __restri
             acc(v0); acc(v1); acc(v2); acc(v3);
         }
         for (; p < P; p += stride) acc(ldT<T>(x, p * C + 4 * q));
-        block_partials(s, ss, q, pl, m, C, G, w, lds);
+        block_partials(s, ss, q, pl, m, C, NG * G, grp * G + blockIdx.x, w, lds);
     }
 }
 
 // One block per channel: fixed-order double sums of its G partial pairs (strided
 // over the block, then an LDS tree).  Returns the sums in thread 0.
-__device__ bool channel_sums(Work w, int G, int C, int c, double& a, double& b) {
+__device__ bool channel_sums(Work w, int rows, int r0, int G, int C, int c, double& a, double& b) {
     __shared__ double red[2][kThreads];
     a = 0.0;
     b = 0.0;
     for (int g = threadIdx.x; g < G; g += kThreads) {
-        a += w.part[(size_t)g * C + c];
-        b += w.part[((size_t)G + g) * C + c];
+        a += w.part[(size_t)(r0 + g) * C + c];
+        b += w.part[((size_t)rows + r0 + g) * C + c];
     }
     red[0][threadIdx.x] = a;
     red[1][threadIdx.x] = b;
@@ -148,26 +153,30 @@ __device__ bool channel_sums(Work w, int G, int C, int c, double& a, double& b) 
     }
     a = red[0][0];
     b = red[1][0];
+    __syncthreads();   // red is reused by the next group
     return threadIdx.x == 0;
 }
 
 // mean, 1/sqrt(var + eps), running statistics (nn.BatchNorm2d: momentum, unbiased var)
-__global__ void __launch_bounds__(kThreads) bn_stats_final_kernel(long long P, int C, int G, float eps,
+__global__ void __launch_bounds__(kThreads) bn_stats_final_kernel(long long P, int C, int G, int NG, float eps,
                                                                   float momentum, float* __restrict__ rmean,
                                                                   float* __restrict__ rvar,
                                                                   float* __restrict__ smean,
                                                                   float* __restrict__ sinvstd, void* ws) {
     const int c = blockIdx.x;
-    double a, b;
-    if (!channel_sums(work(ws, G, C), G, C, c, a, b)) return;
-    const double mean = a / (double)P;
-    double var = b / (double)P - mean * mean;
-    var = var > 0.0 ? var : 0.0;
-    smean[c] = (float)mean;
-    sinvstd[c] = (float)(1.0 / sqrt(var + (double)eps));
-    if (rmean) {
-        rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
-        rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * (double)P / (double)(P - 1));
+    const Work w = work(ws, G, C, NG);
+    for (int grp = 0; grp < NG; ++grp) {   // groups in order: the running statistics update as NG calls
+        double a, b;
+        if (!channel_sums(w, NG * G, grp * G, G, C, c, a, b)) continue;
+        const double mean = a / (double)P;
+        double var = b / (double)P - mean * mean;
+        var = var > 0.0 ? var : 0.0;
+        smean[grp * C + c] = (float)mean;
+        sinvstd[grp * C + c] = (float)(1.0 / sqrt(var + (double)eps));
+        if (rmean) {
+            rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+            rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * (double)P / (double)(P - 1));
+        }
     }
 }
 
@@ -177,10 +186,11 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const void* __restri
                                                             const float* __restrict__ beta,
                                                             const float* __restrict__ smean,
                                                             const float* __restrict__ sinvstd, void* __restrict__ y,
-                                                            long long n4, int Q) {
+                                                            long long n4, int Q, long long q4g) {
     for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long long)gridDim.x * kThreads) {
         const int c = 4 * (int)(i % Q);
-        const float4 v = ldT<T>(x, 4 * i), mu = ld4(smean + c), is = ld4(sinvstd + c), ga = ld4(gamma + c),
+        const int cs = c + (q4g ? 4 * Q * (int)(i / q4g) : 0);   // statistics of this pixel's group
+        const float4 v = ldT<T>(x, 4 * i), mu = ld4(smean + cs), is = ld4(sinvstd + cs), ga = ld4(gamma + c),
                      be = ld4(beta + c);
         float4 o;
         o.x = (v.x - mu.x) * is.x * ga.x + be.x;
@@ -204,11 +214,13 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const void* __r
                                                                  const void* __restrict__ g, long long P, int C,
                                                                  int G, const float* __restrict__ smean, void* ws) {
     const Map m = make_map(C);
-    const Work w = work(ws, G, C);
+    const int NG = gridDim.y, grp = blockIdx.y;
+    const Work w = work(ws, G, C, NG);
+    const size_t base = (size_t)grp * P * C;   // this group's first element
     __shared__ float4 lds[2][kThreads];
     for (int qq = 0; qq < m.QPT; ++qq) {
         const int q = (threadIdx.x % m.Q) + qq * kThreads, pl = threadIdx.x / m.Q;
-        const float4 mu = ld4(smean + 4 * q);
+        const float4 mu = ld4(smean + grp * C + 4 * q);
         float4 s = {0.f, 0.f, 0.f, 0.f}, sx = {0.f, 0.f, 0.f, 0.f};
         auto acc = [&](float4 gv, const float4 yv, const float4 v) {
             if (RELU) {
@@ -223,7 +235,7 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const void* __r
         const float4 zero = {0.f, 0.f, 0.f, 0.f};
         long long p = (long long)blockIdx.x * m.PPB + pl;
         for (; p + stride < P; p += 2 * stride) {   // two pixels (up to six loads) in flight per lane
-            const size_t o0 = p * C + 4 * q, o1 = (p + stride) * C + 4 * q;
+            const size_t o0 = base + p * C + 4 * q, o1 = base + (p + stride) * C + 4 * q;
             const float4 g0 = ldT<T>(g, o0), g1 = ldT<T>(g, o1);
             const float4 y0 = RELU ? ldT<T>(y, o0) : zero, y1 = RELU ? ldT<T>(y, o1) : zero;
             const float4 v0 = ldT<T>(x, o0), v1 = ldT<T>(x, o1);
@@ -231,30 +243,38 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const void* __r
             acc(g1, y1, v1);
         }
         for (; p < P; p += stride) {
-            const size_t o = p * C + 4 * q;
+            const size_t o = base + p * C + 4 * q;
             acc(ldT<T>(g, o), RELU ? ldT<T>(y, o) : zero, ldT<T>(x, o));
         }
-        block_partials(s, sx, q, pl, m, C, G, w, lds);
+        block_partials(s, sx, q, pl, m, C, NG * G, grp * G + blockIdx.x, w, lds);
     }
 }
 
 // dγ = Σg'x̂, dβ = Σg' and the dx coefficients, one block per channel
-__global__ void __launch_bounds__(kThreads) bn_bwd_final_kernel(long long P, int C, int G,
+__global__ void __launch_bounds__(kThreads) bn_bwd_final_kernel(long long P, int C, int G, int NG,
                                                                 const float* __restrict__ gamma,
                                                                 const float* __restrict__ sinvstd,
                                                                 float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                                 void* ws) {
     const int c = blockIdx.x;
-    const Work w = work(ws, G, C);
-    double a, b;
-    if (!channel_sums(w, G, C, c, a, b)) return;
-    const double is = sinvstd[c];
-    const double dg = b * is;   // Σ g'·x̂
-    dgamma[c] = (float)dg;
-    dbeta[c] = (float)a;
-    w.coef[c] = (float)((double)gamma[c] * is);          // γ·invstd
-    w.coef[C + c] = (float)(a / (double)P);              // Σg'/N
-    w.coef[2 * C + c] = (float)(dg * is / (double)P);    // Σg'x̂/N · invstd
+    const Work w = work(ws, G, C, NG);
+    double sdg = 0.0, sdb = 0.0;   // parameter gradients: sum over the groups in order
+    for (int grp = 0; grp < NG; ++grp) {
+        double a, b;
+        if (!channel_sums(w, NG * G, grp * G, G, C, c, a, b)) continue;
+        const double is = sinvstd[grp * C + c];
+        const double dg = b * is;   // Σ g'·x̂
+        sdg += dg;
+        sdb += a;
+        const size_t gc = (size_t)grp * C + c;
+        w.coef[gc] = (float)((double)gamma[c] * is);                     // γ·invstd
+        w.coef[(size_t)NG * C + gc] = (float)(a / (double)P);            // Σg'/N
+        w.coef[2 * (size_t)NG * C + gc] = (float)(dg * is / (double)P);  // Σg'x̂/N · invstd
+    }
+    if (threadIdx.x == 0) {
+        dgamma[c] = (float)sdg;
+        dbeta[c] = (float)sdb;
+    }
 }
 
 template <typename T, bool RELU, bool RES>
@@ -263,17 +283,17 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const void* __re
                                                                 const void* __restrict__ g,
                                                                 const float* __restrict__ smean, const float* coef,
                                                                 void* __restrict__ dx, void* __restrict__ dr,
-                                                                long long n4, int Q, int C) {
+                                                                long long n4, int Q, int C, int NG, long long q4g) {
     for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long long)gridDim.x * kThreads) {
-        const int c = 4 * (int)(i % Q);
+        const int c = 4 * (int)(i % Q) + (q4g ? C * (int)(i / q4g) : 0);   // group * C + channel
         float4 gv = ldT<T>(g, 4 * i);
         if (RELU) {
             const float4 yv = ldT<T>(y, 4 * i);
             gv.x = yv.x > 0.f ? gv.x : 0.f; gv.y = yv.y > 0.f ? gv.y : 0.f;
             gv.z = yv.z > 0.f ? gv.z : 0.f; gv.w = yv.w > 0.f ? gv.w : 0.f;
         }
-        const float4 v = ldT<T>(x, 4 * i), mu = ld4(smean + c), k1 = ld4(coef + c), k2 = ld4(coef + C + c),
-                     k3 = ld4(coef + 2 * C + c);
+        const float4 v = ldT<T>(x, 4 * i), mu = ld4(smean + c), k1 = ld4(coef + c),
+                     k2 = ld4(coef + (size_t)NG * C + c), k3 = ld4(coef + 2 * (size_t)NG * C + c);
         float4 o;
         o.x = k1.x * (gv.x - k2.x - (v.x - mu.x) * k3.x);
         o.y = k1.y * (gv.y - k2.y - (v.y - mu.y) * k3.y);
@@ -296,8 +316,11 @@ int grid_elem(long long n4) {
     return (int)(g < 4096 ? g : 4096);
 }
 
+int groups_of(const md2_bn_desc* d) { return d->groups > 1 ? d->groups : 1; }
+
 bool valid(const md2_bn_desc* d) {
-    if (!d || d->pixels < 2 || d->channels < 4 || d->channels % 4) return false;
+    if (!d || d->channels < 4 || d->channels % 4) return false;
+    if (d->groups < 0 || d->pixels % groups_of(d) || d->pixels / groups_of(d) < 2) return false;
     const int Q = d->channels / 4;
     return Q >= kThreads ? (Q % kThreads == 0) : (kThreads % Q == 0);
 }
@@ -306,36 +329,38 @@ template <typename T>
 void launch_fwd(const md2_bn_desc* d, const void* x, const float* gamma, const float* beta, const void* residual,
                 float* running_mean, float* running_var, void* y, float* save_mean, float* save_invstd,
                 void* workspace, hipStream_t st) {
-    const long long P = d->pixels;
+    const int NG = groups_of(d);
+    const long long P = d->pixels / NG;   // per group
     const int C = d->channels, G = blocks_for_stats(P, C);
-    hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(G), dim3(kThreads), 0, st, x, P, C, G, workspace);
-    hipLaunchKernelGGL(bn_stats_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, d->eps, d->momentum,
+    hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(G, NG), dim3(kThreads), 0, st, x, P, C, G, workspace);
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, NG, d->eps, d->momentum,
                        running_mean, running_var, save_mean, save_invstd, workspace);
-    const long long n4 = P * C / 4;
+    const long long n4 = d->pixels * C / 4, q4g = NG > 1 ? P * C / 4 : 0;
     const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
     auto k = relu ? (res ? bn_apply_kernel<T, true, true> : bn_apply_kernel<T, true, false>)
                   : (res ? bn_apply_kernel<T, false, true> : bn_apply_kernel<T, false, false>);
     hipLaunchKernelGGL(k, dim3(grid_elem(n4)), dim3(kThreads), 0, st, x, residual, gamma, beta, save_mean,
-                       save_invstd, y, n4, C / 4);
+                       save_invstd, y, n4, C / 4, q4g);
 }
 
 template <typename T>
 void launch_bwd(const md2_bn_desc* d, const void* x, const void* y, const void* grad_y, const float* gamma,
                 const float* save_mean, const float* save_invstd, void* grad_x, void* grad_residual,
                 float* grad_gamma, float* grad_beta, void* workspace, hipStream_t st) {
-    const long long P = d->pixels;
+    const int NG = groups_of(d);
+    const long long P = d->pixels / NG;
     const int C = d->channels, G = blocks_for_stats(P, C);
     const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
     auto red = relu ? bn_bwd_reduce_kernel<T, true> : bn_bwd_reduce_kernel<T, false>;
-    hipLaunchKernelGGL(red, dim3(G), dim3(kThreads), 0, st, x, y, grad_y, P, C, G, save_mean, workspace);
-    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, gamma, save_invstd, grad_gamma,
-                       grad_beta, workspace);
-    const long long n4 = P * C / 4;
-    const float* coef = work(workspace, G, C).coef;
+    hipLaunchKernelGGL(red, dim3(G, NG), dim3(kThreads), 0, st, x, y, grad_y, P, C, G, save_mean, workspace);
+    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, NG, gamma, save_invstd,
+                       grad_gamma, grad_beta, workspace);
+    const long long n4 = d->pixels * C / 4, q4g = NG > 1 ? P * C / 4 : 0;
+    const float* coef = work(workspace, G, C, NG).coef;
     auto k = relu ? (res ? bn_bwd_apply_kernel<T, true, true> : bn_bwd_apply_kernel<T, true, false>)
                   : (res ? bn_bwd_apply_kernel<T, false, true> : bn_bwd_apply_kernel<T, false, false>);
     hipLaunchKernelGGL(k, dim3(grid_elem(n4)), dim3(kThreads), 0, st, x, y, grad_y, save_mean, coef, grad_x,
-                       grad_residual, n4, C / 4, C);
+                       grad_residual, n4, C / 4, C, NG, q4g);
 }
 
 }  // namespace
@@ -344,8 +369,9 @@ extern "C" {
 
 size_t md2_bn_workspace_bytes(const md2_bn_desc* d) {
     if (!valid(d)) return 0;
-    const int G = blocks_for_stats(d->pixels, d->channels);
-    return (2 * (size_t)G * d->channels + 3 * (size_t)d->channels) * sizeof(float);
+    const int NG = groups_of(d);
+    const int G = blocks_for_stats(d->pixels / NG, d->channels);
+    return (2 * (size_t)NG * G * d->channels + 3 * (size_t)NG * d->channels) * sizeof(float);
 }
 
 int md2_bn_fwd(const md2_bn_desc* d, const void* x, const float* gamma, const float* beta, const void* residual,

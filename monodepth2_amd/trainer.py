@@ -34,6 +34,7 @@ import torch.optim as optim
 from . import networks
 from .distributed import FlatGradSync, wrap_ddp
 from .hotpath import HotPathConfig, generate_images, photometric_loss, predictive_mask_inputs, selection_maps
+from .bn_ops import bn_groups
 from .layers import compute_depth_errors, disp_to_depth
 from .pose_ops import poses_to_transforms
 
@@ -120,13 +121,19 @@ class Trainer:
         # BatchNorm's num_batches_tracked only matters with momentum=None (never used
         # here or in the reference), yet costs one tiny launch per BN layer per step:
         # keep one step counter instead and write it back into checkpoints.
-        self._bn_layers = []
+        # Calls per step differ: the separate pose encoder runs once per frame pair in
+        # the reference (trainer.py:280-290), so its layers count that many batches.
+        self._bn_layers, self._bn_mult = [], []
+        pairs = sum(1 for f in self.opt.frame_ids[1:] if f != "s")
         for name, m in self.nets.named_modules():
             if isinstance(m, nn.modules.batchnorm._BatchNorm) and m.momentum is not None \
                     and m.num_batches_tracked is not None:
                 self._bn_layers.append(m)
+                self._bn_mult.append(pairs if (name.startswith("models.pose_encoder.")
+                                               and self.num_pose_frames == 2) else 1)
                 m.num_batches_tracked = None
         self._bn_steps = 0
+        self.batch_pose_pairs = True   # one pose-encoder pass over all frame pairs (bn_groups)
 
         # gradient averaging: DDP (hooks, overlapped with backward) for eager steps, flat
         # buckets + one RCCL all-reduce each (graph-capturable) for --hip_graph
@@ -212,15 +219,28 @@ class Trainer:
                 pose_feats = {f_i: features[f_i] for f_i in self.opt.frame_ids}
             else:
                 pose_feats = {f_i: inputs["color_aug", f_i, 0] for f_i in self.opt.frame_ids}
-            for f_i in self.opt.frame_ids[1:]:
-                if f_i == "s":
-                    continue
-                pair = [pose_feats[f_i], pose_feats[0]] if f_i < 0 else [pose_feats[0], pose_feats[f_i]]
-                if self.opt.pose_model_type == "separate_resnet":
-                    pair = [models["pose_encoder"](torch.cat(pair, 1))]
-                elif self.opt.pose_model_type == "posecnn":
-                    pair = torch.cat(pair, 1)
-                axisangle, translation = models["pose"](pair)
+            temporal = [f_i for f_i in self.opt.frame_ids[1:] if f_i != "s"]
+            pairs = [[pose_feats[f_i], pose_feats[0]] if f_i < 0 else [pose_feats[0], pose_feats[f_i]]
+                     for f_i in temporal]
+            if (self.opt.pose_model_type == "separate_resnet" and len(temporal) > 1 and self.device.type == "cuda"
+                    and self.batch_pose_pairs):
+                # every pair through the pose network as ONE batch; BatchNorm keeps per-pair
+                # statistics (bn_groups), so this equals the reference's one call per pair
+                B = self.opt.batch_size
+                with bn_groups(len(temporal)):
+                    feats = models["pose_encoder"](torch.cat([torch.cat(p, 1) for p in pairs], 0))
+                axisangle_all, translation_all = models["pose"]([feats])
+                per_pair = [(axisangle_all[i * B:(i + 1) * B], translation_all[i * B:(i + 1) * B])
+                            for i in range(len(temporal))]
+            else:
+                per_pair = []
+                for pair in pairs:
+                    if self.opt.pose_model_type == "separate_resnet":
+                        pair = [models["pose_encoder"](torch.cat(pair, 1))]
+                    elif self.opt.pose_model_type == "posecnn":
+                        pair = torch.cat(pair, 1)
+                    per_pair.append(models["pose"](pair))
+            for f_i, (axisangle, translation) in zip(temporal, per_pair):
                 outputs[("axisangle", 0, f_i)] = axisangle
                 outputs[("translation", 0, f_i)] = translation
                 aas.append(axisangle[:, 0, 0])
@@ -384,8 +404,8 @@ class Trainer:
 
     def _bn_state(self):
         """Restore the folded BatchNorm counters (checkpoint key parity)."""
-        for m in self._bn_layers:
-            m.num_batches_tracked = torch.tensor(self._bn_steps, dtype=torch.long, device=self.device)
+        for m, k in zip(self._bn_layers, self._bn_mult):
+            m.num_batches_tracked = torch.tensor(self._bn_steps * k, dtype=torch.long, device=self.device)
 
     def _bn_fold(self):
         for m in self._bn_layers:
@@ -478,7 +498,7 @@ class Trainer:
             model_dict.update({k: v for k, v in loaded.items() if k in model_dict})
             self.models[n].load_state_dict(model_dict)
         if self._bn_layers:
-            self._bn_steps = int(self._bn_layers[0].num_batches_tracked)
+            self._bn_steps = int(self._bn_layers[0].num_batches_tracked) // self._bn_mult[0]
         self._bn_fold()
         adam = os.path.join(folder, "adam.pth")
         if os.path.isfile(adam):

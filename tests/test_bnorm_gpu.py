@@ -82,6 +82,36 @@ def test_bn_act_bf16_matches_batchnorm_fp32(relu, res):
         assert float((a.float() - b).norm() / b.norm()) < 1e-2
 
 
+@pytest.mark.parametrize("bf16", [False, True])
+def test_bn_groups_equal_separate_calls(bf16):
+    """bn_groups(2) over a 2-chunk batch == two BatchNorm calls (per-chunk statistics,
+    running statistics updated chunk after chunk)."""
+    torch.manual_seed(4)
+    C, B, H, W = 64, 6, 12, 20
+    dt = torch.bfloat16 if bf16 else torch.float32
+    bn = nn.BatchNorm2d(C).cuda()
+    ref_bn = copy.deepcopy(bn)
+    xb = torch.randn(B, C, H, W, device="cuda")
+    xb[B // 2:] = xb[B // 2:] * 3 - 1   # the chunks differ in statistics
+    xb = xb.to(dt).contiguous(memory_format=CL)
+    rb = torch.randn(B, C, H, W, device="cuda").to(dt).contiguous(memory_format=CL)
+    x, r = xb.clone().requires_grad_(True), rb.clone().requires_grad_(True)
+    xr, rr = xb.float().requires_grad_(True), rb.float().requires_grad_(True)
+    with bn_ops.bn_groups(2):
+        y = bn_ops.bn_act(bn, x, r)
+    yr = torch.cat([_eager(ref_bn, xc, rc, True) for xc, rc in zip(xr.chunk(2), rr.chunk(2))], 0)
+    tol = 1e-2 if bf16 else 2e-5
+    torch.testing.assert_close(y.float(), yr, rtol=tol, atol=tol)
+    torch.testing.assert_close(bn.running_mean, ref_bn.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn.running_var, ref_bn.running_var, rtol=1e-4, atol=1e-5)
+    assert int(bn.num_batches_tracked) == int(ref_bn.num_batches_tracked) == 2
+    g = torch.randn_like(yr)
+    got = torch.autograd.grad(y, [x, r, bn.weight, bn.bias], g.to(dt).contiguous(memory_format=CL))
+    ref = torch.autograd.grad(yr, [xr, rr, ref_bn.weight, ref_bn.bias], g.to(dt).float())
+    for a, b in zip(got, ref):
+        assert float((a.float() - b).norm() / b.norm()) < (1e-2 if bf16 else 1e-4)
+
+
 def test_bn_act_deterministic():
     torch.manual_seed(1)
     bn = nn.BatchNorm2d(64).cuda()

@@ -110,6 +110,31 @@ def test_generate_images_pred_materialises_reference_keys():
             assert outputs[("color_identity", f, s)] is batch[("color", f, 0)]
 
 
+def test_batched_pose_pairs_match_separate_calls():
+    """One pose-encoder pass over both pairs (bn_groups) == one call per pair."""
+    tr, batch = make("mono")
+    tr.set_train()
+    import copy
+    nets_ref = copy.deepcopy(tr.models)
+    out = tr.predict_poses(batch, None)
+    tr.batch_pose_pairs = False
+    ref = tr.predict_poses(batch, None, models=nets_ref)
+    for f in (-1, 1):
+        for key in ("axisangle", "translation", "cam_T_cam"):
+            torch.testing.assert_close(out[(key, 0, f)], ref[(key, 0, f)], rtol=1e-4, atol=1e-6)
+    for (n, a), (_, b) in zip(tr.models["pose_encoder"].named_buffers(), nets_ref["pose_encoder"].named_buffers()):
+        if a.dtype.is_floating_point:
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6, msg=n)
+    loss = sum(out[("cam_T_cam", 0, f)].square().sum() for f in (-1, 1))
+    loss_r = sum(ref[("cam_T_cam", 0, f)].square().sum() for f in (-1, 1))
+    ps = list(tr.models["pose_encoder"].parameters()) + list(tr.models["pose"].parameters())
+    pr = list(nets_ref["pose_encoder"].parameters()) + list(nets_ref["pose"].parameters())
+    ga = torch.autograd.grad(loss, ps, allow_unused=True)
+    gb = torch.autograd.grad(loss_r, pr, allow_unused=True)
+    worst = max(float((a - b).norm() / (b.norm() + 1e-12)) for a, b in zip(ga, gb) if b is not None)
+    assert worst < 1e-3, worst
+
+
 def test_checkpoint_roundtrip(tmp_path):
     tr, batch = make("mono", log_dir=str(tmp_path))
     tr.train_step(batch)
@@ -118,6 +143,8 @@ def test_checkpoint_roundtrip(tmp_path):
     enc = torch.load(os.path.join(folder, "encoder.pth"), weights_only=True)
     assert enc["height"] == H and enc["width"] == W and "encoder.conv1.weight" in enc
     assert int(enc["encoder.bn1.num_batches_tracked"]) == 1   # folded BN counter written back
+    penc = torch.load(os.path.join(folder, "pose_encoder.pth"), weights_only=True)
+    assert int(penc["encoder.bn1.num_batches_tracked"]) == 2   # one pose-encoder call per frame pair
     tr2, _ = make("mono", log_dir=str(tmp_path), load_weights_folder=folder)
     for (n, p), (n2, p2) in zip(tr.nets.named_parameters(), tr2.nets.named_parameters()):
         assert n == n2 and torch.equal(p, p2)
