@@ -40,16 +40,20 @@ def bn_groups(n: int):
         _GROUPS = prev
 
 _CL = torch.channels_last
-_workspaces: Dict[torch.device, torch.Tensor] = {}
+_workspaces: Dict[int, torch.Tensor] = {}
 
 
 def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
-    """Per-device scratch (partial sums + backward coefficients), reused by every
-    call on the device's stream."""
-    ws = _workspaces.get(device)
+    """Scratch (partial sums + backward coefficients) per HIP stream: calls on one
+    stream are ordered, calls on different streams (the trainer runs the pose
+    network beside the depth network) must not share it."""
+    stream = torch.cuda.current_stream(device)
+    key = stream.cuda_stream
+    ws = _workspaces.get(key)
     if ws is None or ws.numel() < nbytes:
-        ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
-        _workspaces[device] = ws
+        with torch.cuda.stream(stream):
+            ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _workspaces[key] = ws
     return ws
 
 

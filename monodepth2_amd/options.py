@@ -77,6 +77,8 @@ _FLAGS = [
     ("--channels_last", dict(type=int, default=1,
                              help="build: 1 (default) NHWC activations/weights for the convolutions, 0 NCHW")),
     ("--hip_graph", dict(action="store_true", help="build: capture the whole training step in one hipGraph")),
+    ("--pose_streams", dict(type=int, default=1,
+                            help="build: 1 runs the pose network on its own HIP stream beside the depth network")),
     ("--amp", dict(type=str, default="none", choices=["none", "bf16"],
                    help="build: bf16 autocast for the networks (the photometric loss stays fp32)")),
     ("--grad_sync", dict(type=str, default="auto", choices=["auto", "ddp", "flat"],

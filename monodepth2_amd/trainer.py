@@ -134,6 +134,11 @@ class Trainer:
                 m.num_batches_tracked = None
         self._bn_steps = 0
         self.batch_pose_pairs = True   # one pose-encoder pass over all frame pairs (bn_groups)
+        # second HIP stream for the pose network (overlaps the depth network); not under
+        # hipGraph capture, whose step is captured on one stream
+        self._pose_stream = (torch.cuda.Stream(self.device)
+                             if self.device.type == "cuda" and not getattr(self.opt, "hip_graph", False)
+                             and getattr(self.opt, "pose_streams", 1) else None)
 
         # gradient averaging: DDP (hooks, overlapped with backward) for eager steps, flat
         # buckets + one RCCL all-reduce each (graph-capturable) for --hip_graph
@@ -191,6 +196,16 @@ class Trainer:
         return outputs
 
     def _networks_body(self, models, inputs):
+        # The pose network does not read the depth network (except pose_model_type
+        # "shared"): it runs on a second HIP stream so the two overlap; autograd runs
+        # its backward on that stream too.
+        side = self._pose_stream if (self.use_pose_net and self.opt.pose_model_type != "shared") else None
+        main = torch.cuda.current_stream(self.device) if side is not None else None
+        pose_out = None
+        if side is not None:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                pose_out = self.predict_poses(inputs, None, models)
         if self.opt.pose_model_type == "shared":
             all_color_aug = torch.cat([inputs[("color_aug", i, 0)] for i in self.opt.frame_ids])
             all_features = models["encoder"](all_color_aug)
@@ -204,7 +219,13 @@ class Trainer:
             outputs["predictive_mask"] = models["predictive_mask"](
                 features[0] if isinstance(features, dict) else features)
         if self.use_pose_net:
-            outputs.update(self.predict_poses(inputs, features, models))
+            if side is not None:
+                main.wait_stream(side)
+                for v in pose_out.values():
+                    v.record_stream(main)
+            else:
+                pose_out = self.predict_poses(inputs, features, models)
+            outputs.update(pose_out)
         return outputs
 
     def predict_poses(self, inputs, features, models=None):
