@@ -279,6 +279,25 @@ int md2_bn_bwd(const md2_bn_desc* desc, const void* x, const void* y, const void
                void* grad_x, void* grad_residual, float* grad_gamma, float* grad_beta,
                void* workspace, void* stream);
 
+/*
+ * The ResNet stem's MaxPool2d(3, stride 2, padding 1) on channels_last activations
+ * (x: (batch, height, width, channels), channels a multiple of 4; fp32, or bf16 with
+ * MD2_POOL_BF16).  idx: one byte per output value, the winning window position 0..8
+ * (first maximum in scan order; NaN propagates, as ATen), uint32-packed per 4
+ * channels: batch * ho * wo * channels / 4 words.  The backward gathers (no atomics).
+ */
+#define MD2_POOL_BF16 (1u << 0)
+
+typedef struct md2_pool_desc {
+    int32_t batch, channels, height, width;
+    uint32_t flags;
+    int32_t reserved;
+} md2_pool_desc;
+
+int md2_maxpool3s2_fwd(const md2_pool_desc* desc, const void* x, void* y, uint32_t* idx, void* stream);
+int md2_maxpool3s2_bwd(const md2_pool_desc* desc, const uint32_t* idx, const void* grad_y, void* grad_x,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,7 +57,7 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_photometric_fwd", "md2_photometric_bwd", "md2_generate_images",
            "md2_timing_begin", "md2_timing_end", "md2_decoder_pad_fwd", "md2_decoder_pad_bwd",
            "md2_pose_fwd", "md2_pose_bwd", "md2_aug_plan_create", "md2_aug_plan_destroy", "md2_aug_run",
-           "md2_bn_workspace_bytes", "md2_bn_fwd", "md2_bn_bwd"]
+           "md2_bn_workspace_bytes", "md2_bn_fwd", "md2_bn_bwd", "md2_maxpool3s2_fwd", "md2_maxpool3s2_bwd"]
 
 PAD_ELU = 1 << 0
 PAD_UPSAMPLE = 1 << 1
@@ -91,6 +91,14 @@ class BnDesc(ctypes.Structure):
     _fields_ = [("pixels", ctypes.c_int64), ("channels", ctypes.c_int32), ("flags", ctypes.c_uint32),
                 ("eps", ctypes.c_float), ("momentum", ctypes.c_float), ("groups", ctypes.c_int32),
                 ("reserved", ctypes.c_int32)]
+
+
+POOL_BF16 = 1 << 0
+
+
+class PoolDesc(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("channels", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("width", ctypes.c_int32), ("flags", ctypes.c_uint32), ("reserved", ctypes.c_int32)]
 
 
 def _declare(L):
@@ -130,6 +138,10 @@ def _declare(L):
     L.md2_bn_fwd.argtypes = [ctypes.POINTER(BnDesc)] + [_vp] * 11
     L.md2_bn_bwd.restype = ctypes.c_int
     L.md2_bn_bwd.argtypes = [ctypes.POINTER(BnDesc)] + [_vp] * 12
+    L.md2_maxpool3s2_fwd.restype = ctypes.c_int
+    L.md2_maxpool3s2_fwd.argtypes = [ctypes.POINTER(PoolDesc), _vp, _vp, _vp, _vp]
+    L.md2_maxpool3s2_bwd.restype = ctypes.c_int
+    L.md2_maxpool3s2_bwd.argtypes = [ctypes.POINTER(PoolDesc), _vp, _vp, _vp, _vp]
     L.md2_timing_begin.restype = ctypes.c_int
     L.md2_timing_begin.argtypes = [ctypes.c_int]
     L.md2_timing_end.restype = ctypes.c_int

@@ -128,3 +128,43 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, residual: Optional[torch.Tensor]
     if residual is not None:
         y = y + residual
     return F.relu(y) if relu else y
+
+
+class _MaxPool(torch.autograd.Function):
+    """MaxPool2d(3, 2, 1) on channels_last tensors (csrc/pool.hip)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        B, C, H, W = x.shape
+        Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        d = _lib.PoolDesc(B, C, H, W, _lib.POOL_BF16 if x.dtype == torch.bfloat16 else 0, 0)
+        y = torch.empty((B, C, Ho, Wo), device=x.device, dtype=x.dtype, memory_format=_CL)
+        idx = torch.empty(B * Ho * Wo * C // 4, device=x.device, dtype=torch.int32)
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        _lib.check(_lib.lib().md2_maxpool3s2_fwd(ctypes.byref(d), x.data_ptr(), y.data_ptr(), idx.data_ptr(), stream),
+                   "md2_maxpool3s2_fwd")
+        ctx.save_for_backward(idx)
+        ctx.desc = (B, C, H, W, d.flags, 0)
+        ctx.xshape, ctx.dtype = x.shape, x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (idx,) = ctx.saved_tensors
+        gy = gy.to(ctx.dtype).contiguous(memory_format=_CL)
+        gx = torch.empty(ctx.xshape, device=gy.device, dtype=ctx.dtype, memory_format=_CL)
+        d = _lib.PoolDesc(*ctx.desc)
+        _lib.check(_lib.lib().md2_maxpool3s2_bwd(ctypes.byref(d), idx.data_ptr(), gy.data_ptr(), gx.data_ptr(),
+                                                 torch.cuda.current_stream(gy.device).cuda_stream),
+                   "md2_maxpool3s2_bwd")
+        return gx
+
+
+def max_pool_3x3s2(pool: nn.MaxPool2d, x: torch.Tensor) -> torch.Tensor:
+    """The ResNet stem pool: HIP kernels for channels_last fp32/bf16 GPU tensors."""
+    if (ENABLED and x.is_cuda and x.dim() == 4 and x.dtype in (torch.float32, torch.bfloat16)
+            and x.shape[1] % 4 == 0 and x.is_contiguous(memory_format=_CL)
+            and pool.kernel_size in (3, (3, 3)) and pool.stride in (2, (2, 2)) and pool.padding in (1, (1, 1))
+            and pool.dilation in (1, (1, 1)) and not pool.ceil_mode and not pool.return_indices):
+        return _MaxPool.apply(x)
+    return pool(x)

@@ -1,0 +1,144 @@
+// pool.hip — the ResNet stem's MaxPool2d(kernel 3, stride 2, padding 1)
+// (torchvision ResNet behind networks/resnet_encoder.py:62-98) for NHWC activations
+// on gfx950, fp32 or bf16 storage.
+//
+// Forward: one thread per (image, output pixel, channel quad): the max of the 3x3
+// window (padding never wins), with PyTorch's rules — the first maximum in scan
+// order wins ties, NaN propagates — and the winning window position (0..8) as one
+// byte per value.  Backward: one thread per input quad gathers from the at most 4
+// windows that contain it the gradients whose window picked it: a fixed-order sum, so
+// deterministic (no atomics, unlike a scatter).
+
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+
+#include "md2_bf16.h"
+#include "md2hot.h"
+
+int md2_report_error(int code, const char* msg);
+
+namespace {
+
+constexpr int kThreads = 256;
+
+struct PoolArgs {
+    int B, H, W, C, Ho, Wo;
+};
+
+__device__ __forceinline__ void take(float v, int k, float& m, int& a) {
+    if (v > m || isnan(v)) {   // ATen max_pool2d: strictly greater, or NaN
+        m = v;
+        a = k;
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(PoolArgs p, const void* __restrict__ x,
+                                                               void* __restrict__ y, uint32_t* __restrict__ idx) {
+    const int C4 = p.C / 4;
+    const long long n = (long long)p.B * p.Ho * p.Wo * C4;
+    for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+        const int c = 4 * (int)(i % C4);
+        long long t = i / C4;
+        const int ox = (int)(t % p.Wo);
+        t /= p.Wo;
+        const int oy = (int)(t % p.Ho);
+        const int b = (int)(t / p.Ho);
+        float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        const int k0 = (oy == 0 ? 3 : 0) + (ox == 0 ? 1 : 0);   // first tap inside the image
+        int a[4] = {k0, k0, k0, k0};
+        for (int ky = 0; ky < 3; ++ky) {
+            const int iy = 2 * oy - 1 + ky;
+            if (iy < 0 || iy >= p.H) continue;
+            for (int kx = 0; kx < 3; ++kx) {
+                const int ix = 2 * ox - 1 + kx;
+                if (ix < 0 || ix >= p.W) continue;
+                const float4 v = md2::ld4T<T>(x, (((size_t)b * p.H + iy) * p.W + ix) * p.C + c);
+                const int k = ky * 3 + kx;
+                take(v.x, k, m[0], a[0]);
+                take(v.y, k, m[1], a[1]);
+                take(v.z, k, m[2], a[2]);
+                take(v.w, k, m[3], a[3]);
+            }
+        }
+        md2::st4T<T>(y, 4 * i, make_float4(m[0], m[1], m[2], m[3]));
+        idx[i] = (uint32_t)a[0] | ((uint32_t)a[1] << 8) | ((uint32_t)a[2] << 16) | ((uint32_t)a[3] << 24);
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) maxpool_bwd_kernel(PoolArgs p, const uint32_t* __restrict__ idx,
+                                                               const void* __restrict__ gy, void* __restrict__ gx) {
+    const int C4 = p.C / 4;
+    const long long n = (long long)p.B * p.H * p.W * C4;
+    for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+        const int c4 = (int)(i % C4);
+        long long t = i / C4;
+        const int ix = (int)(t % p.W);
+        t /= p.W;
+        const int iy = (int)(t % p.H);
+        const int b = (int)(t / p.H);
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+        // windows oy with 2*oy-1 <= iy <= 2*oy+1 (likewise x), in increasing order
+        for (int oy = iy / 2; oy <= (iy + 1) / 2; ++oy) {
+            if (oy < 0 || oy >= p.Ho || 2 * oy - 1 > iy || 2 * oy + 1 < iy) continue;
+            for (int ox = ix / 2; ox <= (ix + 1) / 2; ++ox) {
+                if (ox < 0 || ox >= p.Wo || 2 * ox - 1 > ix || 2 * ox + 1 < ix) continue;
+                const size_t o = (((size_t)b * p.Ho + oy) * p.Wo + ox) * C4 + c4;
+                const uint32_t w = idx[o];
+                const int k = (iy - (2 * oy - 1)) * 3 + (ix - (2 * ox - 1));
+                const float4 g = md2::ld4T<T>(gy, 4 * o);
+                if ((int)(w & 255u) == k) s[0] += g.x;
+                if ((int)((w >> 8) & 255u) == k) s[1] += g.y;
+                if ((int)((w >> 16) & 255u) == k) s[2] += g.z;
+                if ((int)(w >> 24) == k) s[3] += g.w;
+            }
+        }
+        md2::st4T<T>(gx, 4 * i, make_float4(s[0], s[1], s[2], s[3]));
+    }
+}
+
+int grid_for(long long n) {
+    const long long g = (n + kThreads - 1) / kThreads;
+    return (int)(g < 8192 ? g : 8192);
+}
+
+bool make(const md2_pool_desc* d, PoolArgs& p) {
+    if (!d || d->batch < 1 || d->channels < 4 || d->channels % 4 || d->height < 1 || d->width < 1) return false;
+    p.B = d->batch;
+    p.C = d->channels;
+    p.H = d->height;
+    p.W = d->width;
+    p.Ho = (d->height + 2 - 3) / 2 + 1;
+    p.Wo = (d->width + 2 - 3) / 2 + 1;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int md2_maxpool3s2_fwd(const md2_pool_desc* d, const void* x, void* y, uint32_t* idx, void* stream) {
+    PoolArgs p;
+    if (!make(d, p) || !x || !y || !idx) return md2_report_error(MD2_ERR_ARG, "maxpool: bad desc or NULL operand");
+    const long long n = (long long)p.B * p.Ho * p.Wo * (p.C / 4);
+    auto k = (d->flags & MD2_POOL_BF16) ? maxpool_fwd_kernel<uint16_t> : maxpool_fwd_kernel<float>;
+    hipLaunchKernelGGL(k, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, p, x, y, idx);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
+int md2_maxpool3s2_bwd(const md2_pool_desc* d, const uint32_t* idx, const void* grad_y, void* grad_x, void* stream) {
+    PoolArgs p;
+    if (!make(d, p) || !idx || !grad_y || !grad_x)
+        return md2_report_error(MD2_ERR_ARG, "maxpool: bad desc or NULL operand");
+    const long long n = (long long)p.B * p.H * p.W * (p.C / 4);
+    auto k = (d->flags & MD2_POOL_BF16) ? maxpool_bwd_kernel<uint16_t> : maxpool_bwd_kernel<float>;
+    hipLaunchKernelGGL(k, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, p, idx, grad_y, grad_x);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
+}  // extern "C"

@@ -19,7 +19,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..bn_ops import bn_act
+from ..bn_ops import bn_act, max_pool_3x3s2
 
 
 def _conv3x3(cin, cout, stride=1):
@@ -139,7 +139,7 @@ class ResnetEncoder(nn.Module):
         if e.conv1.weight.is_contiguous(memory_format=torch.channels_last):
             x = x.contiguous(memory_format=torch.channels_last)
         f0 = bn_act(e.bn1, e.conv1(x))
-        f1 = e.layer1(e.maxpool(f0))
+        f1 = e.layer1(max_pool_3x3s2(e.maxpool, f0))
         f2 = e.layer2(f1)
         f3 = e.layer3(f2)
         f4 = e.layer4(f3)

@@ -21,7 +21,7 @@ def L():
 
 def header_symbols():
     src = open(os.path.join(INCLUDE, "md2hot.h")).read()
-    return sorted(set(re.findall(r"\b(md2_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(md2_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_exports_match_header(L):

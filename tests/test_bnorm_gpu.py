@@ -159,3 +159,32 @@ def test_encoder_fused_bn_matches_unfused(num_layers):
     for (n, a), (_, b) in zip(enc.named_buffers(), ref.named_buffers()):
         if a.dtype.is_floating_point:
             torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5, msg=n)
+
+
+@pytest.mark.parametrize("shape,dt", [((2, 64, 96, 320), torch.float32), ((3, 64, 7, 9), torch.float32),
+                                      ((2, 64, 24, 80), torch.bfloat16), ((1, 8, 1, 1), torch.float32)])
+def test_maxpool_matches_aten(shape, dt):
+    """MaxPool2d(3, 2, 1) on channels_last (csrc/pool.hip) vs ATen: values exact,
+    gradients exact up to the sum order of overlapping windows; ties (ReLU zeros)
+    resolved to the same element."""
+    torch.manual_seed(5)
+    pool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+    x0 = torch.relu(torch.randn(*shape, device="cuda")).to(dt).contiguous(memory_format=CL)   # many ties at 0
+    x = x0.clone().requires_grad_(True)
+    xr = x0.clone().requires_grad_(True)
+    y = bn_ops.max_pool_3x3s2(pool, x)
+    yr = pool(xr)
+    assert y.is_contiguous(memory_format=CL)
+    assert torch.equal(y, yr)
+    g = torch.randn_like(yr)
+    gx, = torch.autograd.grad(y, x, g.contiguous(memory_format=CL))
+    gxr, = torch.autograd.grad(yr, xr, g)
+    torch.testing.assert_close(gx.float(), gxr.float(), rtol=1e-5, atol=1e-6 if dt == torch.float32 else 2e-2)
+
+
+def test_maxpool_nan_propagates():
+    pool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+    x = torch.zeros(1, 4, 6, 6, device="cuda").contiguous(memory_format=CL)
+    x[0, 1, 2, 3] = float("nan")
+    y = bn_ops.max_pool_3x3s2(pool, x)
+    assert torch.equal(torch.isnan(y), torch.isnan(pool(x)))
