@@ -53,13 +53,31 @@ def ignored_parameters(module: nn.Module):
             or n.endswith("encoder.fc.bias")]
 
 
-def wrap_ddp(module: nn.Module, device: torch.device):
+def _stream_synced_allreduce(state, bucket):
+    """DDP comm hook for a backward that runs on several HIP streams (the trainer's
+    pose network has its own): a bucket's gradients may be written by any of them,
+    and DDP's reducer only orders the all-reduce after the stream that completes the
+    bucket.  Wait for every stream first, then the default mean all-reduce."""
+    from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
+    cur = torch.cuda.current_stream()
+    for s in state["streams"]:
+        if s.cuda_stream != cur.cuda_stream:
+            cur.wait_stream(s)
+    return default_hooks.allreduce_hook(state["group"], bucket)
+
+
+def wrap_ddp(module: nn.Module, device: torch.device, streams=None):
+    """DDP over the networks.  `streams`: every HIP stream the backward writes
+    gradients on (more than one -> the synchronising comm hook above)."""
     from torch.nn.parallel import DistributedDataParallel as DDP
     DDP._set_params_and_buffers_to_ignore_for_model(module, ignored_parameters(module))
     kw = dict(broadcast_buffers=False, bucket_cap_mb=BUCKET_CAP_MB, gradient_as_bucket_view=True)
     if device.type == "cuda":
         kw.update(device_ids=[device.index], output_device=device.index)
-    return DDP(module, **kw)
+    ddp = DDP(module, **kw)
+    if streams and len(streams) > 1:
+        ddp.register_comm_hook({"group": None, "streams": list(streams)}, _stream_synced_allreduce)
+    return ddp
 
 
 def shard(batch: Dict, rank: int, world: int) -> Dict:

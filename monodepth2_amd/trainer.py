@@ -148,7 +148,9 @@ class Trainer:
             sync = "flat" if self.use_graph else "ddp"
         if self.use_graph and sync == "ddp" and world_size > 1:
             raise ValueError("--hip_graph needs --grad_sync flat (DDP hooks are not graph-capturable)")
-        self.ddp = wrap_ddp(self.nets, self.device) if (world_size > 1 and sync == "ddp") else None
+        streams = ([torch.cuda.current_stream(self.device), self._pose_stream]
+                   if self._pose_stream is not None else None)
+        self.ddp = wrap_ddp(self.nets, self.device, streams) if (world_size > 1 and sync == "ddp") else None
         self.flat_sync = FlatGradSync(self.nets.named_parameters(), world_size) \
             if (sync == "flat" or self.use_graph) else None
         self.graph = None
