@@ -1,0 +1,72 @@
+"""Data parallelism through the real Trainer on the GPU: two ranks (gloo, both on
+cuda:0 — the pool's boxes have one GPU; RCCL runs the same DDP code on 8) with the
+pose network on its own HIP stream, so DDP buckets receive gradients from two
+streams.  After the synced backward every rank must hold the mean of the ranks'
+local (no_sync) gradients."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from monodepth2_amd.data import synthetic_batch
+        from monodepth2_amd.options import default_options
+        from monodepth2_amd.trainer import Trainer
+        dev = torch.device("cuda", 0)
+        torch.manual_seed(0)
+        tr = Trainer(default_options(batch_size=2, height=64, width=128, weights_init="scratch",
+                                     log_dir="/tmp/md2_ddp_gpu"), device=dev, rank=rank, world_size=world)
+        assert tr.ddp is not None and tr._pose_stream is not None
+        tr.set_train()
+        batch = synthetic_batch(2, 64, 128, tr.opt.frame_ids, 4, seed=10 + rank, device=dev)
+        params = [p for p in tr.nets.parameters() if p.requires_grad]
+        names = [n for n, p in tr.nets.named_parameters() if p.requires_grad]
+
+        def grads():
+            return [None if p.grad is None else p.grad.detach().clone() for p in params]
+
+        tr.model_optimizer.zero_grad(set_to_none=True)
+        with tr.ddp.no_sync():
+            _, losses = tr.process_batch(batch)
+            losses["loss"].backward()
+        torch.cuda.synchronize()
+        local = grads()
+        tr.model_optimizer.zero_grad(set_to_none=True)
+        _, losses = tr.process_batch(batch)
+        losses["loss"].backward()
+        torch.cuda.synchronize()
+        synced = grads()
+        checked = 0
+        for n, lg, sg in zip(names, local, synced):
+            if lg is None or "fc." in n:
+                continue
+            mean = lg.clone()
+            dist.all_reduce(mean)
+            mean /= world
+            err = float((sg - mean).norm() / (mean.norm() + 1e-12))
+            assert err < 1e-5, (n, err)
+            checked += 1
+        assert checked > 100
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_with_pose_stream_averages_gradients():
+    mp.spawn(_rank, args=(2, _free_port()), nprocs=2, join=True)
