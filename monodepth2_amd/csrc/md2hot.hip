@@ -613,7 +613,8 @@ __device__ __forceinline__ void make_carry(const WarpCtx& c, const FastSample& s
 // all source frames.  Writes dL/d(upsampled disp) for its 60 x kRowsB pixels and one
 // 12-float dL/dP partial per frame.
 template <int NS, bool SSIM_ON, bool MASK>
-__device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int st, int rb, int lane) {
+__device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int st, int rb, int lane,
+                                         float (*ddacc)[kWave]) {
     const int r0 = rb * kRowsB;
     const int h = a.h, w = a.w, HW = h * w;
     const int c = st * kBwdCols - 2 + lane;
@@ -729,8 +730,10 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
                             dP[i * 4 + 3] += dc[i];
                         }
                         const float dd = (dc[0] * k2.u[0] + dc[1] * k2.u[1] + dc[2] * k2.u[2]) * k2.dd;
-                        if (f == 0) dfull[q * w + c] = dd;
-                        else dfull[q * w + c] += dd;
+                        // frames accumulate in LDS; dfull is written once per item
+                        if (NS == 1) dfull[q * w + c] = dd;
+                        else if (f == 0) ddacc[q - r0][lane] = dd;
+                        else ddacc[q - r0][lane] += dd;
                     }
                 }
                 cA = cB;
@@ -761,12 +764,16 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
             if (lane == 0) dst[j] = t;
         }
     }
+    if (NS > 1 && colok) {
+        for (int i = 0; i < kRowsB && r0 + i < h; ++i) dfull[(r0 + i) * w + c] = ddacc[i][lane];
+    }
 }
 
 // Resident waves walk the (image, row block, strip, scale) items; each XCD owns a
 // contiguous item range (its L2 streams a contiguous slice of the images).
 template <int NS, bool SSIM_ON, bool MASK>
 __global__ __launch_bounds__(kBlock, 2) void photo_bwd_kernel(PhotoArgs a) {
+    __shared__ float ddacc[kWavesPerBlock][kRowsB][kWave];   // dL/d(upsampled disp) summed over frames
     const int lane = threadIdx.x & (kWave - 1);
     // G groups of blocks (the 8 XCDs under round-robin dispatch; fewer for tiny grids)
     const int nb = gridDim.x, G = nb < 8 ? nb : 8, grp = blockIdx.x % G;
@@ -784,7 +791,7 @@ __global__ __launch_bounds__(kBlock, 2) void photo_bwd_kernel(PhotoArgs a) {
         t /= a.strips;
         const int rb = t % a.rowblocks;
         const int b = t / a.rowblocks;
-        bwd_item<NS, SSIM_ON, MASK>(a, b, ls, st, rb, lane);
+        bwd_item<NS, SSIM_ON, MASK>(a, b, ls, st, rb, lane, ddacc[threadIdx.x >> 6]);
     }
 }
 
