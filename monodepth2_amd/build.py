@@ -36,12 +36,33 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+# Per-source extra flags.  md2hot.hip: no SLP vectorisation — packed-f32 VALU
+# (v_pk_fma_f32 / v_pk_mul_f32) issues no faster than two scalar ops on gfx950 and the
+# register pairs it needs cost ~100 v_mov per row step of the photometric kernels;
+# measured: photo_bwd 0.306 -> 0.287 ms at B=12 640x192.
+FLAGS = {"md2hot.hip": ["-fno-slp-vectorize"]}
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB_PATH
+    import concurrent.futures as cf
+    objdir = os.path.join(CSRC, "obj")
+    os.makedirs(objdir, exist_ok=True)
+    base = [hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-I" + INCLUDE]
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        cmd = base + FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
     tmp = LIB_PATH + ".tmp"
-    cmd = [hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
-           "-I" + INCLUDE, "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", tmp] + objs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

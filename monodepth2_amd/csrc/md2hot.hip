@@ -93,6 +93,21 @@ __device__ __forceinline__ int xcd_contiguous_block(int bid, int n) {
     return xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
 }
 
+// Loads at a uniform base + a non-negative 32-bit element index: the byte offset is
+// formed in 32 bits, so the compiler emits the SGPR-base + VGPR-offset form of
+// global_load (no 64-bit address arithmetic per lane).  ldf2 fetches two adjacent
+// floats as one global_load_dwordx2 (4-byte alignment suffices on gfx950).  The
+// photo kernels are bound by vector-memory instruction throughput (profiles/r01),
+// so each load instruction saved counts.
+typedef float float2_a4 __attribute__((ext_vector_type(2), aligned(4)));
+__device__ __forceinline__ float ldf(const float* base, int idx) {
+    return *(const float*)((const char*)base + ((uint32_t)idx << 2));
+}
+__device__ __forceinline__ float2_a4 ldf2(const float* base, int idx) {
+    return *(const float2_a4*)((const char*)base + ((uint32_t)idx << 2));
+}
+__device__ __forceinline__ uint8_t ldb(const uint8_t* base, int idx) { return base[(uint32_t)idx]; }
+
 __device__ __forceinline__ float signf(float v) { return (v > 0.f) ? 1.f : ((v < 0.f) ? -1.f : 0.f); }
 
 // counter-based normal deviate for the tie-break noise (trainer.py:468)
@@ -146,17 +161,20 @@ struct WarpCtx {
 
 // bilinear upsample, align_corners=False (ATen area_pixel_compute_source_index)
 __device__ __forceinline__ float disp_at(const WarpCtx& c, int y, int x) {
-    if (c.upsh == 0) return c.disp[y * c.dw + x];
+    if (c.upsh == 0) return ldf(c.disp, y * c.dw + x);
     const float sc = 1.0f / (float)(1 << c.upsh);
     const float sy = fmaxf(((float)y + 0.5f) * sc - 0.5f, 0.f);
     const float sx = fmaxf(((float)x + 0.5f) * sc - 0.5f, 0.f);
     const int y0 = min((int)sy, c.dh - 1), x0 = min((int)sx, c.dw - 1);
-    const int y1 = y0 + (y0 < c.dh - 1 ? 1 : 0), x1 = x0 + (x0 < c.dw - 1 ? 1 : 0);
+    const int y1 = y0 + (y0 < c.dh - 1 ? 1 : 0);
+    const bool xin = x0 < c.dw - 1;   // x1 = x0 + 1, else x1 = x0 (right border)
     const float ly1 = fminf(fmaxf(sy - (float)y0, 0.f), 1.f), lx1 = fminf(fmaxf(sx - (float)x0, 0.f), 1.f);
     const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
-    const float* r0 = c.disp + y0 * c.dw;
-    const float* r1 = c.disp + y1 * c.dw;
-    return ly0 * (lx0 * r0[x0] + lx1 * r0[x1]) + ly1 * (lx0 * r1[x0] + lx1 * r1[x1]);
+    // (x0, x1) as one pair load; at the right border the pair starts one column left
+    const int xa = xin ? x0 : x0 - 1;
+    const float2_a4 t = ldf2(c.disp, y0 * c.dw + xa), u = ldf2(c.disp, y1 * c.dw + xa);
+    const float t0 = xin ? t.x : t.y, u0 = xin ? u.x : u.y;
+    return ly0 * (lx0 * t0 + lx1 * t.y) + ly1 * (lx0 * u0 + lx1 * u.y);
 }
 
 // one projected sample: the forward values the backward chain needs
@@ -253,19 +271,24 @@ struct Corners {
     float nw[3], ne[3], sw[3], se[3];
 };
 
+// Horizontally adjacent corners (nw, ne) and (sw, se) are fetched as one 8-byte pair
+// per row and channel: 6 gather instructions per sample instead of 12, the same
+// bytes.  At the right border (x0 = w-1, where ne is masked) the pair starts one
+// column to the left.
 template <class SampleT>
 __device__ __forceinline__ void gather(const WarpCtx& c, const SampleT& s, Corners& v) {
     const bool vx1 = s.x0 + 1 < c.w, vy1 = s.y0 + 1 < c.h;
-    const int x1 = vx1 ? s.x0 + 1 : s.x0, y1 = vy1 ? s.y0 + 1 : s.y0;
+    const int y1 = vy1 ? s.y0 + 1 : s.y0;
+    const int xa = vx1 ? s.x0 : s.x0 - 1;
     const int HW = c.h * c.w;
-    const int o00 = s.y0 * c.w + s.x0, o01 = s.y0 * c.w + x1, o10 = y1 * c.w + s.x0, o11 = y1 * c.w + x1;
+    const int ot = s.y0 * c.w + xa, ob = y1 * c.w + xa;
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
-        const float* p = c.src + ch * HW;
-        v.nw[ch] = p[o00];
-        v.ne[ch] = vx1 ? p[o01] : 0.f;
-        v.sw[ch] = vy1 ? p[o10] : 0.f;
-        v.se[ch] = (vx1 && vy1) ? p[o11] : 0.f;
+        const float2_a4 t = ldf2(c.src, ch * HW + ot), u = ldf2(c.src, ch * HW + ob);
+        v.nw[ch] = vx1 ? t.x : t.y;
+        v.ne[ch] = vx1 ? t.y : 0.f;
+        v.sw[ch] = vy1 ? (vx1 ? u.x : u.y) : 0.f;
+        v.se[ch] = (vx1 && vy1) ? u.y : 0.f;
     }
 }
 
@@ -388,7 +411,11 @@ __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int 
 // row loop stays rolled (the per-row state lives in LDS, see photo_fwd_kernel).
 // ----------------------------------------------------------------------------
 template <bool SSIM_ON, bool WARPED, class Emit>
-__device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float* tgt, int r0, int cc, Emit emit) {
+__device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float (*trow)[kWave], int r0, int cc, int lane,
+                                            Emit emit) {
+    // trow: the target rows r0-1 .. r0+kRowsF (reflected), [row * 3 + channel][lane],
+    // staged once per wave in LDS (photo_fwd_kernel) instead of re-read from HBM by
+    // every (scale, frame) pass
     const int h = c.h, w = c.w, HW = h * w;
     if (!SSIM_ON) {
         for (int i = 0; i < kRowsF; ++i) {
@@ -398,11 +425,11 @@ __device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float* tgt, 
                 warp_value(c, rr, cc, x);
             } else {
 #pragma unroll
-                for (int ch = 0; ch < 3; ++ch) x[ch] = c.src[ch * HW + rr * w + cc];
+                for (int ch = 0; ch < 3; ++ch) x[ch] = ldf(c.src, ch * HW + rr * w + cc);
             }
             float l1 = 0.f;
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) l1 += fabsf(tgt[ch * HW + rr * w + cc] - x[ch]);
+            for (int ch = 0; ch < 3; ++ch) l1 += fabsf(trow[(i + 1) * 3 + ch][lane] - x[ch]);
             emit(i, l1 / 3.f);
         }
         return;
@@ -416,10 +443,10 @@ __device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float* tgt, 
             warp_value(c, rr, cc, x);
         } else {
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) x[ch] = c.src[ch * HW + rr * w + cc];
+            for (int ch = 0; ch < 3; ++ch) x[ch] = ldf(c.src, ch * HW + rr * w + cc);
         }
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) y[ch] = tgt[ch * HW + rr * w + cc];
+        for (int ch = 0; ch < 3; ++ch) y[ch] = trow[k * 3 + ch][lane];
         H5 hc[3];
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) hc[ch] = hsum(x[ch], y[ch]);
@@ -445,6 +472,7 @@ __device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float* tgt, 
 // per-wave LDS state, lane-major so every access is one conflict-free ds op
 template <int NS>
 struct FwdState {
+    float tgt[(kRowsF + 2) * 3][kWave];   // target rows r0-1 .. r0+kRowsF, 3 channels
     float ident[NS][kRowsF][kWave];
     float best[kRowsF][kWave];
     float accum[kRowsF][kWave];
@@ -472,6 +500,12 @@ __global__ __launch_bounds__(kBlock, 2) void photo_fwd_kernel(PhotoArgs a) {
     const bool avg = (a.flags & MD2_AVG_REPROJECTION) != 0;
     const int C = avg ? 1 : NS;
 
+    for (int k = 0; k < kRowsF + 2; ++k) {
+        const int rr = reflect_clamp(r0 - 1 + k, h);
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) L.tgt[k * 3 + ch][lane] = ldf(tgt, ch * HW + rr * w + cc);
+    }
+
     // identity reprojection losses (trainer.py:432-439); scale-invariant here
     if (automask) {
         for (int f = 0; f < NS; ++f) {
@@ -479,7 +513,7 @@ __global__ __launch_bounds__(kBlock, 2) void photo_fwd_kernel(PhotoArgs a) {
             ctx.src = a.src[f] + (size_t)b * 3 * HW;
             ctx.h = h;
             ctx.w = w;
-            reproj_rows<SSIM_ON, false>(ctx, tgt, r0, cc, [&](int i, float v) { L.ident[f][i][lane] = v; });
+            reproj_rows<SSIM_ON, false>(ctx, L.tgt, r0, cc, lane, [&](int i, float v) { L.ident[f][i][lane] = v; });
         }
     }
 
@@ -519,7 +553,7 @@ __global__ __launch_bounds__(kBlock, 2) void photo_fwd_kernel(PhotoArgs a) {
             WarpCtx ctx;
             make_ctx(a, ls, f, b, ctx);
             const int cand = (automask ? NS : 0) + f;
-            reproj_rows<SSIM_ON, true>(ctx, tgt, r0, cc, [&](int i, float v) {
+            reproj_rows<SSIM_ON, true>(ctx, L.tgt, r0, cc, lane, [&](int i, float v) {
                 if (MASK) v *= pmask[(((size_t)b * NS + f) * h + min(r0 + i, h - 1)) * w + cc];  // trainer.py:455
                 if (avg) {
                     L.accum[i][lane] += v;
@@ -569,7 +603,10 @@ struct Coef {  // horizontally folded SSIM adjoint of one row, 3 channels
 __device__ __forceinline__ float fold_lo(int i) { return i == 0 ? 0.f : (i == 1 ? 2.f : 1.f); }
 __device__ __forceinline__ float fold_hi(int i, int n) { return i == n - 1 ? 0.f : (i == n - 2 ? 2.f : 1.f); }
 
-__device__ __forceinline__ float pick(float wgt, float v) { return wgt == 0.f ? 0.f : wgt * v; }
+// fold weight x value.  The values reaching here are finite (SSIM adjoint terms,
+// zeroed where the loss weight is 0; halo lanes read reflect-clamped pixels), so the
+// plain product equals the select form (w == 0 -> 0) and costs one instruction.
+__device__ __forceinline__ float pick(float wgt, float v) { return wgt * v; }
 
 template <int NS>
 __device__ __forceinline__ float frame_weight(int code, int f, bool automask, bool avg) {
@@ -657,7 +694,7 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
             float x[3], y[3];
             interp(sm, v, x);
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) y[ch] = tgt[ch * HW + rr * w + cc];
+            for (int ch = 0; ch < 3; ++ch) y[ch] = ldf(tgt, ch * HW + rr * w + cc);
             Carry kc;
             if (k >= 2 && k < kRowsB + 2) make_carry(ctx, sm, v, kc);  // only output rows need it
             H5 hc[3];
@@ -670,7 +707,7 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
                 const int p = r - 1;
                 float gp = 0.f;
                 const bool own = colreal && p >= 0 && p < h;
-                if (own) gp = gscale * frame_weight<NS>(sel[p * w + c], f, automask, avg);
+                if (own) gp = gscale * frame_weight<NS>(ldb(sel, p * w + c), f, automask, avg);
                 if (MASK) {
                     // masked = reproj * mask (trainer.py:455): d/dreproj = g*mask, d/dmask = g*reproj
                     const size_t mi = (((size_t)b * NS + f) * h + (own ? p : 0)) * w + (own ? c : 0);
