@@ -299,17 +299,26 @@ def main():
         fwd_ms = kt.fwd_ms / max(kt.n_fwd, 1)
         alg = photo_bwd_bytes(B, H, W, S)
         achieved = alg / (bwd_ms * 1e-3) / 1e9
-        traffic = None
+        traffic, pipe = None, None
         pmc = os.path.join(REPO, "profiles", ROUND, "pmc_traffic.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
-                traffic = json.load(f).get("photo_bwd_kernel_bytes_per_launch")
+                pm = json.load(f)
+            traffic = pm.get("photo_bwd_kernel_bytes_per_launch")
+            # what actually binds the kernel (HBM is not it): the vector-memory pipeline of
+            # its bilinear gathers (texture data unit busy) and VALU issue, from the
+            # committed PMC passes of the same build (rocprofv3, profiles/<round>/)
+            pipe = {"td_busy_frac": pm.get("photo_bwd_td_busy_frac"),
+                    "ta_busy_frac": pm.get("photo_bwd_ta_busy_frac"),
+                    "valu_issue_frac": pm.get("photo_bwd_valu_issue_frac"),
+                    "source": f"profiles/{ROUND}/pmc_traffic.json"}
         roof = {"bound": "hbm", "kernel": "photo_bwd_kernel", "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic, "algorithmic_bytes_per_launch": int(alg),
                 "avg_launch_ms": round(bwd_ms, 5), "launches": kt.n_bwd,
                 "fwd_kernel_avg_ms": round(fwd_ms, 5),
-                "fwd_kernel_gbs": round(photo_fwd_bytes(B, H, W, S) / (fwd_ms * 1e-3) / 1e9, 2)}
+                "fwd_kernel_gbs": round(photo_fwd_bytes(B, H, W, S) / (fwd_ms * 1e-3) / 1e9, 2),
+                "binding_pipeline": pipe}
         log(f"timed: {1e3 * dt / args.steps:.2f} ms/step, photo_bwd {bwd_ms:.3f} ms, photo_fwd {fwd_ms:.3f} ms")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:

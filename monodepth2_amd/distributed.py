@@ -123,7 +123,9 @@ class FlatGradSync:
             buf = torch.zeros(sum(p.numel() for p in plist), dtype=torch.float32, device=plist[0].device)
             off = 0
             for p in plist:
-                p.grad = buf[off:off + p.numel()].view_as(p)
+                # the grad view keeps the parameter's strides (channels_last conv weights):
+                # the gradient layout contract of autograd and the fused Adam kernel
+                p.grad = buf[off:off + p.numel()].as_strided(p.size(), p.stride())
                 off += p.numel()
             self.flat.append(buf)
 

@@ -134,11 +134,11 @@ class Trainer:
                 m.num_batches_tracked = None
         self._bn_steps = 0
         self.batch_pose_pairs = True   # one pose-encoder pass over all frame pairs (bn_groups)
-        # second HIP stream for the pose network (overlaps the depth network); not under
-        # hipGraph capture, whose step is captured on one stream
+        # second HIP stream for the pose network (overlaps the depth network).  Under
+        # hipGraph capture the fork/join (event record + wait) is captured too, so the
+        # graph keeps the two branches independent.
         self._pose_stream = (torch.cuda.Stream(self.device)
-                             if self.device.type == "cuda" and not getattr(self.opt, "hip_graph", False)
-                             and getattr(self.opt, "pose_streams", 1) else None)
+                             if self.device.type == "cuda" and getattr(self.opt, "pose_streams", 1) else None)
 
         # gradient averaging: DDP (hooks, overlapped with backward) for eager steps, flat
         # buckets + one RCCL all-reduce each (graph-capturable) for --hip_graph
@@ -156,9 +156,10 @@ class Trainer:
         self.graph = None
         self.seed_tensor = None
 
-        # one fused multi-tensor Adam kernel per step (not the foreach chain)
+        # one fused multi-tensor Adam kernel per step (not the foreach chain); capturable
+        # (device-side step counters) under hipGraph
         self.model_optimizer = optim.Adam(self.parameters_to_train, self.opt.learning_rate,
-                                          capturable=self.use_graph, fused=not self.use_graph)
+                                          capturable=self.use_graph, fused=self.device.type == "cuda")
         self.model_lr_scheduler = optim.lr_scheduler.StepLR(self.model_optimizer, self.opt.scheduler_step_size, 0.1)
         if self.opt.load_weights_folder is not None:
             self.load_model()

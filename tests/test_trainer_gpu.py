@@ -148,3 +148,44 @@ def test_checkpoint_roundtrip(tmp_path):
     tr2, _ = make("mono", log_dir=str(tmp_path), load_weights_folder=folder)
     for (n, p), (n2, p2) in zip(tr.nets.named_parameters(), tr2.nets.named_parameters()):
         assert n == n2 and torch.equal(p, p2)
+
+
+def test_hip_graph_replay_matches_eager_step():
+    """A replay of the captured step (networks on two streams, fused hot path,
+    backward, capturable fused Adam) computes what the same step does eagerly from
+    the same state: losses and updated parameters."""
+    tr, batch = make("mono", hip_graph=True)
+    tr.train_step(batch)                       # capture (+ warm-up steps) and one replay
+    tr.train_step(batch)
+    torch.cuda.synchronize()
+    opt_state = [(p, {k: v for k, v in st.items()}) for p, st in tr.model_optimizer.state.items()]
+
+    def snapshot():
+        return ([p.detach().clone() for p in tr.nets.parameters()],
+                [b.detach().clone() for b in tr.nets.buffers()],
+                [{k: v.detach().clone() for k, v in st.items()} for _, st in opt_state],
+                tr.seed_tensor.clone())
+
+    def restore(snap):
+        ps, bs, sts, seed = snap
+        with torch.no_grad():
+            for p, v in zip(tr.nets.parameters(), ps):
+                p.copy_(v)
+            for b, v in zip(tr.nets.buffers(), bs):
+                b.copy_(v)
+            for (_, st), saved in zip(opt_state, sts):
+                for k, v in saved.items():
+                    st[k].copy_(v)
+            tr.seed_tensor.copy_(seed)
+
+    snap = snapshot()
+    _, lg = tr.train_step(batch)               # replay
+    torch.cuda.synchronize()
+    loss_graph = float(lg["loss"])
+    params_graph = [p.detach().clone() for p in tr.nets.parameters()]
+    restore(snap)
+    _, le = tr._step_body(tr.static_inputs)    # the same step, eagerly
+    torch.cuda.synchronize()
+    assert abs(loss_graph - float(le["loss"])) < 1e-6, (loss_graph, float(le["loss"]))
+    worst = max(float((a - b).abs().max()) for a, b in zip(params_graph, tr.nets.parameters()))
+    assert worst < 1e-6, worst

@@ -55,6 +55,12 @@ def main():
             d["hbm_traffic_bytes"] = d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]
         if "SQ_INSTS_VALU" in d and "avg_ns" in d:
             d["valu_issue_frac"] = d["SQ_INSTS_VALU"] / (d["avg_ns"] * 1e-9 * VALU_ISSUE_PER_S)
+        if "TD_TD_BUSY_sum" in d and "GRBM_GUI_ACTIVE" in d:
+            # busy cycles summed over the 256 per-CU units / kernel cycles (GRBM_GUI_ACTIVE
+            # summed over the 8 XCDs): the fraction of the kernel each unit is busy
+            cyc = d["GRBM_GUI_ACTIVE"] / 8.0
+            d["td_busy_frac"] = d["TD_TD_BUSY_sum"] / 256.0 / cyc
+            d["ta_busy_frac"] = d["TA_TA_BUSY_sum"] / 256.0 / cyc
         if "TCC_HIT_sum" in d:
             d["l2_hit_rate"] = d["TCC_HIT_sum"] / max(1.0, d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
     json.dump(res, open(os.path.join(dst, "hot_kernels.json"), "w"), indent=1, sort_keys=True)
@@ -64,6 +70,10 @@ def main():
                "photo_fwd_kernel_bytes_per_launch": fwd.get("hbm_traffic_bytes"),
                "photo_bwd_valu_issue_frac": bwd.get("valu_issue_frac"),
                "photo_fwd_valu_issue_frac": fwd.get("valu_issue_frac"),
+               "photo_bwd_td_busy_frac": bwd.get("td_busy_frac"),
+               "photo_fwd_td_busy_frac": fwd.get("td_busy_frac"),
+               "photo_bwd_ta_busy_frac": bwd.get("ta_busy_frac"),
+               "photo_fwd_ta_busy_frac": fwd.get("ta_busy_frac"),
                "photo_bwd_avg_ns_rocprof": bwd.get("avg_ns"),
                "photo_fwd_avg_ns_rocprof": fwd.get("avg_ns"),
                "note": "traffic = 2*FETCH_SIZE + WRITE_SIZE (KB->B) per launch, separate --pmc passes"}
@@ -72,7 +82,7 @@ def main():
     for k, d in sorted(res.items()):
         print(k, {c: round(v, 4) if isinstance(v, float) else v for c, v in d.items()
                   if c in ("calls", "avg_ns", "share_of_gpu_time", "hbm_traffic_bytes", "valu_issue_frac",
-                           "l2_hit_rate")})
+                           "l2_hit_rate", "td_busy_frac", "ta_busy_frac")})
 
 
 if __name__ == "__main__":
