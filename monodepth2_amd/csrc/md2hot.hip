@@ -933,48 +933,66 @@ __device__ __forceinline__ void block_sum_d(double (&v)[N]) {
     __syncthreads();
 }
 
-// one block; wave w < num_scales reduces scale w's photometric partials, thread t < B
-// of each scale the smoothness chunks of image t (both in a fixed order)
-__global__ __launch_bounds__(kBlock) void finalize_fwd_kernel(FinalArgs a) {
-    __shared__ double photo[MD2_MAX_SCALES];
-    __shared__ double smooth[MD2_MAX_SCALES][kBlock];
+// One block of 16 waves, every assignment fixed (deterministic):
+//   photometric partials: wave w sums quarter w%4 of scale w/4's partials (four
+//   independent accumulators per lane, so the loads of a lane are in flight together);
+//   smoothness: wave w sums the chunk partials of (scale, image) pairs w, w+16, ...
+//   one chunk per lane;
+// then thread 0 combines everything in a fixed order.  (The first version used one
+// wave per scale and one thread per image: ~100 dependent load+add steps, 46 us.)
+constexpr int kFinWaves = 16;
+__global__ __launch_bounds__(kWave * kFinWaves) void finalize_fwd_kernel(FinalArgs a) {
+    __shared__ double photo[MD2_MAX_SCALES][4];
+    __shared__ double smooth[MD2_MAX_SCALES][kBlock];   // [scale][image], B <= kBlock
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    if (wid < a.num_scales) {
-        double acc = 0.0;
-        for (int i = lane; i < a.nphoto[wid]; i += kWave) acc += (double)a.photo_part[wid][i];
-        acc = wave_sum_d(acc);
-        if (lane == 0) photo[wid] = acc;
-    }
-    for (int s = 0; s < a.num_scales; ++s) {
-        double sm = 0.0;
-        const int hs = a.hs[s], ws = a.ws[s];
-        if (t < a.B) {
-            double sd = 0.0, sx = 0.0, sy = 0.0;
-            const float* p = a.smooth_part[s] + (size_t)t * a.chunks[s] * 3;
-            for (int k = 0; k < a.chunks[s]; ++k) {
-                sd += p[3 * k];
-                sx += p[3 * k + 1];
-                sy += p[3 * k + 2];
+    {
+        const int sc = wid >> 2, q = wid & 3;
+        if (sc < a.num_scales) {
+            const int n = a.nphoto[sc];
+            const float* p = a.photo_part[sc];
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+            int i = q * kWave + lane;
+            for (; i + 3 * 4 * kWave < n; i += 4 * 4 * kWave) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[u] += (double)p[i + u * 4 * kWave];
             }
+            for (int u = 0; i < n; i += 4 * kWave, ++u) acc[u & 3] += (double)p[i];
+            double v = wave_sum_d((acc[0] + acc[1]) + (acc[2] + acc[3]));
+            if (lane == 0) photo[sc][q] = v;
+        }
+    }
+    for (int pi = wid; pi < a.num_scales * a.B; pi += kFinWaves) {
+        const int sc = pi / a.B, b = pi - sc * a.B;
+        const int hs = a.hs[sc], ws = a.ws[sc], nch = a.chunks[sc];
+        const float* p = a.smooth_part[sc] + (size_t)b * nch * 3;
+        double sd = 0.0, sx = 0.0, sy = 0.0;
+        for (int k = lane; k < nch; k += kWave) {
+            sd += p[3 * k];
+            sx += p[3 * k + 1];
+            sy += p[3 * k + 2];
+        }
+        sd = wave_sum_d(sd);
+        sx = wave_sum_d(sx);
+        sy = wave_sum_d(sy);
+        if (lane == 0) {
             const double m = sd / ((double)hs * ws) + 1e-7;
-            sm = sx / m / ((double)a.B * hs * (ws - 1)) + sy / m / ((double)a.B * (hs - 1) * ws);
-            float* st = a.stats + ((size_t)s * a.B + t) * 4;
+            smooth[sc][b] = sx / m / ((double)a.B * hs * (ws - 1)) + sy / m / ((double)a.B * (hs - 1) * ws);
+            float* st = a.stats + ((size_t)sc * a.B + b) * 4;
             st[0] = (float)m;
             st[1] = (float)sx;
             st[2] = (float)sy;
             st[3] = 0.f;
         }
-        smooth[s][t] = sm;
     }
     __syncthreads();
     if (t == 0) {
         double total = 0.0;
-        for (int s = 0; s < a.num_scales; ++s) {
+        for (int sc = 0; sc < a.num_scales; ++sc) {
             double sm = 0.0;
-            for (int b = 0; b < a.B; ++b) sm += smooth[s][b];
-            const double loss = photo[s] / ((double)a.B * a.lh[s] * a.lw[s]) +
-                                (double)a.smoothness * sm / (double)(1 << s);
-            a.loss_out[s] = (float)loss;
+            for (int b = 0; b < a.B; ++b) sm += smooth[sc][b];
+            const double ph = (photo[sc][0] + photo[sc][1]) + (photo[sc][2] + photo[sc][3]);
+            const double loss = ph / ((double)a.B * a.lh[sc] * a.lw[sc]) + (double)a.smoothness * sm / (double)(1 << sc);
+            a.loss_out[sc] = (float)loss;
             total += loss;
         }
         a.loss_out[a.num_scales] = (float)(total / a.num_scales);
@@ -985,18 +1003,24 @@ __global__ __launch_bounds__(kBlock) void finalize_fwd_kernel(FinalArgs a) {
 // dL/ddisp_s: adjoint of the bilinear upsample (gather form) + smoothness grad
 // ----------------------------------------------------------------------------
 struct DispGradArgs {
-    int B, num_scales, scale;
-    int hs, ws;          // native resolution of this scale
-    int lh, lw;          // loss resolution (= (hs<<upsh, ws<<upsh))
-    int upsh;
-    const float* dfull;  // (B, lh, lw) dL/d(upsampled disp)
-    const float* disp;   // (B, 1, hs, ws)
-    const float* img;    // (B, 3, hs, ws) target colour at this scale
-    const float* stats;  // [scale][B][4]
+    int B, num_scales;
+    int hs[MD2_MAX_SCALES], ws[MD2_MAX_SCALES];   // native resolution of each scale
+    int lh[MD2_MAX_SCALES], lw[MD2_MAX_SCALES];   // loss resolution (= (hs<<upsh, ws<<upsh))
+    int upsh[MD2_MAX_SCALES];
+    int block_base[MD2_MAX_SCALES + 1];           // first block of each scale (one launch)
+    const float* dfull[MD2_MAX_SCALES];           // (B, lh, lw) dL/d(upsampled disp)
+    const float* disp[MD2_MAX_SCALES];            // (B, 1, hs, ws)
+    const float* img[MD2_MAX_SCALES];             // (B, 3, hs, ws) target colour at this scale
+    const float* stats;                           // [scale][B][4]
     const float* grad_loss;
     float smoothness;
-    float* out;          // (B, 1, hs, ws)
+    float* out[MD2_MAX_SCALES];                   // (B, 1, hs, ws)
 };
+
+// threads per native pixel of a scale: one per row of its upsample footprint
+// (2^(upsh+1) full-resolution rows, capped at 16), so the coarse scales still fill
+// the chip; the row sums are combined by a fixed butterfly (deterministic)
+__host__ __device__ __forceinline__ int disp_grad_group(int upsh) { return upsh == 0 ? 1 : min(2 << upsh, 16); }
 
 // weight of low-res index i in the upsample of full-res index y (factor 2^sh)
 __device__ __forceinline__ float up_weight(int y, int i, int n_in, float sc) {
@@ -1008,49 +1032,53 @@ __device__ __forceinline__ float up_weight(int y, int i, int n_in, float sc) {
 }
 
 __global__ __launch_bounds__(kBlock) void disp_grad_kernel(DispGradArgs a) {
-    const int HWs = a.hs * a.ws;
-    const int idx = blockIdx.x * kBlock + threadIdx.x;
-    if (idx >= a.B * HWs) return;
-    const int b = idx / HWs, p = idx - b * HWs;
-    const int i = p / a.ws, j = p - i * a.ws;
-    const float* df = a.dfull + (size_t)b * a.lh * a.lw;
+    int s = 0;
+    while (s + 1 < a.num_scales && (int)blockIdx.x >= a.block_base[s + 1]) ++s;
+    const int T = disp_grad_group(a.upsh[s]);
+    const int hs = a.hs[s], ws = a.ws[s], lh = a.lh[s], lw = a.lw[s], HWs = hs * ws;
+    const int tid = (blockIdx.x - a.block_base[s]) * kBlock + threadIdx.x;
+    const int idx = tid / T, g = tid - idx * T;        // native pixel, footprint row slot
+    const bool live = idx < a.B * HWs;
+    const int b = live ? idx / HWs : 0, p = live ? idx - b * HWs : 0;
+    const int i = p / ws, j = p - i * ws;
+    const float* df = a.dfull[s] + (size_t)b * lh * lw;
     float acc = 0.f;
-    if (a.upsh == 0) {
-        acc = df[i * a.lw + j];
+    if (a.upsh[s] == 0) {
+        if (live) acc = df[i * lw + j];
     } else {
-        const int k = 1 << a.upsh, half = k >> 1;
+        const int k = 1 << a.upsh[s], half = k >> 1;
         const float sc = 1.0f / (float)k;
-        const int ylo = max(0, k * (i - 1) + half), yhi = min(a.lh, k * (i + 1) + half);
-        const int xlo = max(0, k * (j - 1) + half), xhi = min(a.lw, k * (j + 1) + half);
-        for (int y = ylo; y < yhi; ++y) {
-            const float wy = up_weight(y, i, a.hs, sc);
-            if (wy == 0.f) continue;
-            float row = 0.f;
-            for (int x = xlo; x < xhi; ++x) {
-                const float wx = up_weight(x, j, a.ws, sc);
-                row += wx * df[y * a.lw + x];
+        const int ylo = max(0, k * (i - 1) + half), yhi = min(lh, k * (i + 1) + half);
+        const int xlo = max(0, k * (j - 1) + half), xhi = min(lw, k * (j + 1) + half);
+        if (live) {
+            for (int y = ylo + g; y < yhi; y += T) {
+                const float wy = up_weight(y, i, hs, sc);
+                if (wy == 0.f) continue;
+                float row = 0.f;
+                for (int x = xlo; x < xhi; ++x) row += up_weight(x, j, ws, sc) * df[y * lw + x];
+                acc += wy * row;
             }
-            acc += wy * row;
         }
+        for (int o = 1; o < T; o <<= 1) acc += __shfl_xor(acc, o, kWave);   // T divides 64
     }
+    if (!live || g != 0) return;
     // smoothness gradient on disp / (mean + 1e-7)
-    const int s = a.scale;
-    const float g = a.grad_loss[s] + a.grad_loss[a.num_scales] / (float)a.num_scales;
+    const float gl = a.grad_loss[s] + a.grad_loss[a.num_scales] / (float)a.num_scales;
     const float* st = a.stats + ((size_t)s * a.B + b) * 4;
     const float m = st[0];
-    const float wsm = g * a.smoothness / (float)(1 << s);
-    const float ax = wsm / ((float)a.B * a.hs * (a.ws - 1)) / m;
-    const float ay = wsm / ((float)a.B * (a.hs - 1) * a.ws) / m;
-    const float* d = a.disp + (size_t)b * HWs;
-    const float* img = a.img + (size_t)b * 3 * HWs;
+    const float wsm = gl * a.smoothness / (float)(1 << s);
+    const float ax = wsm / ((float)a.B * hs * (ws - 1)) / m;
+    const float ay = wsm / ((float)a.B * (hs - 1) * ws) / m;
+    const float* d = a.disp[s] + (size_t)b * HWs;
+    const float* img = a.img[s] + (size_t)b * 3 * HWs;
     const float v = d[p];
     float sg = 0.f;
-    if (j + 1 < a.ws) sg += ax * signf(v - d[p + 1]) * edge_weight(img, HWs, p, p + 1);
+    if (j + 1 < ws) sg += ax * signf(v - d[p + 1]) * edge_weight(img, HWs, p, p + 1);
     if (j > 0) sg -= ax * signf(d[p - 1] - v) * edge_weight(img, HWs, p - 1, p);
-    if (i + 1 < a.hs) sg += ay * signf(v - d[p + a.ws]) * edge_weight(img, HWs, p, p + a.ws);
-    if (i > 0) sg -= ay * signf(d[p - a.ws] - v) * edge_weight(img, HWs, p - a.ws, p);
+    if (i + 1 < hs) sg += ay * signf(v - d[p + ws]) * edge_weight(img, HWs, p, p + ws);
+    if (i > 0) sg -= ay * signf(d[p - ws] - v) * edge_weight(img, HWs, p - ws, p);
     sg -= (ax * st[1] + ay * st[2]) / (m * (float)HWs);
-    a.out[(size_t)b * HWs + p] = acc + sg;
+    a.out[s][(size_t)b * HWs + p] = acc + sg;
 }
 
 // ----------------------------------------------------------------------------
@@ -1076,26 +1104,27 @@ __global__ __launch_bounds__(kBlock) void grad_T_kernel(DTArgs a) {
     double dT[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) dT[j] = 0.0;
+    // dT = sum_s K_s^T [dP_s; 0] is linear in the partials: every thread maps its own
+    // partials through K_s^T and sums over the scales, then ONE fixed-order block
+    // reduction of the 16 entries (instead of one 12-entry reduction per scale)
     for (int s = 0; s < a.num_scales; ++s) {
         if (a.per_scale && s != ts) continue;
         const int n = a.wpi[s];
         const float* base = a.dP_part[s] + ((size_t)f * a.B * n + (size_t)b * n) * 12;
-        double dP[12];
-#pragma unroll
-        for (int j = 0; j < 12; ++j) dP[j] = 0.0;
-        for (int k = t; k < n; k += kBlock) {
-#pragma unroll
-            for (int j = 0; j < 12; ++j) dP[j] += (double)base[(size_t)k * 12 + j];
-        }
-        block_sum_d<12>(dP);
         const float* K = a.K[s] + b * 16;
+        for (int k = t; k < n; k += kBlock) {
+            double dP[12];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+            for (int j = 0; j < 12; ++j) dP[j] = (double)base[(size_t)k * 12 + j];
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-                dT[r * 4 + c] += (double)K[0 * 4 + r] * dP[0 * 4 + c] + (double)K[1 * 4 + r] * dP[1 * 4 + c] +
-                                 (double)K[2 * 4 + r] * dP[2 * 4 + c];
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    dT[r * 4 + c] += (double)K[0 * 4 + r] * dP[0 * 4 + c] + (double)K[1 * 4 + r] * dP[1 * 4 + c] +
+                                     (double)K[2 * 4 + r] * dP[2 * 4 + c];
+        }
     }
+    block_sum_d<16>(dT);
     if (t < 16) {
         double v = 0.0;
 #pragma unroll
@@ -1470,7 +1499,7 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
     fa.smoothness = d->disparity_smoothness;
     fa.loss_out = loss_out;
     if (L.B > kBlock) return fail(MD2_ERR_ARG, "batch > %d not supported by the finalize kernel", kBlock);
-    hipLaunchKernelGGL(finalize_fwd_kernel, dim3(1), dim3(kBlock), 0, st, fa);
+    hipLaunchKernelGGL(finalize_fwd_kernel, dim3(1), dim3(kWave * kFinWaves), 0, st, fa);
     return hip_check("finalize_fwd_kernel");
 }
 
@@ -1504,27 +1533,30 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
     }
     if ((rc = hip_check("photo_bwd_kernel"))) return rc;
 
-    for (int s = 0; s < L.nscales; ++s) {
-        DispGradArgs g;
-        memset(&g, 0, sizeof(g));
-        g.B = L.B;
-        g.num_scales = L.nscales;
-        g.scale = s;
-        g.hs = L.hs[s];
-        g.ws = L.ws[s];
-        g.lh = L.lh[s];
-        g.lw = L.lw[s];
-        g.upsh = L.v1 ? 0 : s;
-        g.dfull = (const float*)(ws + L.dfull_off[s]);
-        g.disp = t->disp[s];
-        g.img = t->color[s][0];
-        g.stats = (const float*)(ws + L.stats_off);
-        g.grad_loss = grad_loss;
-        g.smoothness = d->disparity_smoothness;
-        g.out = grad_disp[s];
-        const int n = L.B * L.hs[s] * L.ws[s];
-        hipLaunchKernelGGL(disp_grad_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, g);
+    DispGradArgs g;
+    memset(&g, 0, sizeof(g));
+    g.B = L.B;
+    g.num_scales = L.nscales;
+    g.stats = (const float*)(ws + L.stats_off);
+    g.grad_loss = grad_loss;
+    g.smoothness = d->disparity_smoothness;
+    int gblocks = 0;
+    for (int s = 0; s < L.nscales; ++s) {   // all scales in one launch
+        g.hs[s] = L.hs[s];
+        g.ws[s] = L.ws[s];
+        g.lh[s] = L.lh[s];
+        g.lw[s] = L.lw[s];
+        g.upsh[s] = L.v1 ? 0 : s;
+        g.dfull[s] = (const float*)(ws + L.dfull_off[s]);
+        g.disp[s] = t->disp[s];
+        g.img[s] = t->color[s][0];
+        g.out[s] = grad_disp[s];
+        g.block_base[s] = gblocks;
+        const long long n = (long long)L.B * L.hs[s] * L.ws[s] * disp_grad_group(g.upsh[s]);
+        gblocks += (int)((n + kBlock - 1) / kBlock);
     }
+    g.block_base[L.nscales] = gblocks;
+    hipLaunchKernelGGL(disp_grad_kernel, dim3(gblocks), dim3(kBlock), 0, st, g);
     if ((rc = hip_check("disp_grad_kernel"))) return rc;
 
     DTArgs ta;
