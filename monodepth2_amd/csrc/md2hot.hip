@@ -50,6 +50,15 @@ constexpr int kBwdCols = kWave - 4;  // output columns per backward strip
 #ifndef MD2_ROWS_B
 #define MD2_ROWS_B 16
 #endif
+// minimum resident 256-thread blocks per CU (__launch_bounds__): 2 = 2 waves/SIMD
+// (<= 256 VGPRs), 3 = 3 waves/SIMD (<= 168).  The forward's gathers hide better at 3
+// (0.263 -> 0.248 ms, 12 B/lane of spills); the backward spills 164 B/lane at 3.
+#ifndef MD2_FWD_MINB
+#define MD2_FWD_MINB 3
+#endif
+#ifndef MD2_BWD_MINB
+#define MD2_BWD_MINB 2
+#endif
 constexpr int kRowsF = MD2_ROWS_F;   // output rows per forward work item
 constexpr int kRowsB = MD2_ROWS_B;   // output rows per backward work item
 constexpr int kSmoothChunk = 2048;   // pixels per smoothness partial
@@ -480,7 +489,7 @@ struct FwdState {
 };
 
 template <int NS, bool SSIM_ON, bool MASK>
-__global__ __launch_bounds__(kBlock, 2) void photo_fwd_kernel(PhotoArgs a) {
+__global__ __launch_bounds__(kBlock, MD2_FWD_MINB) void photo_fwd_kernel(PhotoArgs a) {
     __shared__ FwdState<NS> lds[kWavesPerBlock];
     const int lane = threadIdx.x & (kWave - 1);
     FwdState<NS>& L = lds[threadIdx.x >> 6];
@@ -809,7 +818,7 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
 // Resident waves walk the (image, row block, strip, scale) items; each XCD owns a
 // contiguous item range (its L2 streams a contiguous slice of the images).
 template <int NS, bool SSIM_ON, bool MASK>
-__global__ __launch_bounds__(kBlock, 2) void photo_bwd_kernel(PhotoArgs a) {
+__global__ __launch_bounds__(kBlock, MD2_BWD_MINB) void photo_bwd_kernel(PhotoArgs a) {
     __shared__ float ddacc[kWavesPerBlock][kRowsB][kWave];   // dL/d(upsampled disp) summed over frames
     const int lane = threadIdx.x & (kWave - 1);
     // G groups of blocks (the 8 XCDs under round-robin dispatch; fewer for tiny grids)
