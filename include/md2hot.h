@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 2
+#define MD2_ABI_VERSION 3
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -171,10 +171,16 @@ typedef struct md2_pad_desc {
     uint32_t flags;                         /* MD2_PAD_* */
 } md2_pad_desc;
 
-int md2_decoder_pad_fwd(const md2_pad_desc* desc, const float* x, const float* skip, float* out,
-                        void* stream);
-int md2_decoder_pad_bwd(const md2_pad_desc* desc, const float* x, const float* grad_out, float* grad_x,
-                        float* grad_skip, void* stream);
+/* bias (nullable, (C,) fp32): the bias of the conv that produced x, added here
+ * before the ELU so the conv runs without one (no separate bias-add pass); the
+ * backward then also returns grad_bias = the fixed-order sum of grad_x over
+ * (B, h, w), with `workspace` of md2_decoder_pad_workspace_bytes.  NHWC with
+ * channels a multiple of 4 dividing 1024 (every DepthDecoder width), else MD2_ERR_ARG. */
+size_t md2_decoder_pad_workspace_bytes(const md2_pad_desc* desc);
+int md2_decoder_pad_fwd(const md2_pad_desc* desc, const float* x, const float* skip, const float* bias,
+                        float* out, void* stream);
+int md2_decoder_pad_bwd(const md2_pad_desc* desc, const float* x, const float* bias, const float* grad_out,
+                        float* grad_x, float* grad_skip, float* grad_bias, void* workspace, void* stream);
 
 /*
  * Fused pose producer: transformation_from_parameters

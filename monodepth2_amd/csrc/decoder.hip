@@ -44,6 +44,8 @@ struct PadArgs {
     const float* gout;
     float* gx;
     float* gskip;
+    const float* bias;         // (C,) fp32 bias of the conv that produced x, or null
+    float* gbias_part;         // bwd with bias: per-block partial sums [C][gridDim.x]
 };
 
 // element (b, c, y, x) of a (B, C, Hh, Ww) tensor
@@ -182,6 +184,7 @@ __global__ __launch_bounds__(kThreads) void pad_fwd_v4_kernel(PadArgs a) {
         if (c < a.C) {
             const int sy = UP ? (yy >> 1) : yy, sx = UP ? (xx >> 1) : xx;
             v = md2::ld4T<T>(a.x, (((size_t)b * a.h + sy) * a.w + sx) * a.C + c);
+            if (a.bias) v = add4(v, ld4(a.bias + c));   // the conv's bias, folded in here
             if (ELU) v = {elu(v.x), elu(v.y), elu(v.z), elu(v.w)};
         } else {
             v = md2::ld4T<T>(a.skip, (((size_t)b * a.H + yy) * a.W + xx) * a.Cs + (c - a.C));
@@ -211,11 +214,17 @@ __device__ __forceinline__ float4 fold4(const float* gout, size_t g0, int Wp, in
     return s;
 }
 
+// With a bias, every thread also sums the x-gradient of its channel quad (the quad is
+// fixed per thread: C/4 divides the block and grid strides), the block folds the
+// threads of each quad in a fixed tree and writes one partial per channel; the bias
+// gradient is the fixed-order sum of those partials (bias_grad_kernel).
 template <typename T, bool ELU, bool UP>
 __global__ __launch_bounds__(kThreads) void pad_bwd_v4_kernel(PadArgs a) {
     const int Hp = a.H + 2, Wp = a.W + 2, Ct = a.C + a.Cs, C4 = a.C / 4, Cs4 = a.Cs / 4;
     const long long nx = (long long)a.B * a.h * a.w * C4;
     const long long ns = (long long)a.B * a.H * a.W * Cs4;
+    float4 bsum = {0.f, 0.f, 0.f, 0.f};
+    const float4 bq = a.bias ? ld4(a.bias + 4 * (threadIdx.x % C4)) : float4{0.f, 0.f, 0.f, 0.f};
     for (long long idx = (long long)blockIdx.x * kThreads + threadIdx.x; idx < nx + ns;
          idx += (long long)gridDim.x * kThreads) {
         if (idx < nx) {
@@ -236,10 +245,12 @@ __global__ __launch_bounds__(kThreads) void pad_bwd_v4_kernel(PadArgs a) {
                 s = fold4<T>(a.gout, g, Wp, a.H, a.W, i, j, Ct);
             }
             if (ELU) {
-                const float4 xv = md2::ld4T<T>(a.x, 4 * idx);
+                float4 xv = md2::ld4T<T>(a.x, 4 * idx);
+                if (a.bias) xv = add4(xv, bq);   // ELU' at the biased pre-activation
                 s = {s.x * elu_grad(xv.x), s.y * elu_grad(xv.y), s.z * elu_grad(xv.z), s.w * elu_grad(xv.w)};
             }
             md2::st4T<T>(a.gx, 4 * idx, s);
+            bsum = add4(bsum, s);
         } else {
             const long long k = idx - nx;
             const int c = 4 * (int)(k % Cs4);
@@ -251,6 +262,37 @@ __global__ __launch_bounds__(kThreads) void pad_bwd_v4_kernel(PadArgs a) {
             md2::st4T<T>(a.gskip, 4 * k, fold4<T>(a.gout, (size_t)b * Hp * Wp * Ct + a.C + c, Wp, a.H, a.W, yy, xx, Ct));
         }
     }
+    if (!a.gbias_part) return;   // uniform: every thread of the grid returns here together
+    __shared__ float4 red[kThreads];
+    red[threadIdx.x] = bsum;
+    __syncthreads();
+    for (int half = kThreads / 2; half >= C4; half >>= 1) {   // threads t and t+half share a quad
+        if ((int)threadIdx.x < half) red[threadIdx.x] = add4(red[threadIdx.x], red[threadIdx.x + half]);
+        __syncthreads();
+    }
+    if ((int)threadIdx.x < C4) {
+        const float4 v = red[threadIdx.x];
+        float* p = a.gbias_part + (size_t)4 * threadIdx.x * gridDim.x + blockIdx.x;
+        p[0] = v.x;
+        p[gridDim.x] = v.y;
+        p[2 * gridDim.x] = v.z;
+        p[3 * gridDim.x] = v.w;
+    }
+}
+
+// bias gradient: one block per channel, fixed-order sum of its G block partials
+__global__ __launch_bounds__(kThreads) void bias_grad_kernel(const float* part, int G, float* gbias) {
+    const float* p = part + (size_t)blockIdx.x * G;
+    float acc = 0.f;
+    for (int g = threadIdx.x; g < G; g += kThreads) acc += p[g];
+    __shared__ float red[kThreads];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int half = kThreads / 2; half > 0; half >>= 1) {
+        if ((int)threadIdx.x < half) red[threadIdx.x] += red[threadIdx.x + half];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) gbias[blockIdx.x] = red[0];
 }
 
 using PadFn = void (*)(PadArgs);
@@ -315,12 +357,22 @@ bool make_args(const md2_pad_desc* d, PadArgs& a) {
 
 extern "C" {
 
-int md2_decoder_pad_fwd(const md2_pad_desc* d, const float* x, const float* skip, float* out, void* stream) {
+size_t md2_decoder_pad_workspace_bytes(const md2_pad_desc* d) {
+    PadArgs a = {};
+    if (!make_args(d, a) || !vec4(d)) return 0;
+    const long long n = (long long)a.B * a.C * a.h * a.w + (long long)a.B * a.Cs * a.H * a.W;
+    return sizeof(float) * (size_t)a.C * grid_for(n / 4);
+}
+
+int md2_decoder_pad_fwd(const md2_pad_desc* d, const float* x, const float* skip, const float* bias, float* out,
+                        void* stream) {
     PadArgs a = {};
     if (!make_args(d, a) || !x || !out || (a.Cs > 0 && !skip)) return MD2_ERR_ARG;
+    if (bias && (!vec4(d) || kThreads % (d->channels / 4) != 0)) return MD2_ERR_ARG;   // as the backward
     a.x = x;
     a.skip = skip;
     a.out = out;
+    a.bias = bias;
     const long long n = (long long)a.B * (a.C + a.Cs) * (a.H + 2) * (a.W + 2);
     if (vec4(d)) {
         const bool elu = d->flags & MD2_PAD_ELU, up = d->flags & MD2_PAD_UPSAMPLE;
@@ -332,20 +384,29 @@ int md2_decoder_pad_fwd(const md2_pad_desc* d, const float* x, const float* skip
     return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
 }
 
-int md2_decoder_pad_bwd(const md2_pad_desc* d, const float* x, const float* grad_out, float* grad_x,
-                        float* grad_skip, void* stream) {
+int md2_decoder_pad_bwd(const md2_pad_desc* d, const float* x, const float* bias, const float* grad_out,
+                        float* grad_x, float* grad_skip, float* grad_bias, void* workspace, void* stream) {
     PadArgs a = {};
     if (!make_args(d, a) || !grad_out || !grad_x || (a.Cs > 0 && !grad_skip)) return MD2_ERR_ARG;
     const bool elu = d->flags & MD2_PAD_ELU, up = d->flags & MD2_PAD_UPSAMPLE;
     if (elu && !x) return MD2_ERR_ARG;
+    // bias: the NHWC float4 kernels, with C/4 dividing the block (per-thread channel quad)
+    if ((bias || grad_bias) && (!vec4(d) || kThreads % (d->channels / 4) != 0)) return MD2_ERR_ARG;
+    if (grad_bias && !workspace) return MD2_ERR_ARG;
     a.x = x;
     a.gout = grad_out;
     a.gx = grad_x;
     a.gskip = grad_skip;
+    a.bias = bias;
+    a.gbias_part = grad_bias ? (float*)workspace : nullptr;
     const long long n = (long long)a.B * a.C * a.h * a.w + (long long)a.B * a.Cs * a.H * a.W;
     if (vec4(d)) {
         PadFn k = (d->flags & MD2_PAD_BF16) ? v4_bwd<uint16_t>(elu, up) : v4_bwd<float>(elu, up);
-        hipLaunchKernelGGL(k, dim3(grid_for(n / 4)), dim3(kThreads), 0, (hipStream_t)stream, a);
+        const int G = grid_for(n / 4);
+        hipLaunchKernelGGL(k, dim3(G), dim3(kThreads), 0, (hipStream_t)stream, a);
+        if (grad_bias)
+            hipLaunchKernelGGL(bias_grad_kernel, dim3(a.C), dim3(kThreads), 0, (hipStream_t)stream,
+                               (const float*)workspace, G, grad_bias);
         return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
     }
     hipLaunchKernelGGL(bwd_kernel(d->flags), dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, a);

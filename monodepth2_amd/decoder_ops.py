@@ -27,7 +27,7 @@ def _flags(elu: bool, upsample: bool, nhwc: bool, bf16: bool = False) -> int:
 class _ConvInput(torch.autograd.Function):
 
     @staticmethod
-    def forward(ctx, x, skip, elu: bool, upsample: bool, nhwc: bool):
+    def forward(ctx, x, skip, bias, elu: bool, upsample: bool, nhwc: bool):
         fmt = _CL if nhwc else torch.contiguous_format
         x = x.contiguous(memory_format=fmt)
         skip = skip.contiguous(memory_format=fmt) if skip is not None else None
@@ -41,19 +41,22 @@ class _ConvInput(torch.autograd.Function):
         if skip is not None and skip.dtype != x.dtype:
             skip = skip.to(x.dtype)
         d = _lib.PadDesc(B, C, h, w, Cs, _flags(elu, upsample, nhwc, bf16))
+        bias32 = bias.detach().float().contiguous() if bias is not None else None
         rc = _lib.lib().md2_decoder_pad_fwd(ctypes.byref(d), x.data_ptr(),
-                                            skip.data_ptr() if skip is not None else None, out.data_ptr(),
+                                            skip.data_ptr() if skip is not None else None,
+                                            bias32.data_ptr() if bias32 is not None else None, out.data_ptr(),
                                             torch.cuda.current_stream(x.device).cuda_stream)
         _lib.check(rc, "md2_decoder_pad_fwd")
         ctx.elu, ctx.upsample, ctx.has_skip, ctx.nhwc, ctx.bf16 = elu, upsample, skip is not None, nhwc, bf16
         ctx.skip_shape = None if skip is None else skip.shape
-        ctx.save_for_backward(x if elu else None)
+        ctx.bias_dtype = None if bias is None else bias.dtype
+        ctx.save_for_backward(x if elu else None, bias32)
         ctx.x_shape = x.shape
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        (x,) = ctx.saved_tensors
+        x, bias32 = ctx.saved_tensors
         fmt = _CL if ctx.nhwc else torch.contiguous_format
         gout = gout.to(torch.bfloat16 if ctx.bf16 else torch.float32).contiguous(memory_format=fmt)
         B, C, h, w = ctx.x_shape
@@ -62,24 +65,43 @@ class _ConvInput(torch.autograd.Function):
                  if ctx.has_skip else None)
         d = _lib.PadDesc(B, C, h, w, 0 if gskip is None else ctx.skip_shape[1],
                          _flags(ctx.elu, ctx.upsample, ctx.nhwc, ctx.bf16))
+        gbias = ws = None
+        if bias32 is not None:
+            gbias = torch.empty(C, device=gout.device, dtype=torch.float32)
+            ws = torch.empty(_lib.lib().md2_decoder_pad_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
+                             device=gout.device)
         rc = _lib.lib().md2_decoder_pad_bwd(ctypes.byref(d), x.data_ptr() if x is not None else None,
+                                            bias32.data_ptr() if bias32 is not None else None,
                                             gout.data_ptr(), gx.data_ptr(),
                                             gskip.data_ptr() if gskip is not None else None,
+                                            gbias.data_ptr() if gbias is not None else None,
+                                            ws.data_ptr() if ws is not None else None,
                                             torch.cuda.current_stream(gout.device).cuda_stream)
         _lib.check(rc, "md2_decoder_pad_bwd")
-        return gx, gskip, None, None, None
+        if gbias is not None and ctx.bias_dtype != torch.float32:
+            gbias = gbias.to(ctx.bias_dtype)
+        return gx, gskip, gbias, None, None, None
 
 
 def supports_bf16(x: torch.Tensor, skip: Optional[torch.Tensor], nhwc: bool) -> bool:
     return nhwc and x.shape[1] % 4 == 0 and (skip is None or skip.shape[1] % 4 == 0)
 
 
+def supports_bias(channels: int, nhwc: bool) -> bool:
+    """A conv bias over `channels` can be folded into conv_input (NHWC, C/4 dividing 256)."""
+    return nhwc and channels % 4 == 0 and 256 % (channels // 4) == 0
+
+
 def conv_input(x: torch.Tensor, skip: Optional[torch.Tensor] = None, elu: bool = False,
-               upsample: bool = False, nhwc: bool = False) -> torch.Tensor:
-    """ReflectionPad2d(1)(cat([upsample?(elu?(x)), skip], 1)) in one fused pass.
-    nhwc: tensors in (and out) channels_last, as the NHWC convolutions around it."""
+               upsample: bool = False, nhwc: bool = False, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """ReflectionPad2d(1)(cat([upsample?(elu?(x + bias)), skip], 1)) in one fused pass.
+    nhwc: tensors in (and out) channels_last, as the NHWC convolutions around it.
+    bias: the bias of the conv that produced x (that conv then runs without one);
+    its gradient comes back from the same backward pass."""
     if x.device.type != "cuda":
         raise RuntimeError("conv_input is a HIP kernel; use the eager chain on the CPU")
     if x.dtype != torch.float32 and not (x.dtype == torch.bfloat16 and supports_bf16(x, skip, nhwc)):
         raise ValueError("conv_input supports float32, and bfloat16 in NHWC with channel counts multiple of 4")
-    return _ConvInput.apply(x, skip, elu, upsample, nhwc)
+    if bias is not None and not supports_bias(x.shape[1], nhwc):
+        raise ValueError("conv_input folds a bias only in NHWC with C/4 dividing 256")
+    return _ConvInput.apply(x, skip, bias, elu, upsample, nhwc)

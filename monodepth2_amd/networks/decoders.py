@@ -10,6 +10,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from ..layers import Conv3x3, ConvBlock, upsample
 
@@ -49,17 +50,27 @@ class DepthDecoder(nn.Module):
         """Same graph with each conv input built by one HIP pass (decoder_ops):
         pad(x) -> conv -> [ELU -> up x2 -> cat skip -> pad] -> conv -> [ELU -> pad] ->
         (dispconv -> sigmoid) and the next level's first conv."""
-        from ..decoder_ops import conv_input
+        from ..decoder_ops import conv_input, supports_bias
         self.outputs = {}
         # NHWC convolutions (channels_last weights): keep every conv input NHWC too
         cl = self.convs[("upconv", 4, 0)].conv.conv.weight.is_contiguous(memory_format=torch.channels_last)
         P = conv_input(input_features[-1], nhwc=cl)               # ReflectionPad2d only
+
+        def conv(block, P):
+            """The block's conv; its bias moves into the next conv_input when that can
+            fold it (NHWC: no separate bias-add pass forward, no bias-grad reduction
+            backward — the pad kernels carry both)."""
+            c = block.conv.conv
+            if c.bias is not None and supports_bias(c.out_channels, cl):
+                return F.conv2d(P, c.weight, None, c.stride, c.padding, c.dilation, c.groups), c.bias
+            return c(P), None
+
         for i in range(4, -1, -1):
-            y0 = self.convs[("upconv", i, 0)].conv.conv(P)
+            y0, b0 = conv(self.convs[("upconv", i, 0)], P)
             skip = input_features[i - 1] if (self.use_skips and i > 0) else None
-            P = conv_input(y0, skip, elu=True, upsample=True, nhwc=cl)
-            y1 = self.convs[("upconv", i, 1)].conv.conv(P)
-            P = conv_input(y1, None, elu=True, upsample=False, nhwc=cl)   # shared by dispconv and the next level
+            P = conv_input(y0, skip, elu=True, upsample=True, nhwc=cl, bias=b0)
+            y1, b1 = conv(self.convs[("upconv", i, 1)], P)
+            P = conv_input(y1, None, elu=True, upsample=False, nhwc=cl, bias=b1)   # shared by dispconv and the next level
             if i in self.scales:
                 self.outputs[("disp", i)] = self.sigmoid(self.convs[("dispconv", i)].conv(P))
         return self.outputs

@@ -40,6 +40,35 @@ def test_conv_input_matches_eager(elu, up, skip_ch, nhwc, C):
         torch.testing.assert_close(gs, gsr, rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("C", [16, 32, 256])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("up,skip_ch", [(True, 64), (False, 0)])
+def test_conv_input_folds_the_conv_bias(C, dtype, up, skip_ch):
+    """conv_input(x, bias=b) == eager pad(cat(up(elu(x + b)), skip)); grads w.r.t. x, skip
+    and b (the fused fixed-order bias-gradient reduction vs autograd's sum)."""
+    torch.manual_seed(1)
+    cl = torch.channels_last
+    x = torch.randn(4, C, 12, 20, device="cuda").to(dtype).contiguous(memory_format=cl).requires_grad_(True)
+    b = torch.randn(C, device="cuda", requires_grad=True)
+    H, W = (24, 40) if up else (12, 20)
+    skip = (torch.randn(4, skip_ch, H, W, device="cuda").to(dtype).contiguous(memory_format=cl).requires_grad_(True)
+            if skip_ch else None)
+    out = conv_input(x, skip, elu=True, upsample=up, nhwc=True, bias=b)
+    y = torch.nn.functional.elu(x.float() + b.view(1, -1, 1, 1))
+    if up:
+        y = torch.nn.functional.interpolate(y, scale_factor=2, mode="nearest")
+    if skip is not None:
+        y = torch.cat([y, skip.float()], 1)
+    ref = torch.nn.functional.pad(y, (1, 1, 1, 1), mode="reflect")
+    tol = dict(rtol=1e-6, atol=1e-6) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(out.float(), ref, **tol)
+    g = torch.randn(ref.shape, device="cuda")
+    gx, gb = torch.autograd.grad(out, (x, b), g.to(dtype).contiguous(memory_format=cl), retain_graph=True)
+    gxr, gbr = torch.autograd.grad(ref, (x, b), g.to(dtype).float())
+    torch.testing.assert_close(gx.float(), gxr.float(), **tol)
+    torch.testing.assert_close(gb, gbr, rtol=1e-4 if dtype == torch.float32 else 2e-2, atol=1e-3)
+
+
 def test_conv_input_bf16_matches_eager():
     """bf16 NHWC (--amp bf16): copies are exact, ELU rounded once to bf16."""
     torch.manual_seed(3)
