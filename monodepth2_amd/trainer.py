@@ -251,8 +251,21 @@ class Trainer:
                 # every pair through the pose network as ONE batch; BatchNorm keeps per-pair
                 # statistics (bn_groups), so this equals the reference's one call per pair
                 B = self.opt.batch_size
+                # the (pairs*B, 6, H, W) encoder input written straight into the layout of
+                # the encoder's first conv (one strided copy per frame slot, no cat chain
+                # + layout conversion); the frames are data, no gradient flows back
+                enc = models["pose_encoder"]
+                w0 = next(enc.parameters())
+                fmt = (torch.channels_last if w0.is_contiguous(memory_format=torch.channels_last)
+                       and w0.dim() == 4 and w0.shape[1] > 1 else torch.contiguous_format)
+                p0 = pairs[0][0]
+                x = torch.empty(len(pairs) * B, 6, p0.shape[2], p0.shape[3], device=p0.device, dtype=p0.dtype,
+                                memory_format=fmt)
+                for k, (a_, b_) in enumerate(pairs):
+                    x[k * B:(k + 1) * B, 0:3].copy_(a_)
+                    x[k * B:(k + 1) * B, 3:6].copy_(b_)
                 with bn_groups(len(temporal)):
-                    feats = models["pose_encoder"](torch.cat([torch.cat(p, 1) for p in pairs], 0))
+                    feats = enc(x)
                 axisangle_all, translation_all = models["pose"]([feats])
                 per_pair = [(axisangle_all[i * B:(i + 1) * B], translation_all[i * B:(i + 1) * B])
                             for i in range(len(temporal))]
@@ -379,9 +392,10 @@ class Trainer:
         losses = {"loss/{}".format(s): loss_vec[s] for s in range(self.num_scales)}
         losses["loss"] = loss_vec[self.num_scales]
         if not self.opt.disable_automasking:
+            # trainer.py:481-482, all scales in one compare + one cast over the packed map
             C = self.hot.noise_channels()
-            for s, m in selection_maps(self.hot, sel).items():
-                outputs["identity_selection/{}".format(s)] = (m > C - 1).float()
+            for s, m in selection_maps(self.hot, sel.gt(C - 1).float()).items():
+                outputs["identity_selection/{}".format(s)] = m
         return losses
 
     def process_batch(self, inputs):
