@@ -319,7 +319,8 @@ def main():
                 "fwd_kernel_avg_ms": round(fwd_ms, 5),
                 "fwd_kernel_gbs": round(photo_fwd_bytes(B, H, W, S) / (fwd_ms * 1e-3) / 1e9, 2),
                 "binding_pipeline": pipe}
-        log(f"timed: {1e3 * dt / args.steps:.2f} ms/step, photo_bwd {bwd_ms:.3f} ms, photo_fwd {fwd_ms:.3f} ms")
+        log(f"timed: {1e3 * dt / args.steps:.2f} ms/step, photo_bwd {bwd_ms:.3f} ms, photo_fwd {fwd_ms:.3f} ms, "
+            f"adam table uploads {getattr(trainer.model_optimizer, 'rebuilds', '-')}")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args)

@@ -183,6 +183,29 @@ int md2_decoder_pad_bwd(const md2_pad_desc* desc, const float* x, const float* b
                         float* grad_x, float* grad_skip, float* grad_bias, void* workspace, void* stream);
 
 /*
+ * The optimizer step (torch.optim.Adam as the reference's trainer.py:102-104, 209;
+ * no weight decay / amsgrad) in one launch per 256 parameters over a device table of
+ * chunks.  Every chunk is a contiguous run of n fp32 elements of one parameter with
+ * its gradient and its two moment buffers in the same layout; `step` is the 1-based
+ * step count the bias corrections use.  Returns MD2_OK / MD2_ERR_*.
+ */
+typedef struct md2_adam_chunk {
+    float* p;         /* parameter elements [off, off + n) */
+    float* m;         /* exp_avg, same elements */
+    float* v;         /* exp_avg_sq, same elements */
+    int64_t off;      /* element offset into the parameter's gradient */
+    int64_t n;
+    int32_t param;    /* index into grads[] */
+    int32_t reserved;
+} md2_adam_chunk;
+
+/* table: device array of chunks ordered by param; chunk_start (host, nparams + 1):
+ * first chunk of each parameter; grads (host, nparams): this step's gradient base
+ * pointers (same layout as their parameters). */
+int md2_adam_step(const md2_adam_chunk* table, const int* chunk_start, int nparams, const float* const* grads,
+                  double lr, double beta1, double beta2, double eps, int step, void* stream);
+
+/*
  * Fused pose producer: transformation_from_parameters
  * (layers.py:28-45, with rot_from_axisangle 64-103 and get_translation_matrix
  * 48-61) for every (frame, image) of a step in one launch, and its adjoint.

@@ -1,0 +1,119 @@
+"""Adam for the training step (trainer.py:102-104, 209) with the update in one HIP
+launch (md2_adam_step, csrc/adam.hip).
+
+`FusedAdam` IS a `torch.optim.Adam`: same constructor, param groups, lr scheduler
+hooks and `state_dict()` layout (per parameter `step` (CPU scalar tensor),
+`exp_avg`, `exp_avg_sq`), so reference checkpoints (`adam.pth`) load and save
+unchanged.  Only `step()` differs: instead of torch's multi-tensor kernels it walks a
+device table of <=CHUNK-element chunks (param, exp_avg, exp_avg_sq), built once (those
+buffers do not move), with the step's gradient pointers as kernel arguments — one
+launch per 256 parameters.  Anything the kernel does not cover (CPU tensors, non-fp32,
+sparse grads, a grad whose strides differ from its parameter's, amsgrad, weight
+decay, maximize, capturable) goes through torch's own Adam step.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+CHUNK = 1 << 16   # elements per table entry (one block)
+
+
+class FusedAdam(torch.optim.Adam):
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        super().__init__(params, lr=lr, betas=betas, eps=eps)
+        self._key = None
+        self._table = None
+        self._starts = None
+        self._grads = None
+        self.rebuilds = 0   # chunk-table uploads (a parameter or moment buffer moved)
+
+    def _eligible(self) -> bool:
+        for g in self.param_groups:
+            if g["weight_decay"] != 0 or g["amsgrad"] or g["maximize"] or g.get("capturable") \
+                    or g.get("differentiable"):
+                return False
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                if (not p.is_cuda or p.dtype != torch.float32 or p.grad.dtype != torch.float32 or p.grad.is_sparse
+                        or p.grad.stride() != p.stride() or not _dense(p)):
+                    return False
+        return len(self.param_groups) == 1   # one lr / betas / eps per launch
+
+    def _state(self, p):
+        st = self.state[p]
+        if len(st) == 0:
+            st["step"] = torch.tensor(0.0)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        return st
+
+    def _build(self, params):
+        rows, starts = [], [0]
+        for k, p in enumerate(params):
+            st = self.state[p]
+            base = [p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()]
+            n = p.numel()
+            for off in range(0, n, CHUNK):
+                rows.append([b + 4 * off for b in base] + [off, min(CHUNK, n - off), k])
+            starts.append(len(rows))
+        host = torch.from_numpy(np.asarray(rows, dtype=np.int64).reshape(-1)).pin_memory()
+        self._table = torch.empty(host.numel(), dtype=torch.int64, device=params[0].device)
+        self._table.copy_(host, non_blocking=True)
+        self._starts = (ctypes.c_int * len(starts))(*starts)
+        self._grads = (ctypes.c_void_p * len(params))()
+        self.rebuilds += 1
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        if not self._eligible():
+            return super().step()
+        group = self.param_groups[0]
+        params = [p for p in group["params"] if p.grad is not None]
+        if not params:
+            return loss
+        states = [self._state(p) for p in params]
+        # the table holds parameters and moments, which do not move; gradients (new
+        # buffers every step) travel as kernel arguments
+        key = tuple((p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), p.numel())
+                    for p, st in zip(params, states))
+        if key != self._key:
+            # (re)validate what the kernel assumes, then upload the chunk table
+            if (len({float(st["step"]) for st in states}) != 1
+                    or any(st["exp_avg"].stride() != p.stride() or st["exp_avg_sq"].stride() != p.stride()
+                           for p, st in zip(params, states))):
+                self._key = None
+                return super().step()   # mixed step counts / layouts (e.g. a loaded partial state)
+            self._build(params)
+            self._key = key
+        steps = [st["step"] for st in states]
+        torch._foreach_add_(steps, 1)   # CPU scalars, as torch's Adam keeps them
+        step = int(steps[0])
+        b1, b2 = group["betas"]
+        lr = group["lr"]
+        lr = float(lr) if not torch.is_tensor(lr) else float(lr.item())
+        for k, p in enumerate(params):
+            self._grads[k] = p.grad.data_ptr()
+        rc = _lib.lib().md2_adam_step(self._table.data_ptr(), self._starts, len(params), self._grads, lr,
+                                      float(b1), float(b2), float(group["eps"]), step,
+                                      torch.cuda.current_stream(params[0].device).cuda_stream)
+        _lib.check(rc, "md2_adam_step")
+        return loss
+
+
+def _dense(t: torch.Tensor) -> bool:
+    """Non-overlapping and dense: the storage span equals numel (any dim order)."""
+    if t.numel() == 0:
+        return True
+    span = 1 + sum((s - 1) * st for s, st in zip(t.shape, t.stride()) if s > 1)
+    return span == t.numel() and all(st >= 0 for st in t.stride())

@@ -36,6 +36,7 @@ from .distributed import FlatGradSync, wrap_ddp
 from .hotpath import HotPathConfig, generate_images, photometric_loss, predictive_mask_inputs, selection_maps
 from .bn_ops import bn_groups
 from .layers import compute_depth_errors, disp_to_depth
+from .optim import FusedAdam
 from .pose_ops import poses_to_transforms
 
 
@@ -156,10 +157,13 @@ class Trainer:
         self.graph = None
         self.seed_tensor = None
 
-        # one fused multi-tensor Adam kernel per step (not the foreach chain); capturable
-        # (device-side step counters) under hipGraph
-        self.model_optimizer = optim.Adam(self.parameters_to_train, self.opt.learning_rate,
-                                          capturable=self.use_graph, fused=self.device.type == "cuda")
+        # Adam (trainer.py:102): one HIP launch per step over every parameter (optim.py);
+        # under hipGraph torch's capturable fused Adam (device-side step counters)
+        if self.device.type == "cuda" and not self.use_graph:
+            self.model_optimizer = FusedAdam(self.parameters_to_train, self.opt.learning_rate)
+        else:
+            self.model_optimizer = optim.Adam(self.parameters_to_train, self.opt.learning_rate,
+                                              capturable=self.use_graph, fused=self.device.type == "cuda")
         self.model_lr_scheduler = optim.lr_scheduler.StepLR(self.model_optimizer, self.opt.scheduler_step_size, 0.1)
         if self.opt.load_weights_folder is not None:
             self.load_model()

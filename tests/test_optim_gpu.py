@@ -1,0 +1,73 @@
+"""FusedAdam (one HIP launch per step, csrc/adam.hip) vs torch.optim.Adam on the same
+parameters and gradients: updated parameters, moments and the state_dict layout
+(reference checkpoints' adam.pth)."""
+import copy
+
+import pytest
+import torch
+
+from monodepth2_amd.optim import FusedAdam
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    shapes = [(64, 3, 7, 7), (16, 32, 3, 3), (1, 16, 3, 3), (256,), (1,), (100003,), (12, 5)]
+    ps = []
+    for i, sh in enumerate(shapes):
+        t = torch.randn(sh, device="cuda", generator=g)
+        if len(sh) == 4 and i % 2 == 0:
+            t = t.contiguous(memory_format=torch.channels_last)
+        ps.append(torch.nn.Parameter(t))
+    return ps
+
+
+def test_fused_adam_matches_torch_adam():
+    pa, pb = _params(0), _params(0)
+    oa = FusedAdam(pa, lr=1e-3)
+    ob = torch.optim.Adam(pb, lr=1e-3)   # the reference's optimizer (foreach on the GPU)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for step in range(4):
+        for a, b in zip(pa, pb):
+            gr = torch.randn(a.shape, device="cuda", generator=g)
+            if a.dim() == 4 and a.is_contiguous(memory_format=torch.channels_last):
+                gr = gr.contiguous(memory_format=torch.channels_last)   # grads follow their params
+            a.grad = gr.clone()
+            b.grad = gr.clone()
+        oa.step()
+        ob.step()
+        if step == 1:   # the scheduler's lr edit reaches the kernel
+            for o in (oa, ob):
+                o.param_groups[0]["lr"] = 5e-4
+    for a, b in zip(pa, pb):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
+        sa, sb = oa.state[a], ob.state[b]
+        # rounding-level differences only (torch's lerp form of the first-moment update)
+        torch.testing.assert_close(sa["exp_avg"], sb["exp_avg"], rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=1e-5, atol=1e-9)
+        assert float(sa["step"]) == float(sb["step"]) == 4.0
+    assert oa.rebuilds == 1   # parameters and moments never moved
+
+
+def test_fused_adam_state_dict_interchanges_with_torch_adam():
+    pa, pb = _params(2), _params(2)
+    ob = torch.optim.Adam(pb, lr=1e-3)
+    for p in pb:
+        p.grad = torch.ones_like(p)
+    ob.step()
+    oa = FusedAdam(pa, lr=1e-3)
+    # a reference adam.pth into the fused optimizer (deep copy: as torch.save/load would,
+    # so the two optimizers do not share moment buffers)
+    oa.load_state_dict(copy.deepcopy(ob.state_dict()))
+    for a, b in zip(pa, pb):
+        with torch.no_grad():
+            a.copy_(b)
+        a.grad = torch.full_like(a, 0.5)
+        b.grad = torch.full_like(b, 0.5)
+    oa.step()
+    ob.step()
+    for a, b in zip(pa, pb):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
+    sd = oa.state_dict()
+    assert set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"} and sd["state"][0]["step"].device.type == "cpu"
