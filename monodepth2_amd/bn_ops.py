@@ -58,8 +58,9 @@ def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
 
 
 def _supported(C: int) -> bool:
+    """Channel counts the kernels take: C/4 a power of two (every ResNet width)."""
     Q = C // 4
-    return C % 4 == 0 and Q > 0 and (Q % 256 == 0 if Q >= 256 else 256 % Q == 0)
+    return C % 4 == 0 and Q > 0 and (Q & (Q - 1)) == 0
 
 
 class _BNAct(torch.autograd.Function):
@@ -116,6 +117,7 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, residual: Optional[torch.Tensor]
         raise ValueError(f"batch {x.shape[0]} does not split into {groups} BatchNorm groups")
     if (ENABLED and bn.training and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.dim() == 4
             and bn.affine and bn.track_running_stats and bn.momentum is not None and _supported(x.shape[1])
+            and x.numel() // 4 // groups < 2 ** 31   # 32-bit element-quad index per group
             and x.is_contiguous(memory_format=_CL) and x.shape[1] > 1
             and (residual is None or residual.is_contiguous(memory_format=_CL))):
         if residual is not None and residual.dtype != x.dtype:

@@ -180,17 +180,23 @@ __global__ void __launch_bounds__(kThreads) bn_stats_final_kernel(long long P, i
     }
 }
 
+// Elementwise passes: blockIdx.y = BatchNorm group, 32-bit quad index inside the group
+// (valid() bounds it), channel quad = index & (Q - 1) (Q a power of two) — no 64-bit
+// division or modulo per element.
 template <typename T, bool RELU, bool RES>
 __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ r,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta,
                                                             const float* __restrict__ smean,
                                                             const float* __restrict__ sinvstd, void* __restrict__ y,
-                                                            long long n4, int Q, long long q4g) {
-    for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long long)gridDim.x * kThreads) {
-        const int c = 4 * (int)(i % Q);
-        const int cs = c + (q4g ? 4 * Q * (int)(i / q4g) : 0);   // statistics of this pixel's group
-        const float4 v = ldT<T>(x, 4 * i), mu = ld4(smean + cs), is = ld4(sinvstd + cs), ga = ld4(gamma + c),
+                                                            int n4g, int Q) {
+    const size_t base = (size_t)blockIdx.y * n4g;   // this group's first quad
+    const float* mug = smean + (size_t)blockIdx.y * 4 * Q;
+    const float* isg = sinvstd + (size_t)blockIdx.y * 4 * Q;
+    for (int j = blockIdx.x * kThreads + threadIdx.x; j < n4g; j += gridDim.x * kThreads) {
+        const size_t i = base + j;
+        const int c = 4 * (j & (Q - 1));
+        const float4 v = ldT<T>(x, 4 * i), mu = ld4(mug + c), is = ld4(isg + c), ga = ld4(gamma + c),
                      be = ld4(beta + c);
         float4 o;
         o.x = (v.x - mu.x) * is.x * ga.x + be.x;
@@ -283,9 +289,12 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const void* __re
                                                                 const void* __restrict__ g,
                                                                 const float* __restrict__ smean, const float* coef,
                                                                 void* __restrict__ dx, void* __restrict__ dr,
-                                                                long long n4, int Q, int C, int NG, long long q4g) {
-    for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long long)gridDim.x * kThreads) {
-        const int c = 4 * (int)(i % Q) + (q4g ? C * (int)(i / q4g) : 0);   // group * C + channel
+                                                                int n4g, int Q, int C, int NG) {
+    const size_t base = (size_t)blockIdx.y * n4g;
+    const size_t gc = (size_t)blockIdx.y * C;   // group * C
+    for (int j = blockIdx.x * kThreads + threadIdx.x; j < n4g; j += gridDim.x * kThreads) {
+        const size_t i = base + j;
+        const size_t c = gc + 4 * (j & (Q - 1));
         float4 gv = ldT<T>(g, 4 * i);
         if (RELU) {
             const float4 yv = ldT<T>(y, 4 * i);
@@ -311,9 +320,10 @@ int blocks_for_stats(long long P, int C) {
     return (int)(g < 1 ? 1 : (g > kMaxBlocks ? kMaxBlocks : g));
 }
 
-int grid_elem(long long n4) {
+int grid_elem(long long n4, int NG) {   // blocks per group (about 4096 in all)
+    const long long cap = (4096 + NG - 1) / NG;
     const long long g = (n4 + kThreads - 1) / kThreads;
-    return (int)(g < 4096 ? g : 4096);
+    return (int)(g < cap ? g : cap);
 }
 
 int groups_of(const md2_bn_desc* d) { return d->groups > 1 ? d->groups : 1; }
@@ -322,6 +332,8 @@ bool valid(const md2_bn_desc* d) {
     if (!d || d->channels < 4 || d->channels % 4) return false;
     if (d->groups < 0 || d->pixels % groups_of(d) || d->pixels / groups_of(d) < 2) return false;
     const int Q = d->channels / 4;
+    if ((Q & (Q - 1)) != 0) return false;   // channel quads a power of two (every ResNet width)
+    if ((long long)d->pixels / groups_of(d) * Q >= (1ll << 31)) return false;   // 32-bit quad index per group
     return Q >= kThreads ? (Q % kThreads == 0) : (kThreads % Q == 0);
 }
 
@@ -335,12 +347,12 @@ void launch_fwd(const md2_bn_desc* d, const void* x, const float* gamma, const f
     hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(G, NG), dim3(kThreads), 0, st, x, P, C, G, workspace);
     hipLaunchKernelGGL(bn_stats_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, NG, d->eps, d->momentum,
                        running_mean, running_var, save_mean, save_invstd, workspace);
-    const long long n4 = d->pixels * C / 4, q4g = NG > 1 ? P * C / 4 : 0;
+    const int n4g = (int)(P * C / 4);
     const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
     auto k = relu ? (res ? bn_apply_kernel<T, true, true> : bn_apply_kernel<T, true, false>)
                   : (res ? bn_apply_kernel<T, false, true> : bn_apply_kernel<T, false, false>);
-    hipLaunchKernelGGL(k, dim3(grid_elem(n4)), dim3(kThreads), 0, st, x, residual, gamma, beta, save_mean,
-                       save_invstd, y, n4, C / 4, q4g);
+    hipLaunchKernelGGL(k, dim3(grid_elem(n4g, NG), NG), dim3(kThreads), 0, st, x, residual, gamma, beta, save_mean,
+                       save_invstd, y, n4g, C / 4);
 }
 
 template <typename T>
@@ -355,12 +367,12 @@ void launch_bwd(const md2_bn_desc* d, const void* x, const void* y, const void* 
     hipLaunchKernelGGL(red, dim3(G, NG), dim3(kThreads), 0, st, x, y, grad_y, P, C, G, save_mean, workspace);
     hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, NG, gamma, save_invstd,
                        grad_gamma, grad_beta, workspace);
-    const long long n4 = d->pixels * C / 4, q4g = NG > 1 ? P * C / 4 : 0;
+    const int n4g = (int)(P * C / 4);
     const float* coef = work(workspace, G, C, NG).coef;
     auto k = relu ? (res ? bn_bwd_apply_kernel<T, true, true> : bn_bwd_apply_kernel<T, true, false>)
                   : (res ? bn_bwd_apply_kernel<T, false, true> : bn_bwd_apply_kernel<T, false, false>);
-    hipLaunchKernelGGL(k, dim3(grid_elem(n4)), dim3(kThreads), 0, st, x, y, grad_y, save_mean, coef, grad_x,
-                       grad_residual, n4, C / 4, C, NG, q4g);
+    hipLaunchKernelGGL(k, dim3(grid_elem(n4g, NG), NG), dim3(kThreads), 0, st, x, y, grad_y, save_mean, coef,
+                       grad_x, grad_residual, n4g, C / 4, C, NG);
 }
 
 }  // namespace

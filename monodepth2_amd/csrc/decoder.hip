@@ -170,15 +170,14 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) { return {a.x + b.x, 
 template <typename T, bool ELU, bool UP>
 __global__ __launch_bounds__(kThreads) void pad_fwd_v4_kernel(PadArgs a) {
     const int Hp = a.H + 2, Wp = a.W + 2, Ct4 = (a.C + a.Cs) / 4;
-    const long long total = (long long)a.B * Hp * Wp * Ct4;
-    for (long long idx = (long long)blockIdx.x * kThreads + threadIdx.x; idx < total;
-         idx += (long long)gridDim.x * kThreads) {
-        const int c = 4 * (int)(idx % Ct4);
-        long long t = idx / Ct4;
-        const int px = (int)(t % Wp);
+    const int total = a.B * Hp * Wp * Ct4;   // < 2^31 (make_args): 32-bit index math
+    for (int idx = blockIdx.x * kThreads + threadIdx.x; idx < total; idx += gridDim.x * kThreads) {
+        const int c = 4 * (idx % Ct4);
+        int t = idx / Ct4;
+        const int px = t % Wp;
         t /= Wp;
-        const int py = (int)(t % Hp);
-        const int b = (int)(t / Hp);
+        const int py = t % Hp;
+        const int b = t / Hp;
         const int yy = reflect1(py - 1, a.H), xx = reflect1(px - 1, a.W);
         float4 v;
         if (c < a.C) {
@@ -189,7 +188,7 @@ __global__ __launch_bounds__(kThreads) void pad_fwd_v4_kernel(PadArgs a) {
         } else {
             v = md2::ld4T<T>(a.skip, (((size_t)b * a.H + yy) * a.W + xx) * a.Cs + (c - a.C));
         }
-        md2::st4T<T>(a.out, 4 * idx, v);
+        md2::st4T<T>(a.out, 4 * (size_t)idx, v);
     }
 }
 
@@ -221,19 +220,18 @@ __device__ __forceinline__ float4 fold4(const float* gout, size_t g0, int Wp, in
 template <typename T, bool ELU, bool UP>
 __global__ __launch_bounds__(kThreads) void pad_bwd_v4_kernel(PadArgs a) {
     const int Hp = a.H + 2, Wp = a.W + 2, Ct = a.C + a.Cs, C4 = a.C / 4, Cs4 = a.Cs / 4;
-    const long long nx = (long long)a.B * a.h * a.w * C4;
-    const long long ns = (long long)a.B * a.H * a.W * Cs4;
+    const int nx = a.B * a.h * a.w * C4;     // nx + ns < 2^31 (make_args)
+    const int ns = a.B * a.H * a.W * Cs4;
     float4 bsum = {0.f, 0.f, 0.f, 0.f};
     const float4 bq = a.bias ? ld4(a.bias + 4 * (threadIdx.x % C4)) : float4{0.f, 0.f, 0.f, 0.f};
-    for (long long idx = (long long)blockIdx.x * kThreads + threadIdx.x; idx < nx + ns;
-         idx += (long long)gridDim.x * kThreads) {
+    for (int idx = blockIdx.x * kThreads + threadIdx.x; idx < nx + ns; idx += gridDim.x * kThreads) {
         if (idx < nx) {
-            const int c = 4 * (int)(idx % C4);
-            long long t = idx / C4;
-            const int j = (int)(t % a.w);
+            const int c = 4 * (idx % C4);
+            int t = idx / C4;
+            const int j = t % a.w;
             t /= a.w;
-            const int i = (int)(t % a.h);
-            const int b = (int)(t / a.h);
+            const int i = t % a.h;
+            const int b = t / a.h;
             const size_t g = (size_t)b * Hp * Wp * Ct + c;
             float4 s;
             if (UP) {
@@ -245,21 +243,21 @@ __global__ __launch_bounds__(kThreads) void pad_bwd_v4_kernel(PadArgs a) {
                 s = fold4<T>(a.gout, g, Wp, a.H, a.W, i, j, Ct);
             }
             if (ELU) {
-                float4 xv = md2::ld4T<T>(a.x, 4 * idx);
+                float4 xv = md2::ld4T<T>(a.x, 4 * (size_t)idx);
                 if (a.bias) xv = add4(xv, bq);   // ELU' at the biased pre-activation
                 s = {s.x * elu_grad(xv.x), s.y * elu_grad(xv.y), s.z * elu_grad(xv.z), s.w * elu_grad(xv.w)};
             }
-            md2::st4T<T>(a.gx, 4 * idx, s);
+            md2::st4T<T>(a.gx, 4 * (size_t)idx, s);
             bsum = add4(bsum, s);
         } else {
-            const long long k = idx - nx;
-            const int c = 4 * (int)(k % Cs4);
-            long long t = k / Cs4;
-            const int xx = (int)(t % a.W);
+            const int k = idx - nx;
+            const int c = 4 * (k % Cs4);
+            int t = k / Cs4;
+            const int xx = t % a.W;
             t /= a.W;
-            const int yy = (int)(t % a.H);
-            const int b = (int)(t / a.H);
-            md2::st4T<T>(a.gskip, 4 * k, fold4<T>(a.gout, (size_t)b * Hp * Wp * Ct + a.C + c, Wp, a.H, a.W, yy, xx, Ct));
+            const int yy = t % a.H;
+            const int b = t / a.H;
+            md2::st4T<T>(a.gskip, 4 * (size_t)k, fold4<T>(a.gout, (size_t)b * Hp * Wp * Ct + a.C + c, Wp, a.H, a.W, yy, xx, Ct));
         }
     }
     if (!a.gbias_part) return;   // uniform: every thread of the grid returns here together
@@ -350,7 +348,8 @@ bool make_args(const md2_pad_desc* d, PadArgs& a) {
     a.w = d->width;
     a.H = up ? 2 * d->height : d->height;
     a.W = up ? 2 * d->width : d->width;
-    return true;
+    // the float4 kernels index element quads in 32 bits
+    return (long long)a.B * (a.C + a.Cs) * (a.H + 2) * (a.W + 2) < (1ll << 33);
 }
 
 }  // namespace

@@ -38,14 +38,14 @@ template <typename T>
 __global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(PoolArgs p, const void* __restrict__ x,
                                                                void* __restrict__ y, uint32_t* __restrict__ idx) {
     const int C4 = p.C / 4;
-    const long long n = (long long)p.B * p.Ho * p.Wo * C4;
-    for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
-        const int c = 4 * (int)(i % C4);
-        long long t = i / C4;
-        const int ox = (int)(t % p.Wo);
+    const int n = p.B * p.Ho * p.Wo * C4;   // < 2^31 (make()); 32-bit index math
+    for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+        const int c = 4 * (i % C4);
+        int t = i / C4;
+        const int ox = t % p.Wo;
         t /= p.Wo;
-        const int oy = (int)(t % p.Ho);
-        const int b = (int)(t / p.Ho);
+        const int oy = t % p.Ho;
+        const int b = t / p.Ho;
         float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
         const int k0 = (oy == 0 ? 3 : 0) + (ox == 0 ? 1 : 0);   // first tap inside the image
         int a[4] = {k0, k0, k0, k0};
@@ -72,14 +72,14 @@ template <typename T>
 __global__ void __launch_bounds__(kThreads) maxpool_bwd_kernel(PoolArgs p, const uint32_t* __restrict__ idx,
                                                                const void* __restrict__ gy, void* __restrict__ gx) {
     const int C4 = p.C / 4;
-    const long long n = (long long)p.B * p.H * p.W * C4;
-    for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
-        const int c4 = (int)(i % C4);
-        long long t = i / C4;
-        const int ix = (int)(t % p.W);
+    const int n = p.B * p.H * p.W * C4;
+    for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+        const int c4 = i % C4;
+        int t = i / C4;
+        const int ix = t % p.W;
         t /= p.W;
-        const int iy = (int)(t % p.H);
-        const int b = (int)(t / p.H);
+        const int iy = t % p.H;
+        const int b = t / p.H;
         float s[4] = {0.f, 0.f, 0.f, 0.f};
         // windows oy with 2*oy-1 <= iy <= 2*oy+1 (likewise x), in increasing order
         for (int oy = iy / 2; oy <= (iy + 1) / 2; ++oy) {
@@ -113,7 +113,7 @@ bool make(const md2_pool_desc* d, PoolArgs& p) {
     p.W = d->width;
     p.Ho = (d->height + 2 - 3) / 2 + 1;
     p.Wo = (d->width + 2 - 3) / 2 + 1;
-    return true;
+    return (long long)p.B * p.H * p.W * (p.C / 4) < (1ll << 31);   // 32-bit quad indices
 }
 
 }  // namespace
