@@ -183,6 +183,17 @@ int md2_decoder_pad_bwd(const md2_pad_desc* desc, const float* x, const float* b
                         float* grad_x, float* grad_skip, float* grad_bias, void* workspace, void* stream);
 
 /*
+ * The encoders' input (networks/resnet_encoder.py:93 normalisation, trainer.py:280-290
+ * frame-pair concatenation) in one pass: src[g * slots + k] is a (batch,3,H,W) NCHW
+ * fp32 frame tensor; out is (groups*batch, H, W, 3*slots) = a channels_last
+ * (groups*batch, 3*slots, H, W) tensor with out = (src - mean) * (1.f / std) per channel
+ * (torch's fp32 arithmetic for a division by a scalar).
+ * groups * slots <= 8.  Returns MD2_OK / MD2_ERR_*.
+ */
+int md2_encoder_input(int groups, int batch, int slots, int height, int width, const float* const* src, float mean,
+                      float std_, float* out, void* stream);
+
+/*
  * The optimizer step (torch.optim.Adam as the reference's trainer.py:102-104, 209;
  * no weight decay / amsgrad) in one launch per 256 parameters over a device table of
  * chunks.  Every chunk is a contiguous run of n fp32 elements of one parameter with

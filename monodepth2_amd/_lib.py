@@ -56,7 +56,7 @@ _lib = None
 EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_select_bytes",
            "md2_photometric_fwd", "md2_photometric_bwd", "md2_generate_images",
            "md2_timing_begin", "md2_timing_end", "md2_decoder_pad_fwd", "md2_decoder_pad_bwd",
-           "md2_decoder_pad_workspace_bytes", "md2_adam_step",
+           "md2_decoder_pad_workspace_bytes", "md2_adam_step", "md2_encoder_input",
            "md2_pose_fwd", "md2_pose_bwd", "md2_aug_plan_create", "md2_aug_plan_destroy", "md2_aug_run",
            "md2_bn_workspace_bytes", "md2_bn_fwd", "md2_bn_bwd", "md2_maxpool3s2_fwd", "md2_maxpool3s2_bwd"]
 
@@ -123,6 +123,9 @@ def _declare(L):
     L.md2_decoder_pad_fwd.argtypes = [ctypes.POINTER(PadDesc), _vp, _vp, _vp, _vp, _vp]
     L.md2_decoder_pad_bwd.restype = ctypes.c_int
     L.md2_decoder_pad_bwd.argtypes = [ctypes.POINTER(PadDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.md2_encoder_input.restype = ctypes.c_int
+    L.md2_encoder_input.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,
+                                    ctypes.c_float, ctypes.c_float, _vp, _vp]
     L.md2_adam_step.restype = ctypes.c_int
     L.md2_adam_step.argtypes = [_vp, _vp, ctypes.c_int, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                 ctypes.c_double, ctypes.c_int, _vp]

@@ -133,11 +133,41 @@ class ResnetEncoder(nn.Module):
         if num_layers > 34:
             self.num_ch_enc[1:] *= 4
 
-    def forward(self, input_image):
-        e = self.encoder
-        x = (input_image - 0.45) / 0.225
-        if e.conv1.weight.is_contiguous(memory_format=torch.channels_last):
+    MEAN, STD = 0.45, 0.225   # resnet_encoder.py:93
+
+    def prepare(self, frames):
+        """The normalised encoder input.  frames: a (B,3,H,W) tensor, or a list of
+        frame pairs [[(B,3,H,W), (B,3,H,W)], ...] concatenated along channels (pose
+        encoder, trainer.py:280-290) and along the batch.  On the GPU with NHWC
+        convolutions: one HIP pass straight into channels_last (md2_encoder_input)."""
+        groups = [[frames]] if torch.is_tensor(frames) else [list(p) for p in frames]
+        f0 = groups[0][0]
+        if (f0.is_cuda and f0.dtype == torch.float32 and f0.dim() == 4 and f0.shape[1] == 3
+                and self.encoder.conv1.weight.is_contiguous(memory_format=torch.channels_last)
+                and len(groups) * len(groups[0]) <= 8
+                and all(t.shape == f0.shape and t.dtype == f0.dtype and t.is_contiguous() for g in groups for t in g)):
+            import ctypes
+            from .. import _lib
+            B, _, H, W = f0.shape
+            S = len(groups[0])
+            out = torch.empty(len(groups) * B, 3 * S, H, W, device=f0.device, memory_format=torch.channels_last)
+            src = (ctypes.c_void_p * (len(groups) * S))(*[t.data_ptr() for g in groups for t in g])
+            rc = _lib.lib().md2_encoder_input(len(groups), B, S, H, W, src, self.MEAN, self.STD, out.data_ptr(),
+                                              torch.cuda.current_stream(f0.device).cuda_stream)
+            _lib.check(rc, "md2_encoder_input")
+            return out
+        x = torch.cat([torch.cat(g, 1) for g in groups], 0) if len(groups) * len(groups[0]) > 1 else f0
+        x = (x - self.MEAN) / self.STD
+        if self.encoder.conv1.weight.is_contiguous(memory_format=torch.channels_last):
             x = x.contiguous(memory_format=torch.channels_last)
+        return x
+
+    def forward(self, input_image):
+        return self.forward_prepared(self.prepare(input_image))
+
+    def forward_prepared(self, x):
+        """The encoder on an input already normalised by `prepare`."""
+        e = self.encoder
         f0 = bn_act(e.bn1, e.conv1(x))
         f1 = e.layer1(max_pool_3x3s2(e.maxpool, f0))
         f2 = e.layer2(f1)

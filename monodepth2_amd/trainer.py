@@ -255,21 +255,12 @@ class Trainer:
                 # every pair through the pose network as ONE batch; BatchNorm keeps per-pair
                 # statistics (bn_groups), so this equals the reference's one call per pair
                 B = self.opt.batch_size
-                # the (pairs*B, 6, H, W) encoder input written straight into the layout of
-                # the encoder's first conv (one strided copy per frame slot, no cat chain
-                # + layout conversion); the frames are data, no gradient flows back
+                # the (pairs*B, 6, H, W) normalised encoder input in one pass, straight
+                # into the encoder's layout (ResnetEncoder.prepare); the frames are data
                 enc = models["pose_encoder"]
-                w0 = next(enc.parameters())
-                fmt = (torch.channels_last if w0.is_contiguous(memory_format=torch.channels_last)
-                       and w0.dim() == 4 and w0.shape[1] > 1 else torch.contiguous_format)
-                p0 = pairs[0][0]
-                x = torch.empty(len(pairs) * B, 6, p0.shape[2], p0.shape[3], device=p0.device, dtype=p0.dtype,
-                                memory_format=fmt)
-                for k, (a_, b_) in enumerate(pairs):
-                    x[k * B:(k + 1) * B, 0:3].copy_(a_)
-                    x[k * B:(k + 1) * B, 3:6].copy_(b_)
+                x = enc.prepare(pairs)
                 with bn_groups(len(temporal)):
-                    feats = enc(x)
+                    feats = enc.forward_prepared(x)
                 axisangle_all, translation_all = models["pose"]([feats])
                 per_pair = [(axisangle_all[i * B:(i + 1) * B], translation_all[i * B:(i + 1) * B])
                             for i in range(len(temporal))]

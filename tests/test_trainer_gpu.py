@@ -189,3 +189,20 @@ def test_hip_graph_replay_matches_eager_step():
     assert abs(loss_graph - float(le["loss"])) < 1e-6, (loss_graph, float(le["loss"]))
     worst = max(float((a - b).abs().max()) for a, b in zip(params_graph, tr.nets.parameters()))
     assert worst < 1e-6, worst
+
+
+def test_encoder_input_matches_eager():
+    """ResnetEncoder.prepare (md2_encoder_input) == (cat(frames) - 0.45) / 0.225 in
+    channels_last, bit for bit, for one frame and for batched frame pairs."""
+    from monodepth2_amd.networks import ResnetEncoder
+    enc = ResnetEncoder(18, False, num_input_images=2).cuda().to(memory_format=torch.channels_last)
+    enc1 = ResnetEncoder(18, False).cuda().to(memory_format=torch.channels_last)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    fr = [torch.rand(3, 3, 16, 24, device="cuda", generator=g) for _ in range(3)]
+    pairs = [[fr[1], fr[0]], [fr[0], fr[2]]]
+    x = enc.prepare(pairs)
+    ref = (torch.cat([torch.cat(p, 1) for p in pairs], 0) - 0.45) / 0.225
+    assert x.is_contiguous(memory_format=torch.channels_last) and x.shape == ref.shape
+    assert torch.equal(x, ref)
+    x1 = enc1.prepare(fr[2])
+    assert torch.equal(x1, (fr[2] - 0.45) / 0.225) and x1.is_contiguous(memory_format=torch.channels_last)
