@@ -64,13 +64,14 @@ def depth_from_disp(disp, min_depth, max_depth):
 def cam_points(depth, inv_K):
     """layers.py:163-168: (B,1,h,w) depth -> (B,4,h*w) homogeneous points."""
     B, _, h, w = depth.shape
-    ys, xs = torch.meshgrid(torch.arange(h, dtype=torch.float32),
-                            torch.arange(w, dtype=torch.float32), indexing="ij")
-    pix = torch.stack([xs.reshape(-1), ys.reshape(-1), torch.ones(h * w)], 0)
+    dev = depth.device
+    ys, xs = torch.meshgrid(torch.arange(h, dtype=torch.float32, device=dev),
+                            torch.arange(w, dtype=torch.float32, device=dev), indexing="ij")
+    pix = torch.stack([xs.reshape(-1), ys.reshape(-1), torch.ones(h * w, device=dev)], 0)
     pix = pix.unsqueeze(0).expand(B, 3, h * w)
     rays = torch.matmul(inv_K[:, :3, :3], pix)
     pts = depth.view(B, 1, -1) * rays
-    return torch.cat([pts, torch.ones(B, 1, h * w)], 1)
+    return torch.cat([pts, torch.ones(B, 1, h * w, device=dev)], 1)
 
 
 def project(points, K, T, h, w, eps=1e-7):
@@ -180,7 +181,7 @@ def hot_path(opt: HotPathOptions, disps: Dict[int, torch.Tensor], inputs: Dict,
             if not opt.v1_multiscale:
                 mask = F.interpolate(mask, [H, W], mode="bilinear", align_corners=False)
             reproj = reproj * mask
-            loss = loss + (0.2 * F.binary_cross_entropy(mask, torch.ones(mask.shape))).mean()
+            loss = loss + (0.2 * F.binary_cross_entropy(mask, torch.ones_like(mask))).mean()
         if opt.avg_reprojection:
             reproj = reproj.mean(1, keepdim=True)
         if not opt.disable_automasking:

@@ -52,6 +52,9 @@ CASES = {
                                  {"disable_automasking": True, "avg_reprojection": True}, 0.05, True),
     "v1_multiscale_b2_64x128": (2, 64, 128, [0, -1, 1], {"v1_multiscale": True}, 0.05, True),
     "full_mono_b2_192x640": (2, 192, 640, [0, -1, 1], {}, 0.01, False),
+    # the C4 resolution, and the C3 frame set (mono+stereo, S=3) at full size
+    "full_mono_b2_320x1024": (2, 320, 1024, [0, -1, 1], {}, 0.01, False),
+    "full_stereo_b2_192x640": (2, 192, 640, [0, -1, 1, "s"], {}, 0.01, False),
     "predictive_mask_b2_32x64": (2, 32, 64, [0, -1, 1],
                                  {"disable_automasking": True, "predictive_mask": True}, 0.05, True),
 }

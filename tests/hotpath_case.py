@@ -70,32 +70,39 @@ def run_hip(case: Case, device="cuda"):
     return cfg, out
 
 
-def run_oracle(case: Case, selection=None):
-    """The CPU oracle on the case's inputs; selection optionally pins the argmin."""
+def run_oracle(case: Case, selection=None, device="cpu"):
+    """The CPU oracle on the case's inputs; selection optionally pins the argmin.
+
+    device="cuda" runs the same ATen formulation on PyTorch-ROCm (the reference's own
+    ops on the GPU): a yardstick for how far two fp32 platforms of the reference
+    itself drift apart at bilinear cell boundaries, never a product path."""
     from oracle.md2_oracle import HotPathOptions, hot_path
     opt = HotPathOptions(height=case.H, width=case.W, frame_ids=case.frame_ids,
                          v1_multiscale="v1_multiscale" in case.flags, no_ssim="no_ssim" in case.flags,
                          avg_reprojection="avg_reprojection" in case.flags,
                          disable_automasking="disable_automasking" in case.flags,
                          predictive_mask="predictive_mask" in case.flags)
-    masks = {s: m.clone().requires_grad_(True) for s, m in case.masks.items()} if case.masks else None
-    disps = {s: d.clone().requires_grad_(True) for s, d in case.disps.items()}
-    axis = case.axisangle.clone().requires_grad_(True)
-    trans = case.translation.clone().requires_grad_(True)
+    dev = torch.device(device)
+    masks = ({s: m.to(dev).clone().requires_grad_(True) for s, m in case.masks.items()}
+             if case.masks else None)
+    disps = {s: d.to(dev).clone().requires_grad_(True) for s, d in case.disps.items()}
+    axis = case.axisangle.to(dev).clone().requires_grad_(True)
+    trans = case.translation.to(dev).clone().requires_grad_(True)
+    inputs = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in case.inputs.items()}
     camT = {}
     for i, f in enumerate(case.temporal):
         camT[f] = transformation_from_parameters(axis[i], trans[i], invert=(f < 0))
     if "s" in case.frame_ids:
-        camT["s"] = case.inputs["stereo_T"]
+        camT["s"] = inputs["stereo_T"]
     sel = None
     if selection is not None:
-        sel = {s: torch.from_numpy(v).long() for s, v in selection.items()}
-    losses, outputs = hot_path(opt, disps, case.inputs, camT, noise=case.noise if case.noise else None,
-                               selection=sel, masks=masks)
+        sel = {s: torch.from_numpy(v).long().to(dev) for s, v in selection.items()}
+    noise = {s: n.to(dev) for s, n in case.noise.items()} if case.noise else None
+    losses, outputs = hot_path(opt, disps, inputs, camT, noise=noise, selection=sel, masks=masks)
     losses["loss"].backward()
     res = {"loss": [float(losses[f"loss/{s}"]) for s in range(4)] + [float(losses["loss"])],
-           "grad_disp": [disps[s].grad.numpy() for s in range(4)],
-           "grad_axis": axis.grad.numpy(), "grad_trans": trans.grad.numpy(), "outputs": outputs}
+           "grad_disp": [disps[s].grad.cpu().numpy() for s in range(4)],
+           "grad_axis": axis.grad.cpu().numpy(), "grad_trans": trans.grad.cpu().numpy(), "outputs": outputs}
     if masks:
-        res["grad_mask"] = {s: m.grad.numpy() for s, m in masks.items()}
+        res["grad_mask"] = {s: m.grad.cpu().numpy() for s, m in masks.items()}
     return res
