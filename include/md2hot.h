@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 3
+#define MD2_ABI_VERSION 4
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -181,6 +181,32 @@ int md2_decoder_pad_fwd(const md2_pad_desc* desc, const float* x, const float* s
                         float* out, void* stream);
 int md2_decoder_pad_bwd(const md2_pad_desc* desc, const float* x, const float* bias, const float* grad_out,
                         float* grad_x, float* grad_skip, float* grad_bias, void* workspace, void* stream);
+
+/*
+ * DepthDecoder disparity heads (networks/depth_decoder.py:63-64, layers.py:121-136):
+ * disp = sigmoid(Conv2d(C, 1, 3)(padded) + bias) on the reflection-padded NHWC fp32
+ * input that md2_decoder_pad_fwd builds, padded = (B, h+2, w+2, C); disp (B,1,h,w).
+ * weight is the (1,C,3,3) parameter in its own memory format (MD2_HEAD_WEIGHT_CL:
+ * channels_last, i.e. [ky][kx][c]; else [c][ky][kx]); grad_weight is written in the
+ * same format.  The backward takes the forward's disp (sigmoid backward from its
+ * output, as torch) and returns grad_padded (B,h+2,w+2,C) plus grad_weight /
+ * grad_bias as fixed-order sums (deterministic), with `workspace` of
+ * md2_disp_head_workspace_bytes.  C a multiple of 4 dividing 1024, C <= 256.
+ * Replaces the dispconv Conv3x3 + nn.Sigmoid of the reference decoder.
+ */
+#define MD2_HEAD_WEIGHT_CL (1u << 0)
+
+typedef struct md2_head_desc {
+    int32_t batch, channels, height, width; /* of the unpadded output */
+    uint32_t flags;                         /* MD2_HEAD_* */
+} md2_head_desc;
+
+size_t md2_disp_head_workspace_bytes(const md2_head_desc* desc);
+int md2_disp_head_fwd(const md2_head_desc* desc, const float* padded, const float* weight, const float* bias,
+                      float* disp, void* stream);
+int md2_disp_head_bwd(const md2_head_desc* desc, const float* padded, const float* weight, const float* disp,
+                      const float* grad_disp, float* grad_padded, float* grad_weight, float* grad_bias,
+                      void* workspace, void* stream);
 
 /*
  * The encoders' input (networks/resnet_encoder.py:93 normalisation, trainer.py:280-290

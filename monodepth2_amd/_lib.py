@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -58,7 +58,8 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_timing_begin", "md2_timing_end", "md2_decoder_pad_fwd", "md2_decoder_pad_bwd",
            "md2_decoder_pad_workspace_bytes", "md2_adam_step", "md2_encoder_input",
            "md2_pose_fwd", "md2_pose_bwd", "md2_aug_plan_create", "md2_aug_plan_destroy", "md2_aug_run",
-           "md2_bn_workspace_bytes", "md2_bn_fwd", "md2_bn_bwd", "md2_maxpool3s2_fwd", "md2_maxpool3s2_bwd"]
+           "md2_bn_workspace_bytes", "md2_bn_fwd", "md2_bn_bwd", "md2_maxpool3s2_fwd", "md2_maxpool3s2_bwd",
+           "md2_disp_head_workspace_bytes", "md2_disp_head_fwd", "md2_disp_head_bwd"]
 
 PAD_ELU = 1 << 0
 PAD_UPSAMPLE = 1 << 1
@@ -102,7 +103,21 @@ class PoolDesc(ctypes.Structure):
                 ("width", ctypes.c_int32), ("flags", ctypes.c_uint32), ("reserved", ctypes.c_int32)]
 
 
+HEAD_WEIGHT_CL = 1 << 0
+
+
+class HeadDesc(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("channels", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("width", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
 def _declare(L):
+    L.md2_disp_head_workspace_bytes.restype = ctypes.c_size_t
+    L.md2_disp_head_workspace_bytes.argtypes = [ctypes.POINTER(HeadDesc)]
+    L.md2_disp_head_fwd.restype = ctypes.c_int
+    L.md2_disp_head_fwd.argtypes = [ctypes.POINTER(HeadDesc)] + [_vp] * 5
+    L.md2_disp_head_bwd.restype = ctypes.c_int
+    L.md2_disp_head_bwd.argtypes = [ctypes.POINTER(HeadDesc)] + [_vp] * 9
     L.md2_abi_version.restype = ctypes.c_int
     L.md2_abi_version.argtypes = []
     L.md2_last_error.restype = ctypes.c_char_p

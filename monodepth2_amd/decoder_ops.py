@@ -83,6 +83,59 @@ class _ConvInput(torch.autograd.Function):
         return gx, gskip, gbias, None, None, None
 
 
+class _DispHead(torch.autograd.Function):
+    """sigmoid(Conv2d(C, 1, 3)(P) + b) on the padded NHWC conv input (md2_disp_head_*)."""
+
+    @staticmethod
+    def forward(ctx, P, weight, bias):
+        B, C, Hp, Wp = P.shape
+        w_cl = weight.is_contiguous(memory_format=_CL)
+        if not w_cl:
+            weight = weight.contiguous()
+        d = _lib.HeadDesc(B, C, Hp - 2, Wp - 2, _lib.HEAD_WEIGHT_CL if w_cl else 0)
+        disp = torch.empty(B, 1, Hp - 2, Wp - 2, device=P.device, dtype=torch.float32)
+        rc = _lib.lib().md2_disp_head_fwd(ctypes.byref(d), P.data_ptr(), weight.data_ptr(), bias.data_ptr(),
+                                          disp.data_ptr(), torch.cuda.current_stream(P.device).cuda_stream)
+        _lib.check(rc, "md2_disp_head_fwd")
+        ctx.d = d
+        ctx.save_for_backward(P, weight, disp)
+        return disp
+
+    @staticmethod
+    def backward(ctx, gdisp):
+        P, weight, disp = ctx.saved_tensors
+        d = ctx.d
+        gdisp = gdisp.float().contiguous()
+        gP = torch.empty_like(P, memory_format=_CL)
+        gw = torch.empty_like(weight)        # keeps the weight's memory format
+        gb = torch.empty(1, device=P.device, dtype=torch.float32)
+        ws = torch.empty(_lib.lib().md2_disp_head_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
+                         device=P.device)
+        rc = _lib.lib().md2_disp_head_bwd(ctypes.byref(d), P.data_ptr(), weight.data_ptr(), disp.data_ptr(),
+                                          gdisp.data_ptr(), gP.data_ptr(), gw.data_ptr(), gb.data_ptr(),
+                                          ws.data_ptr(), torch.cuda.current_stream(P.device).cuda_stream)
+        _lib.check(rc, "md2_disp_head_bwd")
+        return gP, gw, gb
+
+
+def supports_disp_head(P: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
+    """The fused head takes fp32 NHWC inputs, one output channel, C % 4 == 0,
+    C/4 dividing 256, C <= 256."""
+    C = P.shape[1]
+    return (P.is_cuda and P.dtype == torch.float32 and conv.weight.dtype == torch.float32
+            and P.is_contiguous(memory_format=_CL) and conv.out_channels == 1 and conv.bias is not None
+            and tuple(conv.kernel_size) == (3, 3) and tuple(conv.padding) == (0, 0)
+            and tuple(conv.stride) == (1, 1) and C % 4 == 0 and C <= 256 and 256 % (C // 4) == 0)
+
+
+def disp_head(P: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor:
+    """sigmoid(conv(P)) for the decoder's Conv2d(C, 1, 3) disparity head in one HIP
+    pass each way (networks/depth_decoder.py:63-64 dispconv + sigmoid)."""
+    if not supports_disp_head(P, conv):
+        raise ValueError("disp_head: fp32 channels_last input, Conv2d(C, 1, 3) with bias, C/4 dividing 256")
+    return _DispHead.apply(P, conv.weight, conv.bias)
+
+
 def supports_bf16(x: torch.Tensor, skip: Optional[torch.Tensor], nhwc: bool) -> bool:
     return nhwc and x.shape[1] % 4 == 0 and (skip is None or skip.shape[1] % 4 == 0)
 

@@ -45,12 +45,13 @@ class DepthDecoder(nn.Module):
         self.decoder = nn.ModuleList(mods)
         self.sigmoid = nn.Sigmoid()
         self.fused = True   # GPU: build each conv input with the fused HIP pass
+        self.fused_heads = True   # GPU fp32: dispconv + sigmoid as one HIP pass (decoder_ops.disp_head)
 
     def _forward_fused(self, input_features):
         """Same graph with each conv input built by one HIP pass (decoder_ops):
         pad(x) -> conv -> [ELU -> up x2 -> cat skip -> pad] -> conv -> [ELU -> pad] ->
         (dispconv -> sigmoid) and the next level's first conv."""
-        from ..decoder_ops import conv_input, supports_bias
+        from ..decoder_ops import conv_input, disp_head, supports_bias, supports_disp_head
         self.outputs = {}
         # NHWC convolutions (channels_last weights): keep every conv input NHWC too
         cl = self.convs[("upconv", 4, 0)].conv.conv.weight.is_contiguous(memory_format=torch.channels_last)
@@ -72,7 +73,11 @@ class DepthDecoder(nn.Module):
             y1, b1 = conv(self.convs[("upconv", i, 1)], P)
             P = conv_input(y1, None, elu=True, upsample=False, nhwc=cl, bias=b1)   # shared by dispconv and the next level
             if i in self.scales:
-                self.outputs[("disp", i)] = self.sigmoid(self.convs[("dispconv", i)].conv(P))
+                head = self.convs[("dispconv", i)].conv
+                if self.fused_heads and supports_disp_head(P, head) and not torch.is_autocast_enabled():
+                    self.outputs[("disp", i)] = disp_head(P, head)
+                else:
+                    self.outputs[("disp", i)] = self.sigmoid(head(P))
         return self.outputs
 
     def forward(self, input_features):

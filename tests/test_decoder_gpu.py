@@ -89,6 +89,40 @@ def test_conv_input_bf16_matches_eager():
     torch.testing.assert_close(gs.float(), gsr.float(), rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("C,h,w", [(16, 96, 320), (32, 48, 160), (64, 24, 80), (128, 12, 40), (4, 5, 7),
+                                   (256, 3, 9)])
+@pytest.mark.parametrize("w_cl", [True, False])
+def test_disp_head_matches_conv_sigmoid(C, h, w, w_cl):
+    """decoder_ops.disp_head (md2_disp_head_*) vs sigmoid(Conv2d(C, 1, 3)) on MIOpen:
+    disp and the gradients w.r.t. the padded input, weight and bias (fp32 tolerance:
+    reduction order differs; the weight/bias sums run over B*h*w pixels)."""
+    from monodepth2_amd.decoder_ops import disp_head
+    torch.manual_seed(5)
+    CL = torch.channels_last
+    conv = torch.nn.Conv2d(C, 1, 3).cuda()
+    if w_cl:
+        conv = conv.to(memory_format=CL)
+    P = torch.randn(3, C, h + 2, w + 2, device="cuda").contiguous(memory_format=CL).requires_grad_(True)
+    d = disp_head(P, conv)
+    ref = torch.sigmoid(conv(P))
+    torch.testing.assert_close(d, ref, rtol=1e-5, atol=1e-6)
+    g = torch.randn_like(ref)
+    gP, gw, gb = torch.autograd.grad(d, (P, conv.weight, conv.bias), g)
+    gPr, gwr, gbr = torch.autograd.grad(ref, (P, conv.weight, conv.bias), g)
+    assert gw.is_contiguous(memory_format=CL) == w_cl or C == 1
+    torch.testing.assert_close(gP, gPr, rtol=1e-5, atol=1e-6)
+    # weight/bias gradients are sums over B*h*w (up to 92k) products: measure both fp32
+    # orders against fp64 and require ours no worse than 2x MIOpen's drift (+ a floor)
+    P64, w64, b64 = P.detach().double().requires_grad_(True), conv.weight.detach().double(), conv.bias.detach().double()
+    w64.requires_grad_(True)
+    b64.requires_grad_(True)
+    gw64, gb64 = torch.autograd.grad(torch.sigmoid(torch.nn.functional.conv2d(P64, w64, b64)), (w64, b64), g.double())
+    for ours, theirs, exact in ((gw, gwr, gw64), (gb, gbr, gb64)):
+        e_ours = (ours.double() - exact).abs().max().item()
+        e_ref = (theirs.double() - exact).abs().max().item()
+        assert e_ours <= 2 * e_ref + 2e-6 * exact.abs().max().item() + 1e-6, (e_ours, e_ref)
+
+
 @pytest.mark.parametrize("num_layers,H,W,cl", [(18, 64, 128, False), (18, 192, 640, False), (50, 64, 96, False),
                                                (18, 64, 128, True)])
 def test_fused_decoder_matches_eager(num_layers, H, W, cl):
