@@ -8,13 +8,17 @@
 // 1 ms of a 16 ms training step for ~1.5 GFLOP.  They are HBM-bound streams (9·C MACs
 // per output pixel against 4·C bytes of input), so here:
 //   * forward: one pass over P; a pixel's C channels are spread over L lanes as
-//     float4 quads (L = min(C/4, 16)), 9 taps each, shuffle-reduced, bias + sigmoid
-//     fused; writes disp (B,1,h,w).
-//   * backward: one pass over the padded pixels (Y, X): dz = dD·D·(1-D) of the up to
-//     9 output pixels that read (Y, X) gives dP[Y,X,:] = Σ_taps w[tap,:]·dz (a 3x3
+//     float4 quads (L = min(C/4, 16), QL = C/(4L) quads per lane), the lane's 9·QL
+//     weight quads held in registers, 9 taps each, shuffle-reduced, bias + sigmoid
+//     fused; writes disp (B,1,h,w).  32-bit index math throughout.
+//   * backward: blocks walk padded rows (b, Y).  Per row, dz = dD·D·(1-D) of the three
+//     output rows that read it (y = Y-2..Y) is staged in LDS once (one sigmoid-backward
+//     per output pixel and tap row, instead of one per channel quad); then every
+//     (padded pixel, channel quad) gives dP[Y,X,:] = Σ_taps w[tap,:]·dz (a 3x3
 //     transposed conv, written once, float4) and, from the same loads,
-//     dW[tap,:] += P[Y,X,:]·dz[tap] and db += dz — per-block partials, summed by a
-//     second launch in a fixed order (deterministic, no atomics).
+//     dW[tap,:] += P[Y,X,:]·dz[tap] and db += dz.  Per-block partials (wave shuffles,
+//     then LDS) are summed by a second launch in a fixed order (deterministic, no
+//     atomics).
 // Weights are read in the parameter's own memory format (channels_last: [tap][c],
 // contiguous: [c][tap]) and dW is written back in that format.
 
@@ -28,7 +32,9 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxC = 256;
-constexpr int kBwdBlocks = 1024;
+constexpr int kBwdBlocks = 2048;
+constexpr int kFwdBlocks = 4096;
+constexpr int kMaxLds = 64 * 1024;
 
 struct HeadArgs {
     int B, C, h, w;            // output (B,1,h,w); P is (B,h+2,w+2,C) NHWC
@@ -44,117 +50,159 @@ struct HeadArgs {
     float* gb;                 // (1,)
 };
 
-__device__ __forceinline__ float wt_at(const HeadArgs& a, int tap, int c) {
-    return a.w_cl ? a.wt[tap * a.C + c] : a.wt[c * 9 + tap];
+__device__ __forceinline__ float4 wt_quad(const HeadArgs& a, int tap, int q) {
+    if (a.w_cl) return reinterpret_cast<const float4*>(a.wt + tap * a.C)[q];
+    const int c = q * 4;
+    return make_float4(a.wt[c * 9 + tap], a.wt[(c + 1) * 9 + tap], a.wt[(c + 2) * 9 + tap], a.wt[(c + 3) * 9 + tap]);
 }
 
-// L lanes per pixel, Q = C/4 quads, QL = Q/L quads per lane
-template <int L>
+__device__ __forceinline__ float dot4(float4 u, float4 v) { return u.x * v.x + u.y * v.y + u.z * v.z + u.w * v.w; }
+
+// L lanes per pixel, QL quads per lane (C = 4·L·QL)
+template <int L, int QL>
 __global__ __launch_bounds__(kThreads) void head_fwd_kernel(HeadArgs a) {
-    const int Q = a.C >> 2, QL = Q / L;
-    const int Wp = a.w + 2, Hp = a.h + 2;
+    constexpr int Q = L * QL;
+    const unsigned Wp = a.w + 2, Hp = a.h + 2;
     const int sub = threadIdx.x % L;
-    const long long npix = (long long)a.B * a.h * a.w;
-    const long long pix = ((long long)blockIdx.x * kThreads + threadIdx.x) / L;
+    const unsigned npix = (unsigned)a.B * a.h * a.w;
+    const unsigned stride = gridDim.x * (kThreads / L);
+    unsigned pix = (blockIdx.x * kThreads + threadIdx.x) / L;
     if (pix >= npix) return;   // whole L-lane groups exit together (L divides 64)
-    const int x = (int)(pix % a.w);
-    const long long t = pix / a.w;
-    const int y = (int)(t % a.h), b = (int)(t / a.h);
-    const float4* P4 = reinterpret_cast<const float4*>(a.P);
-    float acc = 0.f;
+    float4 wr[9][QL];          // loaded once, reused for every pixel this group walks
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+    for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-            const long long base = (((long long)b * Hp + (y + ky)) * Wp + (x + kx)) * Q;
-            for (int k = 0; k < QL; ++k) {
-                const int q = sub + k * L;
-                const float4 v = P4[base + q];
-                const int tap = ky * 3 + kx, c = q * 4;
-                acc += v.x * wt_at(a, tap, c) + v.y * wt_at(a, tap, c + 1) + v.z * wt_at(a, tap, c + 2) +
-                       v.w * wt_at(a, tap, c + 3);
-            }
+        for (int k = 0; k < QL; ++k) wr[tap][k] = wt_quad(a, tap, sub + k * L);
+    const float bias = a.bias[0];
+    const float4* P4 = reinterpret_cast<const float4*>(a.P) + sub;
+    // U pixels per iteration: 9·QL·U independent loads in flight per lane
+    constexpr int U = QL == 1 ? 2 : 1;
+    for (; pix < npix; pix += U * stride) {
+        unsigned pp[U], base[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            pp[u] = pix + u * stride < npix ? pix + u * stride : pix;   // a lone tail pixel is done twice
+            const unsigned x = pp[u] % a.w, t = pp[u] / a.w;
+            const unsigned y = t % a.h, b = t / a.h;
+            base[u] = ((b * Hp + y) * Wp + x) * Q;
         }
+        float4 v[U][9][QL];
 #pragma unroll
-    for (int o = L / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, L);
-    if (sub == 0) {
-        const float z = acc + a.bias[0];
-        a.disp[pix] = 1.f / (1.f + expf(-z));
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+                    for (int k = 0; k < QL; ++k) v[u][ky * 3 + kx][k] = P4[base[u] + (ky * Wp + kx) * Q + k * L];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float acc = 0.f;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+                for (int k = 0; k < QL; ++k) acc += dot4(v[u][tap][k], wr[tap][k]);
+#pragma unroll
+            for (int o = L / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, L);
+            if (sub == 0) a.disp[pp[u]] = 1.f / (1.f + expf(-(acc + bias)));
+        }
     }
 }
 
-// one thread per (padded pixel, channel quad); grid-stride over all of them.  Block
-// partials: [9 taps x C channels] of dW, then db.
+// Blocks walk padded rows; a thread owns channel quad q = tid % Q and pixels
+// X = tid / Q + k·(256/Q) of the row.  Dynamic LDS: dz[3][Wp + 2] during the walk,
+// then the per-wave partials [4 waves][min(Q,64)][37].
+template <int Q>
 __global__ __launch_bounds__(kThreads) void head_bwd_kernel(HeadArgs a) {
-    const int Q = a.C >> 2;
+    extern __shared__ float lds[];
+    constexpr int TP = kThreads / Q;            // pixels per pass
     const int Wp = a.w + 2, Hp = a.h + 2;
-    const int q = threadIdx.x % Q;              // Q divides kThreads: a thread keeps its quad
-    const long long total = (long long)a.B * Hp * Wp * Q;
+    const int Ws = Wp + 2;                      // dz row stride: x + 2 for x in [-2, Wp)
+    const int q = threadIdx.x % Q, p0 = threadIdx.x / Q;
     const float4* P4 = reinterpret_cast<const float4*>(a.P);
     float4* G4 = reinterpret_cast<float4*>(a.gP);
-    float wq[9][4];
+    float4 wq[9];
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
+    for (int tap = 0; tap < 9; ++tap) wq[tap] = wt_quad(a, tap, q);
+    float4 dw[9];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wq[tap][j] = wt_at(a, tap, q * 4 + j);
-    float dw[9][4];
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) dw[tap][j] = 0.f;
+    for (int tap = 0; tap < 9; ++tap) dw[tap] = make_float4(0.f, 0.f, 0.f, 0.f);
     float db = 0.f;
-    for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < total;
-         i += (long long)gridDim.x * kThreads) {
-        const long long pp = i / Q;             // padded pixel
-        const int X = (int)(pp % Wp);
-        const long long t = pp / Wp;
-        const int Y = (int)(t % Hp), b = (int)(t / Hp);
-        const float4 p = P4[i];
-        float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-            const int y = Y - ky;
-            if (y < 0 || y >= a.h) continue;
-#pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-                const int x = X - kx;
-                if (x < 0 || x >= a.w) continue;
-                const long long o = ((long long)b * a.h + y) * a.w + x;
+    const int rows = a.B * Hp;
+    for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+        const int b = r / Hp, Y = r - b * Hp;
+        __syncthreads();                        // previous row's dz reads are done
+        for (int e = threadIdx.x; e < 3 * Ws; e += kThreads) {
+            const int ky = e / Ws, x = e - ky * Ws - 2, y = Y - ky;
+            float dz = 0.f;
+            if (y >= 0 && y < a.h && x >= 0 && x < a.w) {
+                const int o = (b * a.h + y) * a.w + x;
                 const float d = a.disp[o];
-                const float dz = a.gdisp[o] * d * (1.f - d);   // sigmoid backward from its output
-                const int tap = ky * 3 + kx;
-                g.x += wq[tap][0] * dz;
-                g.y += wq[tap][1] * dz;
-                g.z += wq[tap][2] * dz;
-                g.w += wq[tap][3] * dz;
-                dw[tap][0] += p.x * dz;
-                dw[tap][1] += p.y * dz;
-                dw[tap][2] += p.z * dz;
-                dw[tap][3] += p.w * dz;
-                if (tap == 4 && q == 0) db += dz;   // each output pixel once: its centre tap
+                dz = a.gdisp[o] * d * (1.f - d);   // sigmoid backward from its output
             }
+            lds[e] = dz;
         }
-        G4[i] = g;
+        __syncthreads();
+        const int rowbase = r * Wp;
+        for (int X = p0; X < Wp; X += TP) {
+            const int i = (rowbase + X) * Q + q;
+            const float4 p = P4[i];
+            float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    const float dz = lds[ky * Ws + X + 2 - kx];
+                    const int tap = ky * 3 + kx;
+                    g.x += wq[tap].x * dz;
+                    g.y += wq[tap].y * dz;
+                    g.z += wq[tap].z * dz;
+                    g.w += wq[tap].w * dz;
+                    dw[tap].x += p.x * dz;
+                    dw[tap].y += p.y * dz;
+                    dw[tap].z += p.z * dz;
+                    dw[tap].w += p.w * dz;
+                }
+            if (q == 0) db += lds[Ws + X + 1];      // centre tap: each output pixel once
+            G4[i] = g;
+        }
     }
-    // block reduction of the per-thread partials: threads with equal q share channels
-    __shared__ float red[kThreads][37];
+    // lanes with equal q inside a wave: xor-shuffle over the lane bits above Q
+    float v[37];
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
+    for (int tap = 0; tap < 9; ++tap) {
+        v[tap * 4 + 0] = dw[tap].x;
+        v[tap * 4 + 1] = dw[tap].y;
+        v[tap * 4 + 2] = dw[tap].z;
+        v[tap * 4 + 3] = dw[tap].w;
+    }
+    v[36] = db;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) red[threadIdx.x][tap * 4 + j] = dw[tap][j];
-    red[threadIdx.x][36] = db;
+    for (int o = Q; o < 64; o <<= 1)           // Q divides 64 (C <= 256)
+#pragma unroll
+        for (int j = 0; j < 37; ++j) v[j] += __shfl_xor(v[j], o, 64);
+    const int lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+    __syncthreads();                             // dz reads done: reuse LDS
+    if (lane < Q) {
+        float* dst = lds + (wave * Q + lane) * 37;
+#pragma unroll
+        for (int j = 0; j < 37; ++j) dst[j] = v[j];
+    }
     __syncthreads();
-    const int groups = kThreads / Q;            // threads per quad in this block
     const int n = 9 * a.C + 1;
     float* out = a.part + (size_t)blockIdx.x * n;
+    constexpr int NW = kThreads / 64;
     for (int e = threadIdx.x; e < n; e += kThreads) {
-        float s = 0.f;
+        int off;                                 // db lives on quad 0
         if (e == n - 1) {
-            for (int gi = 0; gi < groups; ++gi) s += red[gi * Q][36];   // q == 0 threads
+            off = 36;
         } else {
-            const int tap = e / a.C, c = e % a.C, qq = c >> 2, j = c & 3;
-            for (int gi = 0; gi < groups; ++gi) s += red[gi * Q + qq][tap * 4 + j];
+            const int tap = e / a.C, c = e - tap * a.C;
+            off = (c >> 2) * 37 + tap * 4 + (c & 3);
         }
+        float s = 0.f;
+#pragma unroll
+        for (int wv = 0; wv < NW; ++wv) s += lds[wv * Q * 37 + off];
         out[e] = s;
     }
 }
@@ -181,10 +229,17 @@ __global__ __launch_bounds__(kThreads) void head_wgrad_kernel(HeadArgs a, int G)
     }
 }
 
+size_t bwd_lds(int C, int w) {
+    const size_t dz = sizeof(float) * 3 * (size_t)(w + 4);
+    const size_t red = sizeof(float) * (kThreads / 64) * (C / 4) * 37;
+    return dz > red ? dz : red;
+}
+
 bool valid(const md2_head_desc* d) {
     return d && d->batch >= 1 && d->height >= 1 && d->width >= 1 && d->channels >= 4 && d->channels % 4 == 0 &&
            d->channels <= kMaxC && (kThreads % (d->channels / 4)) == 0 &&
-           (long long)d->batch * (d->height + 2) * (d->width + 2) * (d->channels / 4) < (1ll << 31);
+           (long long)d->batch * (d->height + 2) * (d->width + 2) * (d->channels / 4) < (1ll << 31) &&
+           bwd_lds(d->channels, d->width) <= (size_t)kMaxLds;
 }
 
 HeadArgs args_of(const md2_head_desc* d) {
@@ -198,9 +253,8 @@ HeadArgs args_of(const md2_head_desc* d) {
 }
 
 int bwd_grid(const HeadArgs& a) {
-    const long long total = (long long)a.B * (a.h + 2) * (a.w + 2) * (a.C / 4);
-    const long long g = (total + kThreads - 1) / kThreads;
-    return (int)(g < kBwdBlocks ? g : kBwdBlocks);
+    const int rows = a.B * (a.h + 2);           // one padded row per block pass
+    return rows < kBwdBlocks ? rows : kBwdBlocks;
 }
 
 }  // namespace
@@ -224,13 +278,16 @@ int md2_disp_head_fwd(const md2_head_desc* d, const float* padded, const float* 
     const int Q = a.C / 4;
     const int L = Q < 16 ? Q : 16;
     const long long threads = (long long)a.B * a.h * a.w * L;
-    const int grid = (int)((threads + kThreads - 1) / kThreads);
-    void (*k)(HeadArgs) = L == 1    ? head_fwd_kernel<1>
-                          : L == 2  ? head_fwd_kernel<2>
-                          : L == 4  ? head_fwd_kernel<4>
-                          : L == 8  ? head_fwd_kernel<8>
-                                    : head_fwd_kernel<16>;
-    if (L != 1 && L != 2 && L != 4 && L != 8 && L != 16) return MD2_ERR_ARG;
+    const long long need = (threads + kThreads - 1) / kThreads;
+    const long long want = (need + 3) / 4;                          // each group walks >= 4 pixels
+    const int grid = (int)(want < kFwdBlocks ? want : kFwdBlocks);
+    void (*k)(HeadArgs) = Q == 1    ? head_fwd_kernel<1, 1>
+                          : Q == 2  ? head_fwd_kernel<2, 1>
+                          : Q == 4  ? head_fwd_kernel<4, 1>
+                          : Q == 8  ? head_fwd_kernel<8, 1>
+                          : Q == 16 ? head_fwd_kernel<16, 1>
+                          : Q == 32 ? head_fwd_kernel<16, 2>
+                                    : head_fwd_kernel<16, 4>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
 }
@@ -251,7 +308,15 @@ int md2_disp_head_bwd(const md2_head_desc* d, const float* padded, const float* 
     a.gw = grad_weight;
     a.gb = grad_bias;
     const int G = bwd_grid(a);
-    hipLaunchKernelGGL(head_bwd_kernel, dim3(G), dim3(kThreads), 0, (hipStream_t)stream, a);
+    const int Q = a.C / 4;
+    void (*k)(HeadArgs) = Q == 1    ? head_bwd_kernel<1>
+                          : Q == 2  ? head_bwd_kernel<2>
+                          : Q == 4  ? head_bwd_kernel<4>
+                          : Q == 8  ? head_bwd_kernel<8>
+                          : Q == 16 ? head_bwd_kernel<16>
+                          : Q == 32 ? head_bwd_kernel<32>
+                                    : head_bwd_kernel<64>;
+    hipLaunchKernelGGL(k, dim3(G), dim3(kThreads), bwd_lds(a.C, a.w), (hipStream_t)stream, a);
     hipLaunchKernelGGL(head_wgrad_kernel, dim3(9 * a.C + 1), dim3(kThreads), 0, (hipStream_t)stream, a, G);
     return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
 }
