@@ -117,6 +117,10 @@ class PoseDecoder(nn.Module):
         self.relu = nn.ReLU()
         self.net = nn.ModuleList([self.convs["squeeze"], self.convs[("pose", 0)], self.convs[("pose", 1)],
                                   self.convs[("pose", 2)]])
+        # True: forward returns the packed (N, frames, 1, 6) [axisangle | translation]
+        # tensor instead of its two slices (the trainer's fused pose producer reads it
+        # whole; one gradient tensor comes back instead of two slice adjoints)
+        self.packed_output = False
 
     def forward(self, input_features):
         x = torch.cat([self.relu(self.convs["squeeze"](f[-1])) for f in input_features], 1)
@@ -124,6 +128,8 @@ class PoseDecoder(nn.Module):
         x = self.relu(self.convs[("pose", 1)](x))
         x = self.convs[("pose", 2)](x)
         x = 0.01 * x.mean(3).mean(2).view(-1, self.num_frames_to_predict_for, 1, 6)
+        if self.packed_output:
+            return x
         return x[..., :3], x[..., 3:]
 
 

@@ -37,7 +37,7 @@ from .hotpath import HotPathConfig, generate_images, photometric_loss, predictiv
 from .bn_ops import bn_groups
 from .layers import compute_depth_errors, disp_to_depth
 from .optim import FusedAdam
-from .pose_ops import poses_to_transforms
+from .pose_ops import packed_poses_to_transforms, poses_to_transforms
 
 
 def _sec_to_hm_str(t):
@@ -242,6 +242,7 @@ class Trainer:
         models = models if models is not None else self.models
         outputs = {}
         aas, trs, invs, fids = [], [], [], []
+        packed = None   # (F,B,6) pose-decoder output when every frame came from one batched call
         if self.num_pose_frames == 2:
             if self.opt.pose_model_type == "shared":
                 pose_feats = {f_i: features[f_i] for f_i in self.opt.frame_ids}
@@ -261,9 +262,17 @@ class Trainer:
                 x = enc.prepare(pairs)
                 with bn_groups(len(temporal)):
                     feats = enc.forward_prepared(x)
-                axisangle_all, translation_all = models["pose"]([feats])
+                dec = getattr(models["pose"], "module", models["pose"])   # DDP-wrapped or not
+                dec.packed_output = True
+                try:
+                    x6 = models["pose"]([feats])                        # (pairs*B, frames, 1, 6)
+                finally:
+                    dec.packed_output = False
+                axisangle_all, translation_all = x6[..., :3], x6[..., 3:]
                 per_pair = [(axisangle_all[i * B:(i + 1) * B], translation_all[i * B:(i + 1) * B])
                             for i in range(len(temporal))]
+                if x6.dtype == torch.float32:   # the first predicted frame, as axisangle[:, 0] below
+                    packed = x6[:, 0, 0].view(len(temporal), B, 6)
             else:
                 per_pair = []
                 for pair in pairs:
@@ -295,10 +304,15 @@ class Trainer:
                     trs.append(translation[:, i, 0])
                     invs.append(False)
                     fids.append(f_i)
+        self._T_all = None
         if fids:
-            T = poses_to_transforms(torch.stack(aas).float(), torch.stack(trs).float(), invs)
+            if packed is not None:
+                T = packed_poses_to_transforms(packed, invs)
+            else:
+                T = poses_to_transforms(torch.stack(aas).float(), torch.stack(trs).float(), invs)
             for i, f_i in enumerate(fids):
                 outputs[("cam_T_cam", 0, f_i)] = T[i]
+            self._T_all = (T, tuple(fids))
         return outputs
 
     # ------------------------------------------------------------- hot path
@@ -322,6 +336,11 @@ class Trainer:
         (trainer.py:366-375)."""
         if self.opt.pose_model_type != "posecnn":
             Ts = [inputs["stereo_T"] if f == "s" else outputs[("cam_T_cam", 0, f)] for f in self.src_frames]
+            T_all = getattr(self, "_T_all", None)
+            if (T_all is not None and T_all[1] == tuple(self.src_frames)
+                    and all(t._base is T_all[0] and t.storage_offset() == i * T_all[0].stride(0)
+                            for i, t in enumerate(Ts))):
+                return T_all[0]    # the fused producer's (S,B,4,4) already is the stack
             return torch.stack(Ts, 0)
         per_scale = []
         for s in range(self.num_scales):

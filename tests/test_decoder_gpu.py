@@ -168,3 +168,21 @@ def test_fused_pose_matches_eager(inv):
     gar, gtr = torch.autograd.grad(Tr, (aa, tr), g)
     torch.testing.assert_close(ga, gar, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(gt, gtr, rtol=1e-5, atol=1e-6)
+
+
+def test_packed_pose_producer_matches_split():
+    """pose_ops.packed_poses_to_transforms on a strided (F,B,6) view of the pose
+    decoder output == poses_to_transforms on its axisangle / translation halves,
+    values and the gradient w.r.t. the packed tensor."""
+    from monodepth2_amd.pose_ops import packed_poses_to_transforms, poses_to_transforms
+    torch.manual_seed(2)
+    F_, B = 2, 5
+    raw = (0.1 * torch.randn(F_ * B, 2, 1, 6, device="cuda")).requires_grad_(True)   # (pairs*B, frames, 1, 6)
+    x6 = raw[:, 0, 0].view(F_, B, 6)
+    T = packed_poses_to_transforms(x6, [True, False])
+    Tr = poses_to_transforms(x6[..., :3], x6[..., 3:], [True, False])
+    assert torch.equal(T, Tr)
+    g = torch.randn_like(T)
+    gp, = torch.autograd.grad(T, raw, g)
+    gr, = torch.autograd.grad(Tr, raw, g)
+    assert torch.equal(gp, gr)
