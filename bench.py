@@ -88,6 +88,8 @@ def parse():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen exhaustive find per conv shape")
     ap.add_argument("--channels-last", type=int, default=1, help="NHWC convolutions (1/0)")
+    ap.add_argument("--pose-last", type=int, default=0,
+                    help="1: pose network forward enqueued after the depth network (its backward first)")
     ap.add_argument("--graph", type=int, default=0, help="capture the whole step in a hipGraph (1/0)")
     ap.add_argument("--miopen-find", type=str, default="fast", help="MIOPEN_FIND_MODE (fast|normal|...)")
     ap.add_argument("--amp", type=str, default="none", choices=["none", "bf16"],
@@ -105,7 +107,9 @@ def make_trainer(args, device, rank, world):
                           num_layers=args.num_layers, weights_init="scratch", use_stereo=args.stereo,
                           frame_ids=[0, -1, 1], log_dir="/tmp/md2_bench",
                           channels_last=bool(args.channels_last), hip_graph=bool(args.graph), amp=args.amp)
-    return Trainer(opt, device=device, rank=rank, world_size=world)
+    tr = Trainer(opt, device=device, rank=rank, world_size=world)
+    tr.pose_last = bool(args.pose_last)
+    return tr
 
 
 def loss_delta_vs_oracle(trainer, batch):

@@ -209,7 +209,16 @@ class Trainer:
         side = self._pose_stream if (self.use_pose_net and self.opt.pose_model_type != "shared") else None
         main = torch.cuda.current_stream(self.device) if side is not None else None
         pose_out = None
-        if side is not None:
+        # Autograd enqueues ready nodes newest-first, so the network whose forward is
+        # enqueued LAST has its backward enqueued FIRST.  pose_last: the pose network
+        # goes second, its backward (needing only dL/dT from the loss) goes onto its
+        # stream before the host spends its time enqueuing the depth backward.
+        pose_last = side is not None and getattr(self, "pose_last", False)
+        inputs_ready = None
+        if pose_last:   # the pose stream waits for the inputs only, not the depth forward
+            inputs_ready = torch.cuda.Event()
+            inputs_ready.record(main)
+        if side is not None and not pose_last:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 pose_out = self.predict_poses(inputs, None, models)
@@ -225,6 +234,10 @@ class Trainer:
         if self.opt.predictive_mask:
             outputs["predictive_mask"] = models["predictive_mask"](
                 features[0] if isinstance(features, dict) else features)
+        if pose_last:
+            side.wait_event(inputs_ready)
+            with torch.cuda.stream(side):
+                pose_out = self.predict_poses(inputs, None, models)
         if self.use_pose_net:
             if side is not None:
                 main.wait_stream(side)
