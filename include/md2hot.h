@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 4
+#define MD2_ABI_VERSION 5
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -207,6 +207,28 @@ int md2_disp_head_fwd(const md2_head_desc* desc, const float* padded, const floa
 int md2_disp_head_bwd(const md2_head_desc* desc, const float* padded, const float* weight, const float* disp,
                       const float* grad_disp, float* grad_padded, float* grad_weight, float* grad_bias,
                       void* workspace, void* stream);
+
+/*
+ * Weight gradient of the ResNet stem convolution (conv1 of networks/resnet_encoder.py
+ * via torchvision ResNet: Conv2d(C, 64, 7, stride 2, padding 3, bias=False)), whose
+ * input is data (the normalised frames), so the input gradient is never needed.
+ * x (batch, height, width, channels) NHWC fp32, channels 3 / 6 / 9 (one, two or three
+ * frames); grad_y (batch, Ho, Wo, 64) NHWC with Ho = (height-1)/2+1, Wo likewise;
+ * grad_weight (64, channels, 7, 7) written (not accumulated) in the weight's memory
+ * format (MD2_STEM_WEIGHT_CL: channels_last [co][ky][kx][ci]; else [co][ci][ky][kx]).
+ * Deterministic (fixed-order sums); workspace of md2_stem_wgrad_workspace_bytes.
+ * Replaces MIOpen's backward-weights convolution for this layer.
+ */
+#define MD2_STEM_WEIGHT_CL (1u << 0)
+
+typedef struct md2_stem_desc {
+    int32_t batch, channels, height, width; /* of the input */
+    uint32_t flags;                         /* MD2_STEM_* */
+} md2_stem_desc;
+
+size_t md2_stem_wgrad_workspace_bytes(const md2_stem_desc* desc);
+int md2_stem_wgrad(const md2_stem_desc* desc, const float* x, const float* grad_y, float* grad_weight,
+                   void* workspace, void* stream);
 
 /*
  * The encoders' input (networks/resnet_encoder.py:93 normalisation, trainer.py:280-290

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -59,7 +59,8 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_decoder_pad_workspace_bytes", "md2_adam_step", "md2_encoder_input",
            "md2_pose_fwd", "md2_pose_bwd", "md2_aug_plan_create", "md2_aug_plan_destroy", "md2_aug_run",
            "md2_bn_workspace_bytes", "md2_bn_fwd", "md2_bn_bwd", "md2_maxpool3s2_fwd", "md2_maxpool3s2_bwd",
-           "md2_disp_head_workspace_bytes", "md2_disp_head_fwd", "md2_disp_head_bwd"]
+           "md2_disp_head_workspace_bytes", "md2_disp_head_fwd", "md2_disp_head_bwd",
+           "md2_stem_wgrad_workspace_bytes", "md2_stem_wgrad"]
 
 PAD_ELU = 1 << 0
 PAD_UPSAMPLE = 1 << 1
@@ -111,7 +112,19 @@ class HeadDesc(ctypes.Structure):
                 ("width", ctypes.c_int32), ("flags", ctypes.c_uint32)]
 
 
+STEM_WEIGHT_CL = 1 << 0
+
+
+class StemDesc(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("channels", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("width", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
 def _declare(L):
+    L.md2_stem_wgrad_workspace_bytes.restype = ctypes.c_size_t
+    L.md2_stem_wgrad_workspace_bytes.argtypes = [ctypes.POINTER(StemDesc)]
+    L.md2_stem_wgrad.restype = ctypes.c_int
+    L.md2_stem_wgrad.argtypes = [ctypes.POINTER(StemDesc)] + [_vp] * 5
     L.md2_disp_head_workspace_bytes.restype = ctypes.c_size_t
     L.md2_disp_head_workspace_bytes.argtypes = [ctypes.POINTER(HeadDesc)]
     L.md2_disp_head_fwd.restype = ctypes.c_int

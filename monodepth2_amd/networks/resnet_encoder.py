@@ -20,6 +20,7 @@ import torch
 import torch.nn as nn
 
 from ..bn_ops import bn_act, max_pool_3x3s2
+from ..stem_ops import stem_conv
 
 
 def _conv3x3(cin, cout, stride=1):
@@ -168,7 +169,7 @@ class ResnetEncoder(nn.Module):
     def forward_prepared(self, x):
         """The encoder on an input already normalised by `prepare`."""
         e = self.encoder
-        f0 = bn_act(e.bn1, e.conv1(x))
+        f0 = bn_act(e.bn1, stem_conv(e.conv1, x))   # weight gradient on f32 MFMA (stem_ops)
         f1 = e.layer1(max_pool_3x3s2(e.maxpool, f0))
         f2 = e.layer2(f1)
         f3 = e.layer3(f2)

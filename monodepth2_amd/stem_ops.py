@@ -1,0 +1,68 @@
+"""The ResNet stem convolution (conv1: 7x7, stride 2, padding 3, C -> 64, no bias) with
+its weight gradient on f32 MFMA (csrc/stem.hip, ABI `md2_stem_*`).
+
+The stem reads the normalised frames, which are data: its backward is the weight
+gradient alone, where MIOpen is at its least efficient (41 / 71 TFLOP/s for the
+depth / pose encoder).  The forward stays MIOpen's.  Same parameter (the torchvision
+`conv1.weight`), same semantics; any other case (an input that needs a gradient,
+bf16, NCHW inputs, a CPU tensor) runs the module itself.
+
+OFF by default (ENABLED): measured in the training step it runs 145 µs (C=3) and
+507 µs (C=6) + 28/53 µs for the partial sums, against MIOpen's 167 / 391 µs — the
+kernel is parity-tested and kept for the next round's work on its issue rate
+(DESIGN.md §8).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+_CL = torch.channels_last
+ENABLED = False   # MIOpen's backward-weights kernel is faster today (see the module docstring)
+
+
+class _StemConv(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        ctx.save_for_backward(x)
+        ctx.w_cl = weight.is_contiguous(memory_format=_CL)
+        ctx.w_shape = weight.shape
+        return F.conv2d(x, weight, None, 2, 3)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=_CL)
+        B, C, H, W = x.shape
+        d = _lib.StemDesc(B, C, H, W, _lib.STEM_WEIGHT_CL if ctx.w_cl else 0)
+        gw = torch.empty(ctx.w_shape, device=x.device, dtype=torch.float32,
+                         memory_format=_CL if ctx.w_cl else torch.contiguous_format)
+        L = _lib.lib()
+        ws = torch.empty(L.md2_stem_wgrad_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=x.device)
+        rc = L.md2_stem_wgrad(ctypes.byref(d), x.data_ptr(), gy.data_ptr(), gw.data_ptr(), ws.data_ptr(),
+                              torch.cuda.current_stream(x.device).cuda_stream)
+        _lib.check(rc, "md2_stem_wgrad")
+        return None, gw
+
+
+def supports_stem(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dtype == torch.float32 and conv.weight.dtype == torch.float32 and not x.requires_grad
+            and x.dim() == 4 and x.shape[1] in (3, 6, 9) and x.is_contiguous(memory_format=_CL)
+            and conv.out_channels == 64 and tuple(conv.kernel_size) == (7, 7) and tuple(conv.stride) == (2, 2)
+            and tuple(conv.padding) == (3, 3) and tuple(conv.dilation) == (1, 1) and conv.groups == 1
+            and conv.bias is None and conv.padding_mode == "zeros" and not torch.is_autocast_enabled()
+            and x.numel() < 2 ** 31)
+
+
+def stem_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """conv(x) for the encoder's stem; the weight gradient runs on md2_stem_wgrad when
+    supports_stem(conv, x), else the module runs as is."""
+    if ENABLED and supports_stem(conv, x) and torch.is_grad_enabled() and conv.weight.requires_grad:
+        return _StemConv.apply(x, conv.weight)
+    return conv(x)

@@ -1,0 +1,50 @@
+"""Stem convolution weight gradient (stem_ops / md2_stem_wgrad, f32 MFMA) vs MIOpen's
+conv2d backward on the same inputs, against an fp64 reference (fixed-order fp32 sums
+over up to 92k pixels: ours must be no worse than 2x MIOpen's drift)."""
+import pytest
+import torch
+
+from monodepth2_amd import stem_ops
+from monodepth2_amd.stem_ops import stem_conv, supports_stem
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _enabled(monkeypatch):
+    monkeypatch.setattr(stem_ops, "ENABLED", True)
+
+
+@pytest.mark.parametrize("B,C,H,W", [(2, 3, 64, 128), (3, 6, 30, 50), (1, 9, 17, 23), (2, 3, 192, 640),
+                                     (1, 6, 7, 9)])
+@pytest.mark.parametrize("w_cl", [True, False])
+def test_stem_wgrad_matches_conv_backward(B, C, H, W, w_cl):
+    torch.manual_seed(7)
+    CL = torch.channels_last
+    conv = torch.nn.Conv2d(C, 64, 7, 2, 3, bias=False).cuda()
+    if w_cl:
+        conv = conv.to(memory_format=CL)
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    assert supports_stem(conv, x)
+    y = stem_conv(conv, x)
+    ref = torch.nn.functional.conv2d(x, conv.weight, None, 2, 3)
+    assert torch.equal(y, ref)                      # the forward is MIOpen's
+    g = torch.randn_like(ref).contiguous(memory_format=CL)
+    assert y.grad_fn is not None and "StemConv" in type(y.grad_fn).__name__
+    gw, = torch.autograd.grad(y, conv.weight, g)
+    gwr, = torch.autograd.grad(ref, conv.weight, g)
+    assert gw.shape == gwr.shape and gw.is_contiguous(memory_format=CL) == w_cl
+    gw64, = torch.autograd.grad(torch.nn.functional.conv2d(x.double(), conv.weight.double(), None, 2, 3),
+                                conv.weight, g.double())
+    e_ours = (gw.double() - gw64).abs().max().item()
+    e_ref = (gwr.double() - gw64).abs().max().item()
+    assert e_ours <= 2 * e_ref + 1e-6 * gw64.abs().max().item() + 1e-6, (e_ours, e_ref)
+
+
+def test_stem_falls_back_when_the_input_needs_a_gradient():
+    conv = torch.nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(1, 3, 20, 24, device="cuda").contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    assert not supports_stem(conv, x)
+    y = stem_conv(conv, x)
+    gx, = torch.autograd.grad(y.sum(), x)
+    assert gx.shape == x.shape
