@@ -12,6 +12,7 @@ import ctypes
 from typing import Optional
 
 import torch
+import torch.nn.functional as F
 
 from . import _lib
 
@@ -134,6 +135,53 @@ def disp_head(P: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor:
     if not supports_disp_head(P, conv):
         raise ValueError("disp_head: fp32 channels_last input, Conv2d(C, 1, 3) with bias, C/4 dividing 256")
     return _DispHead.apply(P, conv.weight, conv.bias)
+
+
+class _ConvBiasAct(torch.autograd.Function):
+    """[relu](conv2d(x, w) + b): the convolution bias-free on MIOpen, the bias (+ ReLU)
+    in one HIP pass each way (md2_bias_act_*)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, relu: bool):
+        z = F.conv2d(x, weight, None, stride, padding)
+        if not z.is_contiguous(memory_format=_CL):
+            z = z.contiguous(memory_format=_CL)
+        B, C, H, W = z.shape
+        d = _lib.BiasActDesc(B * H * W, C, _lib.BIAS_ACT_RELU if relu else 0)
+        _lib.check(_lib.lib().md2_bias_act_fwd(ctypes.byref(d), z.data_ptr(), bias.data_ptr(), z.data_ptr(),
+                                               torch.cuda.current_stream(z.device).cuda_stream),
+                   "md2_bias_act_fwd")                      # in place: z is this op's own buffer
+        ctx.save_for_backward(x, weight, z if relu else None)
+        ctx.conf = (stride, padding, relu, d)
+        return z
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, y = ctx.saved_tensors
+        stride, padding, relu, d = ctx.conf
+        gy = gy.contiguous(memory_format=_CL)
+        gb = torch.empty(gy.shape[1], device=gy.device, dtype=torch.float32)
+        gz = torch.empty_like(gy, memory_format=_CL) if relu else gy
+        _lib.check(_lib.lib().md2_bias_act_bwd(ctypes.byref(d), y.data_ptr() if relu else None, gy.data_ptr(),
+                                               gz.data_ptr() if relu else None, gb.data_ptr(),
+                                               torch.cuda.current_stream(gy.device).cuda_stream),
+                   "md2_bias_act_bwd")
+        gx, gw, _ = torch.ops.aten.convolution_backward(
+            gz, x, weight, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
+            [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
+        return gx, gw, gb, None, None, None
+
+
+def conv_bias_act(conv: torch.nn.Conv2d, x: torch.Tensor, relu: bool) -> torch.Tensor:
+    """relu?(conv(x)) with the bias (+ ReLU) as one HIP pass each way when x is a CUDA
+    fp32 channels_last tensor (the pose decoder of the default build); else eager."""
+    if (x.is_cuda and x.dtype == torch.float32 and conv.weight.dtype == torch.float32 and conv.bias is not None
+            and x.is_contiguous(memory_format=_CL) and conv.weight.is_contiguous(memory_format=_CL)
+            and conv.out_channels % 4 == 0 and conv.groups == 1 and tuple(conv.dilation) == (1, 1)
+            and conv.padding_mode == "zeros" and not torch.is_autocast_enabled() and torch.is_grad_enabled()):
+        return _ConvBiasAct.apply(x, conv.weight, conv.bias, tuple(conv.stride), tuple(conv.padding), relu)
+    y = conv(x)
+    return F.relu(y) if relu else y
 
 
 def supports_bf16(x: torch.Tensor, skip: Optional[torch.Tensor], nhwc: bool) -> bool:

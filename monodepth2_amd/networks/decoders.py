@@ -123,10 +123,12 @@ class PoseDecoder(nn.Module):
         self.packed_output = False
 
     def forward(self, input_features):
-        x = torch.cat([self.relu(self.convs["squeeze"](f[-1])) for f in input_features], 1)
-        x = self.relu(self.convs[("pose", 0)](x))
-        x = self.relu(self.convs[("pose", 1)](x))
-        x = self.convs[("pose", 2)](x)
+        from ..decoder_ops import conv_bias_act   # bias (+ ReLU) as one HIP pass each way on the GPU
+        sq = [conv_bias_act(self.convs["squeeze"], f[-1], True) for f in input_features]
+        x = torch.cat(sq, 1) if len(sq) > 1 else sq[0]
+        x = conv_bias_act(self.convs[("pose", 0)], x, True)
+        x = conv_bias_act(self.convs[("pose", 1)], x, True)
+        x = conv_bias_act(self.convs[("pose", 2)], x, False)
         x = 0.01 * x.mean(3).mean(2).view(-1, self.num_frames_to_predict_for, 1, 6)
         if self.packed_output:
             return x

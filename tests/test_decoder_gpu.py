@@ -186,3 +186,24 @@ def test_packed_pose_producer_matches_split():
     gp, = torch.autograd.grad(T, raw, g)
     gr, = torch.autograd.grad(Tr, raw, g)
     assert torch.equal(gp, gr)
+
+
+@pytest.mark.parametrize("cin,cout,k,relu", [(512, 256, 1, True), (256, 256, 3, True), (256, 12, 1, False)])
+def test_conv_bias_act_matches_eager(cin, cout, k, relu):
+    """decoder_ops.conv_bias_act (bias-free MIOpen conv + md2_bias_act_*) vs the pose
+    decoder's eager relu(conv(x)): values and the gradients w.r.t. x, weight, bias."""
+    from monodepth2_amd.decoder_ops import conv_bias_act
+    torch.manual_seed(4)
+    CL = torch.channels_last
+    conv = torch.nn.Conv2d(cin, cout, k, 1, k // 2).cuda().to(memory_format=CL)
+    x = torch.randn(6, cin, 6, 20, device="cuda").contiguous(memory_format=CL).requires_grad_(True)
+    y = conv_bias_act(conv, x, relu)
+    assert y.grad_fn is not None and "ConvBiasAct" in type(y.grad_fn).__name__
+    ref = conv(x)
+    ref = torch.relu(ref) if relu else ref
+    torch.testing.assert_close(y, ref, rtol=1e-6, atol=1e-6)
+    g = torch.randn_like(ref)
+    got = torch.autograd.grad(y, (x, conv.weight, conv.bias), g)
+    exp = torch.autograd.grad(ref, (x, conv.weight, conv.bias), g)
+    for a, b in zip(got, exp):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
