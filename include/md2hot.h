@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 6
+#define MD2_ABI_VERSION 7
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -236,8 +236,8 @@ int md2_stem_wgrad(const md2_stem_desc* desc, const float* x, const float* grad_
  * bias-free on MIOpen.  x / y / grad (pixels, channels) row-major = channels_last.
  * fwd: y = [relu](x + bias).
  * bwd: grad_x = grad_y · [y > 0] (MD2_BIAS_ACT_RELU only; without it grad_x is unused
- * and may be NULL) and grad_bias = Σ_pixels of that, in a fixed order.
- * channels a multiple of 4.  One launch each way.
+ * and may be NULL) and grad_bias = Σ_pixels of that, in a fixed order, with `workspace`
+ * of md2_bias_act_workspace_bytes.  channels a multiple of 4.
  */
 #define MD2_BIAS_ACT_RELU (1u << 0)
 
@@ -248,8 +248,9 @@ typedef struct md2_bias_act_desc {
 } md2_bias_act_desc;
 
 int md2_bias_act_fwd(const md2_bias_act_desc* desc, const float* x, const float* bias, float* y, void* stream);
+size_t md2_bias_act_workspace_bytes(const md2_bias_act_desc* desc);
 int md2_bias_act_bwd(const md2_bias_act_desc* desc, const float* y, const float* grad_y, float* grad_x,
-                     float* grad_bias, void* stream);
+                     float* grad_bias, void* workspace, void* stream);
 
 /*
  * The encoders' input (networks/resnet_encoder.py:93 normalisation, trainer.py:280-290

@@ -1017,6 +1017,7 @@ struct DispGradArgs {
     int lh[MD2_MAX_SCALES], lw[MD2_MAX_SCALES];   // loss resolution (= (hs<<upsh, ws<<upsh))
     int upsh[MD2_MAX_SCALES];
     int block_base[MD2_MAX_SCALES + 1];           // first block of each scale (one launch)
+    int bpr[MD2_MAX_SCALES];                      // blocks per native row
     const float* dfull[MD2_MAX_SCALES];           // (B, lh, lw) dL/d(upsampled disp)
     const float* disp[MD2_MAX_SCALES];            // (B, 1, hs, ws)
     const float* img[MD2_MAX_SCALES];             // (B, 3, hs, ws) target colour at this scale
@@ -1040,16 +1041,23 @@ __device__ __forceinline__ float up_weight(int y, int i, int n_in, float sc) {
     return (y0 == i ? 1.f - l1 : 0.f) + (y1 == i ? l1 : 0.f);
 }
 
+// Blocks own whole native rows: block_base[s] + (b·hs + i)·bpr[s] + chunk, threads over
+// (column j, footprint slot g) of the row — the (scale, image, row) decode is uniform
+// (scalar) per block and j / g are shifts, so no per-thread integer division.
 __global__ __launch_bounds__(kBlock) void disp_grad_kernel(DispGradArgs a) {
     int s = 0;
     while (s + 1 < a.num_scales && (int)blockIdx.x >= a.block_base[s + 1]) ++s;
-    const int T = disp_grad_group(a.upsh[s]);
+    const int sh = a.upsh[s];
+    const int tsh = sh == 0 ? 0 : min(sh + 1, 4), T = 1 << tsh;   // = disp_grad_group(sh)
     const int hs = a.hs[s], ws = a.ws[s], lh = a.lh[s], lw = a.lw[s], HWs = hs * ws;
-    const int tid = (blockIdx.x - a.block_base[s]) * kBlock + threadIdx.x;
-    const int idx = tid / T, g = tid - idx * T;        // native pixel, footprint row slot
-    const bool live = idx < a.B * HWs;
-    const int b = live ? idx / HWs : 0, p = live ? idx - b * HWs : 0;
-    const int i = p / ws, j = p - i * ws;
+    const int rb = (int)blockIdx.x - a.block_base[s], bpr = a.bpr[s];
+    const int row = rb / bpr, chunk = rb - row * bpr;
+    const int b = row / hs, i = row - b * hs;
+    const int t = chunk * kBlock + threadIdx.x;
+    const int jj = t >> tsh, g = t & (T - 1);
+    const bool live = jj < ws;
+    const int j = live ? jj : ws - 1;
+    const int p = i * ws + j;
     const float* df = a.dfull[s] + (size_t)b * lh * lw;
     float acc = 0.f;
     if (a.upsh[s] == 0) {
@@ -1063,9 +1071,9 @@ __global__ __launch_bounds__(kBlock) void disp_grad_kernel(DispGradArgs a) {
             for (int y = ylo + g; y < yhi; y += T) {
                 const float wy = up_weight(y, i, hs, sc);
                 if (wy == 0.f) continue;
-                float row = 0.f;
-                for (int x = xlo; x < xhi; ++x) row += up_weight(x, j, ws, sc) * df[y * lw + x];
-                acc += wy * row;
+                float row_sum = 0.f;
+                for (int x = xlo; x < xhi; ++x) row_sum += up_weight(x, j, ws, sc) * df[y * lw + x];
+                acc += wy * row_sum;
             }
         }
         for (int o = 1; o < T; o <<= 1) acc += __shfl_xor(acc, o, kWave);   // T divides 64
@@ -1561,8 +1569,8 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
         g.img[s] = t->color[s][0];
         g.out[s] = grad_disp[s];
         g.block_base[s] = gblocks;
-        const long long n = (long long)L.B * L.hs[s] * L.ws[s] * disp_grad_group(g.upsh[s]);
-        gblocks += (int)((n + kBlock - 1) / kBlock);
+        g.bpr[s] = (L.ws[s] * disp_grad_group(g.upsh[s]) + kBlock - 1) / kBlock;
+        gblocks += L.B * L.hs[s] * g.bpr[s];
     }
     g.block_base[L.nscales] = gblocks;
     hipLaunchKernelGGL(disp_grad_kernel, dim3(gblocks), dim3(kBlock), 0, st, g);

@@ -162,9 +162,11 @@ class _ConvBiasAct(torch.autograd.Function):
         gy = gy.contiguous(memory_format=_CL)
         gb = torch.empty(gy.shape[1], device=gy.device, dtype=torch.float32)
         gz = torch.empty_like(gy, memory_format=_CL) if relu else gy
-        _lib.check(_lib.lib().md2_bias_act_bwd(ctypes.byref(d), y.data_ptr() if relu else None, gy.data_ptr(),
-                                               gz.data_ptr() if relu else None, gb.data_ptr(),
-                                               torch.cuda.current_stream(gy.device).cuda_stream),
+        L = _lib.lib()
+        ws = torch.empty(L.md2_bias_act_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=gy.device)
+        _lib.check(L.md2_bias_act_bwd(ctypes.byref(d), y.data_ptr() if relu else None, gy.data_ptr(),
+                                      gz.data_ptr() if relu else None, gb.data_ptr(), ws.data_ptr(),
+                                      torch.cuda.current_stream(gy.device).cuda_stream),
                    "md2_bias_act_bwd")
         gx, gw, _ = torch.ops.aten.convolution_backward(
             gz, x, weight, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
