@@ -336,7 +336,10 @@ def main():
                 "dtype": "f32" if args.amp == "none" else "bf16 networks (autocast) + f32 photometric loss",
                 "data": "synthetic (KITTI-shaped smooth textures, random-init weights)",
                 "config": {"workload": f"{'mono+stereo' if args.stereo else 'mono'}_{W}x{H} ResNet-{args.num_layers}"
-                                       f" batch={B}/GPU full train step (configs[1])"
+                                       f" batch={B}/GPU full train step"
+                                       + (" (configs[1])" if (not args.stereo and (W, H) == (640, 192)
+                                                               and args.num_layers == 18 and args.amp == "none")
+                                          else "")
                                        + (" + GPU input pipeline from 375x1242 uint8" if args.gpu_augment else ""),
                            "global_batch": B * world, "height": H, "width": W, "frame_ids": [str(f) for f in frame_ids],
                            "parallelism": f"dp{world}"},
