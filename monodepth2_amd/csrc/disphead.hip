@@ -65,9 +65,18 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(HeadArgs a) {
     const unsigned Wp = a.w + 2, Hp = a.h + 2;
     const int sub = threadIdx.x % L;
     const unsigned npix = (unsigned)a.B * a.h * a.w;
-    const unsigned stride = gridDim.x * (kThreads / L);
-    unsigned pix = (blockIdx.x * kThreads + threadIdx.x) / L;
-    if (pix >= npix) return;   // whole L-lane groups exit together (L divides 64)
+    // each block walks one contiguous pixel range, and the ranges of an XCD's blocks
+    // (dealt round-robin: block b runs on XCD b % 8) are contiguous too, so the three
+    // padded rows an output row reads are shared in that XCD's L2 (gridDim.x % 8 == 0)
+    constexpr unsigned GPB = kThreads / L;   // pixel groups per block
+    const unsigned lb = (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
+    constexpr int U = QL == 1 ? 2 : 1;
+    const unsigned step = GPB * U;
+    const unsigned chunk = ((npix + gridDim.x - 1) / gridDim.x + step - 1) / step * step;
+    const unsigned start = lb * chunk, end = start + chunk < npix ? start + chunk : npix;
+    const unsigned stride = GPB;
+    unsigned pix = start + threadIdx.x / L;
+    if (pix >= end) return;   // whole L-lane groups exit together (L divides 64)
     float4 wr[9][QL];          // loaded once, reused for every pixel this group walks
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap)
@@ -76,12 +85,11 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(HeadArgs a) {
     const float bias = a.bias[0];
     const float4* P4 = reinterpret_cast<const float4*>(a.P) + sub;
     // U pixels per iteration: 9·QL·U independent loads in flight per lane
-    constexpr int U = QL == 1 ? 2 : 1;
-    for (; pix < npix; pix += U * stride) {
+    for (; pix < end; pix += U * stride) {
         unsigned pp[U], base[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            pp[u] = pix + u * stride < npix ? pix + u * stride : pix;   // a lone tail pixel is done twice
+            pp[u] = pix + u * stride < end ? pix + u * stride : pix;   // a lone tail pixel is done twice
             const unsigned x = pp[u] % a.w, t = pp[u] / a.w;
             const unsigned y = t % a.h, b = t / a.h;
             base[u] = ((b * Hp + y) * Wp + x) * Q;
@@ -279,8 +287,9 @@ int md2_disp_head_fwd(const md2_head_desc* d, const float* padded, const float* 
     const int L = Q < 16 ? Q : 16;
     const long long threads = (long long)a.B * a.h * a.w * L;
     const long long need = (threads + kThreads - 1) / kThreads;
-    const long long want = (need + 3) / 4;                          // each group walks >= 4 pixels
-    const int grid = (int)(want < kFwdBlocks ? want : kFwdBlocks);
+    long long want = (need + 3) / 4;                                // each group walks >= 4 pixels
+    want = want < 8 ? 8 : (want > kFwdBlocks ? kFwdBlocks : want);
+    const int grid = (int)((want + 7) / 8 * 8);                     // whole XCD rounds
     void (*k)(HeadArgs) = Q == 1    ? head_fwd_kernel<1, 1>
                           : Q == 2  ? head_fwd_kernel<2, 1>
                           : Q == 4  ? head_fwd_kernel<4, 1>
