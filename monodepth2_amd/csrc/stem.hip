@@ -121,28 +121,38 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(StemArgs a) {
     const int nseg = a.B * Ho * spr;
     float* dummy = lds + kBufs * L::BUF;
     // exactly L::K DMA instructions per wave (out-of-image lanes copy zeros)
+    // Row r of the window is x[b][iy0 + r][ix0 .. ix0 + 2·kSeg + 4][0 .. C) — one
+    // contiguous run of RW floats starting at element ix0·C of the image row, so a lane's
+    // element e is in the image iff 0 <= ix0·C + e < W·C: no per-lane division.  The
+    // address math is per wave (scalar) except for that one add and compare.
+    const int WC = W * C;
     auto issue = [&](int sg, float* buf) {
         const int sx = sg % spr, t2 = sg / spr, oy = t2 % Ho, b = t2 / Ho;
-        const int ox0 = sx * kSeg, iy0 = 2 * oy - 3, ix0 = 2 * ox0 - 3;
+        const int ox0 = sx * kSeg, iy0 = 2 * oy - 3, e0 = (2 * ox0 - 3) * C;
+        const float* img = a.x + (size_t)b * H * WC;
+#pragma unroll
         for (int k = 0; k < L::NXI; ++k) {
             const int ins = wave + k * kWaves;
             if (ins >= L::XI) {
                 __builtin_amdgcn_global_load_lds(a.zeros + lane, (uint32_t*)dummy, 4, 0, 0);
                 continue;
             }
-            const int r = ins / L::RI, e = (ins - r * L::RI) * 64 + lane;   // element of row r
-            const int iy = iy0 + r, ix = ix0 + e / C;
-            float* dst = buf + r * L::RWP + (ins - r * L::RI) * 64;          // wave-uniform
-            const bool ok = e < L::RW && iy >= 0 && iy < H && ix >= 0 && ix < W;
+            const int r = ins / L::RI, c0 = (ins - r * L::RI) * 64;        // wave-uniform
+            const int iy = iy0 + r;
+            const bool row_ok = iy >= 0 && iy < H;
+            const int e = c0 + lane, eg = e0 + e;                          // element in the image row
+            const bool ok = row_ok && e < L::RW && (unsigned)eg < (unsigned)WC;
             // every lane issues (the per-wave DMA count must be exactly K for the
             // vmcnt waits): outside the image / past the row, it copies a zero
-            const float* src = ok ? a.x + ((size_t)(b * H + iy) * W + ix) * C + (e % C) : a.zeros + lane;
-            __builtin_amdgcn_global_load_lds(src, (uint32_t*)dst, 4, 0, 0);
+            const float* src = ok ? img + (size_t)(row_ok ? iy : 0) * WC + eg : a.zeros + lane;
+            __builtin_amdgcn_global_load_lds(src, (uint32_t*)(buf + r * L::RWP + c0), 4, 0, 0);
         }
         float* dy = buf + L::XS;
+        const float* gyrow = a.gy + (size_t)(b * Ho + oy) * Wo * kCo;
+#pragma unroll
         for (int k = 0; k < kSeg / kWaves; ++k) {
             const int j = wave + k * kWaves, ox = ox0 + j;
-            const float* src = ox < Wo ? a.gy + ((size_t)(b * Ho + oy) * Wo + ox) * kCo + lane : a.zeros + lane;
+            const float* src = ox < Wo ? gyrow + (size_t)ox * kCo + lane : a.zeros + lane;
             __builtin_amdgcn_global_load_lds(src, (uint32_t*)(dy + j * kDyS), 4, 0, 0);
         }
     };

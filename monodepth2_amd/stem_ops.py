@@ -7,10 +7,10 @@ depth / pose encoder).  The forward stays MIOpen's.  Same parameter (the torchvi
 `conv1.weight`), same semantics; any other case (an input that needs a gradient,
 bf16, NCHW inputs, a CPU tensor) runs the module itself.
 
-OFF by default (ENABLED): measured in the training step it runs 145 µs (C=3) and
-507 µs (C=6) + 28/53 µs for the partial sums, against MIOpen's 167 / 391 µs — the
-kernel is parity-tested and kept for the next round's work on its issue rate
-(DESIGN.md §8).
+OFF by default (ENABLED): at the step's shapes it runs 131 µs (C=3) and 496 µs
+(C=6) + 19/25 µs for the partial sums, against MIOpen's 130 / 427 µs
+(tools/stem_bench.py) — the kernel is parity-tested and kept for the next round's
+work on its issue rate.
 """
 from __future__ import annotations
 
