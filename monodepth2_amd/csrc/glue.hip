@@ -42,6 +42,42 @@ __global__ __launch_bounds__(kThreads) void encoder_input_kernel(InputArgs a) {
     }
 }
 
+// Four pixels per thread (HW % 4 == 0): one float4 load per source channel, the
+// 4 x 3·slots output floats written as 3·slots float4 stores (16-B aligned because
+// the thread's first pixel is a multiple of 4).  Same arithmetic as above.
+template <int SLOTS>
+__global__ __launch_bounds__(kThreads) void encoder_input_v4_kernel(InputArgs a) {
+    constexpr int OC = 3 * SLOTS;
+    const int i4 = blockIdx.x * kThreads + threadIdx.x;   // quad of pixels
+    if (i4 * 4 >= a.n) return;
+    const int i = i4 * 4;
+    const int nb = i / a.HW, p = i - nb * a.HW;
+    const int grp = nb / a.B, b = nb - grp * a.B;
+    float v[4][OC];
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k) {
+        const float* s = a.src[grp * SLOTS + k] + (size_t)b * 3 * a.HW + p;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float4 x = *reinterpret_cast<const float4*>(s + (size_t)c * a.HW);
+            v[0][3 * k + c] = (x.x - a.mean) * a.inv_std;
+            v[1][3 * k + c] = (x.y - a.mean) * a.inv_std;
+            v[2][3 * k + c] = (x.z - a.mean) * a.inv_std;
+            v[3][3 * k + c] = (x.w - a.mean) * a.inv_std;
+        }
+    }
+    float4* o = reinterpret_cast<float4*>(a.out + (size_t)i * OC);
+#pragma unroll
+    for (int q = 0; q < OC; ++q) {   // the 4·OC floats in pixel-major order, four at a time
+        float4 w;
+        w.x = v[(4 * q + 0) / OC][(4 * q + 0) % OC];
+        w.y = v[(4 * q + 1) / OC][(4 * q + 1) % OC];
+        w.z = v[(4 * q + 2) / OC][(4 * q + 2) % OC];
+        w.w = v[(4 * q + 3) / OC][(4 * q + 3) % OC];
+        o[q] = w;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -65,8 +101,16 @@ int md2_encoder_input(int groups, int batch, int slots, int height, int width, c
     a.n = (int)n;
     a.mean = mean;
     a.inv_std = 1.f / std_;
-    hipLaunchKernelGGL(encoder_input_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
-                       (hipStream_t)stream, a);
+    bool v4 = a.HW % 4 == 0 && (slots == 1 || slots == 2) && ((uintptr_t)out & 15) == 0;
+    for (int k = 0; k < groups * slots; ++k) v4 = v4 && ((uintptr_t)src[k] & 15) == 0;
+    if (v4) {
+        const long long n4 = n / 4;
+        hipLaunchKernelGGL(slots == 1 ? encoder_input_v4_kernel<1> : encoder_input_v4_kernel<2>,
+                           dim3((unsigned)((n4 + kThreads - 1) / kThreads)), dim3(kThreads), 0, (hipStream_t)stream, a);
+    } else {
+        hipLaunchKernelGGL(encoder_input_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                           (hipStream_t)stream, a);
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }

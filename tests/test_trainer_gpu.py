@@ -206,3 +206,7 @@ def test_encoder_input_matches_eager():
     assert torch.equal(x, ref)
     x1 = enc1.prepare(fr[2])
     assert torch.equal(x1, (fr[2] - 0.45) / 0.225) and x1.is_contiguous(memory_format=torch.channels_last)
+    # H*W not a multiple of 4: the one-pixel-per-thread kernel
+    fo = [torch.rand(2, 3, 15, 23, device="cuda", generator=g) for _ in range(2)]
+    xo = enc.prepare([[fo[0], fo[1]]])
+    assert torch.equal(xo, (torch.cat(fo, 1) - 0.45) / 0.225)
