@@ -100,6 +100,36 @@ __global__ void __launch_bounds__(kThreads) maxpool_bwd_kernel(PoolArgs p, const
     }
 }
 
+// Same gather, one block row per input row (blockIdx.y = b·H + iy, decoded once per
+// block) and C/4 a power of two: the per-element (ix, c4) split is a shift and a mask
+// instead of six integer divisions (the kernel was VALU bound on them).
+template <typename T>
+__global__ void __launch_bounds__(kThreads) maxpool_bwd_rows_kernel(PoolArgs p, int c4_shift,
+                                                                    const uint32_t* __restrict__ idx,
+                                                                    const void* __restrict__ gy, void* __restrict__ gx) {
+    const int C4 = p.C / 4;
+    const int j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= p.W * C4) return;
+    const int row = blockIdx.y, b = row / p.H, iy = row - b * p.H;
+    const int c4 = j & (C4 - 1), ix = j >> c4_shift;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int oy = iy / 2; oy <= (iy + 1) / 2; ++oy) {
+        if (oy >= p.Ho || 2 * oy - 1 > iy || 2 * oy + 1 < iy) continue;
+        for (int ox = ix / 2; ox <= (ix + 1) / 2; ++ox) {
+            if (ox >= p.Wo || 2 * ox - 1 > ix || 2 * ox + 1 < ix) continue;
+            const size_t o = (((size_t)b * p.Ho + oy) * p.Wo + ox) * C4 + c4;
+            const uint32_t w = idx[o];
+            const int k = (iy - (2 * oy - 1)) * 3 + (ix - (2 * ox - 1));
+            const float4 g = md2::ld4T<T>(gy, 4 * o);
+            if ((int)(w & 255u) == k) s[0] += g.x;
+            if ((int)((w >> 8) & 255u) == k) s[1] += g.y;
+            if ((int)((w >> 16) & 255u) == k) s[2] += g.z;
+            if ((int)(w >> 24) == k) s[3] += g.w;
+        }
+    }
+    md2::st4T<T>(gx, 4 * ((size_t)row * p.W * C4 + j), make_float4(s[0], s[1], s[2], s[3]));
+}
+
 int grid_for(long long n) {
     const long long g = (n + kThreads - 1) / kThreads;
     return (int)(g < 8192 ? g : 8192);
@@ -135,8 +165,17 @@ int md2_maxpool3s2_bwd(const md2_pool_desc* d, const uint32_t* idx, const void* 
     if (!make(d, p) || !idx || !grad_y || !grad_x)
         return md2_report_error(MD2_ERR_ARG, "maxpool: bad desc or NULL operand");
     const long long n = (long long)p.B * p.H * p.W * (p.C / 4);
-    auto k = (d->flags & MD2_POOL_BF16) ? maxpool_bwd_kernel<uint16_t> : maxpool_bwd_kernel<float>;
-    hipLaunchKernelGGL(k, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, p, idx, grad_y, grad_x);
+    const int C4 = p.C / 4;
+    if ((C4 & (C4 - 1)) == 0 && (long long)p.B * p.H <= 65535) {
+        int sh = 0;
+        while ((1 << sh) < C4) ++sh;
+        auto k = (d->flags & MD2_POOL_BF16) ? maxpool_bwd_rows_kernel<uint16_t> : maxpool_bwd_rows_kernel<float>;
+        hipLaunchKernelGGL(k, dim3((p.W * C4 + kThreads - 1) / kThreads, p.B * p.H), dim3(kThreads), 0,
+                           (hipStream_t)stream, p, sh, idx, grad_y, grad_x);
+    } else {
+        auto k = (d->flags & MD2_POOL_BF16) ? maxpool_bwd_kernel<uint16_t> : maxpool_bwd_kernel<float>;
+        hipLaunchKernelGGL(k, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, p, idx, grad_y, grad_x);
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }
