@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 7
+#define MD2_ABI_VERSION 8
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -407,6 +407,12 @@ typedef struct md2_pool_desc {
 int md2_maxpool3s2_fwd(const md2_pool_desc* desc, const void* x, void* y, uint32_t* idx, void* stream);
 int md2_maxpool3s2_bwd(const md2_pool_desc* desc, const uint32_t* idx, const void* grad_y, void* grad_x,
                        void* stream);
+/* grad_x = the pool's adjoint of grad_y + grad_add (same shape and layout as x; NULL
+ * = none): the stem activation also feeds the DepthDecoder skip (resnet_encoder.py:96
+ * features[0]), so its two gradients are summed in the gather instead of a separate
+ * add pass. */
+int md2_maxpool3s2_bwd_add(const md2_pool_desc* desc, const uint32_t* idx, const void* grad_y, const void* grad_add,
+                           void* grad_x, void* stream);
 
 #ifdef __cplusplus
 }

@@ -133,10 +133,13 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, residual: Optional[torch.Tensor]
 
 
 class _MaxPool(torch.autograd.Function):
-    """MaxPool2d(3, 2, 1) on channels_last tensors (csrc/pool.hip)."""
+    """MaxPool2d(3, 2, 1) on channels_last tensors (csrc/pool.hip).  with_alias: also
+    return the input itself (a view) for a second consumer; its gradient then comes
+    into this backward and is summed in the pool's gather (md2_maxpool3s2_bwd_add)
+    instead of by a separate add of the two gradients."""
 
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, with_alias: bool = False):
         B, C, H, W = x.shape
         Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
         d = _lib.PoolDesc(B, C, H, W, _lib.POOL_BF16 if x.dtype == torch.bfloat16 else 0, 0)
@@ -148,25 +151,43 @@ class _MaxPool(torch.autograd.Function):
         ctx.save_for_backward(idx)
         ctx.desc = (B, C, H, W, d.flags, 0)
         ctx.xshape, ctx.dtype = x.shape, x.dtype
+        if with_alias:
+            ctx.set_materialize_grads(False)   # an unused alias brings None, not a zero tensor
+            return y, x.view_as(x)
         return y
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, galias=None):
         (idx,) = ctx.saved_tensors
         gy = gy.to(ctx.dtype).contiguous(memory_format=_CL)
+        if galias is not None:
+            galias = galias.to(ctx.dtype).contiguous(memory_format=_CL)
         gx = torch.empty(ctx.xshape, device=gy.device, dtype=ctx.dtype, memory_format=_CL)
         d = _lib.PoolDesc(*ctx.desc)
-        _lib.check(_lib.lib().md2_maxpool3s2_bwd(ctypes.byref(d), idx.data_ptr(), gy.data_ptr(), gx.data_ptr(),
-                                                 torch.cuda.current_stream(gy.device).cuda_stream),
-                   "md2_maxpool3s2_bwd")
-        return gx
+        _lib.check(_lib.lib().md2_maxpool3s2_bwd_add(ctypes.byref(d), idx.data_ptr(), gy.data_ptr(),
+                                                     galias.data_ptr() if galias is not None else None,
+                                                     gx.data_ptr(), torch.cuda.current_stream(gy.device).cuda_stream),
+                   "md2_maxpool3s2_bwd_add")
+        return gx, None
+
+
+def _pool_ok(pool: nn.MaxPool2d, x: torch.Tensor) -> bool:
+    return (ENABLED and x.is_cuda and x.dim() == 4 and x.dtype in (torch.float32, torch.bfloat16)
+            and x.shape[1] % 4 == 0 and x.is_contiguous(memory_format=_CL)
+            and pool.kernel_size in (3, (3, 3)) and pool.stride in (2, (2, 2)) and pool.padding in (1, (1, 1))
+            and pool.dilation in (1, (1, 1)) and not pool.ceil_mode and not pool.return_indices)
 
 
 def max_pool_3x3s2(pool: nn.MaxPool2d, x: torch.Tensor) -> torch.Tensor:
     """The ResNet stem pool: HIP kernels for channels_last fp32/bf16 GPU tensors."""
-    if (ENABLED and x.is_cuda and x.dim() == 4 and x.dtype in (torch.float32, torch.bfloat16)
-            and x.shape[1] % 4 == 0 and x.is_contiguous(memory_format=_CL)
-            and pool.kernel_size in (3, (3, 3)) and pool.stride in (2, (2, 2)) and pool.padding in (1, (1, 1))
-            and pool.dilation in (1, (1, 1)) and not pool.ceil_mode and not pool.return_indices):
-        return _MaxPool.apply(x)
+    if _pool_ok(pool, x):
+        return _MaxPool.apply(x, False)
     return pool(x)
+
+
+def max_pool_3x3s2_with_alias(pool: nn.MaxPool2d, x: torch.Tensor):
+    """(pool(x), x') with x' a view of x for x's other consumer (the decoder skip):
+    on the HIP path both gradients of x meet in the pool's backward gather."""
+    if _pool_ok(pool, x) and torch.is_grad_enabled() and x.requires_grad:
+        return _MaxPool.apply(x, True)
+    return max_pool_3x3s2(pool, x), x

@@ -70,7 +70,8 @@ __global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(PoolArgs p, const
 
 template <typename T>
 __global__ void __launch_bounds__(kThreads) maxpool_bwd_kernel(PoolArgs p, const uint32_t* __restrict__ idx,
-                                                               const void* __restrict__ gy, void* __restrict__ gx) {
+                                                               const void* __restrict__ gy, const void* __restrict__ ga,
+                                                               void* __restrict__ gx) {
     const int C4 = p.C / 4;
     const int n = p.B * p.H * p.W * C4;
     for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
@@ -96,6 +97,10 @@ __global__ void __launch_bounds__(kThreads) maxpool_bwd_kernel(PoolArgs p, const
                 if ((int)(w >> 24) == k) s[3] += g.w;
             }
         }
+        if (ga) {
+            const float4 v = md2::ld4T<T>(ga, 4 * (size_t)i);
+            s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
+        }
         md2::st4T<T>(gx, 4 * i, make_float4(s[0], s[1], s[2], s[3]));
     }
 }
@@ -106,7 +111,8 @@ __global__ void __launch_bounds__(kThreads) maxpool_bwd_kernel(PoolArgs p, const
 template <typename T>
 __global__ void __launch_bounds__(kThreads) maxpool_bwd_rows_kernel(PoolArgs p, int c4_shift,
                                                                     const uint32_t* __restrict__ idx,
-                                                                    const void* __restrict__ gy, void* __restrict__ gx) {
+                                                                    const void* __restrict__ gy,
+                                                                    const void* __restrict__ ga, void* __restrict__ gx) {
     const int C4 = p.C / 4;
     const int j = blockIdx.x * kThreads + threadIdx.x;
     if (j >= p.W * C4) return;
@@ -127,7 +133,12 @@ __global__ void __launch_bounds__(kThreads) maxpool_bwd_rows_kernel(PoolArgs p, 
             if ((int)(w >> 24) == k) s[3] += g.w;
         }
     }
-    md2::st4T<T>(gx, 4 * ((size_t)row * p.W * C4 + j), make_float4(s[0], s[1], s[2], s[3]));
+    const size_t e = 4 * ((size_t)row * p.W * C4 + j);
+    if (ga) {   // a second consumer's gradient of the pool input (the decoder skip)
+        const float4 v = md2::ld4T<T>(ga, e);
+        s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
+    }
+    md2::st4T<T>(gx, e, make_float4(s[0], s[1], s[2], s[3]));
 }
 
 int grid_for(long long n) {
@@ -160,7 +171,8 @@ int md2_maxpool3s2_fwd(const md2_pool_desc* d, const void* x, void* y, uint32_t*
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }
 
-int md2_maxpool3s2_bwd(const md2_pool_desc* d, const uint32_t* idx, const void* grad_y, void* grad_x, void* stream) {
+int md2_maxpool3s2_bwd_add(const md2_pool_desc* d, const uint32_t* idx, const void* grad_y, const void* grad_add,
+                           void* grad_x, void* stream) {
     PoolArgs p;
     if (!make(d, p) || !idx || !grad_y || !grad_x)
         return md2_report_error(MD2_ERR_ARG, "maxpool: bad desc or NULL operand");
@@ -171,13 +183,18 @@ int md2_maxpool3s2_bwd(const md2_pool_desc* d, const uint32_t* idx, const void* 
         while ((1 << sh) < C4) ++sh;
         auto k = (d->flags & MD2_POOL_BF16) ? maxpool_bwd_rows_kernel<uint16_t> : maxpool_bwd_rows_kernel<float>;
         hipLaunchKernelGGL(k, dim3((p.W * C4 + kThreads - 1) / kThreads, p.B * p.H), dim3(kThreads), 0,
-                           (hipStream_t)stream, p, sh, idx, grad_y, grad_x);
+                           (hipStream_t)stream, p, sh, idx, grad_y, grad_add, grad_x);
     } else {
         auto k = (d->flags & MD2_POOL_BF16) ? maxpool_bwd_kernel<uint16_t> : maxpool_bwd_kernel<float>;
-        hipLaunchKernelGGL(k, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, p, idx, grad_y, grad_x);
+        hipLaunchKernelGGL(k, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, p, idx, grad_y, grad_add,
+                           grad_x);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
+int md2_maxpool3s2_bwd(const md2_pool_desc* d, const uint32_t* idx, const void* grad_y, void* grad_x, void* stream) {
+    return md2_maxpool3s2_bwd_add(d, idx, grad_y, nullptr, grad_x, stream);
 }
 
 }  // extern "C"

@@ -19,7 +19,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..bn_ops import bn_act, max_pool_3x3s2
+from ..bn_ops import bn_act, max_pool_3x3s2, max_pool_3x3s2_with_alias
 from ..stem_ops import stem_conv
 
 
@@ -170,7 +170,8 @@ class ResnetEncoder(nn.Module):
         """The encoder on an input already normalised by `prepare`."""
         e = self.encoder
         f0 = bn_act(e.bn1, stem_conv(e.conv1, x))   # weight gradient on f32 MFMA (stem_ops)
-        f1 = e.layer1(max_pool_3x3s2(e.maxpool, f0))
+        pooled, f0 = max_pool_3x3s2_with_alias(e.maxpool, f0)   # f0's two gradients meet in the pool backward
+        f1 = e.layer1(pooled)
         f2 = e.layer2(f1)
         f3 = e.layer3(f2)
         f4 = e.layer4(f3)

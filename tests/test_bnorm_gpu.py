@@ -188,3 +188,25 @@ def test_maxpool_nan_propagates():
     x[0, 1, 2, 3] = float("nan")
     y = bn_ops.max_pool_3x3s2(pool, x)
     assert torch.equal(torch.isnan(y), torch.isnan(pool(x)))
+
+
+def test_maxpool_with_alias_sums_both_gradients():
+    """max_pool_3x3s2_with_alias: the alias's gradient (the decoder skip of the stem
+    activation) is added in the pool's backward gather (md2_maxpool3s2_bwd_add) —
+    same gradient as autograd's sum over the two consumers."""
+    torch.manual_seed(9)
+    CL = torch.channels_last
+    pool = torch.nn.MaxPool2d(3, 2, 1)
+    x = torch.randn(2, 64, 24, 40, device="cuda").contiguous(memory_format=CL).requires_grad_(True)
+    y, xa = bn_ops.max_pool_3x3s2_with_alias(pool, x)
+    assert "MaxPool" in type(xa.grad_fn).__name__ and torch.equal(xa, x)
+    gy, ga = torch.randn_like(y), torch.randn_like(x)
+    gx, = torch.autograd.grad([y, xa], x, [gy, ga])
+    yr = pool(x)
+    gxr, = torch.autograd.grad([yr, x * 1.0], x, [gy, ga])
+    torch.testing.assert_close(gx, gxr, rtol=1e-6, atol=1e-6)
+    # alias unused: the plain pool adjoint
+    y2, _ = bn_ops.max_pool_3x3s2_with_alias(pool, x)
+    g2, = torch.autograd.grad(y2, x, gy)
+    g2r, = torch.autograd.grad(pool(x), x, gy)
+    torch.testing.assert_close(g2, g2r, rtol=1e-6, atol=1e-6)
