@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 8
+#define MD2_ABI_VERSION 9
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -388,6 +388,14 @@ int md2_bn_bwd(const md2_bn_desc* desc, const void* x, const void* y, const void
                const float* gamma, const float* save_mean, const float* save_invstd,
                void* grad_x, void* grad_residual, float* grad_gamma, float* grad_beta,
                void* workspace, void* stream);
+/* md2_bn_bwd with the output gradient given as up to three tensors summed on load
+ * (grad_y + grad_y2 + grad_y3; grad_y2 / grad_y3 may be NULL): the output's other
+ * consumers (the next block's shortcut, the decoder skip) hand their gradients here
+ * instead of autograd adding them in separate passes. */
+int md2_bn_bwd_multi(const md2_bn_desc* desc, const void* x, const void* y, const void* grad_y,
+                     const void* grad_y2, const void* grad_y3, const float* gamma, const float* save_mean,
+                     const float* save_invstd, void* grad_x, void* grad_residual, float* grad_gamma,
+                     float* grad_beta, void* workspace, void* stream);
 
 /*
  * The ResNet stem's MaxPool2d(3, stride 2, padding 1) on channels_last activations

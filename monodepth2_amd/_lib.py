@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -61,7 +61,7 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_bn_workspace_bytes", "md2_bn_fwd", "md2_bn_bwd", "md2_maxpool3s2_fwd", "md2_maxpool3s2_bwd",
            "md2_disp_head_workspace_bytes", "md2_disp_head_fwd", "md2_disp_head_bwd",
            "md2_stem_wgrad_workspace_bytes", "md2_stem_wgrad", "md2_bias_act_fwd", "md2_bias_act_bwd",
-           "md2_bias_act_workspace_bytes", "md2_maxpool3s2_bwd_add"]
+           "md2_bias_act_workspace_bytes", "md2_maxpool3s2_bwd_add", "md2_bn_bwd_multi"]
 
 PAD_ELU = 1 << 0
 PAD_UPSAMPLE = 1 << 1
@@ -193,6 +193,8 @@ def _declare(L):
     L.md2_maxpool3s2_fwd.argtypes = [ctypes.POINTER(PoolDesc), _vp, _vp, _vp, _vp]
     L.md2_maxpool3s2_bwd.restype = ctypes.c_int
     L.md2_maxpool3s2_bwd.argtypes = [ctypes.POINTER(PoolDesc), _vp, _vp, _vp, _vp]
+    L.md2_bn_bwd_multi.restype = ctypes.c_int
+    L.md2_bn_bwd_multi.argtypes = [ctypes.POINTER(BnDesc)] + [_vp] * 14
     L.md2_maxpool3s2_bwd_add.restype = ctypes.c_int
     L.md2_maxpool3s2_bwd_add.argtypes = [ctypes.POINTER(PoolDesc)] + [_vp] * 5
     L.md2_timing_begin.restype = ctypes.c_int

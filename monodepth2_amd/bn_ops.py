@@ -67,7 +67,7 @@ class _BNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu: bool, eps: float,
-                momentum: float, groups: int):
+                momentum: float, groups: int, aliases: int = 0):
         B, C, H, W = x.shape
         flags = ((_lib.BN_RELU if relu else 0) | (_lib.BN_RESIDUAL if residual is not None else 0)
                  | (_lib.BN_BF16 if x.dtype == torch.bfloat16 else 0))
@@ -87,12 +87,20 @@ class _BNAct(torch.autograd.Function):
         ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
         ctx.desc = (B * H * W, C, flags, eps, momentum, groups, 0)
         ctx.has_res = residual is not None
+        if aliases:
+            # views of y for its other consumers: their gradients come into this backward
+            # and are summed on load by the backward kernels (md2_bn_bwd_multi)
+            ctx.set_materialize_grads(False)
+            return (y,) + tuple(y.view_as(y) for _ in range(aliases))
         return y
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, *grads):
         x, y, weight, mean, invstd = ctx.saved_tensors
-        gy = gy.to(x.dtype).contiguous(memory_format=_CL)
+        gs = [g.to(x.dtype).contiguous(memory_format=_CL) for g in grads if g is not None]
+        if not gs:
+            return (None,) * 11
+        gy = gs[0]
         d = _lib.BnDesc(*ctx.desc)
         L = _lib.lib()
         ws = _workspace(x.device, L.md2_bn_workspace_bytes(ctypes.byref(d)))
@@ -100,18 +108,24 @@ class _BNAct(torch.autograd.Function):
         gr = torch.empty_like(x, memory_format=_CL) if ctx.has_res else None
         gw = torch.empty_like(weight)
         gb = torch.empty_like(weight)
-        rc = L.md2_bn_bwd(ctypes.byref(d), x.data_ptr(), y.data_ptr() if y is not None else None, gy.data_ptr(),
-                          weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gx.data_ptr(),
-                          gr.data_ptr() if gr is not None else None, gw.data_ptr(), gb.data_ptr(), ws.data_ptr(),
-                          torch.cuda.current_stream(x.device).cuda_stream)
-        _lib.check(rc, "md2_bn_bwd")
-        return gx, gw, gb, None, None, gr, None, None, None, None
+        rc = L.md2_bn_bwd_multi(ctypes.byref(d), x.data_ptr(), y.data_ptr() if y is not None else None,
+                                gy.data_ptr(), gs[1].data_ptr() if len(gs) > 1 else None,
+                                gs[2].data_ptr() if len(gs) > 2 else None,
+                                weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gx.data_ptr(),
+                                gr.data_ptr() if gr is not None else None, gw.data_ptr(), gb.data_ptr(), ws.data_ptr(),
+                                torch.cuda.current_stream(x.device).cuda_stream)
+        _lib.check(rc, "md2_bn_bwd_multi")
+        return gx, gw, gb, None, None, gr, None, None, None, None, None
 
 
 def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-           relu: bool = True) -> torch.Tensor:
+           relu: bool = True, aliases: int = 0):
     """relu(bn(x) + residual) (ReLU / residual optional) for a training-mode BatchNorm2d
-    (per chunk inside bn_groups)."""
+    (per chunk inside bn_groups).  aliases = k > 0: returns (y, y_1, ..., y_k), views of
+    y for its other consumers, whose gradients the fused backward sums on load (k <= 2);
+    outside the fused path the y_i are y itself."""
+    if not 0 <= aliases <= 2:
+        raise ValueError("bn_act: at most two aliases")
     groups = _GROUPS if bn.training else 1
     if groups > 1 and x.shape[0] % groups:
         raise ValueError(f"batch {x.shape[0]} does not split into {groups} BatchNorm groups")
@@ -124,12 +138,17 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, residual: Optional[torch.Tensor]
             residual = residual.to(x.dtype)
         if bn.num_batches_tracked is not None:   # nn.BatchNorm2d counts training batches
             bn.num_batches_tracked.add_(groups)
-        return _BNAct.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual, relu, bn.eps,
-                            bn.momentum, groups)
+        k = aliases if torch.is_grad_enabled() else 0
+        out = _BNAct.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual, relu, bn.eps,
+                           bn.momentum, groups, k)
+        if aliases and not k:   # no graph: the aliases are y itself
+            return (out,) * (aliases + 1)
+        return out
     y = bn(x) if groups == 1 else torch.cat([bn(xc) for xc in x.chunk(groups)], 0)
     if residual is not None:
         y = y + residual
-    return F.relu(y) if relu else y
+    y = F.relu(y) if relu else y
+    return (y,) * (aliases + 1) if aliases else y
 
 
 class _MaxPool(torch.autograd.Function):

@@ -214,10 +214,28 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const void* __restri
     }
 }
 
+// the output gradient: g (+ g2 + g3, the gradients of the output's aliases — its
+// other consumers, summed here instead of by separate add passes)
+template <typename T>
+__device__ __forceinline__ float4 ld_grad(const void* g, const void* g2, const void* g3, size_t off) {
+    float4 v = ldT<T>(g, off);
+    if (g2) {
+        const float4 u = ldT<T>(g2, off);
+        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    if (g3) {
+        const float4 u = ldT<T>(g3, off);
+        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    return v;
+}
+
 template <typename T, bool RELU>
 __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const void* __restrict__ x,
                                                                  const void* __restrict__ y,
-                                                                 const void* __restrict__ g, long long P, int C,
+                                                                 const void* __restrict__ g,
+                                                                 const void* __restrict__ g2,
+                                                                 const void* __restrict__ g3, long long P, int C,
                                                                  int G, const float* __restrict__ smean, void* ws) {
     const Map m = make_map(C);
     const int NG = gridDim.y, grp = blockIdx.y;
@@ -242,7 +260,7 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const void* __r
         long long p = (long long)blockIdx.x * m.PPB + pl;
         for (; p + stride < P; p += 2 * stride) {   // two pixels (up to six loads) in flight per lane
             const size_t o0 = base + p * C + 4 * q, o1 = base + (p + stride) * C + 4 * q;
-            const float4 g0 = ldT<T>(g, o0), g1 = ldT<T>(g, o1);
+            const float4 g0 = ld_grad<T>(g, g2, g3, o0), g1 = ld_grad<T>(g, g2, g3, o1);
             const float4 y0 = RELU ? ldT<T>(y, o0) : zero, y1 = RELU ? ldT<T>(y, o1) : zero;
             const float4 v0 = ldT<T>(x, o0), v1 = ldT<T>(x, o1);
             acc(g0, y0, v0);
@@ -250,7 +268,7 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const void* __r
         }
         for (; p < P; p += stride) {
             const size_t o = base + p * C + 4 * q;
-            acc(ldT<T>(g, o), RELU ? ldT<T>(y, o) : zero, ldT<T>(x, o));
+            acc(ld_grad<T>(g, g2, g3, o), RELU ? ldT<T>(y, o) : zero, ldT<T>(x, o));
         }
         block_partials(s, sx, q, pl, m, C, NG * G, grp * G + blockIdx.x, w, lds);
     }
@@ -287,6 +305,8 @@ template <typename T, bool RELU, bool RES>
 __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const void* __restrict__ x,
                                                                 const void* __restrict__ y,
                                                                 const void* __restrict__ g,
+                                                                const void* __restrict__ g2,
+                                                                const void* __restrict__ g3,
                                                                 const float* __restrict__ smean, const float* coef,
                                                                 void* __restrict__ dx, void* __restrict__ dr,
                                                                 int n4g, int Q, int C, int NG) {
@@ -295,7 +315,7 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const void* __re
     for (int j = blockIdx.x * kThreads + threadIdx.x; j < n4g; j += gridDim.x * kThreads) {
         const size_t i = base + j;
         const size_t c = gc + 4 * (j & (Q - 1));
-        float4 gv = ldT<T>(g, 4 * i);
+        float4 gv = ld_grad<T>(g, g2, g3, 4 * i);
         if (RELU) {
             const float4 yv = ldT<T>(y, 4 * i);
             gv.x = yv.x > 0.f ? gv.x : 0.f; gv.y = yv.y > 0.f ? gv.y : 0.f;
@@ -356,7 +376,8 @@ void launch_fwd(const md2_bn_desc* d, const void* x, const float* gamma, const f
 }
 
 template <typename T>
-void launch_bwd(const md2_bn_desc* d, const void* x, const void* y, const void* grad_y, const float* gamma,
+void launch_bwd(const md2_bn_desc* d, const void* x, const void* y, const void* grad_y, const void* grad_y2,
+                const void* grad_y3, const float* gamma,
                 const float* save_mean, const float* save_invstd, void* grad_x, void* grad_residual,
                 float* grad_gamma, float* grad_beta, void* workspace, hipStream_t st) {
     const int NG = groups_of(d);
@@ -364,15 +385,16 @@ void launch_bwd(const md2_bn_desc* d, const void* x, const void* y, const void* 
     const int C = d->channels, G = blocks_for_stats(P, C);
     const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
     auto red = relu ? bn_bwd_reduce_kernel<T, true> : bn_bwd_reduce_kernel<T, false>;
-    hipLaunchKernelGGL(red, dim3(G, NG), dim3(kThreads), 0, st, x, y, grad_y, P, C, G, save_mean, workspace);
+    hipLaunchKernelGGL(red, dim3(G, NG), dim3(kThreads), 0, st, x, y, grad_y, grad_y2, grad_y3, P, C, G, save_mean,
+                       workspace);
     hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, NG, gamma, save_invstd,
                        grad_gamma, grad_beta, workspace);
     const int n4g = (int)(P * C / 4);
     const float* coef = work(workspace, G, C, NG).coef;
     auto k = relu ? (res ? bn_bwd_apply_kernel<T, true, true> : bn_bwd_apply_kernel<T, true, false>)
                   : (res ? bn_bwd_apply_kernel<T, false, true> : bn_bwd_apply_kernel<T, false, false>);
-    hipLaunchKernelGGL(k, dim3(grid_elem(n4g, NG), NG), dim3(kThreads), 0, st, x, y, grad_y, save_mean, coef,
-                       grad_x, grad_residual, n4g, C / 4, C, NG);
+    hipLaunchKernelGGL(k, dim3(grid_elem(n4g, NG), NG), dim3(kThreads), 0, st, x, y, grad_y, grad_y2, grad_y3,
+                       save_mean, coef, grad_x, grad_residual, n4g, C / 4, C, NG);
 }
 
 }  // namespace
@@ -404,22 +426,30 @@ int md2_bn_fwd(const md2_bn_desc* d, const void* x, const float* gamma, const fl
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }
 
-int md2_bn_bwd(const md2_bn_desc* d, const void* x, const void* y, const void* grad_y, const float* gamma,
-               const float* save_mean, const float* save_invstd, void* grad_x, void* grad_residual,
-               float* grad_gamma, float* grad_beta, void* workspace, void* stream) {
+int md2_bn_bwd_multi(const md2_bn_desc* d, const void* x, const void* y, const void* grad_y, const void* grad_y2,
+                     const void* grad_y3, const float* gamma, const float* save_mean, const float* save_invstd,
+                     void* grad_x, void* grad_residual, float* grad_gamma, float* grad_beta, void* workspace,
+                     void* stream) {
     if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "bn: unsupported shape");
     const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
     if (!x || !grad_y || !gamma || !save_mean || !save_invstd || !grad_x || !grad_gamma || !grad_beta ||
-        !workspace || (relu && !y) || (res && !grad_residual))
+        !workspace || (relu && !y) || (res && !grad_residual) || (grad_y3 && !grad_y2))
         return md2_report_error(MD2_ERR_ARG, "bn_bwd: NULL operand");
     if (d->flags & MD2_BN_BF16)
-        launch_bwd<uint16_t>(d, x, y, grad_y, gamma, save_mean, save_invstd, grad_x, grad_residual, grad_gamma,
-                             grad_beta, workspace, (hipStream_t)stream);
+        launch_bwd<uint16_t>(d, x, y, grad_y, grad_y2, grad_y3, gamma, save_mean, save_invstd, grad_x,
+                             grad_residual, grad_gamma, grad_beta, workspace, (hipStream_t)stream);
     else
-        launch_bwd<float>(d, x, y, grad_y, gamma, save_mean, save_invstd, grad_x, grad_residual, grad_gamma,
-                          grad_beta, workspace, (hipStream_t)stream);
+        launch_bwd<float>(d, x, y, grad_y, grad_y2, grad_y3, gamma, save_mean, save_invstd, grad_x, grad_residual,
+                          grad_gamma, grad_beta, workspace, (hipStream_t)stream);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
+int md2_bn_bwd(const md2_bn_desc* d, const void* x, const void* y, const void* grad_y, const float* gamma,
+               const float* save_mean, const float* save_invstd, void* grad_x, void* grad_residual,
+               float* grad_gamma, float* grad_beta, void* workspace, void* stream) {
+    return md2_bn_bwd_multi(d, x, y, grad_y, nullptr, nullptr, gamma, save_mean, save_invstd, grad_x, grad_residual,
+                            grad_gamma, grad_beta, workspace, stream);
 }
 
 }  // extern "C"

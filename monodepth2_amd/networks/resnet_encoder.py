@@ -78,6 +78,31 @@ class Bottleneck(nn.Module):
         return bn_act(self.bn3, self.conv3(out), residual=identity)
 
 
+def _run_layer(layer: nn.Sequential, x, xs, skip_alias: bool):
+    """The blocks of one ResNet stage (torchvision BasicBlock / Bottleneck semantics)
+    with each block output handed out as views for its other consumers — the next
+    block's shortcut and, for the stage output, the decoder skip — so the fused
+    BatchNorm backward sums their gradients on load (bn_act aliases) instead of
+    autograd adding them.  x feeds the block's first conv, xs (the same values) its
+    shortcut.  Returns (output, its shortcut view, its skip view)."""
+    n = len(layer)
+    skip = None
+    for bi, blk in enumerate(layer):
+        shortcut = xs if blk.downsample is None else _downsample(blk.downsample, xs)
+        out = bn_act(blk.bn1, blk.conv1(x))
+        if isinstance(blk, Bottleneck):
+            out = bn_act(blk.bn2, blk.conv2(out))
+            bn, conv = blk.bn3, blk.conv3
+        else:
+            bn, conv = blk.bn2, blk.conv2
+        last = bi == n - 1
+        k = (2 if skip_alias else 1) if last else 1
+        res = bn_act(bn, conv(out), residual=shortcut, aliases=k)
+        x, xs = res[0], res[1]
+        skip = res[2] if (last and skip_alias) else x
+    return x, xs, skip
+
+
 _SPECS = {18: (BasicBlock, [2, 2, 2, 2]), 34: (BasicBlock, [3, 4, 6, 3]), 50: (Bottleneck, [3, 4, 6, 3]),
           101: (Bottleneck, [3, 4, 23, 3]), 152: (Bottleneck, [3, 8, 36, 3])}
 
@@ -171,9 +196,12 @@ class ResnetEncoder(nn.Module):
         e = self.encoder
         f0 = bn_act(e.bn1, stem_conv(e.conv1, x))   # weight gradient on f32 MFMA (stem_ops)
         pooled, f0 = max_pool_3x3s2_with_alias(e.maxpool, f0)   # f0's two gradients meet in the pool backward
-        f1 = e.layer1(pooled)
-        f2 = e.layer2(f1)
-        f3 = e.layer3(f2)
-        f4 = e.layer4(f3)
-        self.features = [f0, f1, f2, f3, f4]
+        feats = [f0]
+        x, xs = pooled, pooled
+        layers = [e.layer1, e.layer2, e.layer3, e.layer4]
+        for li, layer in enumerate(layers):
+            # every layer output but the last also feeds the decoder skip
+            x, xs, skip = _run_layer(layer, x, xs, skip_alias=li < len(layers) - 1)
+            feats.append(skip)
+        self.features = feats
         return self.features
