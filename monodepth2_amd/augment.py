@@ -153,7 +153,11 @@ class GpuAugment:
             inputs[("inv_K", s)] = inv_K
         if "s" in self.frame_ids:
             # mono_dataset.py:192-198: t_x = side_sign * baseline_sign * 0.1
-            sides = sides or ["l"] * self.batch_size
+            # the side comes from each split line (mono_dataset.py:136-140); no default:
+            # a wrong side flips the sign of the stereo baseline
+            if sides is None or len(sides) != self.batch_size or any(sd not in ("l", "r") for sd in sides):
+                raise ValueError("GpuAugment: stereo frame ids need one side ('l'/'r') per item, "
+                                 f"got {sides!r} for batch {self.batch_size}")
             T = np.tile(np.eye(4, dtype=np.float32), (self.batch_size, 1, 1))
             for b, (d, side) in enumerate(zip(draws, sides)):
                 T[b, 0, 3] = (-1 if side == "l" else 1) * (-1 if d.do_flip else 1) * 0.1

@@ -178,6 +178,8 @@ class _MaxPool(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy, galias=None):
         (idx,) = ctx.saved_tensors
+        if gy is None:   # only the alias reached the loss: the pool adds nothing
+            return (galias.to(ctx.dtype) if galias is not None else None), None
         gy = gy.to(ctx.dtype).contiguous(memory_format=_CL)
         if galias is not None:
             galias = galias.to(ctx.dtype).contiguous(memory_format=_CL)

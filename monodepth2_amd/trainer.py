@@ -162,7 +162,11 @@ class Trainer:
         if self.device.type == "cuda" and not self.use_graph:
             self.model_optimizer = FusedAdam(self.parameters_to_train, self.opt.learning_rate)
         else:
-            self.model_optimizer = optim.Adam(self.parameters_to_train, self.opt.learning_rate,
+            # under capture the lr is a device tensor: StepLR updates it in place
+            # (lr_scheduler._update_param_group_val -> fill_), so replays see the decay
+            lr = (torch.tensor(float(self.opt.learning_rate), device=self.device)
+                  if self.use_graph else self.opt.learning_rate)
+            self.model_optimizer = optim.Adam(self.parameters_to_train, lr,
                                               capturable=self.use_graph, fused=self.device.type == "cuda")
         self.model_lr_scheduler = optim.lr_scheduler.StepLR(self.model_optimizer, self.opt.scheduler_step_size, 0.1)
         if self.opt.load_weights_folder is not None:
@@ -454,18 +458,55 @@ class Trainer:
 
     def _capture(self, inputs, warmup: int = 3):
         """Capture one whole training step (networks, fused hot path, backward,
-        all-reduce, Adam) into a hipGraph; later steps replay it."""
+        all-reduce, Adam) into a hipGraph; later steps replay it.
+
+        The warm-up runs (allocator pools, MIOpen solver choice, lazily created Adam
+        state) are real steps, so everything they advance — parameters, Adam moments
+        and step counters, BatchNorm running statistics, the noise seed — is put back
+        before the capture: the first replay is then exactly the first eager step."""
         self.static_inputs = {k: v.to(self.device).clone() for k, v in inputs.items()}
         self.seed_tensor = torch.zeros(1, dtype=torch.int64, device=self.device)
+        snap = self._training_state()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             for _ in range(warmup):
                 self._step_body(self.static_inputs)
         torch.cuda.current_stream(self.device).wait_stream(side)
+        self._restore_training_state(snap)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.static_outputs, self.static_losses = self._step_body(self.static_inputs)
+
+    def _training_state(self):
+        """Copies of every tensor a training step advances (see _capture)."""
+        with torch.no_grad():
+            params = [p.detach().clone() for p in self.parameters_to_train]
+            bufs = [b.detach().clone() for m in self.models.values() for b in m.buffers()]
+            opt = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in st.items()}
+                   for p, st in self.model_optimizer.state.items()}
+        return params, bufs, opt
+
+    def _restore_training_state(self, snap):
+        """In place (the graph captures these storages): parameters and buffers back
+        to the snapshot; Adam state back to the snapshot, or to its initial value
+        (zero moments, step 0) where the warm-up created it."""
+        params, bufs, opt = snap
+        with torch.no_grad():
+            for p, v in zip(self.parameters_to_train, params):
+                p.copy_(v)
+            for b, v in zip((b for m in self.models.values() for b in m.buffers()), bufs):
+                b.copy_(v)
+            for p, st in self.model_optimizer.state.items():
+                old = opt.get(id(p))
+                for k, v in st.items():
+                    if not torch.is_tensor(v):
+                        continue
+                    if old is not None and k in old:
+                        v.copy_(old[k])
+                    else:
+                        v.zero_()
+            self.seed_tensor.zero_()
 
     def _bn_state(self):
         """Restore the folded BatchNorm counters (checkpoint key parity)."""

@@ -28,9 +28,9 @@ def _frames(rng, F, B, h, w):
     return out
 
 
-def _check(aug, frames_np, draws, h, w, S):
+def _check(aug, frames_np, draws, h, w, S, sides=None):
     frames = torch.from_numpy(frames_np).cuda()
-    inputs = aug(frames, draws)
+    inputs = aug(frames, draws, sides)
     torch.cuda.synchronize()
     for fi, fid in enumerate(aug.frame_ids):
         for b, d in enumerate(draws):
@@ -63,9 +63,16 @@ def test_upsampling_and_stereo_keys():
     rng = np.random.default_rng(1)
     draws = [ItemDraw(True, True, 1.2, 1.2, 0.8, 0.1, [0, 1, 2, 3]), ItemDraw(False, False)]
     aug = GpuAugment(128, 416, 100, 300, [0, "s"], 2)
-    inputs = _check(aug, _frames(rng, 2, 2, 100, 300), draws, 128, 416, 4)
+    frames = _frames(rng, 2, 2, 100, 300)
+    inputs = _check(aug, frames, draws, 128, 416, 4, sides=["l", "l"])
     T = inputs["stereo_T"].cpu()
     assert float(T[0, 0, 3]) == pytest.approx(0.1) and float(T[1, 0, 3]) == pytest.approx(-0.1)
+    # mono_dataset.py:195-196: side_sign * baseline_sign * 0.1, side from the split line
+    T = aug(torch.from_numpy(frames).cuda(), draws, ["r", "l"])["stereo_T"].cpu()
+    assert float(T[0, 0, 3]) == pytest.approx(-0.1) and float(T[1, 0, 3]) == pytest.approx(-0.1)
+    for bad in (None, ["l"], ["l", "x"]):
+        with pytest.raises(ValueError, match="side"):
+            aug(torch.from_numpy(frames).cuda(), draws, bad)
 
 
 @pytest.mark.parametrize("op", ["hue", "brightness", "contrast", "saturation"])

@@ -210,3 +210,49 @@ def test_maxpool_with_alias_sums_both_gradients():
     g2, = torch.autograd.grad(y2, x, gy)
     g2r, = torch.autograd.grad(pool(x), x, gy)
     torch.testing.assert_close(g2, g2r, rtol=1e-6, atol=1e-6)
+
+
+def test_maxpool_alias_only_gradient():
+    """Only the alias output reaches the loss (the pool output's gradient is None
+    under set_materialize_grads(False)): the input gradient is the alias's."""
+    torch.manual_seed(10)
+    pool = torch.nn.MaxPool2d(3, 2, 1)
+    x = torch.randn(2, 64, 12, 20, device="cuda").contiguous(memory_format=CL).requires_grad_(True)
+    _, xa = bn_ops.max_pool_3x3s2_with_alias(pool, x)
+    ga = torch.randn_like(x)
+    gx, = torch.autograd.grad(xa, x, ga)
+    torch.testing.assert_close(gx, ga, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("groups", [1, 2])
+@pytest.mark.parametrize("used", [(0, 1, 2), (0, 2), (1, 2)])
+def test_bn_bwd_multi_sums_alias_gradients(bf16, groups, used):
+    """bn_act(..., aliases=2): y and its two alias views get three different
+    gradients; the fused backward (md2_bn_bwd_multi) sums them on load.  Reference:
+    nn.BatchNorm2d (+ residual + ReLU) fed the sum of the gradients that reach it.
+    `used` = which of (y, alias1, alias2) reach the loss (the others bring None)."""
+    torch.manual_seed(11 + groups)
+    C, B, H, W = 64, 4, 12, 20
+    dt = torch.bfloat16 if bf16 else torch.float32
+    bn = nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+    ref_bn = copy.deepcopy(bn)
+    xb = (torch.randn(B, C, H, W, device="cuda") * 2 + 0.3).to(dt).contiguous(memory_format=CL)
+    rb = torch.randn(B, C, H, W, device="cuda").to(dt).contiguous(memory_format=CL)
+    x, r = xb.clone().requires_grad_(True), rb.clone().requires_grad_(True)
+    xr, rr = xb.float().requires_grad_(True), rb.float().requires_grad_(True)
+    with bn_ops.bn_groups(groups):
+        outs = bn_ops.bn_act(bn, x, r, True, aliases=2)
+    assert len(outs) == 3 and "BNAct" in type(outs[1].grad_fn).__name__
+    yr = torch.cat([_eager(ref_bn, xc, rc, True) for xc, rc in zip(xr.chunk(groups), rr.chunk(groups))], 0)
+    gs = [torch.randn_like(yr) * (k + 1) for k in range(3)]
+    gs = [g.to(dt).float() for g in gs]
+    got = torch.autograd.grad([outs[k] for k in used], [x, r, bn.weight, bn.bias],
+                              [gs[k].to(dt).contiguous(memory_format=CL) for k in used])
+    ref = torch.autograd.grad(yr, [xr, rr, ref_bn.weight, ref_bn.bias], sum(gs[k] for k in used))
+    tol = 1e-2 if bf16 else 1e-4
+    for a, b, name in zip(got, ref, ["x", "residual", "weight", "bias"]):
+        assert float((a.float() - b).norm() / b.norm()) < tol, name

@@ -191,6 +191,79 @@ def test_hip_graph_replay_matches_eager_step():
     assert worst < 1e-6, worst
 
 
+def _graph_state(tr):
+    return ([p.detach().clone() for p in tr.nets.parameters()],
+            [b.detach().clone() for b in tr.nets.buffers()])
+
+
+def test_hip_graph_first_step_is_one_step():
+    """The capture's warm-up steps leave no trace: after the first hip_graph
+    train_step (warm-up + capture + one replay) the parameters, BatchNorm buffers and
+    Adam state are those of ONE eager step from the same initial state (Adam step 1,
+    not 4)."""
+    tr, batch = make("mono", hip_graph=True)
+    params0, bufs0 = _graph_state(tr)
+    _, lg = tr.train_step(batch)
+    torch.cuda.synchronize()
+    loss_graph = float(lg["loss"])
+    params_g, bufs_g = _graph_state(tr)
+    steps = {float(st["step"]) for st in tr.model_optimizer.state.values()}
+    assert steps == {1.0}, steps
+    # the same first step eagerly, from the same initial state and zero Adam state
+    with torch.no_grad():
+        for p, v in zip(tr.nets.parameters(), params0):
+            p.copy_(v)
+        for b, v in zip(tr.nets.buffers(), bufs0):
+            b.copy_(v)
+        for st in tr.model_optimizer.state.values():
+            for v in st.values():
+                if torch.is_tensor(v):
+                    v.zero_()
+        tr.seed_tensor.zero_()
+    _, le = tr._step_body(tr.static_inputs)
+    torch.cuda.synchronize()
+    assert abs(loss_graph - float(le["loss"])) < 1e-6, (loss_graph, float(le["loss"]))
+    for a, b in zip(params_g, tr.nets.parameters()):
+        assert float((a - b).abs().max()) < 1e-6
+    for a, b in zip(bufs_g, tr.nets.buffers()):
+        assert float((a - b).abs().max()) < 1e-6
+
+
+def test_hip_graph_replay_sees_lr_schedule():
+    """StepLR's decay (trainer.py:505, x0.1 every scheduler_step_size epochs) reaches
+    the replayed Adam: the lr lives in a device tensor the scheduler fills in place.
+    A replay after the decay equals the same step run eagerly at the decayed lr."""
+    tr, batch = make("mono", hip_graph=True)
+    tr.train_step(batch)
+    tr.train_step(batch)
+    lr0 = float(tr.model_optimizer.param_groups[0]["lr"])
+    for _ in range(tr.opt.scheduler_step_size):
+        tr.model_lr_scheduler.step()
+    assert abs(float(tr.model_optimizer.param_groups[0]["lr"]) - 0.1 * lr0) < 1e-12
+    torch.cuda.synchronize()
+    opt_state = [{k: v.detach().clone() for k, v in st.items()} for st in tr.model_optimizer.state.values()]
+    params0, bufs0 = _graph_state(tr)
+    seed0 = tr.seed_tensor.clone()
+    tr.train_step(batch)                        # replay at the decayed lr
+    torch.cuda.synchronize()
+    params_g, _ = _graph_state(tr)
+    with torch.no_grad():
+        for p, v in zip(tr.nets.parameters(), params0):
+            p.copy_(v)
+        for b, v in zip(tr.nets.buffers(), bufs0):
+            b.copy_(v)
+        for st, saved in zip(tr.model_optimizer.state.values(), opt_state):
+            for k, v in saved.items():
+                st[k].copy_(v)
+        tr.seed_tensor.copy_(seed0)
+    tr._step_body(tr.static_inputs)
+    torch.cuda.synchronize()
+    delta = max(float((a - b).abs().max()) for a, b in zip(params_g, params0))
+    worst = max(float((a - b).abs().max()) for a, b in zip(params_g, tr.nets.parameters()))
+    assert delta > 0
+    assert worst < 1e-3 * delta + 1e-9, (worst, delta)
+
+
 def test_encoder_input_matches_eager():
     """ResnetEncoder.prepare (md2_encoder_input) == (cat(frames) - 0.45) / 0.225 in
     channels_last, bit for bit, for one frame and for batched frame pairs."""
