@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 9
+#define MD2_ABI_VERSION 10
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -421,6 +421,41 @@ int md2_maxpool3s2_bwd(const md2_pool_desc* desc, const uint32_t* idx, const voi
  * add pass. */
 int md2_maxpool3s2_bwd_add(const md2_pool_desc* desc, const uint32_t* idx, const void* grad_y, const void* grad_add,
                            void* grad_x, void* stream);
+
+/*
+ * fp32 convolutions as implicit GEMMs on f32 MFMA (csrc/conv.hip): the ResNet
+ * encoders' 3x3 / 1x1 convolutions (networks/resnet_encoder.py, torchvision
+ * BasicBlock/Bottleneck) and the DepthDecoder's 3x3 convolutions on reflection-padded
+ * inputs (networks/depth_decoder.py:50-65 via layers.py:106-136 Conv3x3; the padding
+ * is md2_decoder_pad_fwd's, so pad = 0), forward and backward, replacing MIOpen.
+ * x (batch, height, width, in_channels) NHWC fp32; weight (out_channels, kernel_h,
+ * kernel_w, in_channels) = a channels_last Conv2d weight; y (batch, Ho, Wo,
+ * out_channels) NHWC with Ho = (height + 2 pad - kernel_h) / stride + 1.  No bias.
+ * Channel counts multiples of 4, pad < kernel, every tensor < 2^29 elements.  Zero
+ * padding outside the image.  Deterministic (a K split sums its partials in order);
+ * workspace of md2_conv_workspace_bytes (0 = none needed).
+ */
+#define MD2_CONV_NO_SPLIT  (1u << 1) /* no K split (tests)              */
+#define MD2_CONV_TILE_N32  (1u << 2) /* force the 128 x 32 tile (tests) */
+#define MD2_CONV_TILE_N64  (1u << 3) /* force the 128 x 64 tile         */
+#define MD2_CONV_TILE_N128 (1u << 4) /* force the 128 x 128 tile        */
+
+typedef struct md2_conv_desc {
+    int32_t batch, height, width, in_channels; /* input */
+    int32_t out_channels, kernel_h, kernel_w, stride, pad;
+    uint32_t flags;                            /* MD2_CONV_* */
+} md2_conv_desc;
+
+size_t md2_conv_workspace_bytes(const md2_conv_desc* desc);
+int md2_conv_fwd(const md2_conv_desc* desc, const float* x, const float* weight, float* y, void* workspace,
+                 void* stream);
+/* grad_x (batch, height, width, in_channels) from grad_y (batch, Ho, Wo, out_channels);
+ * stride 1 only (a "full" convolution with the flipped, transposed weight) */
+int md2_conv_dgrad(const md2_conv_desc* desc, const float* grad_y, const float* weight, float* grad_x,
+                   void* workspace, void* stream);
+/* grad_weight (out_channels, kernel_h, kernel_w, in_channels) = channels_last layout */
+int md2_conv_wgrad(const md2_conv_desc* desc, const float* x, const float* grad_y, float* grad_weight,
+                   void* workspace, void* stream);
 
 #ifdef __cplusplus
 }

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -61,7 +61,9 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_bn_workspace_bytes", "md2_bn_fwd", "md2_bn_bwd", "md2_maxpool3s2_fwd", "md2_maxpool3s2_bwd",
            "md2_disp_head_workspace_bytes", "md2_disp_head_fwd", "md2_disp_head_bwd",
            "md2_stem_wgrad_workspace_bytes", "md2_stem_wgrad", "md2_bias_act_fwd", "md2_bias_act_bwd",
-           "md2_bias_act_workspace_bytes", "md2_maxpool3s2_bwd_add", "md2_bn_bwd_multi"]
+           "md2_bias_act_workspace_bytes", "md2_maxpool3s2_bwd_add", "md2_bn_bwd_multi",
+           "md2_conv_fwd", "md2_conv_workspace_bytes",
+           "md2_conv_dgrad", "md2_conv_wgrad"]
 
 PAD_ELU = 1 << 0
 PAD_UPSAMPLE = 1 << 1
@@ -100,6 +102,19 @@ class BnDesc(ctypes.Structure):
 POOL_BF16 = 1 << 0
 
 
+CONV_NO_SPLIT = 1 << 1
+CONV_TILE_N32 = 1 << 2
+CONV_TILE_N64 = 1 << 3
+CONV_TILE_N128 = 1 << 4
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("height", ctypes.c_int32), ("width", ctypes.c_int32),
+                ("in_channels", ctypes.c_int32), ("out_channels", ctypes.c_int32), ("kernel_h", ctypes.c_int32),
+                ("kernel_w", ctypes.c_int32), ("stride", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("flags", ctypes.c_uint32)]
+
+
 class PoolDesc(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int32), ("channels", ctypes.c_int32), ("height", ctypes.c_int32),
                 ("width", ctypes.c_int32), ("flags", ctypes.c_uint32), ("reserved", ctypes.c_int32)]
@@ -135,6 +150,14 @@ def _declare(L):
     L.md2_bias_act_bwd.argtypes = [ctypes.POINTER(BiasActDesc)] + [_vp] * 6
     L.md2_bias_act_workspace_bytes.restype = ctypes.c_size_t
     L.md2_bias_act_workspace_bytes.argtypes = [ctypes.POINTER(BiasActDesc)]
+    L.md2_conv_fwd.restype = ctypes.c_int
+    L.md2_conv_fwd.argtypes = [ctypes.POINTER(ConvDesc)] + [_vp] * 5
+    L.md2_conv_dgrad.restype = ctypes.c_int
+    L.md2_conv_dgrad.argtypes = [ctypes.POINTER(ConvDesc)] + [_vp] * 5
+    L.md2_conv_wgrad.restype = ctypes.c_int
+    L.md2_conv_wgrad.argtypes = [ctypes.POINTER(ConvDesc)] + [_vp] * 5
+    L.md2_conv_workspace_bytes.restype = ctypes.c_size_t
+    L.md2_conv_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc)]
     L.md2_stem_wgrad_workspace_bytes.restype = ctypes.c_size_t
     L.md2_stem_wgrad_workspace_bytes.argtypes = [ctypes.POINTER(StemDesc)]
     L.md2_stem_wgrad.restype = ctypes.c_int

@@ -1,0 +1,178 @@
+"""Convolutions of the ResNet encoders and the DepthDecoder on f32 MFMA
+(csrc/conv.hip, ABI `md2_conv_*`).
+
+`conv2d(conv, x)` computes `conv(x)` for an `nn.Conv2d` module (its own weight, so
+the torchvision / reference state-dict keys are unchanged).  Three implicit GEMMs on
+`v_mfma_f32_32x32x2_f32` (exact f32 fma chains), NHWC activations, the weight in
+PyTorch's channels_last layout:
+
+* forward (md2_conv_fwd);
+* input gradient, stride 1 (md2_conv_dgrad: a "full" convolution of the output
+  gradient with the weight read flipped and transposed);
+* weight gradient (md2_conv_wgrad; deterministic K split, no zero-fill launch).
+
+Each of the three is chosen per shape against MIOpen (aten.convolution /
+aten.convolution_backward) by timing both once, on the first call of that shape
+(`AUTOTUNE`), and the faster one is kept — MIOpen keeps the shapes where its tuned
+kernels win.  Shapes outside the kernels' contract (channel counts
+not multiples of 4, bias, groups, non-fp32, NCHW, autocast) run the module itself.
+Callers: networks/resnet_encoder.py (3x3 / 1x1 convs of every block),
+networks/decoders.py (DepthDecoder convs on the reflection-padded inputs).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+_CL = torch.channels_last
+ENABLED = True     # tests flip this to compare with MIOpen on the same module
+AUTOTUNE = True    # False: always the MFMA kernels (tests)
+_ws: Dict[Tuple[int, int], torch.Tensor] = {}
+_choice: Dict[tuple, bool] = {}    # (op, shape) -> use the MFMA kernel
+
+
+def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+    """K-split partials, one buffer per HIP stream (the pose network runs on its own)."""
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    ws = _ws.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _ws[key] = ws
+    return ws
+
+
+def _desc(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int):
+    B, C, H, W = x.shape
+    N, _, KH, KW = w.shape
+    return _lib.ConvDesc(B, H, W, C, N, KH, KW, stride, pad, 0)
+
+
+def _call(fn: str, d, p0, p1, p2, device):
+    L = _lib.lib()
+    ws = _workspace(device, L.md2_conv_workspace_bytes(ctypes.byref(d)))
+    _lib.check(getattr(L, fn)(ctypes.byref(d), p0, p1, p2, ws.data_ptr(), torch.cuda.current_stream(device).cuda_stream),
+               fn)
+
+
+def _fwd(x, w, stride, pad):
+    B, _, H, W = x.shape
+    N, _, KH, KW = w.shape
+    y = torch.empty(B, N, (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1, device=x.device,
+                    memory_format=_CL)
+    _call("md2_conv_fwd", _desc(x, w, stride, pad), x.data_ptr(), w.data_ptr(), y.data_ptr(), x.device)
+    return y
+
+
+def _dgrad(gy, x, w, pad):
+    gx = torch.empty_like(x, memory_format=_CL)
+    _call("md2_conv_dgrad", _desc(x, w, 1, pad), gy.data_ptr(), w.data_ptr(), gx.data_ptr(), x.device)
+    return gx
+
+
+def _wgrad(gy, x, w, stride, pad):
+    gw = torch.empty_like(w, memory_format=_CL)
+    _call("md2_conv_wgrad", _desc(x, w, stride, pad), x.data_ptr(), gy.data_ptr(), gw.data_ptr(), x.device)
+    return gw
+
+
+def _miopen_bwd(gy, x, w, stride, pad, mask):
+    return torch.ops.aten.convolution_backward(gy, x, w, None, (stride, stride), (pad, pad), (1, 1), False, (0, 0), 1,
+                                               mask)
+
+
+def _faster(op: str, key: tuple, ours, theirs) -> bool:
+    """Time both once per (op, shape) (3 runs each after a warm-up, median) and
+    remember whether ours wins by >= 3 %.  Not while a hipGraph is being captured:
+    then the cached choice, or MIOpen."""
+    k = (op,) + key
+    if not AUTOTUNE:
+        return True
+    if k in _choice:
+        return _choice[k]
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    times = []
+    for fn in (ours, theirs):
+        fn()
+        ts = []
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        times.append(sorted(ts)[1])
+    _choice[k] = times[0] < 0.97 * times[1]
+    return _choice[k]
+
+
+def _fits(cin: int, cout: int) -> bool:
+    return cin % 4 == 0 and cout % 4 == 0
+
+
+class _Conv(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, pad: int):
+        ctx.save_for_backward(x, weight)
+        ctx.stride, ctx.pad = stride, pad
+        ctx.key = (tuple(x.shape), tuple(weight.shape), stride, pad)
+        if _faster("fwd", ctx.key, lambda: _fwd(x, weight, stride, pad),
+                   lambda: F.conv2d(x, weight, None, stride, pad)):
+            return _fwd(x, weight, stride, pad)
+        return F.conv2d(x, weight, None, stride, pad)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        s, p = ctx.stride, ctx.pad
+        gy = gy.contiguous(memory_format=_CL)
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        ours_x = need_x and s == 1 and _faster("dgrad", ctx.key, lambda: _dgrad(gy, x, w, p),
+                                               lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False)))
+        ours_w = need_w and _faster("wgrad", ctx.key, lambda: _wgrad(gy, x, w, s, p),
+                                    lambda: _miopen_bwd(gy, x, w, s, p, (False, True, False)))
+        gx = _dgrad(gy, x, w, p) if ours_x else None
+        gw = _wgrad(gy, x, w, s, p) if ours_w else None
+        mask = (need_x and not ours_x, need_w and not ours_w, False)
+        if mask[0] or mask[1]:
+            gxm, gwm, _ = _miopen_bwd(gy, x, w, s, p, mask)
+            gx = gxm if mask[0] else gx
+            gw = gwm if mask[1] else gw
+        return gx, gw, None, None
+
+
+def _shape_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    return (ENABLED and x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.float32 and x.dim() == 4
+            and weight.shape[2] == weight.shape[3] and _fits(weight.shape[1], weight.shape[0])
+            and x.is_contiguous(memory_format=_CL) and weight.is_contiguous(memory_format=_CL)
+            and not torch.is_autocast_enabled() and x.numel() < 2 ** 29)
+
+
+def supports(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    k, s, p = conv.kernel_size, conv.stride, conv.padding
+    return (conv.bias is None and conv.groups == 1 and tuple(conv.dilation) == (1, 1)
+            and conv.padding_mode == "zeros" and k[0] == k[1] and s[0] == s[1] and p[0] == p[1] and p[0] < k[0]
+            and _shape_ok(x, conv.weight))
+
+
+def conv2d(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """conv(x), on the MFMA kernels when supports(conv, x) (and faster, see _faster)."""
+    if supports(conv, x):
+        return _Conv.apply(x, conv.weight, conv.stride[0], conv.padding[0])
+    return conv(x)
+
+
+def conv2d_w(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad: int = 0) -> torch.Tensor:
+    """F.conv2d(x, weight, None, stride, pad) for a bare weight (decoder convs whose
+    bias is folded elsewhere), on the MFMA kernels when the shape fits."""
+    if _shape_ok(x, weight) and pad < weight.shape[2]:
+        return _Conv.apply(x, weight, stride, pad)
+    return F.conv2d(x, weight, None, stride, pad)

@@ -1,0 +1,523 @@
+// conv.hip — fp32 convolutions of the ResNet encoders and the DepthDecoder as implicit
+// GEMMs on gfx950 f32 MFMA (v_mfma_f32_32x32x2_f32: exact f32 fma chains, the same
+// 157 TFLOP/s as the f32 vector peak), NHWC activations, weights in PyTorch's
+// channels_last layout [co][kh][kw][ci].
+//
+// Callers: networks/resnet_encoder.py (torchvision BasicBlock / Bottleneck 3x3 and 1x1
+// convs) and networks/depth_decoder.py:50-65 (Conv3x3 = ReflectionPad2d(1) +
+// Conv2d(.., 3); the padding is done by csrc/decoder.hip, so the conv is "valid").
+//
+//   forward      y[p][n]   = Σ_{tap,c} x[p's tap][c] · w[n][tap][c]     M = pixels, N = Co, K = taps·Ci
+//   input grad   gx[p][ci] = Σ_{tap,co} gy[p's flipped tap][co] · w[co][tap][ci]   (stride 1: a
+//                "full" convolution of gy, padding k-1-p, the weight read transposed)
+//   weight grad  gw[co][tap][ci] = Σ_p x[p's tap][ci] · gy[p][co]       M = taps·Ci, N = Co, K = pixels
+//                (written transposed: [co][tap][ci] = the channels_last weight)
+//
+// One kernel template: block = 4 waves, tile 128 x BN (BN = 32/64/128), K in chunks of
+// 32.  The next-but-one chunk is loaded into registers (row-coalesced dwordx4 buffer
+// loads; an offset past the buffer end reads zeros = the zero padding outside the
+// image, so no branch surrounds a load) while the MFMAs consume the current chunk from
+// LDS; one barrier per chunk.  Each operand is staged in the orientation it has in
+// HBM: "row-k" tiles (a row of 32 contiguous k values: im2col rows, forward weights)
+// with XOR-swizzled 16-byte quads, read 4 k-values per ds_read_b128; "k-row" tiles (a
+// row per k value: gy and x in the weight gradient, the weight in the input gradient)
+// read with one ds_read_b32 per MFMA.  Lane l feeds k = 16·(l/32) + j of the chunk to
+// MFMA j, A and B alike.  Deterministic: a K split writes partials that a second
+// launch sums in split order.
+
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "md2hot.h"
+
+int md2_report_error(int code, const char* msg);
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kThreads = 256;
+constexpr int BM = 128;         // tile rows (M)
+constexpr int BK = 32;          // K per chunk
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+// physical quad of logical quad q in a row-k LDS row r (32 floats): conflict-free
+// ds_read_b128 of the MFMA operand pattern (16 lanes = 16 rows at one logical quad)
+// and of the staging writes (8 lanes = one row)
+__device__ __forceinline__ int swz(int r, int q) { return (q ^ (r >> 1)) & 7; }
+
+struct ConvArgs {
+    int B, H, W, C;          // input of the GEMM's pixel side (NHWC): x (fwd), gy (dgrad), x (wgrad)
+    int Ho, Wo;              // output spatial (fwd / dgrad: the y / gx pixels; wgrad: gy pixels)
+    int N;                   // fwd: Co; dgrad: Ci; wgrad: taps·Ci
+    int M;                   // fwd / dgrad: pixels; wgrad: Co
+    int P;                   // wgrad: pixels (K)
+    int Cg;                  // wgrad: channels of gy (= N)
+    int KH, KW, stride, pad;
+    int mblocks, nblocks, splits, chunks_per_split, nchunks;
+    int a_elems, b_elems;    // sizes of the two operands (the buffer-descriptor bounds)
+    int bn;                  // tile width chosen by plan()
+    const float* a;          // fwd: x; dgrad: gy; wgrad: x
+    const float* b;          // fwd / dgrad: weight; wgrad: gy
+    float* y;                // output [M][N], or partials [splits][M][N]
+};
+
+__device__ __forceinline__ int xcd_contiguous_block(int bid, int n) {
+    const int q = n >> 3, r = n & 7;
+    const int xcd = bid & 7, idx = bid >> 3;
+    return xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
+}
+
+__device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
+constexpr int kBad = 0x7fffffff;   // a byte offset past every buffer: the load returns zeros
+
+template <int BN, int MODE>
+struct Cfg {
+    static constexpr int WAVES_M = BN == 32 ? 4 : 2;
+    static constexpr int WAVES_N = 4 / WAVES_M;
+    static constexpr int TM = BM / WAVES_M / 32;   // 32x32 MFMA tiles per wave
+    static constexpr int TN = BN / WAVES_N / 32;
+    static constexpr bool A_ROWK = MODE != MODE_WGRAD;   // else k-row
+    static constexpr bool B_ROWK = MODE == MODE_FWD;
+    static constexpr int AQ = BM * BK / 4 / kThreads;    // 16-byte quads per thread per chunk
+    static constexpr int BQ = BN * BK / 4 / kThreads;
+    static constexpr int A_FLOATS = BM * BK, B_FLOATS = BN * BK;
+};
+
+template <int BN, int MODE>
+__global__ __launch_bounds__(kThreads, BN == 128 ? 2 : (BN == 64 ? 3 : 4)) void conv_gemm_kernel(ConvArgs a) {
+    using G = Cfg<BN, MODE>;
+    constexpr int TM = G::TM, TN = G::TN, AQ = G::AQ, BQ = G::BQ;
+    __shared__ float lds[2][G::A_FLOATS + G::B_FLOATS];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / G::WAVES_N, wn = wid % G::WAVES_N;
+    int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int nb = blk % a.nblocks;
+    blk /= a.nblocks;
+    const int mb = blk % a.mblocks, ks = blk / a.mblocks;
+    const int m0 = mb * BM, n0 = nb * BN;
+    const int t0 = ks * a.chunks_per_split;
+    const int nchunks = min(a.chunks_per_split, a.nchunks - t0);
+    const int KT = a.KH * a.KW;
+
+    // ---------------------------------------------------------------- A side
+    // row-k (fwd / dgrad): thread rows r = tid/8 + 32 j of the 128-pixel tile, quad tid%8
+    // k-row (wgrad): quad i = tid + 256 j of the [32 pixels][128 (tap, ci)] tile
+    const int qa = tid & 7, ra = tid >> 3;
+    int aih[AQ], aiw[AQ], apb[AQ];
+    const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.a, 0, a.a_elems * 4, 0x00020000);
+    if (MODE != MODE_WGRAD) {
+#pragma unroll
+        for (int j = 0; j < AQ; ++j) {
+            const int m = m0 + ra + 32 * j;
+            if (m < a.M) {
+                const int b = m / (a.Ho * a.Wo), rem = m - b * a.Ho * a.Wo;
+                const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+                aih[j] = oh * a.stride - a.pad;
+                aiw[j] = ow * a.stride - a.pad;
+                apb[j] = ((b * a.H + aih[j]) * a.W + aiw[j]) * a.C + 4 * qa;
+            } else {
+                aih[j] = -(1 << 20);
+                aiw[j] = 0;
+                apb[j] = 0;
+            }
+        }
+    }
+    // wgrad A side (x): per quad its (tap, ci); every quad of this thread sits in k row
+    // tid/32 + 8 j of the chunk, whose pixel (b, oh, ow) is tracked incrementally
+    int wkh[AQ], wkw[AQ], wci[AQ];
+    int pb_b = 0, pb_oh = 0, pb_ow = 0;
+    if (MODE == MODE_WGRAD) {
+#pragma unroll
+        for (int j = 0; j < AQ; ++j) {
+            const int m = m0 + 4 * (tid % (BM / 4));
+            const int tap = m / a.C, ci = m - tap * a.C;
+            wkh[j] = m < a.M ? tap / a.KW : -(1 << 20);
+            wkw[j] = tap - (tap / a.KW) * a.KW;
+            wci[j] = ci;
+        }
+        const int pk = t0 * BK + tid / (BM / 4);
+        pb_b = pk / (a.Ho * a.Wo);
+        const int rem = pk - pb_b * a.Ho * a.Wo;
+        pb_oh = rem / a.Wo;
+        pb_ow = rem - pb_oh * a.Wo;
+    }
+    // ---------------------------------------------------------------- B side
+    const int qb = tid & 7, rb = tid >> 3;
+    int bofs[BQ];
+    const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * 4, 0x00020000);
+    if (MODE == MODE_FWD) {
+#pragma unroll
+        for (int j = 0; j < BQ; ++j) {
+            const int n = n0 + rb + 32 * j;
+            bofs[j] = n < a.N ? (n * KT * a.C + 4 * qb) : -1;
+        }
+    } else {
+        // k-row tiles [32][BN]: quad i = tid + 256 j covers columns n0 + 4 (i % (BN/4))
+#pragma unroll
+        for (int j = 0; j < BQ; ++j) {
+            const int i = tid + kThreads * j, nq = i % (BN / 4);
+            const int n = n0 + 4 * nq;
+            bofs[j] = n < a.N ? n : -1;
+        }
+    }
+    const int cchunks = (a.C + BK - 1) / BK;   // fwd / dgrad: chunks per tap
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    float4 ra0[AQ], rb0[BQ], ra1[AQ], rb1[BQ];
+
+    // load chunk (t0 + t) into registers RA, RB
+#define CONV_LOAD(t, RA, RB)                                                                                 \
+    {                                                                                                        \
+        const int tt_ = t0 + (t);                                                                            \
+        if (MODE != MODE_WGRAD) {                                                                            \
+            const int tap_ = tt_ / cchunks, c0_ = (tt_ - tap_ * cchunks) * BK;                               \
+            const int kh_ = tap_ / a.KW, kw_ = tap_ - kh_ * a.KW;                                            \
+            const int off_ = (kh_ * a.W + kw_) * a.C + c0_;                                                  \
+            const bool cok_ = c0_ + 4 * qa < a.C;                                                            \
+            _Pragma("unroll") for (int j = 0; j < AQ; ++j) {                                                 \
+                const bool ok = cok_ && (unsigned)(aih[j] + kh_) < (unsigned)a.H &&                          \
+                                (unsigned)(aiw[j] + kw_) < (unsigned)a.W;                                    \
+                RA[j] = bload(ar, ok ? (apb[j] + off_) * 4 : kBad);                                          \
+            }                                                                                                \
+            if (MODE == MODE_FWD) {                                                                          \
+                const int woff_ = tap_ * a.C + c0_;                                                          \
+                const bool bok_ = c0_ + 4 * qb < a.C;                                                        \
+                _Pragma("unroll") for (int j = 0; j < BQ; ++j)                                               \
+                    RB[j] = bload(br, (bofs[j] >= 0 && bok_) ? (bofs[j] + woff_) * 4 : kBad);                \
+            } else {                                                                                         \
+                /* w[co = c0 + k][flipped tap][ci = n]: k row of BN contiguous ci */                         \
+                const int ftap_ = KT - 1 - tap_;                                                             \
+                _Pragma("unroll") for (int j = 0; j < BQ; ++j) {                                             \
+                    const int k_ = (tid + kThreads * j) / (BN / 4);                                          \
+                    const bool ok = bofs[j] >= 0 && c0_ + k_ < a.C;                                          \
+                    RB[j] = bload(br, ok ? (((c0_ + k_) * KT + ftap_) * a.N + bofs[j]) * 4 : kBad);          \
+                }                                                                                            \
+            }                                                                                                \
+        } else {                                                                                             \
+            /* A: x at pixel (k row) shifted by the quad's tap; B: gy[pixel][co] */                          \
+            _Pragma("unroll") for (int j = 0; j < AQ; ++j) {                                                 \
+                int b_ = pb_b, oh_ = pb_oh, ow_ = pb_ow + j * (kThreads / (BM / 4));                         \
+                while (ow_ >= a.Wo) { ow_ -= a.Wo; if (++oh_ == a.Ho) { oh_ = 0; ++b_; } }                    \
+                const int ih_ = oh_ * a.stride - a.pad + wkh[j], iw_ = ow_ * a.stride - a.pad + wkw[j];      \
+                const bool ok = b_ < a.B && (unsigned)ih_ < (unsigned)a.H && (unsigned)iw_ < (unsigned)a.W;  \
+                RA[j] = bload(ar, ok ? (((b_ * a.H + ih_) * a.W + iw_) * a.C + wci[j]) * 4 : kBad);          \
+            }                                                                                                \
+            pb_ow += BK;                                                                                     \
+            while (pb_ow >= a.Wo) { pb_ow -= a.Wo; if (++pb_oh == a.Ho) { pb_oh = 0; ++pb_b; } }             \
+            const int p0_ = tt_ * BK;                                                                        \
+            _Pragma("unroll") for (int j = 0; j < BQ; ++j) {                                                 \
+                const int p_ = p0_ + (tid + kThreads * j) / (BN / 4);                                        \
+                RB[j] = bload(br, (p_ < a.P && bofs[j] >= 0) ? (p_ * a.Cg + bofs[j]) * 4 : kBad);            \
+            }                                                                                                \
+        }                                                                                                    \
+    }
+
+    // registers -> LDS buffer `buf`
+#define CONV_STORE(buf, RA, RB)                                                                              \
+    {                                                                                                        \
+        float* As_ = lds[buf];                                                                               \
+        float* Bs_ = lds[buf] + G::A_FLOATS;                                                                 \
+        _Pragma("unroll") for (int j = 0; j < AQ; ++j) {                                                     \
+            if (G::A_ROWK) {                                                                                 \
+                const int r_ = ra + 32 * j;                                                                  \
+                *(float4*)(As_ + r_ * BK + 4 * swz(r_, qa)) = RA[j];                                         \
+            } else {                                                                                         \
+                *(float4*)(As_ + 4 * (tid + kThreads * j)) = RA[j];                                          \
+            }                                                                                                \
+        }                                                                                                    \
+        _Pragma("unroll") for (int j = 0; j < BQ; ++j) {                                                     \
+            if (G::B_ROWK) {                                                                                 \
+                const int r_ = rb + 32 * j;                                                                  \
+                *(float4*)(Bs_ + r_ * BK + 4 * swz(r_, qb)) = RB[j];                                         \
+            } else {                                                                                         \
+                *(float4*)(Bs_ + 4 * (tid + kThreads * j)) = RB[j];                                          \
+            }                                                                                                \
+        }                                                                                                    \
+    }
+
+    const int arow = wm * (TM * 32) + (lane & 31), brow = wn * (TN * 32) + (lane & 31);
+    const int h = lane >> 5;
+    // multiply the chunk in LDS buffer `buf`: MFMA j (j = 4 kq + e) takes k = 16 h + j
+#define CONV_MMA(buf)                                                                                        \
+    {                                                                                                        \
+        const float* As_ = lds[buf];                                                                         \
+        const float* Bs_ = lds[buf] + G::A_FLOATS;                                                           \
+        _Pragma("unroll") for (int kq = 0; kq < 4; ++kq) {                                                   \
+            float fa[TM][4], fb[TN][4];                                                                      \
+            _Pragma("unroll") for (int i = 0; i < TM; ++i) {                                                 \
+                if (G::A_ROWK) {                                                                             \
+                    const float4 v = *(const float4*)(As_ + (arow + 32 * i) * BK + 4 * swz(arow + 32 * i, 4 * h + kq)); \
+                    fa[i][0] = v.x; fa[i][1] = v.y; fa[i][2] = v.z; fa[i][3] = v.w;                          \
+                } else {                                                                                     \
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e)                                            \
+                        fa[i][e] = As_[(16 * h + 4 * kq + e) * BM + arow + 32 * i];                          \
+                }                                                                                            \
+            }                                                                                                \
+            _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                                 \
+                if (G::B_ROWK) {                                                                             \
+                    const float4 v = *(const float4*)(Bs_ + (brow + 32 * j) * BK + 4 * swz(brow + 32 * j, 4 * h + kq)); \
+                    fb[j][0] = v.x; fb[j][1] = v.y; fb[j][2] = v.z; fb[j][3] = v.w;                          \
+                } else {                                                                                     \
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e)                                            \
+                        fb[j][e] = Bs_[(16 * h + 4 * kq + e) * BN + brow + 32 * j];                          \
+                }                                                                                            \
+            }                                                                                                \
+            _Pragma("unroll") for (int e = 0; e < 4; ++e)                                                    \
+                _Pragma("unroll") for (int i = 0; i < TM; ++i)                                               \
+                    _Pragma("unroll") for (int j = 0; j < TN; ++j)                                           \
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][e], fb[j][e], acc[i][j], 0, 0, 0); \
+        }                                                                                                    \
+        asm volatile("" ::: "memory"); /* keep the next LDS writes behind these reads */                   \
+    }
+
+    CONV_LOAD(0, ra0, rb0);
+    if (nchunks > 1) CONV_LOAD(1, ra1, rb1);
+    CONV_STORE(0, ra0, rb0);
+    __syncthreads();
+    // iteration t: load t+2, multiply t (buffer t&1), store t+1, barrier
+    int t = 0;
+    for (; t + 1 < nchunks; t += 2) {
+        if (t + 2 < nchunks) CONV_LOAD(t + 2, ra0, rb0);
+        CONV_MMA(0);
+        CONV_STORE(1, ra1, rb1);
+        __syncthreads();
+        if (t + 3 < nchunks) CONV_LOAD(t + 3, ra1, rb1);
+        CONV_MMA(1);
+        if (t + 2 < nchunks) CONV_STORE(0, ra0, rb0);
+        __syncthreads();
+    }
+    if (t < nchunks) CONV_MMA(0);
+#undef CONV_LOAD
+#undef CONV_STORE
+#undef CONV_MMA
+
+    // C/D map of 32x32: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+    float* out = a.y + (size_t)ks * a.M * a.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * (TN * 32) + 32 * j + (lane & 31);
+            if (n < a.N) {
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int m = m0 + wm * (TM * 32) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    if (m < a.M) out[MODE == MODE_WGRAD ? n * a.M + m : m * a.N + n] = acc[i][j][e];
+                }
+            }
+        }
+}
+
+// y = Σ_split partial[split] in split order (deterministic), float4 per thread
+__global__ __launch_bounds__(256) void conv_reduce_kernel(const float4* part, float4* y, int n4, int splits) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    float4 s = part[i];
+    for (int k = 1; k < splits; ++k) {
+        const float4 v = part[(size_t)k * n4 + i];
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+    }
+    y[i] = s;
+}
+
+bool valid(const md2_conv_desc* d) {
+    if (!d) return false;
+    if (d->batch < 1 || d->height < 1 || d->width < 1) return false;
+    if (d->in_channels < 4 || d->in_channels % 4 || d->out_channels < 4 || d->out_channels % 4) return false;
+    if (d->kernel_h < 1 || d->kernel_w < 1 || d->stride < 1 || d->pad < 0) return false;
+    if (d->pad >= d->kernel_h || d->pad >= d->kernel_w) return false;
+    const long long ho = (d->height + 2ll * d->pad - d->kernel_h) / d->stride + 1;
+    const long long wo = (d->width + 2ll * d->pad - d->kernel_w) / d->stride + 1;
+    if (ho < 1 || wo < 1) return false;
+    if ((long long)d->batch * d->height * d->width * d->in_channels >= (1ll << 29)) return false;
+    if ((long long)d->batch * ho * wo * d->out_channels >= (1ll << 29)) return false;
+    if ((long long)d->out_channels * d->kernel_h * d->kernel_w * d->in_channels >= (1ll << 29)) return false;
+    return true;
+}
+
+struct Shape {
+    int B, H, W, C, N, KH, KW, s, p, Ho, Wo;
+};
+
+Shape shape_of(const md2_conv_desc* d) {
+    Shape s;
+    s.B = d->batch;
+    s.H = d->height;
+    s.W = d->width;
+    s.C = d->in_channels;
+    s.N = d->out_channels;
+    s.KH = d->kernel_h;
+    s.KW = d->kernel_w;
+    s.s = d->stride;
+    s.p = d->pad;
+    s.Ho = (s.H + 2 * s.p - s.KH) / s.s + 1;
+    s.Wo = (s.W + 2 * s.p - s.KW) / s.s + 1;
+    return s;
+}
+
+int resident_blocks(int BN) { return 256 * (BN == 128 ? 2 : (BN == 64 ? 3 : 4)); }   // 256 CUs
+
+// Tile width and K split from a wave-quantisation model: time ~ rounds of resident
+// blocks x chunks per block x tile width, plus a small charge per split for the
+// partials' round trip.  Forced by MD2_CONV_TILE_* / MD2_CONV_NO_SPLIT.
+void plan(ConvArgs& a, uint32_t flags, int min_chunks) {
+    int best_bn = 64, best_s = 1;
+    double best_t = 1e30;
+    for (int BN = 32; BN <= 128; BN *= 2) {
+        if ((flags & MD2_CONV_TILE_N32) && BN != 32) continue;
+        if ((flags & MD2_CONV_TILE_N64) && BN != 64) continue;
+        if ((flags & MD2_CONV_TILE_N128) && BN != 128) continue;
+        if (BN > 32 && a.N <= BN / 2 && !(flags & (MD2_CONV_TILE_N64 | MD2_CONV_TILE_N128))) continue;
+        const int mblocks = (a.M + BM - 1) / BM, nblocks = (a.N + BN - 1) / BN;
+        const int base = mblocks * nblocks, res = resident_blocks(BN);
+        const int smax = (flags & MD2_CONV_NO_SPLIT) ? 1 : (a.nchunks / min_chunks > 1 ? a.nchunks / min_chunks : 1);
+        for (int sp = 1; sp <= smax && sp <= 64; ++sp) {
+            const int per = (a.nchunks + sp - 1) / sp;
+            const int splits = (a.nchunks + per - 1) / per;
+            const int rounds = (base * splits + res - 1) / res;
+            const double t = (double)rounds * per * BN + (splits > 1 ? 8.0 * splits : 0.0);
+            if (t < best_t - 1e-9) {
+                best_t = t;
+                best_bn = BN;
+                best_s = splits;
+            }
+        }
+    }
+    a.bn = best_bn;
+    a.mblocks = (a.M + BM - 1) / BM;
+    a.nblocks = (a.N + best_bn - 1) / best_bn;
+    a.chunks_per_split = (a.nchunks + best_s - 1) / best_s;
+    a.splits = (a.nchunks + a.chunks_per_split - 1) / a.chunks_per_split;
+}
+
+ConvArgs args_of(const md2_conv_desc* d, int mode) {
+    const Shape s = shape_of(d);
+    ConvArgs a = {};
+    a.KH = s.KH;
+    a.KW = s.KW;
+    if (mode == MODE_FWD) {
+        a.B = s.B; a.H = s.H; a.W = s.W; a.C = s.C;
+        a.Ho = s.Ho; a.Wo = s.Wo; a.stride = s.s; a.pad = s.p;
+        a.N = s.N;
+        a.M = s.B * s.Ho * s.Wo;
+        a.nchunks = s.KH * s.KW * ((s.C + BK - 1) / BK);
+        a.a_elems = s.B * s.H * s.W * s.C;            // x
+        a.b_elems = s.N * s.KH * s.KW * s.C;          // weight
+    } else if (mode == MODE_DGRAD) {
+        // full convolution of gy (B, Ho, Wo, N) -> gx (B, H, W, C), stride 1
+        a.B = s.B; a.H = s.Ho; a.W = s.Wo; a.C = s.N;
+        a.Ho = s.H; a.Wo = s.W; a.stride = 1; a.pad = s.KH - 1 - s.p;
+        a.N = s.C;
+        a.Cg = s.N;
+        a.M = s.B * s.H * s.W;
+        a.nchunks = s.KH * s.KW * ((s.N + BK - 1) / BK);
+        a.a_elems = s.B * s.Ho * s.Wo * s.N;          // gy
+        a.b_elems = s.N * s.KH * s.KW * s.C;          // weight
+    } else {
+        a.B = s.B; a.H = s.H; a.W = s.W; a.C = s.C;
+        a.Ho = s.Ho; a.Wo = s.Wo; a.stride = s.s; a.pad = s.p;
+        a.M = s.KH * s.KW * s.C;   // (tap, ci): the output is written transposed, [co][tap][ci]
+        a.Cg = s.N;
+        a.N = s.N;
+        a.P = s.B * s.Ho * s.Wo;
+        a.nchunks = (a.P + BK - 1) / BK;
+        a.a_elems = s.B * s.H * s.W * s.C;            // x
+        a.b_elems = s.B * s.Ho * s.Wo * s.N;          // gy
+    }
+    return a;
+}
+
+template <int MODE>
+void launch(const ConvArgs& a, int BN, hipStream_t st) {
+    const dim3 grid(a.mblocks * a.nblocks * a.splits);
+    if (BN == 128)
+        hipLaunchKernelGGL((conv_gemm_kernel<128, MODE>), grid, dim3(kThreads), 0, st, a);
+    else if (BN == 64)
+        hipLaunchKernelGGL((conv_gemm_kernel<64, MODE>), grid, dim3(kThreads), 0, st, a);
+    else
+        hipLaunchKernelGGL((conv_gemm_kernel<32, MODE>), grid, dim3(kThreads), 0, st, a);
+}
+
+int min_chunks_of(int mode) { return mode == MODE_WGRAD ? 8 : 6; }
+
+int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float* out, void* ws, void* stream,
+        const char* name) {
+    ConvArgs a = args_of(d, mode);
+    plan(a, d->flags, min_chunks_of(mode));
+    const int BN = a.bn;
+    a.a = A;
+    a.b = B;
+    if (a.splits > 1 && !ws) return md2_report_error(MD2_ERR_ARG, name);
+    a.y = a.splits > 1 ? (float*)ws : out;
+    const hipStream_t st = (hipStream_t)stream;
+    if (mode == MODE_FWD) launch<MODE_FWD>(a, BN, st);
+    else if (mode == MODE_DGRAD) launch<MODE_DGRAD>(a, BN, st);
+    else launch<MODE_WGRAD>(a, BN, st);
+    if (a.splits > 1) {
+        const int n4 = a.M * a.N / 4;
+        hipLaunchKernelGGL(conv_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, st, (const float4*)ws,
+                           (float4*)out, n4, a.splits);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
+size_t ws_bytes(const md2_conv_desc* d, int mode) {
+    ConvArgs a = args_of(d, mode);
+    plan(a, d->flags, min_chunks_of(mode));
+    return a.splits > 1 ? sizeof(float) * (size_t)a.splits * a.M * a.N : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t md2_conv_workspace_bytes(const md2_conv_desc* d) {
+    if (!valid(d)) return 0;
+    size_t m = ws_bytes(d, MODE_FWD);
+    if (d->stride == 1) m = m > ws_bytes(d, MODE_DGRAD) ? m : ws_bytes(d, MODE_DGRAD);
+    const size_t w = ws_bytes(d, MODE_WGRAD);
+    return m > w ? m : w;
+}
+
+int md2_conv_fwd(const md2_conv_desc* d, const float* x, const float* weight, float* y, void* workspace,
+                 void* stream) {
+    if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "conv_fwd: channels % 4, pad < kernel, sizes < 2^29");
+    if (!x || !weight || !y) return md2_report_error(MD2_ERR_ARG, "conv_fwd: NULL operand");
+    return run(d, MODE_FWD, x, weight, y, workspace, stream, "conv_fwd: workspace required (K split)");
+}
+
+int md2_conv_dgrad(const md2_conv_desc* d, const float* grad_y, const float* weight, float* grad_x,
+                   void* workspace, void* stream) {
+    if (!valid(d) || d->stride != 1)
+        return md2_report_error(MD2_ERR_ARG, "conv_dgrad: stride 1, channels % 4, pad < kernel, sizes < 2^29");
+    if (!grad_y || !weight || !grad_x) return md2_report_error(MD2_ERR_ARG, "conv_dgrad: NULL operand");
+    return run(d, MODE_DGRAD, grad_y, weight, grad_x, workspace, stream, "conv_dgrad: workspace required (K split)");
+}
+
+int md2_conv_wgrad(const md2_conv_desc* d, const float* x, const float* grad_y, float* grad_weight,
+                   void* workspace, void* stream) {
+    if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "conv_wgrad: channels % 4, pad < kernel, sizes < 2^29");
+    if (!x || !grad_y || !grad_weight) return md2_report_error(MD2_ERR_ARG, "conv_wgrad: NULL operand");
+    return run(d, MODE_WGRAD, x, grad_y, grad_weight, workspace, stream, "conv_wgrad: workspace required (K split)");
+}
+
+}  // extern "C"

@@ -51,6 +51,7 @@ class DepthDecoder(nn.Module):
         """Same graph with each conv input built by one HIP pass (decoder_ops):
         pad(x) -> conv -> [ELU -> up x2 -> cat skip -> pad] -> conv -> [ELU -> pad] ->
         (dispconv -> sigmoid) and the next level's first conv."""
+        from ..conv_ops import conv2d_w
         from ..decoder_ops import conv_input, disp_head, supports_bias, supports_disp_head
         self.outputs = {}
         # NHWC convolutions (channels_last weights): keep every conv input NHWC too
@@ -62,8 +63,10 @@ class DepthDecoder(nn.Module):
             fold it (NHWC: no separate bias-add pass forward, no bias-grad reduction
             backward — the pad kernels carry both)."""
             c = block.conv.conv
-            if c.bias is not None and supports_bias(c.out_channels, cl):
-                return F.conv2d(P, c.weight, None, c.stride, c.padding, c.dilation, c.groups), c.bias
+            if c.bias is not None and supports_bias(c.out_channels, cl) and c.groups == 1 \
+                    and tuple(c.dilation) == (1, 1) and c.stride[0] == c.stride[1] and c.padding[0] == c.padding[1]:
+                # f32 MFMA implicit GEMM where the channel counts fit (conv_ops), else MIOpen
+                return conv2d_w(P, c.weight, c.stride[0], c.padding[0]), c.bias
             return c(P), None
 
         for i in range(4, -1, -1):

@@ -20,6 +20,7 @@ import torch
 import torch.nn as nn
 
 from ..bn_ops import bn_act, max_pool_3x3s2, max_pool_3x3s2_with_alias
+from ..conv_ops import conv2d
 from ..stem_ops import stem_conv
 
 
@@ -53,7 +54,7 @@ class BasicBlock(nn.Module):
 
 def _downsample(down: nn.Sequential, x):
     """The (conv1x1, BatchNorm2d) shortcut: BN without ReLU."""
-    return bn_act(down[1], down[0](x), relu=False)
+    return bn_act(down[1], conv2d(down[0], x), relu=False)
 
 
 class Bottleneck(nn.Module):
@@ -89,15 +90,15 @@ def _run_layer(layer: nn.Sequential, x, xs, skip_alias: bool):
     skip = None
     for bi, blk in enumerate(layer):
         shortcut = xs if blk.downsample is None else _downsample(blk.downsample, xs)
-        out = bn_act(blk.bn1, blk.conv1(x))
+        out = bn_act(blk.bn1, conv2d(blk.conv1, x))
         if isinstance(blk, Bottleneck):
-            out = bn_act(blk.bn2, blk.conv2(out))
+            out = bn_act(blk.bn2, conv2d(blk.conv2, out))
             bn, conv = blk.bn3, blk.conv3
         else:
             bn, conv = blk.bn2, blk.conv2
         last = bi == n - 1
         k = (2 if skip_alias else 1) if last else 1
-        res = bn_act(bn, conv(out), residual=shortcut, aliases=k)
+        res = bn_act(bn, conv2d(conv, out), residual=shortcut, aliases=k)
         x, xs = res[0], res[1]
         skip = res[2] if (last and skip_alias) else x
     return x, xs, skip

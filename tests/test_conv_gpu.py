@@ -1,0 +1,162 @@
+"""f32 MFMA implicit-GEMM convolutions (csrc/conv.hip via conv_ops) vs MIOpen
+(F.conv2d, fp32) on the encoder / decoder shapes: outputs and gradients.
+
+f32 MFMA is an exact f32 fma chain, so the two differ only in summation order:
+the bar is 2e-5 of the output's magnitude (forward) and 1e-4 (gradients)."""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from monodepth2_amd import _lib, conv_ops
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+
+SHAPES = [  # (B, Cin, Cout, k, stride, pad, H, W)
+    (2, 64, 64, 3, 1, 1, 24, 40),      # ResNet layer1 conv
+    (3, 128, 128, 3, 1, 1, 12, 20),    # 128x128 tile
+    (2, 64, 128, 3, 2, 1, 24, 40),     # stage-entry conv, stride 2
+    (2, 64, 128, 1, 2, 0, 24, 40),     # downsample shortcut
+    (2, 256, 256, 3, 1, 1, 6, 10),     # deep layer: K split
+    (2, 512, 512, 3, 1, 1, 3, 5),      # layer4 at 96x320: K split, M tail
+    (2, 96, 64, 3, 1, 0, 18, 34),      # decoder conv on a padded input (pad 0), C = 3 chunks
+    (1, 32, 64, 3, 1, 1, 7, 9),        # odd sizes, M not a tile multiple
+]
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+
+@pytest.fixture(autouse=True)
+def _mfma_always(monkeypatch):
+    """These tests check the MFMA kernels themselves: no per-shape fallback to MIOpen."""
+    monkeypatch.setattr(conv_ops, "AUTOTUNE", False)
+
+
+@pytest.mark.parametrize("B,C,N,k,s,p,H,W", SHAPES)
+def test_conv_matches_miopen(B, C, N, k, s, p, H, W):
+    torch.manual_seed(B * 1000 + C + N + k + s + H)
+    conv = torch.nn.Conv2d(C, N, k, s, p, bias=False).cuda().to(memory_format=CL)
+    ref = torch.nn.Conv2d(C, N, k, s, p, bias=False).cuda().to(memory_format=CL)
+    ref.weight.data.copy_(conv.weight.data)
+    x0 = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    x = x0.clone().requires_grad_(True)
+    xr = x0.clone().requires_grad_(True)
+    assert conv_ops.supports(conv, x)
+    y = conv_ops.conv2d(conv, x)
+    yr = ref(xr)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=CL)
+    assert _rel(y, yr) < 2e-5
+    g = torch.randn_like(yr)
+    gx, gw = torch.autograd.grad(y, [x, conv.weight], g)
+    gxr, gwr = torch.autograd.grad(yr, [xr, ref.weight], g)
+    assert _rel(gx, gxr) < 1e-4
+    assert _rel(gw, gwr) < 1e-4
+
+
+def test_autotune_keeps_a_choice_per_shape(monkeypatch):
+    """With AUTOTUNE the first call of a shape times the MFMA kernel against MIOpen
+    and caches the winner; either way the result is the convolution."""
+    monkeypatch.setattr(conv_ops, "AUTOTUNE", True)
+    monkeypatch.setattr(conv_ops, "_choice", {})
+    conv = torch.nn.Conv2d(64, 64, 3, 1, 1, bias=False).cuda().to(memory_format=CL)
+    x = torch.randn(2, 64, 24, 40, device="cuda").contiguous(memory_format=CL).requires_grad_(True)
+    y = conv_ops.conv2d(conv, x)
+    y.backward(torch.ones_like(y))
+    assert {k[0] for k in conv_ops._choice} == {"fwd", "dgrad", "wgrad"}
+    assert _rel(y, F.conv2d(x, conv.weight, padding=1)) < 2e-5
+
+
+def test_conv_tile_and_split_variants_agree():
+    """The 128x64 / 128x128 tiles and the K split (partials summed in split order)
+    give the same result up to rounding; each run is bitwise deterministic."""
+    torch.manual_seed(7)
+    B, C, N, H, W = 2, 256, 256, 12, 20
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    w = torch.randn(N, C, 3, 3, device="cuda").contiguous(memory_format=CL) / 48
+    outs = {}
+    for flags in (0, _lib.CONV_TILE_N64, _lib.CONV_TILE_N32, _lib.CONV_NO_SPLIT,
+                  _lib.CONV_TILE_N64 | _lib.CONV_NO_SPLIT):
+        d = _lib.ConvDesc(B, H, W, C, N, 3, 3, 1, 1, flags)
+        L = _lib.lib()
+        ws = torch.empty(max(L.md2_conv_workspace_bytes(ctypes.byref(d)), 4), dtype=torch.uint8, device="cuda")
+        res = []
+        for _ in range(2):
+            y = torch.empty(B, N, H, W, device="cuda", memory_format=CL)
+            _lib.check(L.md2_conv_fwd(ctypes.byref(d), x.data_ptr(), w.data_ptr(), y.data_ptr(), ws.data_ptr(),
+                                      torch.cuda.current_stream().cuda_stream), "md2_conv_fwd")
+            res.append(y)
+        assert torch.equal(res[0], res[1])
+        outs[flags] = res[0]
+    ref = F.conv2d(x, w, padding=1)
+    for y in outs.values():
+        assert _rel(y, ref) < 2e-5
+
+
+def test_conv_rejects_unsupported_shapes():
+    d = _lib.ConvDesc(1, 8, 8, 6, 64, 3, 3, 1, 1, 0)   # in_channels not a multiple of 4
+    assert _lib.lib().md2_conv_fwd(ctypes.byref(d), 1, 1, 1, 1, None) == -1
+    d = _lib.ConvDesc(1, 8, 8, 8, 64, 3, 3, 2, 1, 0)   # the input gradient is stride 1 only
+    assert _lib.lib().md2_conv_dgrad(ctypes.byref(d), 1, 1, 1, 1, None) == -1
+
+
+def test_encoder_on_mfma_convs_matches_miopen():
+    """Whole ResNet-18 encoder, training mode: MFMA convs vs MIOpen convs (same fused
+    BatchNorm), features and every parameter gradient."""
+    import copy
+    from monodepth2_amd import networks
+    torch.manual_seed(0)
+    enc = networks.ResnetEncoder(18, False).cuda().to(memory_format=CL)
+    ref = copy.deepcopy(enc)
+    img = torch.rand(2, 3, 64, 128, device="cuda")
+
+    def run(e, on):
+        conv_ops.ENABLED = on
+        try:
+            feats = e(img)
+        finally:
+            conv_ops.ENABLED = True
+        loss = sum((f * (i + 1)).mean() for i, f in enumerate(feats))
+        return feats, torch.autograd.grad(loss, list(e.parameters()), allow_unused=True)
+
+    fa, ga = run(enc, True)
+    fb, gb = run(ref, False)
+    for a, b in zip(fa, fb):
+        assert float((a - b).norm() / b.norm()) < 1e-5
+    for a, b in zip(ga, gb):
+        if b is not None:
+            assert float((a - b).norm() / (b.norm() + 1e-12)) < 1e-3
+
+
+@pytest.mark.parametrize("B,C,N,k,s,p,H,W", SHAPES + [(2, 16, 16, 3, 1, 0, 20, 34), (2, 32, 16, 3, 1, 0, 12, 18),
+                                                      (2, 96, 32, 3, 1, 0, 10, 12), (2, 64, 32, 3, 1, 0, 9, 11)])
+def test_conv_abi_dgrad_wgrad(B, C, N, k, s, p, H, W):
+    """md2_conv_dgrad / md2_conv_wgrad directly (every tile width, K split on),
+    including the decoder's narrow full-resolution convs (16 / 32 channels)."""
+    torch.manual_seed(3 + C + N + H)
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    w = (torch.randn(N, C, k, k, device="cuda") / (C * k * k) ** 0.5).contiguous(memory_format=CL)
+    y = F.conv2d(x, w, stride=s, padding=p)
+    gy = torch.randn_like(y).contiguous(memory_format=CL)
+    gx_ref, gw_ref, _ = torch.ops.aten.convolution_backward(gy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
+                                                            (True, True, False))
+    L = _lib.lib()
+    d = _lib.ConvDesc(B, H, W, C, N, k, k, s, p, 0)
+    ws = torch.empty(max(L.md2_conv_workspace_bytes(ctypes.byref(d)), 4), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    yo = torch.empty_like(y, memory_format=CL)
+    _lib.check(L.md2_conv_fwd(ctypes.byref(d), x.data_ptr(), w.data_ptr(), yo.data_ptr(), ws.data_ptr(), st), "fwd")
+    assert _rel(yo, y) < 2e-5
+    gw = torch.empty_like(w, memory_format=CL)
+    _lib.check(L.md2_conv_wgrad(ctypes.byref(d), x.data_ptr(), gy.data_ptr(), gw.data_ptr(), ws.data_ptr(), st),
+               "wgrad")
+    assert _rel(gw, gw_ref) < 1e-4
+    if s == 1:
+        gx = torch.empty_like(x, memory_format=CL)
+        _lib.check(L.md2_conv_dgrad(ctypes.byref(d), gy.data_ptr(), w.data_ptr(), gx.data_ptr(), ws.data_ptr(), st),
+                   "dgrad")
+        assert _rel(gx, gx_ref) < 1e-4
