@@ -117,6 +117,15 @@ __device__ __forceinline__ float2_a4 ldf2(const float* base, int idx) {
 }
 __device__ __forceinline__ uint8_t ldb(const uint8_t* base, int idx) { return base[(uint32_t)idx]; }
 
+// x / 3 correctly rounded (the channel mean of trainer.py:396-397 divides by 3), in
+// three VALU ops instead of the IEEE division sequence: q = x * RN(1/3), one exact
+// fma residual, one fma correction (Markstein)
+__device__ __forceinline__ float div3(float x) {
+    const float c = 1.0f / 3.0f;
+    const float q = x * c;
+    return fmaf(fmaf(-3.0f, q, x), c, q);
+}
+
 __device__ __forceinline__ float signf(float v) { return (v > 0.f) ? 1.f : ((v < 0.f) ? -1.f : 0.f); }
 
 // counter-based normal deviate for the tie-break noise (trainer.py:468)
@@ -247,9 +256,14 @@ struct FastSample {
     float tx, ty;
 };
 
-__device__ __forceinline__ void project_fast(const WarpCtx& c, int y, int x, FastSample& s) {
-    const float d = disp_at(c, y, x);
-    s.depth = rcpf(c.min_disp + c.range * d);
+// depth of the upsampled disparity at (y, x) (layers.py:16-25 with v_rcp_f32)
+__device__ __forceinline__ float depth_at(const WarpCtx& c, int y, int x) {
+    return rcpf(c.min_disp + c.range * disp_at(c, y, x));
+}
+
+// projection of pixel (y, x) at a given depth
+__device__ __forceinline__ void project_depth(const WarpCtx& c, int y, int x, float depth, FastSample& s) {
+    s.depth = depth;
     const float fx = (float)x, fy = (float)y;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -273,6 +287,10 @@ __device__ __forceinline__ void project_fast(const WarpCtx& c, int y, int x, Fas
     s.y0 = (int)fy0;
     s.tx = ixc - fx0;
     s.ty = iyc - fy0;
+}
+
+__device__ __forceinline__ void project_fast(const WarpCtx& c, int y, int x, FastSample& s) {
+    project_depth(c, y, x, depth_at(c, y, x), s);
 }
 
 // the four (masked) source corners of a sample for the 3 channels
@@ -309,9 +327,9 @@ __device__ __forceinline__ void interp(const SampleT& s, const Corners& v, float
     for (int ch = 0; ch < 3; ++ch) out[ch] = v.nw[ch] * wnw + v.ne[ch] * wne + v.sw[ch] * wsw + v.se[ch] * wse;
 }
 
-__device__ __forceinline__ void warp_value(const WarpCtx& c, int y, int x, float out[3]) {
+__device__ __forceinline__ void warp_value(const WarpCtx& c, int y, int x, float depth, float out[3]) {
     FastSample s;
-    project_fast(c, y, x, s);
+    project_depth(c, y, x, depth, s);
     Corners v;
     gather(c, s, v);
     interp(s, v, out);
@@ -420,8 +438,8 @@ __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int 
 // row loop stays rolled (the per-row state lives in LDS, see photo_fwd_kernel).
 // ----------------------------------------------------------------------------
 template <bool SSIM_ON, bool WARPED, class Emit>
-__device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float (*trow)[kWave], int r0, int cc, int lane,
-                                            Emit emit) {
+__device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float (*trow)[kWave], const float (*dep)[kWave],
+                                            int r0, int cc, int lane, Emit emit) {
     // trow: the target rows r0-1 .. r0+kRowsF (reflected), [row * 3 + channel][lane],
     // staged once per wave in LDS (photo_fwd_kernel) instead of re-read from HBM by
     // every (scale, frame) pass
@@ -431,7 +449,7 @@ __device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float (*trow
             const int rr = reflect_clamp(r0 + i, h);
             float x[3];
             if (WARPED) {
-                warp_value(c, rr, cc, x);
+                warp_value(c, rr, cc, dep[i + 1][lane], x);
             } else {
 #pragma unroll
                 for (int ch = 0; ch < 3; ++ch) x[ch] = ldf(c.src, ch * HW + rr * w + cc);
@@ -439,7 +457,7 @@ __device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float (*trow
             float l1 = 0.f;
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) l1 += fabsf(trow[(i + 1) * 3 + ch][lane] - x[ch]);
-            emit(i, l1 / 3.f);
+            emit(i, div3(l1));
         }
         return;
     }
@@ -449,7 +467,7 @@ __device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float (*trow
         const int rr = reflect_clamp(r0 - 1 + k, h);
         float x[3], y[3];
         if (WARPED) {
-            warp_value(c, rr, cc, x);
+            warp_value(c, rr, cc, dep[k][lane], x);
         } else {
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) x[ch] = ldf(c.src, ch * HW + rr * w + cc);
@@ -466,7 +484,7 @@ __device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float (*trow
                 ss += ssim_from_sums(hA[ch], hB[ch], hc[ch]);
                 l1 += fabsf(yB[ch] - xB[ch]);
             }
-            emit(k - 2, 0.85f * (ss / 3.f) + 0.15f * (l1 / 3.f));
+            emit(k - 2, 0.85f * div3(ss) + 0.15f * div3(l1));
         }
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) {
@@ -482,6 +500,7 @@ __device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float (*trow
 template <int NS>
 struct FwdState {
     float tgt[(kRowsF + 2) * 3][kWave];   // target rows r0-1 .. r0+kRowsF, 3 channels
+    float dep[kRowsF + 2][kWave];         // depth of rows r0-1 .. r0+kRowsF at the current scale
     float ident[NS][kRowsF][kWave];
     float best[kRowsF][kWave];
     float accum[kRowsF][kWave];
@@ -522,7 +541,8 @@ __global__ __launch_bounds__(kBlock, MD2_FWD_MINB) void photo_fwd_kernel(PhotoAr
             ctx.src = a.src[f] + (size_t)b * 3 * HW;
             ctx.h = h;
             ctx.w = w;
-            reproj_rows<SSIM_ON, false>(ctx, L.tgt, r0, cc, lane, [&](int i, float v) { L.ident[f][i][lane] = v; });
+            reproj_rows<SSIM_ON, false>(ctx, L.tgt, L.dep, r0, cc, lane,
+                                        [&](int i, float v) { L.ident[f][i][lane] = v; });
         }
     }
 
@@ -558,11 +578,18 @@ __global__ __launch_bounds__(kBlock, MD2_FWD_MINB) void photo_fwd_kernel(PhotoAr
             L.accum[i][lane] = 0.f;
         }
         const float* pmask = MASK ? a.mask[ls] : nullptr;
+        {
+            // the rows' depths once per scale (every frame warps the same upsampled disparity)
+            WarpCtx ctx;
+            make_ctx(a, ls, 0, b, ctx);
+#pragma unroll
+            for (int k = 0; k < kRowsF + 2; ++k) L.dep[k][lane] = depth_at(ctx, reflect_clamp(r0 - 1 + k, h), cc);
+        }
         for (int f = 0; f < NS; ++f) {
             WarpCtx ctx;
             make_ctx(a, ls, f, b, ctx);
             const int cand = (automask ? NS : 0) + f;
-            reproj_rows<SSIM_ON, true>(ctx, L.tgt, r0, cc, lane, [&](int i, float v) {
+            reproj_rows<SSIM_ON, true>(ctx, L.tgt, L.dep, r0, cc, lane, [&](int i, float v) {
                 if (MASK) v *= pmask[(((size_t)b * NS + f) * h + min(r0 + i, h - 1)) * w + cc];  // trainer.py:455
                 if (avg) {
                     L.accum[i][lane] += v;
@@ -655,153 +682,181 @@ __device__ __forceinline__ void make_carry(const WarpCtx& c, const FastSample& s
     k.dd = -c.range * s.depth * s.depth;
 }
 
+// One evaluated row of the backward window (row r = r0 - 2 + k of the item).
+struct RowS {
+    H5 h[3];           // horizontal 3-tap sums (SSIM)
+    float x[3], y[3];  // warped source / target colour at this lane
+    Carry k;           // what the output step needs from this row's sample
+};
+
+// Per-(item, frame) constants of the backward.
+struct BwdFrame {
+    WarpCtx ctx;
+    const float* tgt;
+    const uint8_t* sel;
+    const float* pmask;
+    float* pgmask;
+    const float (*dep)[kWave];   // LDS: depth of window rows k = 0 .. kRowsB+3 (frame-independent)
+    int b, f, r0, c, cc;
+    bool colok, colreal, automask, avg;
+    float wl, wr, gscale;
+};
+
+// One step of the backward row walk at window index k (row r = r0 - 2 + k):
+//   evaluate row r (warp, target, horizontal sums, carry) into `cur`;
+//   k >= 2: SSIM adjoint coefficients of row p = r - 1 into `cnew` (from the sums of
+//           rows r-2, r-1, r = m2, m1, cur);
+//   k >= 4: output row q = r - 2: dL/dwarp from coefficient rows q-1, q, q+1
+//           (cm3, cm2, cnew) + the L1 term, through the carried bilinear slopes and
+//           projection into dL/dP and dL/d(upsampled disp).
+// The window state lives in three statically named ring slots (rows and coefficient
+// rows mod 3) that the caller rotates by unrolling three steps, so moving the window
+// down costs no register copies; every slot is updated unconditionally.
+template <int NS, bool SSIM_ON, bool MASK>
+__device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, RowS& cur, const RowS& m1, const RowS& m2,
+                                         Coef& cnew, const Coef& cm2, const Coef& cm3, float (&dP)[12],
+                                         float* dfull, float (*ddacc)[kWave], int lane) {
+    constexpr float kThird = 1.0f / 3.0f;
+    const float l1w = SSIM_ON ? 0.15f : 1.0f;
+    const int h = F.ctx.h, w = F.ctx.w, HW = h * w;
+    const int r = F.r0 - 2 + k;
+    const int rr = reflect_clamp(r, h);
+    FastSample sm;
+    project_depth(F.ctx, rr, F.cc, F.dep[k][lane], sm);
+    Corners v;
+    gather(F.ctx, sm, v);
+    interp(sm, v, cur.x);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) cur.y[ch] = ldf(F.tgt, ch * HW + rr * w + F.cc);
+    if (k >= 2 && k < kRowsB + 2) make_carry(F.ctx, sm, v, cur.k);  // only output rows need it
+    if (SSIM_ON) {
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) cur.h[ch] = hsum(cur.x[ch], cur.y[ch]);
+    }
+    if (k < 2) return;
+    // coefficient row p = r - 1
+    const int p = r - 1;
+    float gp = 0.f;
+    const bool own = F.colreal && p >= 0 && p < h;
+    if (own) gp = F.gscale * frame_weight<NS>(ldb(F.sel, p * w + F.c), F.f, F.automask, F.avg);
+    if (MASK) {
+        // masked = reproj * mask (trainer.py:455): d/dreproj = g*mask, d/dmask = g*reproj
+        const size_t mi = (((size_t)F.b * NS + F.f) * h + (own ? p : 0)) * w + (own ? F.c : 0);
+        if (F.pgmask && F.colok && p >= F.r0 && p < F.r0 + kRowsB && p < h) {
+            float ss = 0.f, l1 = 0.f;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                if (SSIM_ON) ss += ssim_from_sums(m2.h[ch], m1.h[ch], cur.h[ch]);
+                l1 += fabsf(m1.y[ch] - m1.x[ch]);
+            }
+            const float rep = SSIM_ON ? 0.85f * div3(ss) + 0.15f * div3(l1) : div3(l1);
+            F.pgmask[mi] = gp * rep;
+        }
+        gp *= own ? F.pmask[mi] : 0.f;
+    }
+    cnew.g = gp;
+    if (SSIM_ON) {
+        const float gS = gp * (0.85f / 3.f);
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            float dA, dB, dC;
+            ssim_adjoint(m2.h[ch], m1.h[ch], cur.h[ch], gS, dA, dB, dC);
+            if (gp == 0.f) dA = dB = dC = 0.f;
+            cnew.A[ch] = pick(F.wl, shfl_prev(dA)) + dA + pick(F.wr, shfl_next(dA));
+            cnew.B[ch] = pick(F.wl, shfl_prev(dB)) + dB + pick(F.wr, shfl_next(dB));
+            cnew.C[ch] = pick(F.wl, shfl_prev(dC)) + dC + pick(F.wr, shfl_next(dC));
+        }
+    }
+    if (k < 4) return;
+    // output row q = r - 2 (coefficient rows q-1, q, q+1 = cm3, cm2, cnew)
+    const int q = r - 2;
+    if (!(F.colok && q < h)) return;
+    const Carry& k2 = m2.k;
+    const float l1c = cm2.g * (l1w * kThird);
+    float dpx = 0.f, dpy = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        float g = l1c * signf(m2.x[ch] - m2.y[ch]);
+        if (SSIM_ON) {
+            const float wu = fold_lo(q), wd = fold_hi(q, h);
+            const float aA = pick(wu, cm3.A[ch]) + cm2.A[ch] + pick(wd, cnew.A[ch]);
+            const float aB = pick(wu, cm3.B[ch]) + cm2.B[ch] + pick(wd, cnew.B[ch]);
+            const float aC = pick(wu, cm3.C[ch]) + cm2.C[ch] + pick(wd, cnew.C[ch]);
+            g += (aA + 2.f * m2.x[ch] * aB + m2.y[ch] * aC) * kInv9;
+        }
+        dpx += g * k2.jx[ch];
+        dpy += g * k2.jy[ch];
+    }
+    float dc[3];
+    dc[0] = dpx * k2.inv_den;
+    dc[1] = dpy * k2.inv_den;
+    dc[2] = -(dpx * k2.px + dpy * k2.py) * k2.inv_den;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) dP[i * 4 + j] += dc[i] * k2.pt[j];
+        dP[i * 4 + 3] += dc[i];
+    }
+    const float dd = (dc[0] * k2.u[0] + dc[1] * k2.u[1] + dc[2] * k2.u[2]) * k2.dd;
+    // frames accumulate in LDS; dfull is written once per item
+    if (NS == 1) dfull[q * w + F.c] = dd;
+    else if (F.f == 0) ddacc[q - F.r0][lane] = dd;
+    else ddacc[q - F.r0][lane] += dd;
+}
+
 // One work item of the backward: (image b, local scale ls, strip st, row block rb),
 // all source frames.  Writes dL/d(upsampled disp) for its 60 x kRowsB pixels and one
 // 12-float dL/dP partial per frame.
 template <int NS, bool SSIM_ON, bool MASK>
 __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int st, int rb, int lane,
-                                         float (*ddacc)[kWave]) {
-    const int r0 = rb * kRowsB;
+                                         float (*ddacc)[kWave], float (*dep)[kWave]) {
+    BwdFrame F;
+    F.r0 = rb * kRowsB;
     const int h = a.h, w = a.w, HW = h * w;
-    const int c = st * kBwdCols - 2 + lane;
-    const int cc = reflect_clamp(c, w);
-    const bool colok = lane >= 2 && lane < 2 + kBwdCols && c < w;
-    const bool colreal = c >= 0 && c < w;
-    const float wl = fold_lo(c), wr = fold_hi(c, w);
-    const float* tgt = a.tgt + (size_t)b * 3 * HW;
-    const bool automask = !(a.flags & MD2_NO_AUTOMASK);
-    const bool avg = (a.flags & MD2_AVG_REPROJECTION) != 0;
-    const float l1w = SSIM_ON ? 0.15f : 1.0f;
+    F.b = b;
+    F.c = st * kBwdCols - 2 + lane;
+    F.cc = reflect_clamp(F.c, w);
+    F.colok = lane >= 2 && lane < 2 + kBwdCols && F.c < w;
+    F.colreal = F.c >= 0 && F.c < w;
+    F.wl = fold_lo(F.c);
+    F.wr = fold_hi(F.c, w);
+    F.tgt = a.tgt + (size_t)b * 3 * HW;
+    F.automask = !(a.flags & MD2_NO_AUTOMASK);
+    F.avg = (a.flags & MD2_AVG_REPROJECTION) != 0;
     const int gsc = a.gscale[ls];
-    const float gscale = (a.grad_loss[gsc] + a.grad_loss[a.num_scales] / (float)a.num_scales) /
-                         ((float)a.B * (float)HW);
-    const uint8_t* sel = a.sel[ls] + (size_t)b * HW;
+    F.gscale = (a.grad_loss[gsc] + a.grad_loss[a.num_scales] / (float)a.num_scales) / ((float)a.B * (float)HW);
+    F.sel = a.sel[ls] + (size_t)b * HW;
     float* dfull = a.dfull[ls] + (size_t)b * HW;
     const int item_in_scale = b * a.wpi + rb * a.strips + st;
-    const float* pmask = MASK ? a.mask[ls] : nullptr;
-    float* pgmask = MASK ? a.gmask[ls] : nullptr;
+    F.pmask = MASK ? a.mask[ls] : nullptr;
+    F.pgmask = MASK ? a.gmask[ls] : nullptr;
+    F.dep = dep;
+    // the window's depths once per item (both frames warp the same upsampled disparity):
+    // all taps issued together instead of one dependent load pair per row and frame
+    make_ctx(a, ls, 0, b, F.ctx);
+#pragma unroll
+    for (int k = 0; k < kRowsB + 4; ++k) dep[k][lane] = depth_at(F.ctx, reflect_clamp(F.r0 - 2 + k, h), F.cc);
 
     for (int f = 0; f < NS; ++f) {
-        WarpCtx ctx;
-        make_ctx(a, ls, f, b, ctx);
+        F.f = f;
+        make_ctx(a, ls, f, b, F.ctx);
         float dP[12];
 #pragma unroll
         for (int j = 0; j < 12; ++j) dP[j] = 0.f;
-        H5 hA[3], hB[3];
-        float x1[3] = {0.f, 0.f, 0.f}, y1[3] = {0.f, 0.f, 0.f};  // row r-1
-        float x2[3] = {0.f, 0.f, 0.f}, y2[3] = {0.f, 0.f, 0.f};  // row r-2
-        Coef cA, cB;
-        Carry k1, k2;
-#pragma unroll 2
-        for (int k = 0; k < kRowsB + 4; ++k) {
-            const int r = r0 - 2 + k;
-            const int rr = reflect_clamp(r, h);
-            FastSample sm;
-            project_fast(ctx, rr, cc, sm);
-            Corners v;
-            gather(ctx, sm, v);
-            float x[3], y[3];
-            interp(sm, v, x);
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) y[ch] = ldf(tgt, ch * HW + rr * w + cc);
-            Carry kc;
-            if (k >= 2 && k < kRowsB + 2) make_carry(ctx, sm, v, kc);  // only output rows need it
-            H5 hc[3];
-            if (SSIM_ON) {
-#pragma unroll
-                for (int ch = 0; ch < 3; ++ch) hc[ch] = hsum(x[ch], y[ch]);
-            }
-            if (k >= 2) {
-                // coefficient row p = r - 1
-                const int p = r - 1;
-                float gp = 0.f;
-                const bool own = colreal && p >= 0 && p < h;
-                if (own) gp = gscale * frame_weight<NS>(ldb(sel, p * w + c), f, automask, avg);
-                if (MASK) {
-                    // masked = reproj * mask (trainer.py:455): d/dreproj = g*mask, d/dmask = g*reproj
-                    const size_t mi = (((size_t)b * NS + f) * h + (own ? p : 0)) * w + (own ? c : 0);
-                    if (pgmask && colok && p >= r0 && p < r0 + kRowsB && p < h) {
-                        float ss = 0.f, l1 = 0.f;
-#pragma unroll
-                        for (int ch = 0; ch < 3; ++ch) {
-                            if (SSIM_ON) ss += ssim_from_sums(hA[ch], hB[ch], hc[ch]);
-                            l1 += fabsf(y1[ch] - x1[ch]);
-                        }
-                        const float rep = SSIM_ON ? 0.85f * (ss / 3.f) + 0.15f * (l1 / 3.f) : l1 / 3.f;
-                        pgmask[mi] = gp * rep;
-                    }
-                    gp *= own ? pmask[mi] : 0.f;
-                }
-                Coef cC;
-                cC.g = gp;
-                if (SSIM_ON) {
-                    const float gS = gp * (0.85f / 3.f);
-#pragma unroll
-                    for (int ch = 0; ch < 3; ++ch) {
-                        float dA, dB, dC;
-                        ssim_adjoint(hA[ch], hB[ch], hc[ch], gS, dA, dB, dC);
-                        if (gp == 0.f) dA = dB = dC = 0.f;
-                        cC.A[ch] = pick(wl, shfl_prev(dA)) + dA + pick(wr, shfl_next(dA));
-                        cC.B[ch] = pick(wl, shfl_prev(dB)) + dB + pick(wr, shfl_next(dB));
-                        cC.C[ch] = pick(wl, shfl_prev(dC)) + dC + pick(wr, shfl_next(dC));
-                    }
-                }
-                if (k >= 4) {
-                    // output row q = r - 2 (coefficient rows q-1, q, q+1 = cA, cB, cC)
-                    const int q = r - 2;
-                    if (colok && q < h) {
-                        const float l1c = cB.g * (l1w / 3.f);
-                        float dpx = 0.f, dpy = 0.f;
-#pragma unroll
-                        for (int ch = 0; ch < 3; ++ch) {
-                            float g = l1c * signf(x2[ch] - y2[ch]);
-                            if (SSIM_ON) {
-                                const float wu = fold_lo(q), wd = fold_hi(q, h);
-                                const float aA = pick(wu, cA.A[ch]) + cB.A[ch] + pick(wd, cC.A[ch]);
-                                const float aB = pick(wu, cA.B[ch]) + cB.B[ch] + pick(wd, cC.B[ch]);
-                                const float aC = pick(wu, cA.C[ch]) + cB.C[ch] + pick(wd, cC.C[ch]);
-                                g += (aA + 2.f * x2[ch] * aB + y2[ch] * aC) * kInv9;
-                            }
-                            dpx += g * k2.jx[ch];
-                            dpy += g * k2.jy[ch];
-                        }
-                        float dc[3];
-                        dc[0] = dpx * k2.inv_den;
-                        dc[1] = dpy * k2.inv_den;
-                        dc[2] = -(dpx * k2.px + dpy * k2.py) * k2.inv_den;
-#pragma unroll
-                        for (int i = 0; i < 3; ++i) {
-#pragma unroll
-                            for (int j = 0; j < 3; ++j) dP[i * 4 + j] += dc[i] * k2.pt[j];
-                            dP[i * 4 + 3] += dc[i];
-                        }
-                        const float dd = (dc[0] * k2.u[0] + dc[1] * k2.u[1] + dc[2] * k2.u[2]) * k2.dd;
-                        // frames accumulate in LDS; dfull is written once per item
-                        if (NS == 1) dfull[q * w + c] = dd;
-                        else if (f == 0) ddacc[q - r0][lane] = dd;
-                        else ddacc[q - r0][lane] += dd;
-                    }
-                }
-                cA = cB;
-                cB = cC;
-            }
-            if (SSIM_ON) {
-#pragma unroll
-                for (int ch = 0; ch < 3; ++ch) {
-                    hA[ch] = hB[ch];
-                    hB[ch] = hc[ch];
-                }
-            }
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-                x2[ch] = x1[ch];
-                y2[ch] = y1[ch];
-                x1[ch] = x[ch];
-                y1[ch] = y[ch];
-            }
-            k2 = k1;
-            k1 = kc;
+        RowS S0, S1, S2;
+        Coef C0, C1, C2;
+        // window indices k = 0 .. kRowsB+3; slots: row k -> S[k%3], coefficient row
+        // k-1 -> C[(k-1)%3]
+        constexpr int kSteps = kRowsB + 4;
+        int k = 0;
+#pragma unroll 1
+        for (; k + 3 <= kSteps; k += 3) {
+            bwd_step<NS, SSIM_ON, MASK>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, dfull, ddacc, lane);
+            bwd_step<NS, SSIM_ON, MASK>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, dfull, ddacc, lane);
+            bwd_step<NS, SSIM_ON, MASK>(F, k + 2, S2, S1, S0, C1, C0, C2, dP, dfull, ddacc, lane);
         }
+        if (kSteps % 3 >= 1) bwd_step<NS, SSIM_ON, MASK>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, dfull, ddacc, lane);
+        if (kSteps % 3 >= 2) bwd_step<NS, SSIM_ON, MASK>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, dfull, ddacc, lane);
         // one 12-float partial of dL/dP per (item, frame)
         float* dst = a.dP_part[ls] + ((size_t)f * a.B * a.wpi + item_in_scale) * 12;
 #pragma unroll
@@ -810,8 +865,8 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
             if (lane == 0) dst[j] = t;
         }
     }
-    if (NS > 1 && colok) {
-        for (int i = 0; i < kRowsB && r0 + i < h; ++i) dfull[(r0 + i) * w + c] = ddacc[i][lane];
+    if (NS > 1 && F.colok) {
+        for (int i = 0; i < kRowsB && F.r0 + i < h; ++i) dfull[(F.r0 + i) * w + F.c] = ddacc[i][lane];
     }
 }
 
@@ -820,6 +875,7 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
 template <int NS, bool SSIM_ON, bool MASK>
 __global__ __launch_bounds__(kBlock, MD2_BWD_MINB) void photo_bwd_kernel(PhotoArgs a) {
     __shared__ float ddacc[kWavesPerBlock][kRowsB][kWave];   // dL/d(upsampled disp) summed over frames
+    __shared__ float dep[kWavesPerBlock][kRowsB + 4][kWave]; // depth of the item's window rows
     const int lane = threadIdx.x & (kWave - 1);
     // G groups of blocks (the 8 XCDs under round-robin dispatch; fewer for tiny grids)
     const int nb = gridDim.x, G = nb < 8 ? nb : 8, grp = blockIdx.x % G;
@@ -837,7 +893,7 @@ __global__ __launch_bounds__(kBlock, MD2_BWD_MINB) void photo_bwd_kernel(PhotoAr
         t /= a.strips;
         const int rb = t % a.rowblocks;
         const int b = t / a.rowblocks;
-        bwd_item<NS, SSIM_ON, MASK>(a, b, ls, st, rb, lane, ddacc[threadIdx.x >> 6]);
+        bwd_item<NS, SSIM_ON, MASK>(a, b, ls, st, rb, lane, ddacc[threadIdx.x >> 6], dep[threadIdx.x >> 6]);
     }
 }
 
