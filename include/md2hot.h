@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 10
+#define MD2_ABI_VERSION 11
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -139,11 +139,21 @@ int md2_generate_images(const md2_desc* desc, const md2_tensors* t,
                         float* const* color_out, void* stream);
 
 /*
+ * The tie-break noise the forward draws in-kernel when tensors.noise is NULL
+ * (trainer.py:468, unit normal before the 1e-5 scale), for scale s: writes
+ * (B, C, h_s, w_s) with C = S (or 1 with AVG_REPROJECTION) at the loss resolution.
+ * seed_ptr as in md2_tensors (nullable).  Lets tests hand the exact draw of a
+ * seeded forward to the CPU oracle.
+ */
+int md2_tiebreak_noise(const md2_desc* desc, const uint64_t* seed_ptr, int scale,
+                       float* out, void* stream);
+
+/*
  * Optional kernel timing for benchmarks: between md2_timing_begin and
- * md2_timing_end every launch of the two photometric kernels (the forward
- * photo kernel and the backward photo kernel, which dominate the hot path) is
- * launched with hipExtLaunchKernelGGL, which stamps a start/stop hipEvent pair on
- * the kernel dispatch itself (v1_multiscale's per-scale launches are not timed).
+ * md2_timing_end every launch of the photometric kernels (the forward's three
+ * launches — identity, reprojection, combine — as one interval, and the backward
+ * photo kernel; they dominate the hot path) is launched with hipExtLaunchKernelGGL,
+ * which stamps a start/stop hipEvent pair on the kernel dispatches themselves (v1_multiscale's per-scale launches are not timed).
  * md2_timing_end waits
  * for the last event and returns the summed durations (ms) and launch counts.
  * Not for use under graph capture (events are recorded eagerly).

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -54,7 +54,7 @@ _lock = threading.Lock()
 _lib = None
 
 EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_select_bytes",
-           "md2_photometric_fwd", "md2_photometric_bwd", "md2_generate_images",
+           "md2_photometric_fwd", "md2_photometric_bwd", "md2_generate_images", "md2_tiebreak_noise",
            "md2_timing_begin", "md2_timing_end", "md2_decoder_pad_fwd", "md2_decoder_pad_bwd",
            "md2_decoder_pad_workspace_bytes", "md2_adam_step", "md2_encoder_input",
            "md2_pose_fwd", "md2_pose_bwd", "md2_aug_plan_create", "md2_aug_plan_destroy", "md2_aug_run",
@@ -184,6 +184,8 @@ def _declare(L):
     L.md2_generate_images.restype = ctypes.c_int
     L.md2_generate_images.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(Tensors),
                                       ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp]
+    L.md2_tiebreak_noise.restype = ctypes.c_int
+    L.md2_tiebreak_noise.argtypes = [ctypes.POINTER(Desc), _vp, ctypes.c_int, _vp, _vp]
     L.md2_decoder_pad_fwd.restype = ctypes.c_int
     L.md2_decoder_pad_fwd.argtypes = [ctypes.POINTER(PadDesc), _vp, _vp, _vp, _vp, _vp]
     L.md2_decoder_pad_bwd.restype = ctypes.c_int

@@ -44,22 +44,14 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kFwdCols = kWave - 2;  // output columns per forward strip
 constexpr int kBwdCols = kWave - 4;  // output columns per backward strip
-#ifndef MD2_ROWS_F
-#define MD2_ROWS_F 4
-#endif
 #ifndef MD2_ROWS_B
 #define MD2_ROWS_B 16
 #endif
-// minimum resident 256-thread blocks per CU (__launch_bounds__): 2 = 2 waves/SIMD
-// (<= 256 VGPRs), 3 = 3 waves/SIMD (<= 168).  The forward's gathers hide better at 3
-// (0.263 -> 0.248 ms, 12 B/lane of spills); the backward spills 164 B/lane at 3.
-#ifndef MD2_FWD_MINB
-#define MD2_FWD_MINB 3
-#endif
+// minimum resident 256-thread blocks per CU (__launch_bounds__) of the backward:
+// 2 = 2 waves/SIMD (<= 256 VGPRs); it spills 164 B/lane at 3 (<= 168).
 #ifndef MD2_BWD_MINB
 #define MD2_BWD_MINB 2
 #endif
-constexpr int kRowsF = MD2_ROWS_F;   // output rows per forward work item
 constexpr int kRowsB = MD2_ROWS_B;   // output rows per backward work item
 constexpr int kSmoothChunk = 2048;   // pixels per smoothness partial
 constexpr float kC1 = 0.0001f;       // 0.01 ** 2   layers.py:231
@@ -128,21 +120,32 @@ __device__ __forceinline__ float div3(float x) {
 
 __device__ __forceinline__ float signf(float v) { return (v > 0.f) ? 1.f : ((v < 0.f) ? -1.f : 0.f); }
 
-// counter-based normal deviate for the tie-break noise (trainer.py:468)
-__device__ __forceinline__ uint32_t mix64to32(uint64_t x) {
-    x ^= x >> 33;
-    x *= 0xff51afd7ed558ccdULL;
-    x ^= x >> 33;
-    x *= 0xc4ceb9fe1a85ec53ULL;
-    x ^= x >> 33;
-    return (uint32_t)x;
+// Tie-break noise of the forward (trainer.py:468 draws N(0,1) * 1e-5 per
+// (image, candidate, pixel) and scale): one 32-bit counter hash per (scale, image
+// pixel, candidate pair) -> two uniforms -> a Box-Muller pair, i.e. two deviates per
+// hash, log and sqrt.  Deterministic in (seed, scale, pixel); the draw itself cannot
+// match torch.randn, so parity tests pass the noise in explicitly.
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
 }
-__device__ __forceinline__ float hash_normal(uint64_t seed, uint64_t idx) {
-    const uint64_t h = seed * 0x9E3779B97F4A7C15ULL + idx * 0xD1B54A32D192ED03ULL;
-    const uint32_t a = mix64to32(h), c = mix64to32(h ^ 0x5851F42D4C957F2DULL);
-    const float u1 = (float)(a >> 8) * (1.0f / 16777216.0f) + (0.5f / 16777216.0f);
-    const float u2 = (float)(c >> 8) * (1.0f / 16777216.0f);
-    return sqrtf(-2.0f * __logf(u1)) * __cosf(6.28318530718f * u2);
+__device__ __forceinline__ uint32_t noise_key(uint64_t seed, int gsc) {
+    return lowbias32((uint32_t)seed ^ lowbias32((uint32_t)(seed >> 32) + 0x9E3779B9u * (uint32_t)(gsc + 1)));
+}
+// candidates 2j and 2j+1 of pixel q (= b*HW + p) at the scale keyed by `key`
+__device__ __forceinline__ float2 noise_pair(uint32_t key, uint32_t q, int j) {
+    const uint32_t h1 = lowbias32(q * 0x9E3779B1u + key + (uint32_t)j * 0x85EBCA77u);
+    const uint32_t h2 = lowbias32(h1 ^ 0x68E31DA4u);
+    const float u1 = (float)(h1 >> 8) * (1.0f / 16777216.0f) + (0.5f / 16777216.0f);
+    const float u2 = (float)(h2 >> 8) * (1.0f / 16777216.0f);
+    const float r = sqrtf(-2.0f * __logf(u1));
+    float sn, cs;
+    __sincosf(6.28318530718f * u2, &sn, &cs);
+    return make_float2(r * cs, r * sn);
 }
 
 // ----------------------------------------------------------------------------
@@ -414,6 +417,11 @@ struct PhotoArgs {
     // predictive mask (MD2_PREDICTIVE_MASK): per local scale (B,S,h,w)
     const float* mask[MD2_MAX_SCALES];
     float* gmask[MD2_MAX_SCALES];
+    // split forward: identity losses [S][B][h][w], reprojection losses per local scale
+    // [S][B][h][w], combine blocks per image
+    float* ident;
+    float* rep[MD2_MAX_SCALES];
+    int cblk;
 };
 
 __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int b, WarpCtx& c) {
@@ -433,179 +441,243 @@ __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int 
 }
 
 // ----------------------------------------------------------------------------
-// forward: one pass of reprojection losses for kRowsF output rows of one strip.
-// `emit(i, v)` receives the loss of output row r0+i at this lane's column; the
-// row loop stays rolled (the per-row state lives in LDS, see photo_fwd_kernel).
+// Forward: three launches (instead of one wave doing every (scale, frame) of a
+// 4-row item, the round-1 design).
+//   photo_ident_kernel   identity losses of every source frame, once per step
+//                        (scale-invariant, trainer.py:432-439)
+//   photo_reproj_kernel  one wave per (image, 16-row block, strip, scale, frame):
+//                        warp + SSIM/L1 per pixel -> loss plane (trainer.py:426-430)
+//   photo_combine_kernel per pixel: identity + noise vs reprojection candidates,
+//                        first-index argmin (trainer.py:466-482), automask code,
+//                        fixed-order block partial sums of the per-pixel minimum
+// A 16-row item evaluates 18 rows (1.125x) where the fused 4-row item evaluated 6
+// (1.5x), and the identity pass is no longer repeated per item; the loss planes
+// (8 x 5.9 MB at B=12) stay L2/Infinity-cache resident between the launches.
 // ----------------------------------------------------------------------------
-template <bool SSIM_ON, bool WARPED, class Emit>
-__device__ __forceinline__ void reproj_rows(const WarpCtx& c, const float (*trow)[kWave], const float (*dep)[kWave],
-                                            int r0, int cc, int lane, Emit emit) {
-    // trow: the target rows r0-1 .. r0+kRowsF (reflected), [row * 3 + channel][lane],
-    // staged once per wave in LDS (photo_fwd_kernel) instead of re-read from HBM by
-    // every (scale, frame) pass
-    const int h = c.h, w = c.w, HW = h * w;
-    if (!SSIM_ON) {
-        for (int i = 0; i < kRowsF; ++i) {
-            const int rr = reflect_clamp(r0 + i, h);
-            float x[3];
-            if (WARPED) {
-                warp_value(c, rr, cc, dep[i + 1][lane], x);
-            } else {
+constexpr int kRowsP = 16;   // output rows per item of the split forward passes
+
+// one evaluated window row of the forward walk
+struct FRow {
+    H5 h[3];
+    float x[3], y[3];
+};
+
+template <bool SSIM_ON, bool WARPED>
+__device__ __forceinline__ void frow_eval(const WarpCtx& c, const float* tgt, const float (*dep)[kWave], int k,
+                                          int rr, int cc, int lane, FRow& o) {
+    const int HW = c.h * c.w;
+    if (WARPED) {
+        warp_value(c, rr, cc, dep[k][lane], o.x);
+    } else {
 #pragma unroll
-                for (int ch = 0; ch < 3; ++ch) x[ch] = ldf(c.src, ch * HW + rr * w + cc);
-            }
-            float l1 = 0.f;
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) l1 += fabsf(trow[(i + 1) * 3 + ch][lane] - x[ch]);
-            emit(i, div3(l1));
-        }
-        return;
+        for (int ch = 0; ch < 3; ++ch) o.x[ch] = ldf(c.src, ch * HW + rr * c.w + cc);
     }
-    H5 hA[3], hB[3];
-    float xB[3], yB[3];
-    for (int k = 0; k < kRowsF + 2; ++k) {
-        const int rr = reflect_clamp(r0 - 1 + k, h);
-        float x[3], y[3];
-        if (WARPED) {
-            warp_value(c, rr, cc, dep[k][lane], x);
-        } else {
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) x[ch] = ldf(c.src, ch * HW + rr * w + cc);
-        }
+    for (int ch = 0; ch < 3; ++ch) o.y[ch] = ldf(tgt, ch * HW + rr * c.w + cc);
+    if (SSIM_ON) {
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) y[ch] = trow[k * 3 + ch][lane];
-        H5 hc[3];
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) hc[ch] = hsum(x[ch], y[ch]);
-        if (k >= 2) {
-            float ss = 0.f, l1 = 0.f;
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-                ss += ssim_from_sums(hA[ch], hB[ch], hc[ch]);
-                l1 += fabsf(yB[ch] - xB[ch]);
-            }
-            emit(k - 2, 0.85f * div3(ss) + 0.15f * div3(l1));
-        }
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) {
-            hA[ch] = hB[ch];
-            hB[ch] = hc[ch];
-            xB[ch] = x[ch];
-            yB[ch] = y[ch];
-        }
+        for (int ch = 0; ch < 3; ++ch) o.h[ch] = hsum(o.x[ch], o.y[ch]);
     }
 }
 
-// per-wave LDS state, lane-major so every access is one conflict-free ds op
-template <int NS>
-struct FwdState {
-    float tgt[(kRowsF + 2) * 3][kWave];   // target rows r0-1 .. r0+kRowsF, 3 channels
-    float dep[kRowsF + 2][kWave];         // depth of rows r0-1 .. r0+kRowsF at the current scale
-    float ident[NS][kRowsF][kWave];
-    float best[kRowsF][kWave];
-    float accum[kRowsF][kWave];
-    int code[kRowsF][kWave];
+// loss of the middle row of (a, b, c) at this lane (trainer.py:393-405)
+template <bool SSIM_ON>
+__device__ __forceinline__ float frow_loss(const FRow& a, const FRow& b, const FRow& c) {
+    float ss = 0.f, l1 = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        if (SSIM_ON) ss += ssim_from_sums(a.h[ch], b.h[ch], c.h[ch]);
+        l1 += fabsf(b.y[ch] - b.x[ch]);
+    }
+    return SSIM_ON ? 0.85f * div3(ss) + 0.15f * div3(l1) : div3(l1);
+}
+
+// Losses of output rows r0 .. r0+kRowsP-1 at this lane's column; emit(i, v) per row.
+// The 3-row window rotates through three statically named slots (unrolled by 3).
+template <bool SSIM_ON, bool WARPED, class Emit>
+__device__ __forceinline__ void loss_rows(const WarpCtx& c, const float* tgt, const float (*dep)[kWave], int r0,
+                                          int cc, int lane, Emit emit) {
+    const int h = c.h;
+    FRow R0, R1, R2;
+    // window row k = 0 .. kRowsP+1 is image row r0 - 1 + k; output row i = k - 2 + ... :
+    // after evaluating row k (k >= 2) the rows k-2, k-1, k give output row k-2
+    static_assert((kRowsP + 2) % 3 == 0, "window rows must be a multiple of 3");
+#pragma unroll 1
+    for (int k = 0; k < kRowsP + 2; k += 3) {
+        frow_eval<SSIM_ON, WARPED>(c, tgt, dep, k, reflect_clamp(r0 - 1 + k, h), cc, lane, R0);
+        if (k >= 2) emit(k - 2, frow_loss<SSIM_ON>(R1, R2, R0));
+        frow_eval<SSIM_ON, WARPED>(c, tgt, dep, k + 1, reflect_clamp(r0 + k, h), cc, lane, R1);
+        if (k >= 1) emit(k - 1, frow_loss<SSIM_ON>(R2, R0, R1));
+        frow_eval<SSIM_ON, WARPED>(c, tgt, dep, k + 2, reflect_clamp(r0 + 1 + k, h), cc, lane, R2);
+        emit(k, frow_loss<SSIM_ON>(R0, R1, R2));
+    }
+}
+
+// item geometry of the split forward: 62-column strips with one halo lane per side
+struct FItem {
+    int b, rb, st, r0, c, cc;
+    bool colok;
 };
 
-template <int NS, bool SSIM_ON, bool MASK>
-__global__ __launch_bounds__(kBlock, MD2_FWD_MINB) void photo_fwd_kernel(PhotoArgs a) {
-    __shared__ FwdState<NS> lds[kWavesPerBlock];
+__device__ __forceinline__ FItem fitem(const PhotoArgs& a, int t, int lane) {
+    FItem it;
+    it.st = t % a.strips;
+    t /= a.strips;
+    it.rb = t % a.rowblocks;
+    it.b = t / a.rowblocks;
+    it.r0 = it.rb * kRowsP;
+    it.c = it.st * kFwdCols - 1 + lane;
+    it.cc = reflect_clamp(it.c, a.w);
+    it.colok = lane >= 1 && lane <= kFwdCols && it.c < a.w;
+    return it;
+}
+
+template <int NS, bool SSIM_ON>
+__global__ __launch_bounds__(kBlock) void photo_ident_kernel(PhotoArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
-    FwdState<NS>& L = lds[threadIdx.x >> 6];
     const int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
     const int wv = __builtin_amdgcn_readfirstlane(blk * kWavesPerBlock + (threadIdx.x >> 6));
-    if (wv >= a.B * a.wpi) return;
-    const int b = wv / a.wpi, rem = wv - b * a.wpi;
-    const int rb = rem / a.strips, st = rem - rb * a.strips;
-    const int r0 = rb * kRowsF;
-    const uint64_t seed = a.seed_ptr ? (a.seed ^ (*a.seed_ptr * 0x9E3779B97F4A7C15ULL)) : a.seed;
+    if (wv >= a.B * a.wpi * NS) return;
+    const int f = wv % NS;
+    const FItem it = fitem(a, wv / NS, lane);
     const int h = a.h, w = a.w, HW = h * w;
-    const int c = st * kFwdCols - 1 + lane;
-    const int cc = reflect_clamp(c, w);
-    const bool colok = lane >= 1 && lane <= kFwdCols && c < w;
-    const float* tgt = a.tgt + (size_t)b * 3 * HW;
+    WarpCtx ctx;
+    ctx.src = a.src[f] + (size_t)it.b * 3 * HW;
+    ctx.h = h;
+    ctx.w = w;
+    float* out = a.ident + ((size_t)f * a.B + it.b) * HW;
+    loss_rows<SSIM_ON, false>(ctx, a.tgt + (size_t)it.b * 3 * HW, nullptr, it.r0, it.cc, lane, [&](int i, float v) {
+        const int r = it.r0 + i;
+        if (it.colok && r < h) out[r * w + it.c] = v;
+    });
+}
+
+template <int NS, bool SSIM_ON, bool MASK>
+__global__ __launch_bounds__(kBlock) void photo_reproj_kernel(PhotoArgs a) {
+    __shared__ float dep_all[kWavesPerBlock][kRowsP + 2][kWave];
+    const int lane = threadIdx.x & (kWave - 1);
+    float (*dep)[kWave] = dep_all[threadIdx.x >> 6];
+    const int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int wv = __builtin_amdgcn_readfirstlane(blk * kWavesPerBlock + (threadIdx.x >> 6));
+    if (wv >= a.B * a.wpi * a.nsc * NS) return;
+    // item order: frame fastest, then scale, so the waves sharing a strip's target and
+    // source rows run together on one XCD
+    const int f = wv % NS, ls = (wv / NS) % a.nsc;
+    const FItem it = fitem(a, wv / (NS * a.nsc), lane);
+    const int h = a.h, w = a.w, HW = h * w;
+    WarpCtx ctx;
+    make_ctx(a, ls, f, it.b, ctx);
+#pragma unroll
+    for (int k = 0; k < kRowsP + 2; ++k) dep[k][lane] = depth_at(ctx, reflect_clamp(it.r0 - 1 + k, h), it.cc);
+    float* out = a.rep[ls] + ((size_t)f * a.B + it.b) * HW;
+    const float* pmask = MASK ? a.mask[ls] + ((size_t)it.b * NS + f) * HW : nullptr;
+    loss_rows<SSIM_ON, true>(ctx, a.tgt + (size_t)it.b * 3 * HW, dep, it.r0, it.cc, lane, [&](int i, float v) {
+        const int r = it.r0 + i;
+        if (it.colok && r < h) {
+            if (MASK) v *= pmask[r * w + it.c];  // trainer.py:455
+            out[r * w + it.c] = v;
+        }
+    });
+}
+
+// Four consecutive pixels of one image per thread, every local scale (the identity
+// losses are read once for all scales); blocks cover kCombinePix pixels of an image.
+// Candidate order and tie rule as torch.min over cat(identity + noise, reprojection)
+// (first index wins, trainer.py:471-482).  One partial sum of the per-pixel minimum
+// per (scale, block), folded in a fixed order (deterministic).
+constexpr int kCombinePix = 4 * kBlock;
+
+template <int NS>
+__global__ __launch_bounds__(kBlock) void photo_combine_kernel(PhotoArgs a) {
+    __shared__ float red[MD2_MAX_SCALES][kWavesPerBlock];
+    const int b = blockIdx.x / a.cblk, cb = blockIdx.x - b * a.cblk;
+    const int HW = a.h * a.w;
+    const int p0 = cb * kCombinePix + 4 * threadIdx.x;
     const bool automask = !(a.flags & MD2_NO_AUTOMASK);
     const bool avg = (a.flags & MD2_AVG_REPROJECTION) != 0;
     const int C = avg ? 1 : NS;
-
-    for (int k = 0; k < kRowsF + 2; ++k) {
-        const int rr = reflect_clamp(r0 - 1 + k, h);
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) L.tgt[k * 3 + ch][lane] = ldf(tgt, ch * HW + rr * w + cc);
-    }
-
-    // identity reprojection losses (trainer.py:432-439); scale-invariant here
+    const uint64_t seed = a.seed_ptr ? (a.seed ^ (*a.seed_ptr * 0x9E3779B97F4A7C15ULL)) : a.seed;
+    const bool vec = (HW & 3) == 0 && p0 + 3 < HW;
+    const int npx = p0 >= HW ? 0 : min(4, HW - p0);
+    float id[NS][4];
     if (automask) {
+#pragma unroll
         for (int f = 0; f < NS; ++f) {
-            WarpCtx ctx;
-            ctx.src = a.src[f] + (size_t)b * 3 * HW;
-            ctx.h = h;
-            ctx.w = w;
-            reproj_rows<SSIM_ON, false>(ctx, L.tgt, L.dep, r0, cc, lane,
-                                        [&](int i, float v) { L.ident[f][i][lane] = v; });
+            const float* src = a.ident + ((size_t)f * a.B + b) * HW;
+            if (vec) {
+                const float4 v = *(const float4*)(src + p0);
+                id[f][0] = v.x, id[f][1] = v.y, id[f][2] = v.z, id[f][3] = v.w;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) id[f][i] = i < npx ? src[p0 + i] : 0.f;
+            }
         }
     }
-
     for (int ls = 0; ls < a.nsc; ++ls) {
-        const int gsc = a.gscale[ls];
+        float rp[NS][4];
+#pragma unroll
+        for (int f = 0; f < NS; ++f) {
+            const float* src = a.rep[ls] + ((size_t)f * a.B + b) * HW;
+            if (vec) {
+                const float4 v = *(const float4*)(src + p0);
+                rp[f][0] = v.x, rp[f][1] = v.y, rp[f][2] = v.z, rp[f][3] = v.w;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) rp[f][i] = i < npx ? src[p0 + i] : 0.f;
+            }
+        }
         const float* nz = a.noise[ls];
-        for (int i = 0; i < kRowsF; ++i) {
+        const uint32_t key = noise_key(seed, a.gscale[ls]);
+        float lsum = 0.f;
+        uint32_t codes = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int p = p0 + i;
             float best = INFINITY;
             int code = 0;
             if (automask) {
-                const int r = min(r0 + i, h - 1);
+                float nv[NS];
+                if (nz) {
+#pragma unroll
+                    for (int ch = 0; ch < NS; ++ch) nv[ch] = ch < C && i < npx ? nz[((size_t)b * C + ch) * HW + p] : 0.f;
+                } else {
+#pragma unroll
+                    for (int j = 0; 2 * j < NS; ++j) {
+                        const float2 n2 = noise_pair(key, (uint32_t)(b * HW + p), j);
+                        nv[2 * j] = n2.x;
+                        if (2 * j + 1 < NS) nv[2 * j + 1] = n2.y;
+                    }
+                }
                 for (int ch = 0; ch < C; ++ch) {
                     float v;
                     if (avg) {
                         v = 0.f;
-                        for (int f = 0; f < NS; ++f) v += L.ident[f][i][lane];
+#pragma unroll
+                        for (int f = 0; f < NS; ++f) v += id[f][i];
                         v = v / (float)NS;
                     } else {
-                        v = L.ident[ch][i][lane];
+                        v = id[ch][i];
                     }
-                    const size_t nidx = (((size_t)b * C + ch) * h + r) * w + cc;
-                    const float n = nz ? nz[nidx]
-                                       : hash_normal(seed, ((uint64_t)gsc << 56) ^ (uint64_t)nidx);
-                    v = v + n * 1e-5f;
+                    v = v + nv[ch] * 1e-5f;
                     if (v < best) {
                         best = v;
                         code = ch;
                     }
                 }
             }
-            L.best[i][lane] = best;
-            L.code[i][lane] = code;
-            L.accum[i][lane] = 0.f;
-        }
-        const float* pmask = MASK ? a.mask[ls] : nullptr;
-        {
-            // the rows' depths once per scale (every frame warps the same upsampled disparity)
-            WarpCtx ctx;
-            make_ctx(a, ls, 0, b, ctx);
+            float accum = 0.f;
 #pragma unroll
-            for (int k = 0; k < kRowsF + 2; ++k) L.dep[k][lane] = depth_at(ctx, reflect_clamp(r0 - 1 + k, h), cc);
-        }
-        for (int f = 0; f < NS; ++f) {
-            WarpCtx ctx;
-            make_ctx(a, ls, f, b, ctx);
-            const int cand = (automask ? NS : 0) + f;
-            reproj_rows<SSIM_ON, true>(ctx, L.tgt, L.dep, r0, cc, lane, [&](int i, float v) {
-                if (MASK) v *= pmask[(((size_t)b * NS + f) * h + min(r0 + i, h - 1)) * w + cc];  // trainer.py:455
+            for (int f = 0; f < NS; ++f) {
+                const float v = rp[f][i];
                 if (avg) {
-                    L.accum[i][lane] += v;
-                } else if (v < L.best[i][lane]) {
-                    L.best[i][lane] = v;
-                    L.code[i][lane] = cand;
+                    accum += v;
+                } else if (v < best) {
+                    best = v;
+                    code = (automask ? NS : 0) + f;
                 }
-            });
-        }
-        float lsum = 0.f;
-        uint8_t* sel = a.sel[ls] + (size_t)b * HW;
-        for (int i = 0; i < kRowsF; ++i) {
-            float best = L.best[i][lane];
-            int code = L.code[i][lane];
+            }
             if (avg) {
-                const float ra = L.accum[i][lane] / (float)NS;
+                const float ra = accum / (float)NS;
                 if (automask) {
                     if (ra < best) {
                         best = ra;
@@ -615,14 +687,22 @@ __global__ __launch_bounds__(kBlock, MD2_FWD_MINB) void photo_fwd_kernel(PhotoAr
                     best = ra;
                 }
             }
-            const int r = r0 + i;
-            if (colok && r < h) {
-                lsum += best;
-                sel[r * w + c] = (uint8_t)code;
-            }
+            if (i < npx) lsum += best;
+            codes |= (uint32_t)code << (8 * i);
         }
-        lsum = wave_sum(lsum);
-        if (lane == 0) a.photo_part[ls][wv] = lsum;
+        uint8_t* sel = a.sel[ls] + (size_t)b * HW;
+        if (vec) {
+            *(uint32_t*)(sel + p0) = codes;
+        } else {
+            for (int i = 0; i < npx; ++i) sel[p0 + i] = (uint8_t)(codes >> (8 * i));
+        }
+        const float t = wave_sum(lsum);
+        if ((threadIdx.x & 63) == 0) red[ls][threadIdx.x >> 6] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < a.nsc) {
+        const int ls = threadIdx.x;
+        a.photo_part[ls][(size_t)b * a.cblk + cb] = ((red[ls][0] + red[ls][1]) + red[ls][2]) + red[ls][3];
     }
 }
 
@@ -1250,6 +1330,27 @@ __global__ __launch_bounds__(kBlock) void generate_kernel(GenArgs g) {
 // ----------------------------------------------------------------------------
 thread_local char g_err[512] = "";
 
+// md2_tiebreak_noise: the combine kernel's in-kernel draw, one thread per pixel
+struct NoiseArgs {
+    int B, HW, C, gsc;
+    uint64_t seed;
+    const uint64_t* seed_ptr;
+    float* out;
+};
+
+__global__ __launch_bounds__(kBlock) void tiebreak_noise_kernel(NoiseArgs a) {
+    const int idx = blockIdx.x * kBlock + threadIdx.x;
+    if (idx >= a.B * a.HW) return;
+    const int b = idx / a.HW, p = idx - b * a.HW;
+    const uint64_t seed = a.seed_ptr ? (a.seed ^ (*a.seed_ptr * 0x9E3779B97F4A7C15ULL)) : a.seed;
+    const uint32_t key = noise_key(seed, a.gsc);
+    for (int j = 0; 2 * j < a.C; ++j) {
+        const float2 n2 = noise_pair(key, (uint32_t)idx, j);
+        a.out[((size_t)b * a.C + 2 * j) * a.HW + p] = n2.x;
+        if (2 * j + 1 < a.C) a.out[((size_t)b * a.C + 2 * j + 1) * a.HW + p] = n2.y;
+    }
+}
+
 // optional benchmark timing of the photometric kernels (md2_timing_begin/end)
 struct Timing {
     std::mutex mu;
@@ -1289,6 +1390,8 @@ struct Layout {
     int fstrips[MD2_MAX_SCALES], frows[MD2_MAX_SCALES], fwpi[MD2_MAX_SCALES];
     int bstrips[MD2_MAX_SCALES], brows[MD2_MAX_SCALES], bwpi[MD2_MAX_SCALES];
     int chunks[MD2_MAX_SCALES];
+    int cblk[MD2_MAX_SCALES];                        // combine blocks per image (split forward)
+    size_t rep_off[MD2_MAX_SCALES], ident_off;
     size_t photo_off[MD2_MAX_SCALES], dP_off[MD2_MAX_SCALES], smooth_off[MD2_MAX_SCALES];
     size_t dfull_off[MD2_MAX_SCALES], stats_off, total;
     size_t sel_off[MD2_MAX_SCALES], sel_total;
@@ -1325,14 +1428,17 @@ int make_layout(const md2_desc* d, Layout& L) {
         L.lh[s] = L.v1 ? L.hs[s] : d->height;
         L.lw[s] = L.v1 ? L.ws[s] : d->width;
         L.fstrips[s] = (L.lw[s] + kFwdCols - 1) / kFwdCols;
-        L.frows[s] = (L.lh[s] + kRowsF - 1) / kRowsF;
+        L.frows[s] = (L.lh[s] + kRowsP - 1) / kRowsP;
         L.fwpi[s] = L.fstrips[s] * L.frows[s];
+        L.cblk[s] = (L.lh[s] * L.lw[s] + kCombinePix - 1) / kCombinePix;
         L.bstrips[s] = (L.lw[s] + kBwdCols - 1) / kBwdCols;
         L.brows[s] = (L.lh[s] + kRowsB - 1) / kRowsB;
         L.bwpi[s] = L.bstrips[s] * L.brows[s];
         L.chunks[s] = (L.hs[s] * L.ws[s] + kSmoothChunk - 1) / kSmoothChunk;
         L.photo_off[s] = off;
-        off = align256(off + sizeof(float) * (size_t)L.B * L.fwpi[s]);
+        off = align256(off + sizeof(float) * (size_t)L.B * L.cblk[s]);
+        L.rep_off[s] = off;
+        off = align256(off + sizeof(float) * (size_t)L.S * L.B * L.lh[s] * L.lw[s]);
         L.dP_off[s] = off;
         off = align256(off + sizeof(float) * (size_t)L.S * L.B * L.bwpi[s] * 12);
         L.smooth_off[s] = off;
@@ -1346,6 +1452,8 @@ int make_layout(const md2_desc* d, Layout& L) {
         L.mask_off[s] = moff;
         moff += (size_t)L.B * L.S * L.lh[s] * L.lw[s];
     }
+    L.ident_off = off;   // identity losses of one scale group (the largest: scale 0)
+    off = align256(off + sizeof(float) * (size_t)L.S * L.B * L.lh[0] * L.lw[0]);
     L.stats_off = off;
     off = align256(off + sizeof(float) * (size_t)L.nscales * L.B * 4);
     L.total = off;
@@ -1418,17 +1526,24 @@ void photo_args(const md2_desc* d, const md2_tensors* t, const Layout& L, int s_
         a.dP_part[ls] = (float*)(ws + L.dP_off[s]);
         a.mask[ls] = t->mask ? t->mask + L.mask_off[s] : nullptr;
         a.gmask[ls] = grad_mask ? grad_mask + L.mask_off[s] : nullptr;
+        a.rep[ls] = ws ? (float*)(ws + L.rep_off[s]) : nullptr;
     }
+    a.ident = ws ? (float*)(ws + L.ident_off) : nullptr;
+    a.cblk = L.cblk[s_begin];
 }
 
 template <int NS, bool SSIM, bool MASK>
 void launch_fwd_t(const PhotoArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-    const int waves = a.B * a.wpi;
-    const int blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (e0)
-        hipExtLaunchKernelGGL((photo_fwd_kernel<NS, SSIM, MASK>), dim3(blocks), dim3(kBlock), 0, st, e0, e1, 0, a);
-    else
-        hipLaunchKernelGGL((photo_fwd_kernel<NS, SSIM, MASK>), dim3(blocks), dim3(kBlock), 0, st, a);
+    // the timing events bracket the three launches (start on the first, stop on the last)
+    const bool automask = !(a.flags & MD2_NO_AUTOMASK);
+    if (automask) {
+        const int blocks = (a.B * a.wpi * NS + kWavesPerBlock - 1) / kWavesPerBlock;
+        hipExtLaunchKernelGGL((photo_ident_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, e0, nullptr, 0, a);
+    }
+    const int rblocks = (a.B * a.wpi * a.nsc * NS + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipExtLaunchKernelGGL((photo_reproj_kernel<NS, SSIM, MASK>), dim3(rblocks), dim3(kBlock), 0, st,
+                          automask ? nullptr : e0, nullptr, 0, a);
+    hipExtLaunchKernelGGL((photo_combine_kernel<NS>), dim3(a.B * a.cblk), dim3(kBlock), 0, st, nullptr, e1, 0, a);
 }
 // number of workgroups that can be resident at once for a kernel (cached per
 // kernel and device); the persistent-loop kernels launch exactly that many
@@ -1533,7 +1648,7 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
         photo_args(d, t, L, 0, L.nscales, false, ws, select_out, a);
         launch_photo(a, false, st, e0, e1);
     }
-    if ((rc = hip_check("photo_fwd_kernel"))) return rc;
+    if ((rc = hip_check("photo forward kernels"))) return rc;
 
     SmoothArgs sa;
     memset(&sa, 0, sizeof(sa));
@@ -1564,7 +1679,7 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
         fa.hs[s] = L.hs[s];
         fa.ws[s] = L.ws[s];
         fa.chunks[s] = L.chunks[s];
-        fa.nphoto[s] = L.B * L.fwpi[s];
+        fa.nphoto[s] = L.B * L.cblk[s];
         fa.photo_part[s] = (const float*)(ws + L.photo_off[s]);
         fa.smooth_part[s] = (const float*)(ws + L.smooth_off[s]);
     }
@@ -1670,6 +1785,25 @@ int md2_generate_images(const md2_desc* d, const md2_tensors* t, float* const* d
         hipLaunchKernelGGL(generate_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, g);
     }
     return hip_check("generate_kernel");
+}
+
+int md2_tiebreak_noise(const md2_desc* d, const uint64_t* seed_ptr, int scale, float* out, void* stream) {
+    Layout L;
+    int rc = make_layout(d, L);
+    if (rc) return rc;
+    if (scale < 0 || scale >= L.nscales) return fail(MD2_ERR_ARG, "scale %d out of range", scale);
+    if (!out) return fail(MD2_ERR_ARG, "out is NULL");
+    NoiseArgs na;
+    na.B = L.B;
+    na.HW = L.lh[scale] * L.lw[scale];
+    na.C = (d->flags & MD2_AVG_REPROJECTION) ? 1 : L.S;
+    na.gsc = scale;
+    na.seed = d->seed;
+    na.seed_ptr = seed_ptr;
+    na.out = out;
+    const int n = na.B * na.HW;
+    hipLaunchKernelGGL(tiebreak_noise_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, (hipStream_t)stream, na);
+    return hip_check("tiebreak_noise_kernel");
 }
 
 int md2_timing_begin(int max_launches) {

@@ -292,3 +292,21 @@ def generate_images(cfg: HotPathConfig, disps, colors, K, inv_K, T, want_depth=T
     _lib.check(L.md2_generate_images(ctypes.byref(desc), ctypes.byref(st), dptr, sptr, cptr, _stream_ptr(dev)),
                "md2_generate_images")
     return {"depth": depth, "sample": sample, "color": color}
+
+
+def tiebreak_noise(cfg: HotPathConfig, seed: int = 0, seed_tensor: Optional[torch.Tensor] = None,
+                   device="cuda") -> Dict[int, torch.Tensor]:
+    """The unit-normal tie-break noise a forward with noise=None draws in-kernel
+    (trainer.py:468), {scale: (B,C,h,w)} — what `photometric_loss(..., seed=seed,
+    seed_tensor=seed_tensor)` adds (x 1e-5) to the identity losses."""
+    L = _lib.lib()
+    dev = torch.device(device)
+    desc = cfg.desc(seed)
+    C = 1 if cfg.avg_reprojection else cfg.num_src
+    out = {}
+    for s in range(cfg.num_scales):
+        h, w = cfg.loss_res(s)
+        out[s] = torch.empty(cfg.batch, C, h, w, device=dev)
+        _lib.check(L.md2_tiebreak_noise(ctypes.byref(desc), seed_tensor.data_ptr() if seed_tensor is not None else None,
+                                        s, out[s].data_ptr(), _stream_ptr(dev)), "md2_tiebreak_noise")
+    return out
