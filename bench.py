@@ -181,7 +181,7 @@ def cpu_baseline(args):
     pdec = networks.PoseDecoder(penc.num_ch_enc, 1, 2)
     params = [p for m in (enc, dec, penc, pdec) for p in m.parameters()]
     adam = optim.Adam(params, 1e-4)
-    inputs = synthetic_batch(B, H, W, frame_ids, 4, seed=5)
+    inputs = synthetic_batch(B, H, W, frame_ids, 4, seed=5, eight_bit=True)
     opt = HotPathOptions(height=H, width=W, frame_ids=frame_ids)
 
     def step():
@@ -241,7 +241,10 @@ def main():
 
     trainer = make_trainer(args, device, rank, world)
     frame_ids = trainer.opt.frame_ids
-    batch = synthetic_batch(args.batch, args.height, args.width, frame_ids, 4, seed=100 + rank, device=device)
+    # colours as the reference's loader delivers them: uint8 frames through to_tensor,
+    # i.e. exactly k/255 (datasets/mono_dataset.py:199-200)
+    batch = synthetic_batch(args.batch, args.height, args.width, frame_ids, 4, seed=100 + rank, device=device,
+                            eight_bit=True)
     next_batch = lambda: batch   # noqa: E731
     if args.gpu_augment:
         next_batch = make_augmenting_source(args, frame_ids, device, rank)
@@ -334,7 +337,7 @@ def main():
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                 "dtype": "f32" if args.amp == "none" else "bf16 networks (autocast) + f32 photometric loss",
-                "data": "synthetic (KITTI-shaped smooth textures, random-init weights)",
+                "data": "synthetic (KITTI-shaped smooth textures as 8-bit k/255 colours like the loader's to_tensor output, random-init weights)",
                 "config": {"workload": f"{'mono+stereo' if args.stereo else 'mono'}_{W}x{H} ResNet-{args.num_layers}"
                                        f" batch={B}/GPU full train step"
                                        + (" (configs[1])" if (not args.stereo and (W, H) == (640, 192)

@@ -174,6 +174,7 @@ struct WarpCtx {
     const float* disp;  // (dh, dw) disparity of this image at its native scale
     int dh, dw, upsh;   // upsample factor 2^upsh to the loss resolution
     const float* src;   // (3, h, w) source colours at the loss resolution
+    const uint32_t* src8;  // the same colours as 8-bit RGBx per pixel (k/255 exact), or null
     int h, w;
     float sx, sy;       // W/(W-1), H/(H-1): pixel -> grid_sample source coordinate
     float min_disp, range;
@@ -305,13 +306,36 @@ struct Corners {
 // per row and channel: 6 gather instructions per sample instead of 12, the same
 // bytes.  At the right border (x0 = w-1, where ne is masked) the pair starts one
 // column to the left.
-template <class SampleT>
+//
+// 8-bit sources (src8): colours that are exactly k/255 — what to_tensor makes of the
+// decoded frames (datasets/mono_dataset.py:199-200, the GPU input pipeline likewise) —
+// are gathered from one RGBx dword per pixel: 2 gather instructions per sample
+// instead of 6, a third of the texture-path work, which binds these kernels when
+// the warp scatters (tools/gather_model.hip).  The corners come back as k; interp and
+// the bilinear slopes scale by cs = 1/255 once per channel (differences O(1 ulp)).
+typedef uint32_t uint2_a4 __attribute__((ext_vector_type(2), aligned(4)));
+
+template <bool U8, class SampleT>
 __device__ __forceinline__ void gather(const WarpCtx& c, const SampleT& s, Corners& v) {
     const bool vx1 = s.x0 + 1 < c.w, vy1 = s.y0 + 1 < c.h;
     const int y1 = vy1 ? s.y0 + 1 : s.y0;
     const int xa = vx1 ? s.x0 : s.x0 - 1;
     const int HW = c.h * c.w;
     const int ot = s.y0 * c.w + xa, ob = y1 * c.w + xa;
+    if (U8) {
+        const uint2_a4 t = *(const uint2_a4*)((const char*)c.src8 + ((uint32_t)ot << 2));
+        const uint2_a4 u = *(const uint2_a4*)((const char*)c.src8 + ((uint32_t)ob << 2));
+        const uint32_t pnw = vx1 ? t.x : t.y, pne = vx1 ? t.y : 0u;
+        const uint32_t psw = vy1 ? (vx1 ? u.x : u.y) : 0u, pse = (vx1 && vy1) ? u.y : 0u;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            v.nw[ch] = (float)((pnw >> (8 * ch)) & 255u);
+            v.ne[ch] = (float)((pne >> (8 * ch)) & 255u);
+            v.sw[ch] = (float)((psw >> (8 * ch)) & 255u);
+            v.se[ch] = (float)((pse >> (8 * ch)) & 255u);
+        }
+        return;
+    }
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
         const float2_a4 t = ldf2(c.src, ch * HW + ot), u = ldf2(c.src, ch * HW + ob);
@@ -322,20 +346,24 @@ __device__ __forceinline__ void gather(const WarpCtx& c, const SampleT& s, Corne
     }
 }
 
-template <class SampleT>
+template <bool U8, class SampleT>
 __device__ __forceinline__ void interp(const SampleT& s, const Corners& v, float out[3]) {
     const float e = 1.f - s.tx, so = 1.f - s.ty;
     const float wnw = so * e, wne = so * s.tx, wsw = s.ty * e, wse = s.ty * s.tx;
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) out[ch] = v.nw[ch] * wnw + v.ne[ch] * wne + v.sw[ch] * wsw + v.se[ch] * wse;
+    for (int ch = 0; ch < 3; ++ch) {
+        out[ch] = v.nw[ch] * wnw + v.ne[ch] * wne + v.sw[ch] * wsw + v.se[ch] * wse;
+        if (U8) out[ch] *= 1.0f / 255.0f;
+    }
 }
 
+template <bool U8>
 __device__ __forceinline__ void warp_value(const WarpCtx& c, int y, int x, float depth, float out[3]) {
     FastSample s;
     project_depth(c, y, x, depth, s);
     Corners v;
-    gather(c, s, v);
-    interp(s, v, out);
+    gather<U8>(c, s, v);
+    interp<U8>(s, v, out);
 }
 
 // ----------------------------------------------------------------------------
@@ -422,6 +450,10 @@ struct PhotoArgs {
     float* ident;
     float* rep[MD2_MAX_SCALES];
     int cblk;
+    // 8-bit copies of the source frames (B,h,w) RGBx and per (frame, image) flags
+    // "every colour is exactly k/255" (null: fp32 planes only)
+    const uint32_t* src8[MD2_MAX_SRC];
+    const int* exact;
 };
 
 __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int b, WarpCtx& c) {
@@ -431,6 +463,7 @@ __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int 
     c.upsh = a.upsh[ls];
     c.disp = a.disp[ls] + (size_t)b * c.dh * c.dw;
     c.src = a.src[f] + (size_t)b * 3 * HW;
+    c.src8 = (a.src8[f] && a.exact[f * a.B + b]) ? a.src8[f] + (size_t)b * HW : nullptr;
     c.h = a.h;
     c.w = a.w;
     c.sx = (float)a.w / (float)(a.w - 1);
@@ -462,12 +495,12 @@ struct FRow {
     float x[3], y[3];
 };
 
-template <bool SSIM_ON, bool WARPED>
+template <bool SSIM_ON, bool WARPED, bool U8>
 __device__ __forceinline__ void frow_eval(const WarpCtx& c, const float* tgt, const float (*dep)[kWave], int k,
                                           int rr, int cc, int lane, FRow& o) {
     const int HW = c.h * c.w;
     if (WARPED) {
-        warp_value(c, rr, cc, dep[k][lane], o.x);
+        warp_value<U8>(c, rr, cc, dep[k][lane], o.x);
     } else {
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) o.x[ch] = ldf(c.src, ch * HW + rr * c.w + cc);
@@ -494,7 +527,7 @@ __device__ __forceinline__ float frow_loss(const FRow& a, const FRow& b, const F
 
 // Losses of output rows r0 .. r0+kRowsP-1 at this lane's column; emit(i, v) per row.
 // The 3-row window rotates through three statically named slots (unrolled by 3).
-template <bool SSIM_ON, bool WARPED, class Emit>
+template <bool SSIM_ON, bool WARPED, bool U8, class Emit>
 __device__ __forceinline__ void loss_rows(const WarpCtx& c, const float* tgt, const float (*dep)[kWave], int r0,
                                           int cc, int lane, Emit emit) {
     const int h = c.h;
@@ -504,11 +537,11 @@ __device__ __forceinline__ void loss_rows(const WarpCtx& c, const float* tgt, co
     static_assert((kRowsP + 2) % 3 == 0, "window rows must be a multiple of 3");
 #pragma unroll 1
     for (int k = 0; k < kRowsP + 2; k += 3) {
-        frow_eval<SSIM_ON, WARPED>(c, tgt, dep, k, reflect_clamp(r0 - 1 + k, h), cc, lane, R0);
+        frow_eval<SSIM_ON, WARPED, U8>(c, tgt, dep, k, reflect_clamp(r0 - 1 + k, h), cc, lane, R0);
         if (k >= 2) emit(k - 2, frow_loss<SSIM_ON>(R1, R2, R0));
-        frow_eval<SSIM_ON, WARPED>(c, tgt, dep, k + 1, reflect_clamp(r0 + k, h), cc, lane, R1);
+        frow_eval<SSIM_ON, WARPED, U8>(c, tgt, dep, k + 1, reflect_clamp(r0 + k, h), cc, lane, R1);
         if (k >= 1) emit(k - 1, frow_loss<SSIM_ON>(R2, R0, R1));
-        frow_eval<SSIM_ON, WARPED>(c, tgt, dep, k + 2, reflect_clamp(r0 + 1 + k, h), cc, lane, R2);
+        frow_eval<SSIM_ON, WARPED, U8>(c, tgt, dep, k + 2, reflect_clamp(r0 + 1 + k, h), cc, lane, R2);
         emit(k, frow_loss<SSIM_ON>(R0, R1, R2));
     }
 }
@@ -543,10 +576,11 @@ __global__ __launch_bounds__(kBlock) void photo_ident_kernel(PhotoArgs a) {
     const int h = a.h, w = a.w, HW = h * w;
     WarpCtx ctx;
     ctx.src = a.src[f] + (size_t)it.b * 3 * HW;
+    ctx.src8 = nullptr;
     ctx.h = h;
     ctx.w = w;
     float* out = a.ident + ((size_t)f * a.B + it.b) * HW;
-    loss_rows<SSIM_ON, false>(ctx, a.tgt + (size_t)it.b * 3 * HW, nullptr, it.r0, it.cc, lane, [&](int i, float v) {
+    loss_rows<SSIM_ON, false, false>(ctx, a.tgt + (size_t)it.b * 3 * HW, nullptr, it.r0, it.cc, lane, [&](int i, float v) {
         const int r = it.r0 + i;
         if (it.colok && r < h) out[r * w + it.c] = v;
     });
@@ -571,13 +605,18 @@ __global__ __launch_bounds__(kBlock) void photo_reproj_kernel(PhotoArgs a) {
     for (int k = 0; k < kRowsP + 2; ++k) dep[k][lane] = depth_at(ctx, reflect_clamp(it.r0 - 1 + k, h), it.cc);
     float* out = a.rep[ls] + ((size_t)f * a.B + it.b) * HW;
     const float* pmask = MASK ? a.mask[ls] + ((size_t)it.b * NS + f) * HW : nullptr;
-    loss_rows<SSIM_ON, true>(ctx, a.tgt + (size_t)it.b * 3 * HW, dep, it.r0, it.cc, lane, [&](int i, float v) {
+    auto emit = [&](int i, float v) {
         const int r = it.r0 + i;
         if (it.colok && r < h) {
             if (MASK) v *= pmask[r * w + it.c];  // trainer.py:455
             out[r * w + it.c] = v;
         }
-    });
+    };
+    const float* tgt = a.tgt + (size_t)it.b * 3 * HW;
+    if (ctx.src8)   // wave-uniform: this image's sources are 8-bit exact
+        loss_rows<SSIM_ON, true, true>(ctx, tgt, dep, it.r0, it.cc, lane, emit);
+    else
+        loss_rows<SSIM_ON, true, false>(ctx, tgt, dep, it.r0, it.cc, lane, emit);
 }
 
 // Four consecutive pixels of one image per thread, every local scale (the identity
@@ -706,6 +745,62 @@ __global__ __launch_bounds__(kBlock) void photo_combine_kernel(PhotoArgs a) {
     }
 }
 
+// 8-bit source copies: every source colour x with x == RN(k/255) for k = rint(255 x)
+// (k/255 by a correctly rounded 3-op Markstein division, exhaustively checked for
+// k = 0..255) is stored as byte k of its pixel's RGBx dword; one inexact colour of an
+// image clears that image's flag and its gathers read the fp32 planes instead.
+struct PackArgs {
+    int B, HW, S;
+    const float* src[MD2_MAX_SRC];   // (B,3,h,w)
+    uint32_t* out;                   // [S][B][HW]
+    int* exact;                      // [S][B], preset to nonzero
+};
+
+__device__ __forceinline__ float div255(float k) {
+    const float c = 1.0f / 255.0f;
+    const float q = k * c;
+    return fmaf(fmaf(-255.0f, q, k), c, q);
+}
+
+__global__ __launch_bounds__(kBlock) void pack_src8_kernel(PackArgs a) {
+    const int per_img = (a.HW + 4 * kBlock - 1) / (4 * kBlock);
+    const int fb = blockIdx.x / per_img, chunk = blockIdx.x - fb * per_img;
+    const int f = fb / a.B, b = fb - f * a.B;
+    const int p0 = (chunk * kBlock + threadIdx.x) * 4;
+    const float* src = a.src[f] + (size_t)b * 3 * a.HW;
+    uint32_t* out = a.out + ((size_t)f * a.B + b) * a.HW;
+    bool ok = true;
+    if (p0 < a.HW) {
+        const int n = min(4, a.HW - p0);
+        uint32_t px[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            float x[4];
+            if (n == 4 && (a.HW & 3) == 0) {
+                const float4 v = *(const float4*)(src + ch * a.HW + p0);
+                x[0] = v.x, x[1] = v.y, x[2] = v.z, x[3] = v.w;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[i] = i < n ? src[ch * a.HW + p0 + i] : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float k = rintf(x[i] * 255.0f);
+                ok = ok && k >= 0.f && k <= 255.f && div255(k) == x[i];
+                px[i] |= (uint32_t)(k >= 0.f && k <= 255.f ? k : 0.f) << (8 * ch);
+            }
+        }
+        if (n == 4 && (a.HW & 3) == 0) {
+            *(uint4*)(out + p0) = make_uint4(px[0], px[1], px[2], px[3]);
+        } else {
+            for (int i = 0; i < n; ++i) out[p0 + i] = px[i];
+        }
+    }
+    // a wave that saw an inexact colour clears the image's flag: a plain store of 0
+    // (flags only ever go 1 -> 0, so racing writers agree; no read-modify-write)
+    if (__ballot(!ok) != 0ull && (threadIdx.x & 63) == 0) a.exact[f * a.B + b] = 0;
+}
+
 // ----------------------------------------------------------------------------
 // backward: SSIM/L1 adjoint -> grid_sample backward -> projection chain
 // ----------------------------------------------------------------------------
@@ -743,9 +838,11 @@ struct Carry {
     float dd;            // d depth / d disp = -range * depth^2
 };
 
+template <bool U8>
 __device__ __forceinline__ void make_carry(const WarpCtx& c, const FastSample& s, const Corners& v, Carry& k) {
     const float e = 1.f - s.tx, so = 1.f - s.ty;
-    const float mx = s.gmx * c.sx, my = s.gmy * c.sy;
+    const float cs = U8 ? 1.0f / 255.0f : 1.0f;
+    const float mx = s.gmx * c.sx * cs, my = s.gmy * c.sy * cs;
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
         k.jx[ch] = ((v.ne[ch] - v.nw[ch]) * so + (v.se[ch] - v.sw[ch]) * s.ty) * mx;
@@ -792,7 +889,7 @@ struct BwdFrame {
 // The window state lives in three statically named ring slots (rows and coefficient
 // rows mod 3) that the caller rotates by unrolling three steps, so moving the window
 // down costs no register copies; every slot is updated unconditionally.
-template <int NS, bool SSIM_ON, bool MASK>
+template <int NS, bool SSIM_ON, bool MASK, bool U8>
 __device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, RowS& cur, const RowS& m1, const RowS& m2,
                                          Coef& cnew, const Coef& cm2, const Coef& cm3, float (&dP)[12],
                                          float* dfull, float (*ddacc)[kWave], int lane) {
@@ -804,11 +901,11 @@ __device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, RowS& cur, co
     FastSample sm;
     project_depth(F.ctx, rr, F.cc, F.dep[k][lane], sm);
     Corners v;
-    gather(F.ctx, sm, v);
-    interp(sm, v, cur.x);
+    gather<U8>(F.ctx, sm, v);
+    interp<U8>(sm, v, cur.x);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) cur.y[ch] = ldf(F.tgt, ch * HW + rr * w + F.cc);
-    if (k >= 2 && k < kRowsB + 2) make_carry(F.ctx, sm, v, cur.k);  // only output rows need it
+    if (k >= 2 && k < kRowsB + 2) make_carry<U8>(F.ctx, sm, v, cur.k);  // only output rows need it
     if (SSIM_ON) {
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) cur.h[ch] = hsum(cur.x[ch], cur.y[ch]);
@@ -887,6 +984,39 @@ __device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, RowS& cur, co
 // One work item of the backward: (image b, local scale ls, strip st, row block rb),
 // all source frames.  Writes dL/d(upsampled disp) for its 60 x kRowsB pixels and one
 // 12-float dL/dP partial per frame.
+// One source frame of a backward item: the row walk and its dL/dP partial.  U8:
+// this (frame, image)'s gathers read the 8-bit copy (wave-uniform choice).
+template <int NS, bool SSIM_ON, bool MASK, bool U8>
+__device__ __forceinline__ void bwd_frame_walk(const BwdFrame& F, float* dfull, float (*ddacc)[kWave], float* dst,
+                                            int lane) {
+    float dP[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) dP[j] = 0.f;
+    RowS S0, S1, S2;
+    Coef C0, C1, C2;
+    // window indices k = 0 .. kRowsB+3; slots: row k -> S[k%3], coefficient row
+    // k-1 -> C[(k-1)%3]
+    constexpr int kSteps = kRowsB + 4;
+    int k = 0;
+#pragma unroll 1
+    for (; k + 3 <= kSteps; k += 3) {
+        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, dfull, ddacc, lane);
+        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, dfull, ddacc, lane);
+        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 2, S2, S1, S0, C1, C0, C2, dP, dfull, ddacc, lane);
+    }
+    if (kSteps % 3 >= 1) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, dfull, ddacc, lane);
+    if (kSteps % 3 >= 2) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, dfull, ddacc, lane);
+    // one 12-float partial of dL/dP per (item, frame)
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        const float t = wave_sum(dP[j]);
+        if (lane == 0) dst[j] = t;
+    }
+}
+
+// One work item of the backward: (image b, local scale ls, strip st, row block rb),
+// all source frames.  Writes dL/d(upsampled disp) for its 60 x kRowsB pixels and one
+// 12-float dL/dP partial per frame.
 template <int NS, bool SSIM_ON, bool MASK>
 __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int st, int rb, int lane,
                                          float (*ddacc)[kWave], float (*dep)[kWave]) {
@@ -920,30 +1050,11 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
     for (int f = 0; f < NS; ++f) {
         F.f = f;
         make_ctx(a, ls, f, b, F.ctx);
-        float dP[12];
-#pragma unroll
-        for (int j = 0; j < 12; ++j) dP[j] = 0.f;
-        RowS S0, S1, S2;
-        Coef C0, C1, C2;
-        // window indices k = 0 .. kRowsB+3; slots: row k -> S[k%3], coefficient row
-        // k-1 -> C[(k-1)%3]
-        constexpr int kSteps = kRowsB + 4;
-        int k = 0;
-#pragma unroll 1
-        for (; k + 3 <= kSteps; k += 3) {
-            bwd_step<NS, SSIM_ON, MASK>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, dfull, ddacc, lane);
-            bwd_step<NS, SSIM_ON, MASK>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, dfull, ddacc, lane);
-            bwd_step<NS, SSIM_ON, MASK>(F, k + 2, S2, S1, S0, C1, C0, C2, dP, dfull, ddacc, lane);
-        }
-        if (kSteps % 3 >= 1) bwd_step<NS, SSIM_ON, MASK>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, dfull, ddacc, lane);
-        if (kSteps % 3 >= 2) bwd_step<NS, SSIM_ON, MASK>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, dfull, ddacc, lane);
-        // one 12-float partial of dL/dP per (item, frame)
         float* dst = a.dP_part[ls] + ((size_t)f * a.B * a.wpi + item_in_scale) * 12;
-#pragma unroll
-        for (int j = 0; j < 12; ++j) {
-            const float t = wave_sum(dP[j]);
-            if (lane == 0) dst[j] = t;
-        }
+        if (F.ctx.src8)
+            bwd_frame_walk<NS, SSIM_ON, MASK, true>(F, dfull, ddacc, dst, lane);
+        else
+            bwd_frame_walk<NS, SSIM_ON, MASK, false>(F, dfull, ddacc, dst, lane);
     }
     if (NS > 1 && F.colok) {
         for (int i = 0; i < kRowsB && F.r0 + i < h; ++i) dfull[(F.r0 + i) * w + F.c] = ddacc[i][lane];
@@ -1317,9 +1428,9 @@ __global__ __launch_bounds__(kBlock) void generate_kernel(GenArgs g) {
         }
         if (g.color[f]) {
             Corners v;
-            gather(ctx, s, v);
+            gather<false>(ctx, s, v);
             float o[3];
-            interp(s, v, o);
+            interp<false>(s, v, o);
             for (int ch = 0; ch < 3; ++ch) g.color[f][((size_t)b * 3 + ch) * HW + p] = o[ch];
         }
     }
@@ -1391,7 +1502,7 @@ struct Layout {
     int bstrips[MD2_MAX_SCALES], brows[MD2_MAX_SCALES], bwpi[MD2_MAX_SCALES];
     int chunks[MD2_MAX_SCALES];
     int cblk[MD2_MAX_SCALES];                        // combine blocks per image (split forward)
-    size_t rep_off[MD2_MAX_SCALES], ident_off;
+    size_t rep_off[MD2_MAX_SCALES], ident_off, src8_off, exact_off;
     size_t photo_off[MD2_MAX_SCALES], dP_off[MD2_MAX_SCALES], smooth_off[MD2_MAX_SCALES];
     size_t dfull_off[MD2_MAX_SCALES], stats_off, total;
     size_t sel_off[MD2_MAX_SCALES], sel_total;
@@ -1454,6 +1565,10 @@ int make_layout(const md2_desc* d, Layout& L) {
     }
     L.ident_off = off;   // identity losses of one scale group (the largest: scale 0)
     off = align256(off + sizeof(float) * (size_t)L.S * L.B * L.lh[0] * L.lw[0]);
+    L.src8_off = off;    // 8-bit source copies (full resolution; not with V1_MULTISCALE)
+    off = align256(off + (L.v1 ? 0 : sizeof(uint32_t) * (size_t)L.S * L.B * L.lh[0] * L.lw[0]));
+    L.exact_off = off;
+    off = align256(off + sizeof(int) * (size_t)L.S * L.B);
     L.stats_off = off;
     off = align256(off + sizeof(float) * (size_t)L.nscales * L.B * 4);
     L.total = off;
@@ -1530,6 +1645,11 @@ void photo_args(const md2_desc* d, const md2_tensors* t, const Layout& L, int s_
     }
     a.ident = ws ? (float*)(ws + L.ident_off) : nullptr;
     a.cblk = L.cblk[s_begin];
+    if (ws && !L.v1) {
+        for (int f = 0; f < L.S; ++f)
+            a.src8[f] = (const uint32_t*)(ws + L.src8_off) + (size_t)f * L.B * L.lh[0] * L.lw[0];
+        a.exact = (const int*)(ws + L.exact_off);
+    }
 }
 
 template <int NS, bool SSIM, bool MASK>
@@ -1643,6 +1763,19 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
             launch_photo(a, false, st);
         }
     } else {
+        // 8-bit source copies for the gathers of this forward and its backward
+        PackArgs pk;
+        memset(&pk, 0, sizeof(pk));
+        pk.B = L.B;
+        pk.HW = L.lh[0] * L.lw[0];
+        pk.S = L.S;
+        for (int f = 0; f < L.S; ++f) pk.src[f] = t->color[0][f + 1];
+        pk.out = (uint32_t*)(ws + L.src8_off);
+        pk.exact = (int*)(ws + L.exact_off);
+        if (hipMemsetAsync(pk.exact, 0x01, sizeof(int) * (size_t)L.S * L.B, st) != hipSuccess)
+            return fail(MD2_ERR_HIP, "hipMemsetAsync failed");
+        const int per_img = (pk.HW + 4 * kBlock - 1) / (4 * kBlock);
+        hipLaunchKernelGGL(pack_src8_kernel, dim3(L.S * L.B * per_img), dim3(kBlock), 0, st, pk);
         hipEvent_t e0, e1;
         timing_slot(0, &e0, &e1);
         photo_args(d, t, L, 0, L.nscales, false, ws, select_out, a);

@@ -77,8 +77,13 @@ def _texture(gen: torch.Generator, batch: int, height: int, width: int,
 def synthetic_batch(batch_size: int, height: int, width: int,
                     frame_ids: Sequence[FrameId] = (0, -1, 1), num_scales: int = 4,
                     seed: int = 0, device: Union[str, torch.device] = "cpu",
-                    side_sign: float = 1.0) -> Dict:
-    """A reference-keyed input dict for `Trainer.process_batch` (trainer.py:228)."""
+                    side_sign: float = 1.0, eight_bit: bool = False) -> Dict:
+    """A reference-keyed input dict for `Trainer.process_batch` (trainer.py:228).
+
+    eight_bit: colours quantised to k/255 at every scale, as the reference's loader
+    delivers them (uint8 PIL images through to_tensor, datasets/mono_dataset.py:
+    199-200: float32 k / 255); default off to keep the committed fixtures' inputs.
+    """
     gen = torch.Generator().manual_seed(int(seed))
     shifts = []
     for f in frame_ids:
@@ -93,8 +98,9 @@ def synthetic_batch(batch_size: int, height: int, width: int,
         for s in range(num_scales):
             if s > 0:
                 cur = F.avg_pool2d(cur, 2)
-            inputs[("color", f, s)] = cur
-            inputs[("color_aug", f, s)] = cur
+            level = torch.round(cur * 255.0) / 255.0 if eight_bit else cur
+            inputs[("color", f, s)] = level
+            inputs[("color_aug", f, s)] = level
     for s in range(num_scales):
         K, inv_K = scaled_intrinsics(height, width, s)
         inputs[("K", s)] = torch.from_numpy(K).unsqueeze(0).repeat(batch_size, 1, 1)

@@ -31,11 +31,12 @@ def main():
     ap.add_argument("--src", type=int, default=2)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-ssim", action="store_true")
+    ap.add_argument("--eight-bit", action="store_true", help="colours quantised to k/255 (loader output)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, H, W, S = a.batch, a.height, a.width, a.src
     frame_ids = [0, -1, 1, "s"][:S + 1]
-    inputs = synthetic_batch(B, H, W, frame_ids, 4, seed=0, device=dev)
+    inputs = synthetic_batch(B, H, W, frame_ids, 4, seed=0, device=dev, eight_bit=a.eight_bit)
     hp = synthetic_hotpath(B, H, W, num_src=S, seed=0, pose_scale=0.02, device=dev)
     cfg = HotPathConfig(batch=B, height=H, width=W, num_src=S, no_ssim=a.no_ssim)
     disps = [d.clone().requires_grad_(True) for d in hp["disps"]]
