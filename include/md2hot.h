@@ -449,6 +449,7 @@ int md2_maxpool3s2_bwd_add(const md2_pool_desc* desc, const uint32_t* idx, const
 #define MD2_CONV_TILE_N32  (1u << 2) /* force the 128 x 32 tile (tests) */
 #define MD2_CONV_TILE_N64  (1u << 3) /* force the 128 x 64 tile         */
 #define MD2_CONV_TILE_N128 (1u << 4) /* force the 128 x 128 tile        */
+#define MD2_CONV_X6        (1u << 5) /* split-bf16 (3 planes, 6 products) f32-class MFMA path */
 
 typedef struct md2_conv_desc {
     int32_t batch, height, width, in_channels; /* input */

@@ -106,6 +106,7 @@ CONV_NO_SPLIT = 1 << 1
 CONV_TILE_N32 = 1 << 2
 CONV_TILE_N64 = 1 << 3
 CONV_TILE_N128 = 1 << 4
+CONV_X6 = 1 << 5
 
 
 class ConvDesc(ctypes.Structure):

@@ -323,6 +323,252 @@ __global__ __launch_bounds__(kThreads, BN == 128 ? 2 : (BN == 64 ? 3 : 4)) void 
         }
 }
 
+// ----------------------------------------------------------------------------
+// Split-bf16 ("x6") forward: f32 operands split exactly into three bf16 planes
+// (x = x0 + x1 + x2: 8 + 8 + 8 significand bits = all 24 of an f32; see split3), products by v_mfma_f32_32x32x16_bf16 keeping the six terms xi*yj with
+// i + j <= 2 (the three dropped ones are below 2^-24 relative), f32 accumulation.
+// Error per product <= ~3 * 2^-24 relative: f32-class accuracy (tests compare it
+// with the exact-f32 MFMA path against an fp64 reference) at 6 bf16 MFMAs of 32
+// cycles per 16 k instead of 8 f32 MFMAs of 64 cycles: 2.7x the MFMA rate.
+// Block 128 x BN, 4 waves as 2 x 2 (wave tile 64 x BN/2), K chunks of 32 staged
+// from f32 registers (split on the way) into LDS planes [row][32 k] bf16 whose 16-byte
+// quads are XOR-swizzled by (row >> 2) & 3 (conflict-free ds_read_b128 fragments).
+// ----------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+constexpr int XBK = 32;
+
+// Exact three-way split by truncation: x0 = x with the low 16 bits cleared (the top 8
+// significand bits), r1 = x - x0 exact (<= 16 significant bits), x1 = r1 truncated the
+// same way, x2 = r1 - x1 exact with <= 8 significant bits, so its bf16 (the high half)
+// is exact too: x == x0 + x1 + x2.  Pairs of elements are packed with one v_perm per
+// plane (the high halves of two dwords).
+__device__ __forceinline__ uint32_t hi16x2(float lo, float hi) {
+    return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo), 0x07060302u);
+}
+__device__ __forceinline__ float trunc16(float x) {
+    return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, x) & 0xFFFF0000u);
+}
+__device__ __forceinline__ void split3(float4 v, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
+    const float x[4] = {v.x, v.y, v.z, v.w};
+    float a[4], b[4], c[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        a[i] = trunc16(x[i]);
+        const float r1 = x[i] - a[i];
+        b[i] = trunc16(r1);
+        c[i] = r1 - b[i];
+    }
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 q0, q1, q2;
+    q0.x = hi16x2(a[0], a[1]), q0.y = hi16x2(a[2], a[3]);
+    q1.x = hi16x2(b[0], b[1]), q1.y = hi16x2(b[2], b[3]);
+    q2.x = hi16x2(c[0], c[1]), q2.y = hi16x2(c[2], c[3]);
+    p0 = __builtin_bit_cast(bf16x4, q0);
+    p1 = __builtin_bit_cast(bf16x4, q1);
+    p2 = __builtin_bit_cast(bf16x4, q2);
+}
+
+// element index of (row r, k) in a [rows][32] bf16 plane, 16-byte quads swizzled
+__device__ __forceinline__ int xidx(int r, int k) { return r * XBK + ((((k >> 3) ^ (r >> 2)) & 3) << 3) + (k & 7); }
+
+// Weights split once per call into three bf16 planes [3][R][KT][Ck] in row-k order:
+// forward R = Co, Ck = Ci (w as is); input gradient R = Ci, Ck = Co with the taps
+// flipped (the "full" convolution's operand), so both GEMMs read B as row-k.
+__global__ __launch_bounds__(256) void conv_wsplit_kernel(const float* w, __bf16* out, int Co, int KT, int Ci,
+                                                          int dgrad) {
+    const int n = Co * KT * Ci;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float v;
+    if (!dgrad) {
+        v = w[i];
+    } else {
+        const int co = i % Co, rest = i / Co, t = rest % KT, ci = rest / KT;   // out [ci][t][co]
+        v = w[((size_t)co * KT + (KT - 1 - t)) * Ci + ci];
+    }
+    const float a = trunc16(v), r1 = v - a, b = trunc16(r1), c = r1 - b;
+    out[i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, a) >> 16));
+    out[n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, b) >> 16));
+    out[2 * n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, c) >> 16));
+}
+
+// NT threads: BN = 128 runs 8 waves (2 x 4, wave tile 64 x 32) so that two waves share
+// each SIMD and one's split VALU overlaps the other's MFMAs; BN = 64 runs 4 waves
+// (2 x 2, wave tile 64 x 32) at two blocks per CU.
+template <int BN>
+struct X6Geo {
+    static constexpr int NT = BN == 128 ? 512 : 256;
+    static constexpr int WN = BN / 32;            // waves along N (wave tile 32 wide)
+    static constexpr int WM = NT / 64 / WN;       // waves along M
+    static constexpr int TM = BM / 32 / WM;
+};
+
+// A (activations, NHWC f32, im2col rows) is split while staged; B comes pre-split
+// (conv_wsplit_kernel) and is copied in 16-byte quads.  Forward and stride-1 input
+// gradient alike (ConvArgs as the f32 path builds them; b = the planes).
+template <int BN>
+__global__ __launch_bounds__(X6Geo<BN>::NT, BN == 128 ? 1 : 2) void conv_x6_kernel(ConvArgs a) {
+    using G = X6Geo<BN>;
+    constexpr int NT = G::NT, TM = G::TM;
+    constexpr int AQ = BM * XBK / 4 / NT;          // f32 quads of A per thread
+    constexpr int BQ = 3 * BN * (XBK / 8) / NT;    // bf16 quads (8 values) of B per thread
+    constexpr int PA = BM * XBK, PB = BN * XBK;    // bf16 elements per plane
+    __shared__ __bf16 lds[2][3 * (PA + PB)];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / G::WN, wn = wid % G::WN;
+    int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int nb = blk % a.nblocks;
+    blk /= a.nblocks;
+    const int mb = blk % a.mblocks, ks = blk / a.mblocks;
+    const int m0 = mb * BM, n0 = nb * BN;
+    const int t0 = ks * a.chunks_per_split;
+    const int nchunks = min(a.chunks_per_split, a.nchunks - t0);
+    const int KT = a.KH * a.KW;
+    const int cchunks = (a.C + XBK - 1) / XBK;
+
+    // A staging: rows ra + (NT/8) j of the tile, f32 quad qa (k = 4 qa .. 4 qa + 3)
+    const int qa = tid & 7, ra = tid >> 3;
+    int aih[AQ], aiw[AQ], apb[AQ];
+    const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * 4, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < AQ; ++j) {
+        const int m = m0 + ra + (NT / 8) * j;
+        if (m < a.M) {
+            const int b = m / (a.Ho * a.Wo), rem = m - b * a.Ho * a.Wo;
+            const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+            aih[j] = oh * a.stride - a.pad;
+            aiw[j] = ow * a.stride - a.pad;
+            apb[j] = ((b * a.H + aih[j]) * a.W + aiw[j]) * a.C + 4 * qa;
+        } else {
+            aih[j] = -(1 << 20);
+            aiw[j] = 0;
+            apb[j] = 0;
+        }
+    }
+    // B staging: quad i = tid + NT j -> plane, row, quad (k = 8 q .. 8 q + 7)
+    int bpl[BQ], brow[BQ], bq[BQ], bbase[BQ];
+    const __amdgpu_buffer_rsrc_t br =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * 2, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < BQ; ++j) {
+        const int i = tid + NT * j;
+        bpl[j] = i / (BN * 4);
+        const int rem = i - bpl[j] * BN * 4;
+        brow[j] = rem >> 2;
+        bq[j] = rem & 3;
+        const int n = n0 + brow[j];
+        bbase[j] = n < a.N ? ((bpl[j] * a.N + n) * KT) * a.C + 8 * bq[j] : -1;
+    }
+
+    f32x16 acc[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+
+    float4 fa0[AQ], fa1[AQ];
+    uint4 qb0[BQ], qb1[BQ];
+    auto load = [&](int t, float4 (&RA)[AQ], uint4 (&RB)[BQ]) {
+        const int tt = t0 + t;
+        const int tap = tt / cchunks, c0 = (tt - tap * cchunks) * XBK;
+        const int kh = tap / a.KW, kw = tap - kh * a.KW;
+        const int off = (kh * a.W + kw) * a.C + c0;
+        const bool live = t < nchunks;
+        const bool cok = live && c0 + 4 * qa < a.C;
+#pragma unroll
+        for (int j = 0; j < AQ; ++j) {
+            const bool ok = cok && (unsigned)(aih[j] + kh) < (unsigned)a.H && (unsigned)(aiw[j] + kw) < (unsigned)a.W;
+            RA[j] = bload(ar, ok ? (apb[j] + off) * 4 : kBad);
+        }
+#pragma unroll
+        for (int j = 0; j < BQ; ++j) {
+            const bool ok = live && bbase[j] >= 0 && c0 + 8 * bq[j] < a.C;
+            RB[j] = __builtin_bit_cast(uint4, bload(br, ok ? (bbase[j] + tap * a.C + c0) * 2 : kBad));
+        }
+    };
+    bf16x4 sa[AQ][3];
+    auto split = [&](const float4 (&RA)[AQ]) {
+#pragma unroll
+        for (int j = 0; j < AQ; ++j) split3(RA[j], sa[j][0], sa[j][1], sa[j][2]);
+    };
+    auto store = [&](int buf, const uint4 (&RB)[BQ]) {
+        __bf16* L = lds[buf];
+#pragma unroll
+        for (int j = 0; j < AQ; ++j) {
+            const int e = xidx(ra + (NT / 8) * j, 4 * qa);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) *(bf16x4*)(L + pl * PA + e) = sa[j][pl];
+        }
+#pragma unroll
+        for (int j = 0; j < BQ; ++j) *(uint4*)(L + 3 * PA + bpl[j] * PB + xidx(brow[j], 8 * bq[j])) = RB[j];
+    };
+    const int lr = lane & 31, h = lane >> 5;
+    auto mma = [&](int buf) {
+        const __bf16* L = lds[buf];
+#pragma unroll
+        for (int s = 0; s < XBK / 16; ++s) {
+            bf16x8 fa[TM][3], fb[3];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int e = xidx(wm * (TM * 32) + 32 * i + lr, 16 * s + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fa[i][pl] = *(const bf16x8*)(L + pl * PA + e);
+            }
+            const int eb = xidx(wn * 32 + lr, 16 * s + 8 * h);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                // small terms first: x2y0, x1y1, x0y2, x1y0, x0y1, x0y0
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[2], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[0], acc[i], 0, 0, 0);
+            }
+        }
+    };
+
+    // chunk t+2 is fetched while chunk t is multiplied; chunk t+1 (fetched one
+    // iteration earlier) is split beside the MFMAs and stored to the other LDS buffer
+    // afterwards; one barrier per chunk.  Loads past the last chunk read zeros.
+    load(0, fa0, qb0);
+    load(1, fa1, qb1);
+    split(fa0);
+    store(0, qb0);
+    __syncthreads();
+    for (int t = 0; t < nchunks; t += 2) {
+        load(t + 2, fa0, qb0);
+        split(fa1);
+        mma(0);
+        asm volatile("" ::: "memory");
+        store(1, qb1);
+        __syncthreads();
+        if (t + 1 >= nchunks) break;
+        load(t + 3, fa1, qb1);
+        split(fa0);
+        mma(1);
+        asm volatile("" ::: "memory");
+        store(0, qb0);
+        __syncthreads();
+    }
+
+    float* out = a.y + (size_t)ks * a.M * a.N;
+    const int n = n0 + wn * 32 + lr;
+    if (n < a.N) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int m = m0 + wm * (TM * 32) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (m < a.M) out[m * a.N + n] = acc[i][e];
+            }
+    }
+}
+
 // y = Σ_split partial[split] in split order (deterministic), float4 per thread
 __global__ __launch_bounds__(256) void conv_reduce_kernel(const float4* part, float4* y, int n4, int splits) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -445,6 +691,37 @@ ConvArgs args_of(const md2_conv_desc* d, int mode) {
     return a;
 }
 
+int resident_blocks_x6(int BN) { return 256 * (BN == 128 ? 1 : 2); }
+
+// x6 forward plan: BN = 128 unless N <= 64, K split by the same wave-quantisation model
+void plan_x6(ConvArgs& a, uint32_t flags) {
+    a.nchunks = (a.nchunks + 0);   // chunks of 32 k, as the f32 path
+    const int BN = a.N <= 64 ? 64 : 128;
+    const int mblocks = (a.M + BM - 1) / BM, nblocks = (a.N + BN - 1) / BN;
+    const int base = mblocks * nblocks, res = resident_blocks_x6(BN);
+    int best_s = 1;
+    double best_t = 1e30;
+    const int smax = (flags & MD2_CONV_NO_SPLIT) ? 1 : (a.nchunks / 6 > 1 ? a.nchunks / 6 : 1);
+    for (int sp = 1; sp <= smax && sp <= 64; ++sp) {
+        const int per = (a.nchunks + sp - 1) / sp;
+        const int splits = (a.nchunks + per - 1) / per;
+        const int rounds = (base * splits + res - 1) / res;
+        // a chunk-round of blocks ~1.5k cycles; the split reduction moves (splits + 1)
+        // M x N floats at ~2.4 KB/cycle chip-wide
+        const double red = splits > 1 ? (double)(splits + 1) * a.M * a.N * 4.0 / 2400.0 / 1536.0 : 0.0;
+        const double t = (double)rounds * per + red;
+        if (t < best_t - 1e-9) {
+            best_t = t;
+            best_s = splits;
+        }
+    }
+    a.bn = BN;
+    a.mblocks = mblocks;
+    a.nblocks = nblocks;
+    a.chunks_per_split = (a.nchunks + best_s - 1) / best_s;
+    a.splits = (a.nchunks + a.chunks_per_split - 1) / a.chunks_per_split;
+}
+
 template <int MODE>
 void launch(const ConvArgs& a, int BN, hipStream_t st) {
     const dim3 grid(a.mblocks * a.nblocks * a.splits);
@@ -458,22 +735,44 @@ void launch(const ConvArgs& a, int BN, hipStream_t st) {
 
 int min_chunks_of(int mode) { return mode == MODE_WGRAD ? 8 : 6; }
 
+bool use_x6(const md2_conv_desc* d, int mode) {
+    return (d->flags & MD2_CONV_X6) && mode != MODE_WGRAD && d->in_channels % 8 == 0 && d->out_channels % 8 == 0;
+}
+
+size_t x6_planes_bytes(const md2_conv_desc* d) {
+    return (3 * sizeof(uint16_t) * (size_t)d->out_channels * d->kernel_h * d->kernel_w * d->in_channels + 255) &
+           ~(size_t)255;
+}
+
 int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float* out, void* ws, void* stream,
         const char* name) {
     ConvArgs a = args_of(d, mode);
-    plan(a, d->flags, min_chunks_of(mode));
+    if (use_x6(d, mode)) plan_x6(a, d->flags);
+    else plan(a, d->flags, min_chunks_of(mode));
     const int BN = a.bn;
     a.a = A;
     a.b = B;
-    if (a.splits > 1 && !ws) return md2_report_error(MD2_ERR_ARG, name);
+    if ((a.splits > 1 || use_x6(d, mode)) && !ws) return md2_report_error(MD2_ERR_ARG, name);
     a.y = a.splits > 1 ? (float*)ws : out;
     const hipStream_t st = (hipStream_t)stream;
-    if (mode == MODE_FWD) launch<MODE_FWD>(a, BN, st);
+    if (use_x6(d, mode)) {
+        // B: the weights split into bf16 planes at the front of the workspace
+        __bf16* planes = (__bf16*)ws;
+        a.b = (const float*)planes;
+        a.b_elems = 3 * d->out_channels * d->kernel_h * d->kernel_w * d->in_channels;
+        if (a.splits > 1) a.y = (float*)((char*)ws + x6_planes_bytes(d));
+        const int nw = a.b_elems / 3;
+        hipLaunchKernelGGL(conv_wsplit_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, B, planes, d->out_channels,
+                           d->kernel_h * d->kernel_w, d->in_channels, mode == MODE_DGRAD ? 1 : 0);
+        const dim3 grid(a.mblocks * a.nblocks * a.splits);
+        if (BN == 128) hipLaunchKernelGGL((conv_x6_kernel<128>), grid, dim3(X6Geo<128>::NT), 0, st, a);
+        else hipLaunchKernelGGL((conv_x6_kernel<64>), grid, dim3(X6Geo<64>::NT), 0, st, a);
+    } else if (mode == MODE_FWD) launch<MODE_FWD>(a, BN, st);
     else if (mode == MODE_DGRAD) launch<MODE_DGRAD>(a, BN, st);
     else launch<MODE_WGRAD>(a, BN, st);
     if (a.splits > 1) {
         const int n4 = a.M * a.N / 4;
-        hipLaunchKernelGGL(conv_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, st, (const float4*)ws,
+        hipLaunchKernelGGL(conv_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, st, (const float4*)a.y,
                            (float4*)out, n4, a.splits);
     }
     const hipError_t e = hipGetLastError();
@@ -482,6 +781,10 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
 
 size_t ws_bytes(const md2_conv_desc* d, int mode) {
     ConvArgs a = args_of(d, mode);
+    if (use_x6(d, mode)) {
+        plan_x6(a, d->flags);
+        return x6_planes_bytes(d) + (a.splits > 1 ? sizeof(float) * (size_t)a.splits * a.M * a.N : 0);
+    }
     plan(a, d->flags, min_chunks_of(mode));
     return a.splits > 1 ? sizeof(float) * (size_t)a.splits * a.M * a.N : 0;
 }

@@ -160,3 +160,28 @@ def test_conv_abi_dgrad_wgrad(B, C, N, k, s, p, H, W):
         _lib.check(L.md2_conv_dgrad(ctypes.byref(d), gy.data_ptr(), w.data_ptr(), gx.data_ptr(), ws.data_ptr(), st),
                    "dgrad")
         assert _rel(gx, gx_ref) < 1e-4
+
+
+@pytest.mark.parametrize("B,C,N,k,s,p,H,W", [sh for sh in SHAPES if sh[1] % 8 == 0 and sh[2] % 8 == 0])
+def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
+    """The split-bf16 path (MD2_CONV_X6: exact three-plane split, six bf16 MFMA
+    products, f32 accumulation) against an fp64 reference: its error is of the order
+    of MIOpen's own f32 error (within 3x of it, and below 2e-6 of the output's
+    magnitude), forward and input gradient — f32-class, not reduced precision."""
+    torch.manual_seed(11 + C + N + H)
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    w = (torch.randn(N, C, k, k, device="cuda") / (C * k * k) ** 0.5).contiguous(memory_format=CL)
+    ref = F.conv2d(x.double().cpu(), w.double().cpu(), None, s, p)
+    y_x6 = conv_ops._fwd(x, w, s, p, conv_ops.X6).double().cpu()
+    y_mi = F.conv2d(x, w, None, s, p).double().cpu()
+    e_x6, e_mi = _rel(y_x6, ref), _rel(y_mi, ref)
+    assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, (e_x6, e_mi)
+    if s == 1:
+        gy = torch.randn(ref.shape, device="cuda").contiguous(memory_format=CL)
+        gref = torch.ops.aten.convolution_backward(gy.double().cpu(), x.double().cpu(), w.double().cpu(), None, (s, s),
+                                                   (p, p), (1, 1), False, (0, 0), 1, (True, False, False))[0]
+        g_x6 = conv_ops._dgrad(gy, x, w, p, conv_ops.X6).double().cpu()
+        g_mi = torch.ops.aten.convolution_backward(gy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
+                                                   (True, False, False))[0].double().cpu()
+        e_x6, e_mi = _rel(g_x6, gref), _rel(g_mi, gref)
+        assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, (e_x6, e_mi)
