@@ -11,7 +11,7 @@ PyTorch's channels_last layout:
   gradient with the weight read flipped and transposed);
 * weight gradient (md2_conv_wgrad; deterministic K split, no zero-fill launch).
 
-The forward and the input gradient also have a split-bf16 form (`md2_conv_*` with
+The three also have a split-bf16 form (`md2_conv_*` with
 MD2_CONV_X6): every f32 operand split exactly into three bf16 planes, products by
 v_mfma_f32_32x32x16_bf16 keeping the six terms above 2^-24 relative, f32
 accumulation — f32-class accuracy (tests/test_conv_gpu.py pins it to an fp64
@@ -86,9 +86,9 @@ def _x6_ok(x, w) -> bool:
     return x.shape[1] % 8 == 0 and w.shape[0] % 8 == 0
 
 
-def _wgrad(gy, x, w, stride, pad):
+def _wgrad(gy, x, w, stride, pad, flags=0):
     gw = torch.empty_like(w, memory_format=_CL)
-    _call("md2_conv_wgrad", _desc(x, w, stride, pad), x.data_ptr(), gy.data_ptr(), gw.data_ptr(), x.device)
+    _call("md2_conv_wgrad", _desc(x, w, stride, pad, flags), x.data_ptr(), gy.data_ptr(), gw.data_ptr(), x.device)
     return gw
 
 
@@ -161,9 +161,11 @@ class _Conv(torch.autograd.Function):
             else:
                 mi_x = True
         if need_w:
-            cands = [lambda: _wgrad(gy, x, w, s, p), lambda: _miopen_bwd(gy, x, w, s, p, (False, True, False))[1]]
-            if _fastest("wgrad", ctx.key, cands) == 0:
-                gw = cands[0]()
+            cands = ([lambda: _wgrad(gy, x, w, s, p, X6)] if _x6_ok(x, w) else []) + \
+                [lambda: _wgrad(gy, x, w, s, p), lambda: _miopen_bwd(gy, x, w, s, p, (False, True, False))[1]]
+            i = _fastest("wgrad", ctx.key, cands)
+            if i < len(cands) - 1:
+                gw = cands[i]()
             else:
                 mi_w = True
         if mi_x or mi_w:

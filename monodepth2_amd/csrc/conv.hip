@@ -569,6 +569,190 @@ __global__ __launch_bounds__(X6Geo<BN>::NT, BN == 128 ? 1 : 2) void conv_x6_kern
     }
 }
 
+// Split-bf16 weight gradient: gw[co][tap][ci] = Σ_p gy[p][co] · x[p + tap][ci] as a
+// GEMM with rows m = co, columns n = (tap, ci), K = output pixels.  Both operands are
+// stored k-row in HBM (channels contiguous per pixel), the MFMA wants 8 consecutive k
+// per lane: each staging thread loads a 4-pixel x 4-channel micro-tile (four 16-byte
+// loads), splits it, and writes it transposed — per plane and channel one 8-byte run of
+// 4 consecutive k — into the same swizzled [row][32 k] planes as the forward.
+// 512 threads: waves 0-3 stage gy (A), waves 4-7 stage x (B); all 8 multiply (2 x 4,
+// wave tile 64 x 32).  ConvArgs: M = Co, N = KT*Ci, P = pixels, C = Ci, Cg = Co.
+__global__ __launch_bounds__(512, 1) void conv_x6_wgrad_kernel(ConvArgs a) {
+    constexpr int NT = 512, BNW = 128, TM = 2;
+    constexpr int PA = BM * XBK, PB = BNW * XBK;
+    __shared__ __bf16 lds[2][3 * (PA + PB)];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 2, wn = wid & 3;
+    int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int nb = blk % a.nblocks;
+    blk /= a.nblocks;
+    const int mb = blk % a.mblocks, ks = blk / a.mblocks;
+    const int m0 = mb * BM, n0 = nb * BNW;
+    const int t0 = ks * a.chunks_per_split;
+    const int nchunks = min(a.chunks_per_split, a.nchunks - t0);
+    const int HoWo = a.Ho * a.Wo;
+
+    // staging role: side 0 (gy, rows co) or 1 (x, rows (tap, ci)); micro-tile
+    // rows 4 mq .. 4 mq + 3, pixels 4 kq .. 4 kq + 3 of the chunk
+    const int side = tid >> 8, u = tid & 255, kq = u & 7, mq = u >> 3;
+    const int row = 4 * mq;
+    int ci = 0, kh = 0, kw = 0;
+    bool rok;
+    if (side == 0) {
+        rok = m0 + row < a.M;
+    } else {
+        const int n = n0 + row;
+        rok = n < a.N;
+        const int tap = n / a.C;
+        ci = n - tap * a.C;
+        kh = tap / a.KW;
+        kw = tap - kh * a.KW;
+    }
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * 4, 0x00020000);
+
+    // two-level accumulation: the MFMAs sum one chunk (32 pixels x 6 products) into
+    // `acc`, which is then added into `tot` with rounded f32 adds — K here runs over
+    // up to millions of pixels, and one MFMA accumulator over all of them drifts
+    // (measured 1e-5 relative at 1.5 M pixels vs 4e-7 with this)
+    f32x16 acc[TM], tot[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) tot[i][e] = 0.f;
+
+    float4 v0[4], v1[4];
+    auto load = [&](int t, float4 (&V)[4]) {
+        const int p0 = (t0 + t) * XBK + 4 * kq;
+        const bool live = t < nchunks && rok;
+        if (side == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int p = p0 + i;
+                V[i] = bload(gr, (live && p < a.P) ? (p * a.Cg + m0 + row) * 4 : kBad);
+            }
+        } else {
+            int b = p0 / HoWo;
+            const int rem = p0 - b * HoWo;
+            int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
+                const bool ok = live && p0 + i < a.P && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+                V[i] = bload(xr, ok ? (((b * a.H + ih) * a.W + iw) * a.C + ci) * 4 : kBad);
+                if (++ow == a.Wo) {
+                    ow = 0;
+                    if (++oh == a.Ho) {
+                        oh = 0;
+                        ++b;
+                    }
+                }
+            }
+        }
+    };
+    uint32_t pk[3][4][2];   // plane, channel j, (k0k1, k2k3) packed bf16 pairs
+    auto split = [&](const float4 (&V)[4]) {
+        float c[3][4][4];   // plane, pixel i, channel j
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float x[4] = {V[i].x, V[i].y, V[i].z, V[i].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float a0 = trunc16(x[j]), r1 = x[j] - a0, a1 = trunc16(r1);
+                c[0][i][j] = a0;
+                c[1][i][j] = a1;
+                c[2][i][j] = r1 - a1;
+            }
+        }
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                pk[pl][j][0] = hi16x2(c[pl][0][j], c[pl][1][j]);
+                pk[pl][j][1] = hi16x2(c[pl][2][j], c[pl][3][j]);
+            }
+    };
+    auto store = [&](int buf) {
+        __bf16* L = lds[buf] + (side ? 3 * PA : 0);
+        const int P = side ? PB : PA;
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                u32x2 q;
+                q.x = pk[pl][j][0];
+                q.y = pk[pl][j][1];
+                *(u32x2*)(L + pl * P + xidx(row + j, 4 * kq)) = q;
+            }
+    };
+    const int lr = lane & 31, h = lane >> 5;
+    auto mma = [&](int buf) {
+        const __bf16* L = lds[buf];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+#pragma unroll
+        for (int s = 0; s < XBK / 16; ++s) {
+            bf16x8 fa[TM][3], fb[3];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int e = xidx(wm * (TM * 32) + 32 * i + lr, 16 * s + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fa[i][pl] = *(const bf16x8*)(L + pl * PA + e);
+            }
+            const int eb = xidx(wn * 32 + lr, 16 * s + 8 * h);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[2], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[0], acc[i], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) tot[i] += acc[i];
+    };
+
+    load(0, v0);
+    load(1, v1);
+    split(v0);
+    store(0);
+    __syncthreads();
+    for (int t = 0; t < nchunks; t += 2) {
+        load(t + 2, v0);
+        split(v1);
+        mma(0);
+        asm volatile("" ::: "memory");
+        store(1);
+        __syncthreads();
+        if (t + 1 >= nchunks) break;
+        load(t + 3, v1);
+        split(v0);
+        mma(1);
+        asm volatile("" ::: "memory");
+        store(0);
+        __syncthreads();
+    }
+
+    float* out = a.y + (size_t)ks * a.M * a.N;
+    const int n = n0 + wn * 32 + lr;
+    if (n < a.N) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int m = m0 + wm * (TM * 32) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (m < a.M) out[m * a.N + n] = tot[i][e];
+            }
+    }
+}
+
 // y = Σ_split partial[split] in split order (deterministic), float4 per thread
 __global__ __launch_bounds__(256) void conv_reduce_kernel(const float4* part, float4* y, int n4, int splits) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -694,9 +878,8 @@ ConvArgs args_of(const md2_conv_desc* d, int mode) {
 int resident_blocks_x6(int BN) { return 256 * (BN == 128 ? 1 : 2); }
 
 // x6 forward plan: BN = 128 unless N <= 64, K split by the same wave-quantisation model
-void plan_x6(ConvArgs& a, uint32_t flags) {
-    a.nchunks = (a.nchunks + 0);   // chunks of 32 k, as the f32 path
-    const int BN = a.N <= 64 ? 64 : 128;
+void plan_x6(ConvArgs& a, uint32_t flags, bool wgrad = false) {
+    const int BN = (a.N <= 64 && !wgrad) ? 64 : 128;   // the weight-gradient kernel is 128 wide
     const int mblocks = (a.M + BM - 1) / BM, nblocks = (a.N + BN - 1) / BN;
     const int base = mblocks * nblocks, res = resident_blocks_x6(BN);
     int best_s = 1;
@@ -736,7 +919,25 @@ void launch(const ConvArgs& a, int BN, hipStream_t st) {
 int min_chunks_of(int mode) { return mode == MODE_WGRAD ? 8 : 6; }
 
 bool use_x6(const md2_conv_desc* d, int mode) {
-    return (d->flags & MD2_CONV_X6) && mode != MODE_WGRAD && d->in_channels % 8 == 0 && d->out_channels % 8 == 0;
+    return (d->flags & MD2_CONV_X6) && d->in_channels % 8 == 0 && d->out_channels % 8 == 0;
+}
+
+// the weight gradient's x6 GEMM: rows co, columns (tap, ci), K = output pixels
+ConvArgs args_x6_wgrad(const md2_conv_desc* d) {
+    const Shape s = shape_of(d);
+    ConvArgs a = {};
+    a.KH = s.KH;
+    a.KW = s.KW;
+    a.B = s.B; a.H = s.H; a.W = s.W; a.C = s.C;
+    a.Ho = s.Ho; a.Wo = s.Wo; a.stride = s.s; a.pad = s.p;
+    a.M = s.N;
+    a.N = s.KH * s.KW * s.C;
+    a.Cg = s.N;
+    a.P = s.B * s.Ho * s.Wo;
+    a.nchunks = (a.P + XBK - 1) / XBK;
+    a.a_elems = s.B * s.H * s.W * s.C;    // x
+    a.b_elems = s.B * s.Ho * s.Wo * s.N;  // gy
+    return a;
 }
 
 size_t x6_planes_bytes(const md2_conv_desc* d) {
@@ -746,16 +947,19 @@ size_t x6_planes_bytes(const md2_conv_desc* d) {
 
 int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float* out, void* ws, void* stream,
         const char* name) {
-    ConvArgs a = args_of(d, mode);
-    if (use_x6(d, mode)) plan_x6(a, d->flags);
+    ConvArgs a = (mode == MODE_WGRAD && use_x6(d, mode)) ? args_x6_wgrad(d) : args_of(d, mode);
+    if (use_x6(d, mode)) plan_x6(a, d->flags, mode == MODE_WGRAD);
     else plan(a, d->flags, min_chunks_of(mode));
     const int BN = a.bn;
     a.a = A;
     a.b = B;
-    if ((a.splits > 1 || use_x6(d, mode)) && !ws) return md2_report_error(MD2_ERR_ARG, name);
+    if ((a.splits > 1 || (use_x6(d, mode) && mode != MODE_WGRAD)) && !ws) return md2_report_error(MD2_ERR_ARG, name);
     a.y = a.splits > 1 ? (float*)ws : out;
     const hipStream_t st = (hipStream_t)stream;
-    if (use_x6(d, mode)) {
+    if (use_x6(d, mode) && mode == MODE_WGRAD) {
+        const dim3 grid(a.mblocks * a.nblocks * a.splits);
+        hipLaunchKernelGGL(conv_x6_wgrad_kernel, grid, dim3(512), 0, st, a);
+    } else if (use_x6(d, mode)) {
         // B: the weights split into bf16 planes at the front of the workspace
         __bf16* planes = (__bf16*)ws;
         a.b = (const float*)planes;
@@ -780,7 +984,11 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
 }
 
 size_t ws_bytes(const md2_conv_desc* d, int mode) {
-    ConvArgs a = args_of(d, mode);
+    ConvArgs a = (mode == MODE_WGRAD && use_x6(d, mode)) ? args_x6_wgrad(d) : args_of(d, mode);
+    if (use_x6(d, mode) && mode == MODE_WGRAD) {
+        plan_x6(a, d->flags, true);
+        return a.splits > 1 ? sizeof(float) * (size_t)a.splits * a.M * a.N : 0;
+    }
     if (use_x6(d, mode)) {
         plan_x6(a, d->flags);
         return x6_planes_bytes(d) + (a.splits > 1 ? sizeof(float) * (size_t)a.splits * a.M * a.N : 0);

@@ -167,7 +167,7 @@ def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
     """The split-bf16 path (MD2_CONV_X6: exact three-plane split, six bf16 MFMA
     products, f32 accumulation) against an fp64 reference: its error is of the order
     of MIOpen's own f32 error (within 3x of it, and below 2e-6 of the output's
-    magnitude), forward and input gradient — f32-class, not reduced precision."""
+    magnitude), forward, input and weight gradient — f32-class, not reduced precision."""
     torch.manual_seed(11 + C + N + H)
     x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
     w = (torch.randn(N, C, k, k, device="cuda") / (C * k * k) ** 0.5).contiguous(memory_format=CL)
@@ -185,3 +185,11 @@ def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
                                                    (True, False, False))[0].double().cpu()
         e_x6, e_mi = _rel(g_x6, gref), _rel(g_mi, gref)
         assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, (e_x6, e_mi)
+    gy = torch.randn(ref.shape, device="cuda").contiguous(memory_format=CL)
+    wref = torch.ops.aten.convolution_backward(gy.double().cpu(), x.double().cpu(), w.double().cpu(), None, (s, s),
+                                               (p, p), (1, 1), False, (0, 0), 1, (False, True, False))[1]
+    w_x6 = conv_ops._wgrad(gy, x, w, s, p, conv_ops.X6).double().cpu()
+    w_mi = torch.ops.aten.convolution_backward(gy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
+                                               (False, True, False))[1].double().cpu()
+    e_x6, e_mi = _rel(w_x6, wref), _rel(w_mi, wref)
+    assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, ("wgrad", e_x6, e_mi)

@@ -55,6 +55,20 @@ def main():
                         "dgrad_miopen_tf": round(gf / t_mi, 1),
                         "dgrad_err_x6": errs(dgrad(gy, x, w, s, p, X6), ref),
                         "dgrad_err_f32": errs(dgrad(gy, x, w, s, p), ref), "dgrad_err_miopen": errs(mi(), ref)})
+        if "wgrad" in modes:
+            y = F.conv2d(x, w, None, s, p)
+            gy = torch.randn_like(y).contiguous(memory_format=CL)
+            ref = torch.ops.aten.convolution_backward(gy.double().cpu(), x.double().cpu(), w.double().cpu(), None, (s, s),
+                                                      (p, p), (1, 1), False, (0, 0), 1, (False, True, False))[1].cuda()
+            mi = lambda: torch.ops.aten.convolution_backward(gy, x, w, None, (s, s), (p, p), (1, 1), False,  # noqa: E731
+                                                             (0, 0), 1, (False, True, False))[1]
+            t_x6 = timeit(lambda: wgrad(gy, x, w, s, p, X6))
+            t_f32 = timeit(lambda: wgrad(gy, x, w, s, p))
+            t_mi = timeit(mi)
+            row.update({"wgrad_x6_tf": round(gf / t_x6, 1), "wgrad_f32_tf": round(gf / t_f32, 1),
+                        "wgrad_miopen_tf": round(gf / t_mi, 1),
+                        "wgrad_err_x6": errs(wgrad(gy, x, w, s, p, X6), ref),
+                        "wgrad_err_miopen": errs(mi(), ref)})
         print(json.dumps(row), flush=True)
 
 
