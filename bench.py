@@ -46,8 +46,10 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "training images/sec at 640x192 mono, 1/2/4/8 GPUs; loss delta vs ref"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, HBM3E spec
+F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, dense f32 matrix (= f32 vector) peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0 # dense bf16; the split-bf16 convs issue 6 bf16 products per f32 product
 VALU_ISSUE_PEAK = 256 * 4 * 0.5 * 2.4e9   # wave-instructions/s: 256 CU x 4 SIMD x 1 per 2 clk x 2.4 GHz
-ROUND = "r01"
+ROUND = "r02"
 
 
 def photo_bwd_bytes(B, H, W, S, nscales=4):
@@ -157,6 +159,36 @@ def time_hot_kernels(trainer, batch, n=10):
             loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=2 + i)
             loss[hot.num_scales].backward()
     return kt
+
+
+def conv_mfma_roofline(device):
+    """The split-bf16 convolution (csrc/conv.hip conv_x6_kernel, the step's dominant
+    hand-written MFMA kernel class) on the depth encoder's layer2 3x3 shape at B=12
+    (M = 23,040 pixels, N = 128, K = 1,152), HIP-event timed on its stream: f32-class
+    TFLOP/s against the f32 matrix peak, and the bf16 issue bound the six products
+    per f32 product imply (2.5 PF / 6)."""
+    from monodepth2_amd import conv_ops
+    B, C, N, H, W = 12, 128, 128, 24, 80
+    x = torch.randn(B, C, H, W, device=device).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(N, C, 3, 3, device=device) / 34.0).contiguous(memory_format=torch.channels_last)
+    for _ in range(3):
+        conv_ops._fwd(x, w, 1, 1, conv_ops.X6)
+    torch.cuda.synchronize()
+    n = 20
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        conv_ops._fwd(x, w, 1, 1, conv_ops.X6)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    flops = 2.0 * B * H * W * N * C * 9
+    tf = flops / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "kernel": "conv_x6_kernel (split-bf16, f32-class)",
+            "shape": f"fwd B={B} {C}->{N} 3x3 {H}x{W}", "achieved": round(tf, 1), "peak": F32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(tf / F32_MFMA_PEAK_TFLOPS, 3),
+            "bf16_issue_bound": round(BF16_MFMA_PEAK_TFLOPS / 6, 1), "avg_call_ms": round(ms, 4),
+            "flops_per_call": int(flops)}
 
 
 def cpu_baseline(args):
@@ -328,6 +360,8 @@ def main():
                 "binding_pipeline": pipe}
         log(f"timed: {1e3 * dt / args.steps:.2f} ms/step, photo_bwd {bwd_ms:.3f} ms, photo_fwd {fwd_ms:.3f} ms, "
             f"adam table uploads {getattr(trainer.model_optimizer, 'rebuilds', '-')}")
+        conv_roof = conv_mfma_roofline(device)
+        log(f"conv_x6: {conv_roof['achieved']} TFLOP/s ({conv_roof['frac']} of the f32 matrix peak)")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args)
@@ -346,7 +380,7 @@ def main():
                                        + (" + GPU input pipeline from 375x1242 uint8" if args.gpu_augment else ""),
                            "global_batch": B * world, "height": H, "width": W, "frame_ids": [str(f) for f in frame_ids],
                            "parallelism": f"dp{world}"},
-                "roofline": roof, "cpu_baseline": cpu,
+                "roofline": roof, "conv_roofline": conv_roof, "cpu_baseline": cpu,
                 "loss_delta_vs_oracle": delta, "final_loss": round(final_loss, 6),
                 "host_enqueue_ms_per_step": round(host_ms, 3)}
         print(json.dumps(line), flush=True)

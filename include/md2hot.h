@@ -142,7 +142,7 @@ int md2_generate_images(const md2_desc* desc, const md2_tensors* t,
  * The tie-break noise the forward draws in-kernel when tensors.noise is NULL
  * (trainer.py:468, unit normal before the 1e-5 scale), for scale s: writes
  * (B, C, h_s, w_s) with C = S (or 1 with AVG_REPROJECTION) at the loss resolution.
- * seed_ptr as in md2_tensors (nullable).  Lets tests hand the exact draw of a
+ * seed_ptr: the same optional device seed the forward takes.  Lets tests hand the exact draw of a
  * seeded forward to the CPU oracle.
  */
 int md2_tiebreak_noise(const md2_desc* desc, const uint64_t* seed_ptr, int scale,
@@ -450,6 +450,7 @@ int md2_maxpool3s2_bwd_add(const md2_pool_desc* desc, const uint32_t* idx, const
 #define MD2_CONV_TILE_N64  (1u << 3) /* force the 128 x 64 tile         */
 #define MD2_CONV_TILE_N128 (1u << 4) /* force the 128 x 128 tile        */
 #define MD2_CONV_X6        (1u << 5) /* split-bf16 (3 planes, 6 products) f32-class MFMA path */
+#define MD2_CONV_BM256     (1u << 6) /* x6 forward / input grad: 256 x 128 tiles (N > 64)     */
 
 typedef struct md2_conv_desc {
     int32_t batch, height, width, in_channels; /* input */

@@ -107,6 +107,7 @@ CONV_TILE_N32 = 1 << 2
 CONV_TILE_N64 = 1 << 3
 CONV_TILE_N128 = 1 << 4
 CONV_X6 = 1 << 5
+CONV_BM256 = 1 << 6
 
 
 class ConvDesc(ctypes.Structure):

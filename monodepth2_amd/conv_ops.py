@@ -42,6 +42,7 @@ AUTOTUNE = True    # False: always the MFMA kernels (tests)
 _ws: Dict[Tuple[int, int], torch.Tensor] = {}
 _choice: Dict[tuple, int] = {}     # (op, shape) -> index of the fastest candidate
 X6 = _lib.CONV_X6
+BM256 = _lib.CONV_BM256
 
 
 def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
@@ -137,7 +138,8 @@ class _Conv(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.stride, ctx.pad = stride, pad
         ctx.key = (tuple(x.shape), tuple(weight.shape), stride, pad)
-        cands = ([lambda: _fwd(x, weight, stride, pad, X6)] if _x6_ok(x, weight) else []) + \
+        cands = ([lambda: _fwd(x, weight, stride, pad, X6), lambda: _fwd(x, weight, stride, pad, X6 | BM256)]
+                 if _x6_ok(x, weight) else []) + \
             [lambda: _fwd(x, weight, stride, pad), lambda: F.conv2d(x, weight, None, stride, pad)]
         return cands[_fastest("fwd", ctx.key, cands)]()
 
@@ -151,7 +153,8 @@ class _Conv(torch.autograd.Function):
         mi_x = mi_w = False
         if need_x:
             if s == 1:
-                cands = ([lambda: _dgrad(gy, x, w, p, X6)] if _x6_ok(x, w) else []) + \
+                cands = ([lambda: _dgrad(gy, x, w, p, X6), lambda: _dgrad(gy, x, w, p, X6 | BM256)]
+                         if _x6_ok(x, w) else []) + \
                     [lambda: _dgrad(gy, x, w, p), lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
                 i = _fastest("dgrad", ctx.key, cands)
                 if i < len(cands) - 1:

@@ -59,6 +59,7 @@ struct ConvArgs {
     int mblocks, nblocks, splits, chunks_per_split, nchunks;
     int a_elems, b_elems;    // sizes of the two operands (the buffer-descriptor bounds)
     int bn;                  // tile width chosen by plan()
+    int bm;                  // x6 tile height (128 or 256)
     const float* a;          // fwd: x; dgrad: gy; wgrad: x
     const float* b;          // fwd / dgrad: weight; wgrad: gy
     float* y;                // output [M][N], or partials [splits][M][N]
@@ -393,27 +394,30 @@ __global__ __launch_bounds__(256) void conv_wsplit_kernel(const float* w, __bf16
     out[2 * n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, c) >> 16));
 }
 
-// NT threads: BN = 128 runs 8 waves (2 x 4, wave tile 64 x 32) so that two waves share
-// each SIMD and one's split VALU overlaps the other's MFMAs; BN = 64 runs 4 waves
-// (2 x 2, wave tile 64 x 32) at two blocks per CU.
-template <int BN>
+// Tiles BMX x BN.  NT threads: 8 waves (2 x 4 / 4 x 2 / 2 x 4, wave tiles 64/128 x 32)
+// whenever BN = 128 or BMX = 256, so that two waves share each SIMD and one's split
+// VALU overlaps the other's MFMAs; 128 x 64 runs 4 waves at two blocks per CU.  The
+// 256-row tile loads 1.5x the bytes of the 128-row one for 2x the MFMA work.
+template <int BN, int BMX>
 struct X6Geo {
-    static constexpr int NT = BN == 128 ? 512 : 256;
+    static constexpr int NT = (BN == 128 || BMX == 256) ? 512 : 256;
     static constexpr int WN = BN / 32;            // waves along N (wave tile 32 wide)
     static constexpr int WM = NT / 64 / WN;       // waves along M
-    static constexpr int TM = BM / 32 / WM;
+    static constexpr int TM = BMX / 32 / WM;
+    static constexpr int MINB = (BN == 64 && BMX == 128) ? 2 : 1;
 };
 
 // A (activations, NHWC f32, im2col rows) is split while staged; B comes pre-split
 // (conv_wsplit_kernel) and is copied in 16-byte quads.  Forward and stride-1 input
 // gradient alike (ConvArgs as the f32 path builds them; b = the planes).
-template <int BN>
-__global__ __launch_bounds__(X6Geo<BN>::NT, BN == 128 ? 1 : 2) void conv_x6_kernel(ConvArgs a) {
-    using G = X6Geo<BN>;
+template <int BN, int BMX>
+__global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void conv_x6_kernel(ConvArgs a) {
+    using G = X6Geo<BN, BMX>;
     constexpr int NT = G::NT, TM = G::TM;
-    constexpr int AQ = BM * XBK / 4 / NT;          // f32 quads of A per thread
+    constexpr int AQ = BMX * XBK / 4 / NT;         // f32 quads of A per thread
     constexpr int BQ = 3 * BN * (XBK / 8) / NT;    // bf16 quads (8 values) of B per thread
-    constexpr int PA = BM * XBK, PB = BN * XBK;    // bf16 elements per plane
+    constexpr int PA = BMX * XBK, PB = BN * XBK;   // bf16 elements per plane
+    static_assert(AQ * NT * 4 == BMX * XBK && BQ * NT == 3 * BN * (XBK / 8), "staging must tile the chunk");
     __shared__ __bf16 lds[2][3 * (PA + PB)];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(X6Geo<BN>::NT, BN == 128 ? 1 : 2) void conv_x6_kern
     const int nb = blk % a.nblocks;
     blk /= a.nblocks;
     const int mb = blk % a.mblocks, ks = blk / a.mblocks;
-    const int m0 = mb * BM, n0 = nb * BN;
+    const int m0 = mb * BMX, n0 = nb * BN;
     const int t0 = ks * a.chunks_per_split;
     const int nchunks = min(a.chunks_per_split, a.nchunks - t0);
     const int KT = a.KH * a.KW;
@@ -509,25 +513,23 @@ __global__ __launch_bounds__(X6Geo<BN>::NT, BN == 128 ? 1 : 2) void conv_x6_kern
         const __bf16* L = lds[buf];
 #pragma unroll
         for (int s = 0; s < XBK / 16; ++s) {
-            bf16x8 fa[TM][3], fb[3];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int e = xidx(wm * (TM * 32) + 32 * i + lr, 16 * s + 8 * h);
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl) fa[i][pl] = *(const bf16x8*)(L + pl * PA + e);
-            }
+            bf16x8 fb[3];
             const int eb = xidx(wn * 32 + lr, 16 * s + 8 * h);
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
+                bf16x8 fa[3];
+                const int e = xidx(wm * (TM * 32) + 32 * i + lr, 16 * s + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(L + pl * PA + e);
                 // small terms first: x2y0, x1y1, x0y2, x1y0, x0y1, x0y0
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[0], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[1], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[2], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[0], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[1], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
             }
         }
     };
@@ -875,13 +877,15 @@ ConvArgs args_of(const md2_conv_desc* d, int mode) {
     return a;
 }
 
-int resident_blocks_x6(int BN) { return 256 * (BN == 128 ? 1 : 2); }
+int resident_blocks_x6(int BN, int BMX) { return 256 * ((BN == 64 && BMX == 128) ? 2 : 1); }
 
-// x6 forward plan: BN = 128 unless N <= 64, K split by the same wave-quantisation model
+// x6 plan: BN = 128 unless N <= 64; BMX = 256 with MD2_CONV_BM256 (the caller's
+// autotune tries both); K split by the wave-quantisation model
 void plan_x6(ConvArgs& a, uint32_t flags, bool wgrad = false) {
     const int BN = (a.N <= 64 && !wgrad) ? 64 : 128;   // the weight-gradient kernel is 128 wide
-    const int mblocks = (a.M + BM - 1) / BM, nblocks = (a.N + BN - 1) / BN;
-    const int base = mblocks * nblocks, res = resident_blocks_x6(BN);
+    const int BMX = (!wgrad && BN == 128 && (flags & MD2_CONV_BM256)) ? 256 : 128;
+    const int mblocks = (a.M + BMX - 1) / BMX, nblocks = (a.N + BN - 1) / BN;
+    const int base = mblocks * nblocks, res = resident_blocks_x6(BN, BMX);
     int best_s = 1;
     double best_t = 1e30;
     const int smax = (flags & MD2_CONV_NO_SPLIT) ? 1 : (a.nchunks / 6 > 1 ? a.nchunks / 6 : 1);
@@ -889,15 +893,16 @@ void plan_x6(ConvArgs& a, uint32_t flags, bool wgrad = false) {
         const int per = (a.nchunks + sp - 1) / sp;
         const int splits = (a.nchunks + per - 1) / per;
         const int rounds = (base * splits + res - 1) / res;
-        // a chunk-round of blocks ~1.5k cycles; the split reduction moves (splits + 1)
-        // M x N floats at ~2.4 KB/cycle chip-wide
+        // a chunk-round of blocks ~1.5k cycles (x BMX/128); the split reduction moves
+        // (splits + 1) M x N floats at ~2.4 KB/cycle chip-wide
         const double red = splits > 1 ? (double)(splits + 1) * a.M * a.N * 4.0 / 2400.0 / 1536.0 : 0.0;
-        const double t = (double)rounds * per + red;
+        const double t = (double)rounds * per * (BMX / 128) + red;
         if (t < best_t - 1e-9) {
             best_t = t;
             best_s = splits;
         }
     }
+    a.bm = BMX;
     a.bn = BN;
     a.mblocks = mblocks;
     a.nblocks = nblocks;
@@ -969,8 +974,12 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
         hipLaunchKernelGGL(conv_wsplit_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, B, planes, d->out_channels,
                            d->kernel_h * d->kernel_w, d->in_channels, mode == MODE_DGRAD ? 1 : 0);
         const dim3 grid(a.mblocks * a.nblocks * a.splits);
-        if (BN == 128) hipLaunchKernelGGL((conv_x6_kernel<128>), grid, dim3(X6Geo<128>::NT), 0, st, a);
-        else hipLaunchKernelGGL((conv_x6_kernel<64>), grid, dim3(X6Geo<64>::NT), 0, st, a);
+        if (a.bm == 256) {
+            hipLaunchKernelGGL((conv_x6_kernel<128, 256>), grid, dim3(X6Geo<128, 256>::NT), 0, st, a);
+        } else {
+            if (BN == 128) hipLaunchKernelGGL((conv_x6_kernel<128, 128>), grid, dim3(X6Geo<128, 128>::NT), 0, st, a);
+            else hipLaunchKernelGGL((conv_x6_kernel<64, 128>), grid, dim3(X6Geo<64, 128>::NT), 0, st, a);
+        }
     } else if (mode == MODE_FWD) launch<MODE_FWD>(a, BN, st);
     else if (mode == MODE_DGRAD) launch<MODE_DGRAD>(a, BN, st);
     else launch<MODE_WGRAD>(a, BN, st);

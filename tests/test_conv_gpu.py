@@ -172,19 +172,21 @@ def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
     x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
     w = (torch.randn(N, C, k, k, device="cuda") / (C * k * k) ** 0.5).contiguous(memory_format=CL)
     ref = F.conv2d(x.double().cpu(), w.double().cpu(), None, s, p)
-    y_x6 = conv_ops._fwd(x, w, s, p, conv_ops.X6).double().cpu()
     y_mi = F.conv2d(x, w, None, s, p).double().cpu()
-    e_x6, e_mi = _rel(y_x6, ref), _rel(y_mi, ref)
-    assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, (e_x6, e_mi)
+    e_mi = _rel(y_mi, ref)
+    for fl in (conv_ops.X6, conv_ops.X6 | conv_ops.BM256):
+        e_x6 = _rel(conv_ops._fwd(x, w, s, p, fl).double().cpu(), ref)
+        assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, (fl, e_x6, e_mi)
     if s == 1:
         gy = torch.randn(ref.shape, device="cuda").contiguous(memory_format=CL)
         gref = torch.ops.aten.convolution_backward(gy.double().cpu(), x.double().cpu(), w.double().cpu(), None, (s, s),
                                                    (p, p), (1, 1), False, (0, 0), 1, (True, False, False))[0]
-        g_x6 = conv_ops._dgrad(gy, x, w, p, conv_ops.X6).double().cpu()
         g_mi = torch.ops.aten.convolution_backward(gy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
                                                    (True, False, False))[0].double().cpu()
-        e_x6, e_mi = _rel(g_x6, gref), _rel(g_mi, gref)
-        assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, (e_x6, e_mi)
+        e_mi = _rel(g_mi, gref)
+        for fl in (conv_ops.X6, conv_ops.X6 | conv_ops.BM256):
+            e_x6 = _rel(conv_ops._dgrad(gy, x, w, p, fl).double().cpu(), gref)
+            assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, (fl, e_x6, e_mi)
     gy = torch.randn(ref.shape, device="cuda").contiguous(memory_format=CL)
     wref = torch.ops.aten.convolution_backward(gy.double().cpu(), x.double().cpu(), w.double().cpu(), None, (s, s),
                                                (p, p), (1, 1), False, (0, 0), 1, (False, True, False))[1]

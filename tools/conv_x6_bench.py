@@ -34,6 +34,9 @@ def main():
             ref = F.conv2d(x.double().cpu(), w.double().cpu(), None, s, p).cuda() if gf < 8 else \
                 F.conv2d(x.double(), w.double(), None, s, p)
             t_x6 = timeit(lambda: fwd(x, w, s, p, X6))
+            t_256 = timeit(lambda: fwd(x, w, s, p, X6 | _lib.CONV_BM256))
+            row["fwd_x6_256_tf"] = round(gf / t_256, 1)
+            row["err_x6_256"] = errs(fwd(x, w, s, p, X6 | _lib.CONV_BM256), ref)
             t_f32 = timeit(lambda: fwd(x, w, s, p))
             t_mi = timeit(lambda: F.conv2d(x, w, None, s, p))
             row.update({"fwd_x6_tf": round(gf / t_x6, 1), "fwd_f32_tf": round(gf / t_f32, 1),
@@ -49,6 +52,7 @@ def main():
             mi = lambda: torch.ops.aten.convolution_backward(gy, x, w, None, (s, s), (p, p), (1, 1), False,  # noqa: E731
                                                              (0, 0), 1, (True, False, False))[0]
             t_x6 = timeit(lambda: dgrad(gy, x, w, s, p, X6))
+            row["dgrad_x6_256_tf"] = round(gf / timeit(lambda: dgrad(gy, x, w, s, p, X6 | _lib.CONV_BM256)), 1)
             t_f32 = timeit(lambda: dgrad(gy, x, w, s, p))
             t_mi = timeit(mi)
             row.update({"dgrad_x6_tf": round(gf / t_x6, 1), "dgrad_f32_tf": round(gf / t_f32, 1),
