@@ -451,6 +451,7 @@ int md2_maxpool3s2_bwd_add(const md2_pool_desc* desc, const uint32_t* idx, const
 #define MD2_CONV_TILE_N128 (1u << 4) /* force the 128 x 128 tile        */
 #define MD2_CONV_X6        (1u << 5) /* split-bf16 (3 planes, 6 products) f32-class MFMA path */
 #define MD2_CONV_BM256     (1u << 6) /* x6 forward / input grad: 256 x 128 tiles (N > 64)     */
+#define MD2_CONV_PRESPLIT  (1u << 7) /* x6: `weight` holds md2_conv_split_weights planes      */
 
 typedef struct md2_conv_desc {
     int32_t batch, height, width, in_channels; /* input */
@@ -459,6 +460,12 @@ typedef struct md2_conv_desc {
 } md2_conv_desc;
 
 size_t md2_conv_workspace_bytes(const md2_conv_desc* desc);
+/* The split-bf16 weight planes of md2_conv_fwd / md2_conv_dgrad with MD2_CONV_X6 in
+ * one pass: planes_fwd [3][Co][KH*KW][Ci] bf16 and (nullable) planes_dgrad
+ * [3][Ci][KH*KW][Co] (taps flipped); pass them as `weight` with MD2_CONV_PRESPLIT.
+ * Channels must be multiples of 8. */
+int md2_conv_split_weights(const md2_conv_desc* desc, const float* weight, void* planes_fwd, void* planes_dgrad,
+                           void* stream);
 int md2_conv_fwd(const md2_conv_desc* desc, const float* x, const float* weight, float* y, void* workspace,
                  void* stream);
 /* grad_x (batch, height, width, in_channels) from grad_y (batch, Ho, Wo, out_channels);

@@ -62,7 +62,7 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_disp_head_workspace_bytes", "md2_disp_head_fwd", "md2_disp_head_bwd",
            "md2_stem_wgrad_workspace_bytes", "md2_stem_wgrad", "md2_bias_act_fwd", "md2_bias_act_bwd",
            "md2_bias_act_workspace_bytes", "md2_maxpool3s2_bwd_add", "md2_bn_bwd_multi",
-           "md2_conv_fwd", "md2_conv_workspace_bytes",
+           "md2_conv_fwd", "md2_conv_workspace_bytes", "md2_conv_split_weights",
            "md2_conv_dgrad", "md2_conv_wgrad"]
 
 PAD_ELU = 1 << 0
@@ -108,6 +108,7 @@ CONV_TILE_N64 = 1 << 3
 CONV_TILE_N128 = 1 << 4
 CONV_X6 = 1 << 5
 CONV_BM256 = 1 << 6
+CONV_PRESPLIT = 1 << 7
 
 
 class ConvDesc(ctypes.Structure):
@@ -158,6 +159,8 @@ def _declare(L):
     L.md2_conv_dgrad.argtypes = [ctypes.POINTER(ConvDesc)] + [_vp] * 5
     L.md2_conv_wgrad.restype = ctypes.c_int
     L.md2_conv_wgrad.argtypes = [ctypes.POINTER(ConvDesc)] + [_vp] * 5
+    L.md2_conv_split_weights.restype = ctypes.c_int
+    L.md2_conv_split_weights.argtypes = [ctypes.POINTER(ConvDesc)] + [_vp] * 4
     L.md2_conv_workspace_bytes.restype = ctypes.c_size_t
     L.md2_conv_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc)]
     L.md2_stem_wgrad_workspace_bytes.restype = ctypes.c_size_t

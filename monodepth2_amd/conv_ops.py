@@ -43,6 +43,8 @@ _ws: Dict[Tuple[int, int], torch.Tensor] = {}
 _choice: Dict[tuple, int] = {}     # (op, shape) -> index of the fastest candidate
 X6 = _lib.CONV_X6
 BM256 = _lib.CONV_BM256
+PRESPLIT = _lib.CONV_PRESPLIT
+_FLAGS = (X6, X6 | BM256)    # the x6 candidates, in candidate order
 
 
 def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
@@ -85,6 +87,36 @@ def _dgrad(gy, x, w, pad, flags=0):
 
 def _x6_ok(x, w) -> bool:
     return x.shape[1] % 8 == 0 and w.shape[0] % 8 == 0
+
+
+def _split_weights(x, w, stride, pad, dgrad: bool):
+    """The weight's split-bf16 planes for the forward and (stride 1) the input
+    gradient, one launch (md2_conv_split_weights); used with MD2_CONV_PRESPLIT."""
+    n = w.numel()
+    pf = torch.empty(3 * n, dtype=torch.bfloat16, device=w.device)
+    pd = torch.empty(3 * n, dtype=torch.bfloat16, device=w.device) if dgrad else None
+    _lib.check(_lib.lib().md2_conv_split_weights(ctypes.byref(_desc(x, w, stride, pad)), w.data_ptr(), pf.data_ptr(),
+                                                 pd.data_ptr() if pd is not None else None,
+                                                 torch.cuda.current_stream(w.device).cuda_stream),
+               "md2_conv_split_weights")
+    return pf, pd
+
+
+def _fwd_planes(x, w, planes, stride, pad, flags):
+    B, _, H, W = x.shape
+    N, _, KH, KW = w.shape
+    y = torch.empty(B, N, (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1, device=x.device,
+                    memory_format=_CL)
+    _call("md2_conv_fwd", _desc(x, w, stride, pad, flags | PRESPLIT), x.data_ptr(), planes.data_ptr(), y.data_ptr(),
+          x.device)
+    return y
+
+
+def _dgrad_planes(gy, x, w, planes, pad, flags):
+    gx = torch.empty_like(x, memory_format=_CL)
+    _call("md2_conv_dgrad", _desc(x, w, 1, pad, flags | PRESPLIT), gy.data_ptr(), planes.data_ptr(), gx.data_ptr(),
+          x.device)
+    return gx
 
 
 def _wgrad(gy, x, w, stride, pad, flags=0):
@@ -135,17 +167,27 @@ class _Conv(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, stride: int, pad: int):
-        ctx.save_for_backward(x, weight)
         ctx.stride, ctx.pad = stride, pad
         ctx.key = (tuple(x.shape), tuple(weight.shape), stride, pad)
+        x6 = _x6_ok(x, weight)
         cands = ([lambda: _fwd(x, weight, stride, pad, X6), lambda: _fwd(x, weight, stride, pad, X6 | BM256)]
-                 if _x6_ok(x, weight) else []) + \
+                 if x6 else []) + \
             [lambda: _fwd(x, weight, stride, pad), lambda: F.conv2d(x, weight, None, stride, pad)]
-        return cands[_fastest("fwd", ctx.key, cands)]()
+        i = _fastest("fwd", ctx.key, cands)
+        planes_dg = None
+        if x6 and i < 2:
+            # the x6 forward: split the weight once for it and for the input gradient
+            # (one launch), the dgrad planes kept for the backward
+            pf, planes_dg = _split_weights(x, weight, stride, pad, stride == 1)
+            y = _fwd_planes(x, weight, pf, stride, pad, _FLAGS[i])
+        else:
+            y = cands[i]()
+        ctx.save_for_backward(x, weight, planes_dg)
+        return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, w = ctx.saved_tensors
+        x, w, planes_dg = ctx.saved_tensors
         s, p = ctx.stride, ctx.pad
         gy = gy.contiguous(memory_format=_CL)
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
@@ -153,11 +195,13 @@ class _Conv(torch.autograd.Function):
         mi_x = mi_w = False
         if need_x:
             if s == 1:
-                cands = ([lambda: _dgrad(gy, x, w, p, X6), lambda: _dgrad(gy, x, w, p, X6 | BM256)]
-                         if _x6_ok(x, w) else []) + \
+                x6 = _x6_ok(x, w)
+                cands = ([lambda: _dgrad(gy, x, w, p, X6), lambda: _dgrad(gy, x, w, p, X6 | BM256)] if x6 else []) + \
                     [lambda: _dgrad(gy, x, w, p), lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
                 i = _fastest("dgrad", ctx.key, cands)
-                if i < len(cands) - 1:
+                if x6 and i < 2 and planes_dg is not None:
+                    gx = _dgrad_planes(gy, x, w, planes_dg, p, _FLAGS[i])
+                elif i < len(cands) - 1:
                     gx = cands[i]()
                 else:
                     mi_x = True

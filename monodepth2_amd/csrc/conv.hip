@@ -394,6 +394,30 @@ __global__ __launch_bounds__(256) void conv_wsplit_kernel(const float* w, __bf16
     out[2 * n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, c) >> 16));
 }
 
+// Both layouts in one pass (md2_conv_split_weights): the forward planes [3][Co][KT][Ci]
+// and, if `dg` is non-null, the input gradient's flipped/transposed [3][Ci][KT][Co].
+__global__ __launch_bounds__(256) void conv_wsplit2_kernel(const float* w, __bf16* fw, __bf16* dg, int Co, int KT,
+                                                           int Ci) {
+    const int n = Co * KT * Ci;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float v = w[i];
+    const float a = trunc16(v), r1 = v - a, b = trunc16(r1), c = r1 - b;
+    const __bf16 p0 = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, a) >> 16));
+    const __bf16 p1 = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, b) >> 16));
+    const __bf16 p2 = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, c) >> 16));
+    fw[i] = p0;
+    fw[n + i] = p1;
+    fw[2 * n + i] = p2;
+    if (dg) {
+        const int ci = i % Ci, rest = i / Ci, t = rest % KT, co = rest / KT;
+        const int j = (ci * KT + (KT - 1 - t)) * Co + co;
+        dg[j] = p0;
+        dg[n + j] = p1;
+        dg[2 * n + j] = p2;
+    }
+}
+
 // Tiles BMX x BN.  NT threads: 8 waves (2 x 4 / 4 x 2 / 2 x 4, wave tiles 64/128 x 32)
 // whenever BN = 128 or BMX = 256, so that two waves share each SIMD and one's split
 // VALU overlaps the other's MFMAs; 128 x 64 runs 4 waves at two blocks per CU.  The
@@ -965,14 +989,16 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
         const dim3 grid(a.mblocks * a.nblocks * a.splits);
         hipLaunchKernelGGL(conv_x6_wgrad_kernel, grid, dim3(512), 0, st, a);
     } else if (use_x6(d, mode)) {
-        // B: the weights split into bf16 planes at the front of the workspace
-        __bf16* planes = (__bf16*)ws;
+        // B: the weights split into bf16 planes at the front of the workspace, or
+        // already split by the caller (MD2_CONV_PRESPLIT: `weight` is the planes)
+        __bf16* planes = (d->flags & MD2_CONV_PRESPLIT) ? (__bf16*)B : (__bf16*)ws;
         a.b = (const float*)planes;
         a.b_elems = 3 * d->out_channels * d->kernel_h * d->kernel_w * d->in_channels;
         if (a.splits > 1) a.y = (float*)((char*)ws + x6_planes_bytes(d));
         const int nw = a.b_elems / 3;
-        hipLaunchKernelGGL(conv_wsplit_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, B, planes, d->out_channels,
-                           d->kernel_h * d->kernel_w, d->in_channels, mode == MODE_DGRAD ? 1 : 0);
+        if (!(d->flags & MD2_CONV_PRESPLIT))
+            hipLaunchKernelGGL(conv_wsplit_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, B, planes,
+                               d->out_channels, d->kernel_h * d->kernel_w, d->in_channels, mode == MODE_DGRAD ? 1 : 0);
         const dim3 grid(a.mblocks * a.nblocks * a.splits);
         if (a.bm == 256) {
             hipLaunchKernelGGL((conv_x6_kernel<128, 256>), grid, dim3(X6Geo<128, 256>::NT), 0, st, a);
@@ -1016,6 +1042,19 @@ size_t md2_conv_workspace_bytes(const md2_conv_desc* d) {
     if (d->stride == 1) m = m > ws_bytes(d, MODE_DGRAD) ? m : ws_bytes(d, MODE_DGRAD);
     const size_t w = ws_bytes(d, MODE_WGRAD);
     return m > w ? m : w;
+}
+
+int md2_conv_split_weights(const md2_conv_desc* d, const float* weight, void* planes_fwd, void* planes_dgrad,
+                           void* stream) {
+    if (!valid(d) || d->in_channels % 8 || d->out_channels % 8)
+        return md2_report_error(MD2_ERR_ARG, "conv_split_weights: channels % 8, pad < kernel, sizes < 2^29");
+    if (!weight || !planes_fwd) return md2_report_error(MD2_ERR_ARG, "conv_split_weights: NULL operand");
+    const int n = d->out_channels * d->kernel_h * d->kernel_w * d->in_channels;
+    hipLaunchKernelGGL(conv_wsplit2_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, weight,
+                       (__bf16*)planes_fwd, (__bf16*)planes_dgrad, d->out_channels, d->kernel_h * d->kernel_w,
+                       d->in_channels);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }
 
 int md2_conv_fwd(const md2_conv_desc* d, const float* x, const float* weight, float* y, void* workspace,

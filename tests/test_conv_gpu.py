@@ -195,3 +195,17 @@ def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
                                                (False, True, False))[1].double().cpu()
     e_x6, e_mi = _rel(w_x6, wref), _rel(w_mi, wref)
     assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, ("wgrad", e_x6, e_mi)
+
+
+def test_x6_presplit_planes_match_in_call_split():
+    """md2_conv_split_weights (both layouts in one pass) + MD2_CONV_PRESPLIT gives
+    bitwise the result of the x6 calls that split the weight themselves."""
+    torch.manual_seed(5)
+    B, C, N, H, W = 2, 64, 128, 12, 20
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    w = (torch.randn(N, C, 3, 3, device="cuda") / 24).contiguous(memory_format=CL)
+    gy = torch.randn(B, N, H, W, device="cuda").contiguous(memory_format=CL)
+    pf, pd = conv_ops._split_weights(x, w, 1, 1, True)
+    for fl in (conv_ops.X6, conv_ops.X6 | conv_ops.BM256):
+        assert torch.equal(conv_ops._fwd_planes(x, w, pf, 1, 1, fl), conv_ops._fwd(x, w, 1, 1, fl))
+        assert torch.equal(conv_ops._dgrad_planes(gy, x, w, pd, 1, fl), conv_ops._dgrad(gy, x, w, 1, fl))
