@@ -394,28 +394,29 @@ __global__ __launch_bounds__(256) void conv_wsplit_kernel(const float* w, __bf16
     out[2 * n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, c) >> 16));
 }
 
-// Both layouts in one pass (md2_conv_split_weights): the forward planes [3][Co][KT][Ci]
-// and, if `dg` is non-null, the input gradient's flipped/transposed [3][Ci][KT][Co].
+// Both layouts in one launch (md2_conv_split_weights): threads [0, n) write the
+// forward planes [3][Co][KT][Ci], threads [n, 2n) (if `dg` is non-null) the input
+// gradient's flipped/transposed [3][Ci][KT][Co], each indexed by its OUTPUT element
+// so that the 2-byte stores coalesce (the gather of w is the strided side).
 __global__ __launch_bounds__(256) void conv_wsplit2_kernel(const float* w, __bf16* fw, __bf16* dg, int Co, int KT,
                                                            int Ci) {
     const int n = Co * KT * Ci;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const float v = w[i];
-    const float a = trunc16(v), r1 = v - a, b = trunc16(r1), c = r1 - b;
-    const __bf16 p0 = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, a) >> 16));
-    const __bf16 p1 = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, b) >> 16));
-    const __bf16 p2 = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, c) >> 16));
-    fw[i] = p0;
-    fw[n + i] = p1;
-    fw[2 * n + i] = p2;
-    if (dg) {
-        const int ci = i % Ci, rest = i / Ci, t = rest % KT, co = rest / KT;
-        const int j = (ci * KT + (KT - 1 - t)) * Co + co;
-        dg[j] = p0;
-        dg[n + j] = p1;
-        dg[2 * n + j] = p2;
+    int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= (dg ? 2 * n : n)) return;
+    __bf16* out = fw;
+    float v;
+    if (i < n) {
+        v = w[i];
+    } else {
+        i -= n;
+        out = dg;
+        const int co = i % Co, rest = i / Co, t = rest % KT, ci = rest / KT;   // out [ci][t][co]
+        v = w[((size_t)co * KT + (KT - 1 - t)) * Ci + ci];
     }
+    const float a = trunc16(v), r1 = v - a, b = trunc16(r1), c = r1 - b;
+    out[i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, a) >> 16));
+    out[n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, b) >> 16));
+    out[2 * n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, c) >> 16));
 }
 
 // Tiles BMX x BN.  NT threads: 8 waves (2 x 4 / 4 x 2 / 2 x 4, wave tiles 64/128 x 32)
@@ -1050,7 +1051,8 @@ int md2_conv_split_weights(const md2_conv_desc* d, const float* weight, void* pl
         return md2_report_error(MD2_ERR_ARG, "conv_split_weights: channels % 8, pad < kernel, sizes < 2^29");
     if (!weight || !planes_fwd) return md2_report_error(MD2_ERR_ARG, "conv_split_weights: NULL operand");
     const int n = d->out_channels * d->kernel_h * d->kernel_w * d->in_channels;
-    hipLaunchKernelGGL(conv_wsplit2_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, weight,
+    const int total = planes_dgrad ? 2 * n : n;
+    hipLaunchKernelGGL(conv_wsplit2_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, weight,
                        (__bf16*)planes_fwd, (__bf16*)planes_dgrad, d->out_channels, d->kernel_h * d->kernel_w,
                        d->in_channels);
     const hipError_t e = hipGetLastError();

@@ -3,11 +3,11 @@
 # WRITE_SIZE in separate --pmc passes over the bench command); summarise with
 # tools/kernel_hbm_table.py.  Output: gpurun_out/$ROUND/hbm{0,1}/
 set -o pipefail
-ROUND=${ROUND:-r01}
+ROUND=${ROUND:-r02}
 OUT=gpurun_out/$ROUND
 mkdir -p $OUT
 export TMPDIR=/tmp
-RE="photo_|disp_grad|smooth_fwd|grad_T|finalize|pad_fwd|pad_bwd|bias_grad|pose_|bn_|head_|adam|maxpool|encoder_input|bias_act"
+RE="photo_|pack_src8|disp_grad|smooth_fwd|grad_T|finalize|pad_fwd|pad_bwd|bias_grad|pose_|bn_|head_|adam|maxpool|encoder_input|bias_act|conv_x6|conv_wsplit|conv_reduce"
 i=0
 for p in "FETCH_SIZE" "WRITE_SIZE"; do
     timeout -k 10 300 rocprofv3 --pmc $p --kernel-include-regex "$RE" \

@@ -38,7 +38,8 @@ def main():
     res = {}
     for r in rows:
         k = short(r["Name"])
-        if any(t in k for t in ("photo_", "disp_grad", "smooth_fwd", "grad_T", "finalize_fwd")):
+        if any(t in k for t in ("photo_", "pack_src8", "disp_grad", "smooth_fwd", "grad_T", "finalize_fwd", "conv_x6",
+                                "conv_wsplit")):
             res.setdefault(k, {}).update(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
                                          share_of_gpu_time=float(r["TotalDurationNs"]) / total)
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -53,6 +54,9 @@ def main():
             d["hbm_read_bytes_corrected"] = 2 * d["FETCH_SIZE"] * 1024
             d["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
             d["hbm_traffic_bytes"] = d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in d and "GRBM_GUI_ACTIVE" in d:
+            # MFMA-busy cycles summed over the 1024 SIMDs / kernel cycles
+            d["mfma_busy_frac"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024.0 / (d["GRBM_GUI_ACTIVE"] / 8.0)
         if "SQ_INSTS_VALU" in d and "avg_ns" in d:
             d["valu_issue_frac"] = d["SQ_INSTS_VALU"] / (d["avg_ns"] * 1e-9 * VALU_ISSUE_PER_S)
         if "TD_TD_BUSY_sum" in d and "GRBM_GUI_ACTIVE" in d:
@@ -65,7 +69,11 @@ def main():
             d["l2_hit_rate"] = d["TCC_HIT_sum"] / max(1.0, d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
     json.dump(res, open(os.path.join(dst, "hot_kernels.json"), "w"), indent=1, sort_keys=True)
     bwd = next(v for k, v in res.items() if k.startswith("photo_bwd"))
-    fwd = next(v for k, v in res.items() if k.startswith("photo_fwd"))
+    # the forward is three launches (identity, reprojection, combine); its main kernel
+    # is the reprojection pass, the byte total sums the three
+    fwd = dict(next(v for k, v in res.items() if k.startswith("photo_reproj")))
+    fwd["hbm_traffic_bytes"] = sum(v.get("hbm_traffic_bytes", 0.0) for k, v in res.items()
+                                   if k.startswith(("photo_ident", "photo_reproj", "photo_combine")))
     traffic = {"photo_bwd_kernel_bytes_per_launch": bwd.get("hbm_traffic_bytes"),
                "photo_fwd_kernel_bytes_per_launch": fwd.get("hbm_traffic_bytes"),
                "photo_bwd_valu_issue_frac": bwd.get("valu_issue_frac"),
@@ -82,7 +90,7 @@ def main():
     for k, d in sorted(res.items()):
         print(k, {c: round(v, 4) if isinstance(v, float) else v for c, v in d.items()
                   if c in ("calls", "avg_ns", "share_of_gpu_time", "hbm_traffic_bytes", "valu_issue_frac",
-                           "l2_hit_rate", "td_busy_frac", "ta_busy_frac")})
+                           "l2_hit_rate", "td_busy_frac", "ta_busy_frac", "mfma_busy_frac")})
 
 
 if __name__ == "__main__":
