@@ -254,6 +254,14 @@ def lib():
     return _lib
 
 
+def stream(device) -> int:
+    """The raw hipStream_t of `device`'s current stream (what torch.cuda.current_stream(
+    device).cuda_stream returns, without building a Stream object: ~10x cheaper on the
+    host, and this is called for every kernel the step launches)."""
+    idx = device.index if isinstance(device, torch.device) else device
+    return torch._C._cuda_getCurrentRawStream(torch.cuda.current_device() if idx is None else idx)
+
+
 def check(rc: int, what: str):
     if rc != 0:
         msg = lib().md2_last_error().decode(errors="replace")

@@ -135,7 +135,7 @@ class GpuAugment:
             color_aug.append(torch.empty(shp, device=self.device))
         cp = (ctypes.c_void_p * self.num_scales)(*[t.data_ptr() for t in color])
         ap = (ctypes.c_void_p * self.num_scales)(*[t.data_ptr() for t in color_aug])
-        stream = torch.cuda.current_stream(self.device).cuda_stream
+        stream = _lib.stream(self.device)
         _lib.check(_lib.lib().md2_aug_run(self._plan, frames.data_ptr(), ctypes.byref(items), cp, ap, stream),
                    "md2_aug_run")
         return color, color_aug

@@ -47,11 +47,10 @@ def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
     """Scratch (partial sums + backward coefficients) per HIP stream: calls on one
     stream are ordered, calls on different streams (the trainer runs the pose
     network beside the depth network) must not share it."""
-    stream = torch.cuda.current_stream(device)
-    key = stream.cuda_stream
+    key = _lib.stream(device)
     ws = _workspaces.get(key)
     if ws is None or ws.numel() < nbytes:
-        with torch.cuda.stream(stream):
+        with torch.cuda.stream(torch.cuda.current_stream(device)):
             ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
         _workspaces[key] = ws
     return ws
@@ -77,7 +76,7 @@ class _BNAct(torch.autograd.Function):
         y = torch.empty_like(x, memory_format=_CL)
         mean = torch.empty(groups, C, device=x.device)
         invstd = torch.empty(groups, C, device=x.device)
-        stream = torch.cuda.current_stream(x.device).cuda_stream
+        stream = _lib.stream(x.device)
         rc = L.md2_bn_fwd(ctypes.byref(d), x.data_ptr(), weight.data_ptr(), bias.data_ptr(),
                           residual.data_ptr() if residual is not None else None,
                           running_mean.data_ptr() if running_mean is not None else None,
@@ -113,7 +112,7 @@ class _BNAct(torch.autograd.Function):
                                 gs[2].data_ptr() if len(gs) > 2 else None,
                                 weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gx.data_ptr(),
                                 gr.data_ptr() if gr is not None else None, gw.data_ptr(), gb.data_ptr(), ws.data_ptr(),
-                                torch.cuda.current_stream(x.device).cuda_stream)
+                                _lib.stream(x.device))
         _lib.check(rc, "md2_bn_bwd_multi")
         return gx, gw, gb, None, None, gr, None, None, None, None, None
 
@@ -164,7 +163,7 @@ class _MaxPool(torch.autograd.Function):
         d = _lib.PoolDesc(B, C, H, W, _lib.POOL_BF16 if x.dtype == torch.bfloat16 else 0, 0)
         y = torch.empty((B, C, Ho, Wo), device=x.device, dtype=x.dtype, memory_format=_CL)
         idx = torch.empty(B * Ho * Wo * C // 4, device=x.device, dtype=torch.int32)
-        stream = torch.cuda.current_stream(x.device).cuda_stream
+        stream = _lib.stream(x.device)
         _lib.check(_lib.lib().md2_maxpool3s2_fwd(ctypes.byref(d), x.data_ptr(), y.data_ptr(), idx.data_ptr(), stream),
                    "md2_maxpool3s2_fwd")
         ctx.save_for_backward(idx)
@@ -187,7 +186,7 @@ class _MaxPool(torch.autograd.Function):
         d = _lib.PoolDesc(*ctx.desc)
         _lib.check(_lib.lib().md2_maxpool3s2_bwd_add(ctypes.byref(d), idx.data_ptr(), gy.data_ptr(),
                                                      galias.data_ptr() if galias is not None else None,
-                                                     gx.data_ptr(), torch.cuda.current_stream(gy.device).cuda_stream),
+                                                     gx.data_ptr(), _lib.stream(gy.device)),
                    "md2_maxpool3s2_bwd_add")
         return gx, None
 

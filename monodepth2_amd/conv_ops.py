@@ -49,7 +49,7 @@ _FLAGS = (X6, X6 | BM256)    # the x6 candidates, in candidate order
 
 def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
     """K-split partials, one buffer per HIP stream (the pose network runs on its own)."""
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    key = (device.index, _lib.stream(device))
     ws = _ws.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
@@ -57,17 +57,31 @@ def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
     return ws
 
 
+_descs: Dict[tuple, tuple] = {}   # (shape, stride, pad, flags) -> (ConvDesc, workspace bytes)
+
+
+def _desc_ws(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, flags: int = 0):
+    """The call's ConvDesc and workspace size, built once per (shape, flags): the conv
+    path runs ~100 times per step and its host cost counts (the step is close to
+    launch-bound)."""
+    k = (tuple(x.shape), tuple(w.shape), stride, pad, flags)
+    hit = _descs.get(k)
+    if hit is None:
+        B, C, H, W = x.shape
+        N, _, KH, KW = w.shape
+        d = _lib.ConvDesc(B, H, W, C, N, KH, KW, stride, pad, flags)
+        hit = _descs[k] = (d, _lib.lib().md2_conv_workspace_bytes(ctypes.byref(d)))
+    return hit
+
+
 def _desc(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, flags: int = 0):
-    B, C, H, W = x.shape
-    N, _, KH, KW = w.shape
-    return _lib.ConvDesc(B, H, W, C, N, KH, KW, stride, pad, flags)
+    return _desc_ws(x, w, stride, pad, flags)[0]
 
 
-def _call(fn: str, d, p0, p1, p2, device):
-    L = _lib.lib()
-    ws = _workspace(device, L.md2_conv_workspace_bytes(ctypes.byref(d)))
-    _lib.check(getattr(L, fn)(ctypes.byref(d), p0, p1, p2, ws.data_ptr(), torch.cuda.current_stream(device).cuda_stream),
-               fn)
+def _call(fn: str, x, w, stride, pad, flags, p0, p1, p2, device):
+    d, nbytes = _desc_ws(x, w, stride, pad, flags)
+    ws = _workspace(device, nbytes)
+    _lib.check(getattr(_lib.lib(), fn)(ctypes.byref(d), p0, p1, p2, ws.data_ptr(), _lib.stream(device)), fn)
 
 
 def _fwd(x, w, stride, pad, flags=0):
@@ -75,13 +89,13 @@ def _fwd(x, w, stride, pad, flags=0):
     N, _, KH, KW = w.shape
     y = torch.empty(B, N, (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1, device=x.device,
                     memory_format=_CL)
-    _call("md2_conv_fwd", _desc(x, w, stride, pad, flags), x.data_ptr(), w.data_ptr(), y.data_ptr(), x.device)
+    _call("md2_conv_fwd", x, w, stride, pad, flags, x.data_ptr(), w.data_ptr(), y.data_ptr(), x.device)
     return y
 
 
 def _dgrad(gy, x, w, pad, flags=0):
     gx = torch.empty_like(x, memory_format=_CL)
-    _call("md2_conv_dgrad", _desc(x, w, 1, pad, flags), gy.data_ptr(), w.data_ptr(), gx.data_ptr(), x.device)
+    _call("md2_conv_dgrad", x, w, 1, pad, flags, gy.data_ptr(), w.data_ptr(), gx.data_ptr(), x.device)
     return gx
 
 
@@ -97,7 +111,7 @@ def _split_weights(x, w, stride, pad, dgrad: bool):
     pd = torch.empty(3 * n, dtype=torch.bfloat16, device=w.device) if dgrad else None
     _lib.check(_lib.lib().md2_conv_split_weights(ctypes.byref(_desc(x, w, stride, pad)), w.data_ptr(), pf.data_ptr(),
                                                  pd.data_ptr() if pd is not None else None,
-                                                 torch.cuda.current_stream(w.device).cuda_stream),
+                                                 _lib.stream(w.device)),
                "md2_conv_split_weights")
     return pf, pd
 
@@ -107,27 +121,34 @@ def _fwd_planes(x, w, planes, stride, pad, flags):
     N, _, KH, KW = w.shape
     y = torch.empty(B, N, (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1, device=x.device,
                     memory_format=_CL)
-    _call("md2_conv_fwd", _desc(x, w, stride, pad, flags | PRESPLIT), x.data_ptr(), planes.data_ptr(), y.data_ptr(),
+    _call("md2_conv_fwd", x, w, stride, pad, flags | PRESPLIT, x.data_ptr(), planes.data_ptr(), y.data_ptr(),
           x.device)
     return y
 
 
 def _dgrad_planes(gy, x, w, planes, pad, flags):
     gx = torch.empty_like(x, memory_format=_CL)
-    _call("md2_conv_dgrad", _desc(x, w, 1, pad, flags | PRESPLIT), gy.data_ptr(), planes.data_ptr(), gx.data_ptr(),
+    _call("md2_conv_dgrad", x, w, 1, pad, flags | PRESPLIT, gy.data_ptr(), planes.data_ptr(), gx.data_ptr(),
           x.device)
     return gx
 
 
 def _wgrad(gy, x, w, stride, pad, flags=0):
     gw = torch.empty_like(w, memory_format=_CL)
-    _call("md2_conv_wgrad", _desc(x, w, stride, pad, flags), x.data_ptr(), gy.data_ptr(), gw.data_ptr(), x.device)
+    _call("md2_conv_wgrad", x, w, stride, pad, flags, x.data_ptr(), gy.data_ptr(), gw.data_ptr(), x.device)
     return gw
 
 
 def _miopen_bwd(gy, x, w, stride, pad, mask):
     return torch.ops.aten.convolution_backward(gy, x, w, None, (stride, stride), (pad, pad), (1, 1), False, (0, 0), 1,
                                                mask)
+
+
+def _cached(op: str, key: tuple):
+    """The remembered choice for (op, shape), 0 without AUTOTUNE, None if not timed yet."""
+    if not AUTOTUNE:
+        return 0
+    return _choice.get((op,) + key)
 
 
 def _fastest(op: str, key: tuple, cands) -> int:
@@ -170,10 +191,14 @@ class _Conv(torch.autograd.Function):
         ctx.stride, ctx.pad = stride, pad
         ctx.key = (tuple(x.shape), tuple(weight.shape), stride, pad)
         x6 = _x6_ok(x, weight)
-        cands = ([lambda: _fwd(x, weight, stride, pad, X6), lambda: _fwd(x, weight, stride, pad, X6 | BM256)]
-                 if x6 else []) + \
-            [lambda: _fwd(x, weight, stride, pad), lambda: F.conv2d(x, weight, None, stride, pad)]
-        i = _fastest("fwd", ctx.key, cands)
+        cands = None
+        i = _cached("fwd", ctx.key)
+        if i is None or not (x6 and i < 2):
+            cands = ([lambda: _fwd(x, weight, stride, pad, X6), lambda: _fwd(x, weight, stride, pad, X6 | BM256)]
+                     if x6 else []) + \
+                [lambda: _fwd(x, weight, stride, pad), lambda: F.conv2d(x, weight, None, stride, pad)]
+            if i is None:
+                i = _fastest("fwd", ctx.key, cands)
         planes_dg = None
         if x6 and i < 2:
             # the x6 forward: split the weight once for it and for the input gradient

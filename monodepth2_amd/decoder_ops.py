@@ -46,7 +46,7 @@ class _ConvInput(torch.autograd.Function):
         rc = _lib.lib().md2_decoder_pad_fwd(ctypes.byref(d), x.data_ptr(),
                                             skip.data_ptr() if skip is not None else None,
                                             bias32.data_ptr() if bias32 is not None else None, out.data_ptr(),
-                                            torch.cuda.current_stream(x.device).cuda_stream)
+                                            _lib.stream(x.device))
         _lib.check(rc, "md2_decoder_pad_fwd")
         ctx.elu, ctx.upsample, ctx.has_skip, ctx.nhwc, ctx.bf16 = elu, upsample, skip is not None, nhwc, bf16
         ctx.skip_shape = None if skip is None else skip.shape
@@ -77,7 +77,7 @@ class _ConvInput(torch.autograd.Function):
                                             gskip.data_ptr() if gskip is not None else None,
                                             gbias.data_ptr() if gbias is not None else None,
                                             ws.data_ptr() if ws is not None else None,
-                                            torch.cuda.current_stream(gout.device).cuda_stream)
+                                            _lib.stream(gout.device))
         _lib.check(rc, "md2_decoder_pad_bwd")
         if gbias is not None and ctx.bias_dtype != torch.float32:
             gbias = gbias.to(ctx.bias_dtype)
@@ -96,7 +96,7 @@ class _DispHead(torch.autograd.Function):
         d = _lib.HeadDesc(B, C, Hp - 2, Wp - 2, _lib.HEAD_WEIGHT_CL if w_cl else 0)
         disp = torch.empty(B, 1, Hp - 2, Wp - 2, device=P.device, dtype=torch.float32)
         rc = _lib.lib().md2_disp_head_fwd(ctypes.byref(d), P.data_ptr(), weight.data_ptr(), bias.data_ptr(),
-                                          disp.data_ptr(), torch.cuda.current_stream(P.device).cuda_stream)
+                                          disp.data_ptr(), _lib.stream(P.device))
         _lib.check(rc, "md2_disp_head_fwd")
         ctx.d = d
         ctx.save_for_backward(P, weight, disp)
@@ -114,7 +114,7 @@ class _DispHead(torch.autograd.Function):
                          device=P.device)
         rc = _lib.lib().md2_disp_head_bwd(ctypes.byref(d), P.data_ptr(), weight.data_ptr(), disp.data_ptr(),
                                           gdisp.data_ptr(), gP.data_ptr(), gw.data_ptr(), gb.data_ptr(),
-                                          ws.data_ptr(), torch.cuda.current_stream(P.device).cuda_stream)
+                                          ws.data_ptr(), _lib.stream(P.device))
         _lib.check(rc, "md2_disp_head_bwd")
         return gP, gw, gb
 
@@ -149,7 +149,7 @@ class _ConvBiasAct(torch.autograd.Function):
         B, C, H, W = z.shape
         d = _lib.BiasActDesc(B * H * W, C, _lib.BIAS_ACT_RELU if relu else 0)
         _lib.check(_lib.lib().md2_bias_act_fwd(ctypes.byref(d), z.data_ptr(), bias.data_ptr(), z.data_ptr(),
-                                               torch.cuda.current_stream(z.device).cuda_stream),
+                                               _lib.stream(z.device)),
                    "md2_bias_act_fwd")                      # in place: z is this op's own buffer
         ctx.save_for_backward(x, weight, z if relu else None)
         ctx.conf = (stride, padding, relu, d)
@@ -166,7 +166,7 @@ class _ConvBiasAct(torch.autograd.Function):
         ws = torch.empty(L.md2_bias_act_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=gy.device)
         _lib.check(L.md2_bias_act_bwd(ctypes.byref(d), y.data_ptr() if relu else None, gy.data_ptr(),
                                       gz.data_ptr() if relu else None, gb.data_ptr(), ws.data_ptr(),
-                                      torch.cuda.current_stream(gy.device).cuda_stream),
+                                      _lib.stream(gy.device)),
                    "md2_bias_act_bwd")
         gx, gw, _ = torch.ops.aten.convolution_backward(
             gz, x, weight, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,

@@ -72,7 +72,7 @@ class HotPathConfig:
 
 
 def _stream_ptr(device: torch.device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    return _lib.stream(device)
 
 
 def _require(t: torch.Tensor, name: str, shape, device):

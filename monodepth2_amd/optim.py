@@ -106,7 +106,7 @@ class FusedAdam(torch.optim.Adam):
             self._grads[k] = p.grad.data_ptr()
         rc = _lib.lib().md2_adam_step(self._table.data_ptr(), self._starts, len(params), self._grads, lr,
                                       float(b1), float(b2), float(group["eps"]), step,
-                                      torch.cuda.current_stream(params[0].device).cuda_stream)
+                                      _lib.stream(params[0].device))
         _lib.check(rc, "md2_adam_step")
         return loss
 

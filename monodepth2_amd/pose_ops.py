@@ -23,7 +23,7 @@ class _PoseToT(torch.autograd.Function):
         aa, tr = axisangle.contiguous(), translation.contiguous()
         F_, B = aa.shape[0], aa.shape[1]
         T = torch.empty(F_, B, 4, 4, device=aa.device, dtype=aa.dtype)
-        st = torch.cuda.current_stream(aa.device).cuda_stream
+        st = _lib.stream(aa.device)
         _lib.check(_lib.lib().md2_pose_fwd(F_, B, mask, aa.data_ptr(), tr.data_ptr(), T.data_ptr(), st),
                    "md2_pose_fwd")
         ctx.save_for_backward(aa, tr)
@@ -35,7 +35,7 @@ class _PoseToT(torch.autograd.Function):
         aa, tr = ctx.saved_tensors
         gT = gT.contiguous()
         gaa, gtr = torch.empty_like(aa), torch.empty_like(tr)
-        st = torch.cuda.current_stream(aa.device).cuda_stream
+        st = _lib.stream(aa.device)
         _lib.check(_lib.lib().md2_pose_bwd(aa.shape[0], aa.shape[1], ctx.mask, aa.data_ptr(), tr.data_ptr(),
                                            gT.data_ptr(), gaa.data_ptr(), gtr.data_ptr(), st), "md2_pose_bwd")
         return gaa, gtr, None
@@ -50,7 +50,7 @@ class _Pose6ToT(torch.autograd.Function):
         aa, tr = x6[..., :3].contiguous(), x6[..., 3:].contiguous()
         F_, B = aa.shape[0], aa.shape[1]
         T = torch.empty(F_, B, 4, 4, device=aa.device, dtype=aa.dtype)
-        st = torch.cuda.current_stream(aa.device).cuda_stream
+        st = _lib.stream(aa.device)
         _lib.check(_lib.lib().md2_pose_fwd(F_, B, mask, aa.data_ptr(), tr.data_ptr(), T.data_ptr(), st),
                    "md2_pose_fwd")
         ctx.save_for_backward(aa, tr)
@@ -62,7 +62,7 @@ class _Pose6ToT(torch.autograd.Function):
         aa, tr = ctx.saved_tensors
         gT = gT.contiguous()
         gaa, gtr = torch.empty_like(aa), torch.empty_like(tr)
-        st = torch.cuda.current_stream(aa.device).cuda_stream
+        st = _lib.stream(aa.device)
         _lib.check(_lib.lib().md2_pose_bwd(aa.shape[0], aa.shape[1], ctx.mask, aa.data_ptr(), tr.data_ptr(),
                                            gT.data_ptr(), gaa.data_ptr(), gtr.data_ptr(), st), "md2_pose_bwd")
         return torch.cat([gaa, gtr], -1), None

@@ -46,7 +46,7 @@ class _StemConv(torch.autograd.Function):
         L = _lib.lib()
         ws = torch.empty(L.md2_stem_wgrad_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=x.device)
         rc = L.md2_stem_wgrad(ctypes.byref(d), x.data_ptr(), gy.data_ptr(), gw.data_ptr(), ws.data_ptr(),
-                              torch.cuda.current_stream(x.device).cuda_stream)
+                              _lib.stream(x.device))
         _lib.check(rc, "md2_stem_wgrad")
         return None, gw
 
