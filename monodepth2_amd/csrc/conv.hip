@@ -603,10 +603,14 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
 // loads), splits it, and writes it transposed — per plane and channel one 8-byte run of
 // 4 consecutive k — into the same swizzled [row][32 k] planes as the forward.
 // 512 threads: waves 0-3 stage gy (A), waves 4-7 stage x (B); all 8 multiply (2 x 4,
-// wave tile 64 x 32).  ConvArgs: M = Co, N = KT*Ci, P = pixels, C = Ci, Cg = Co.
-__global__ __launch_bounds__(512, 1) void conv_x6_wgrad_kernel(ConvArgs a) {
-    constexpr int NT = 512, BNW = 128, TM = 2;
-    constexpr int PA = BM * XBK, PB = BNW * XBK;
+// wave tile BMW/2 x 32).  BMW = 128 rows (co) per tile, or 64 for the 64-channel
+// layers (half the MFMA work of a 128 tile there; only waves 0-1 stage gy, and two
+// blocks fit a CU).  ConvArgs: M = Co, N = KT*Ci, P = pixels, C = Ci, Cg = Co.
+template <int BMW>
+__global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel(ConvArgs a) {
+    constexpr int NT = 512, BNW = 128, TM = BMW / 64;
+    constexpr int PA = BMW * XBK, PB = BNW * XBK;
+    static_assert(BMW == 64 || BMW == 128, "wgrad row tile");
     __shared__ __bf16 lds[2][3 * (PA + PB)];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 2, wn = wid & 3;
@@ -614,19 +618,21 @@ __global__ __launch_bounds__(512, 1) void conv_x6_wgrad_kernel(ConvArgs a) {
     const int nb = blk % a.nblocks;
     blk /= a.nblocks;
     const int mb = blk % a.mblocks, ks = blk / a.mblocks;
-    const int m0 = mb * BM, n0 = nb * BNW;
+    const int m0 = mb * BMW, n0 = nb * BNW;
     const int t0 = ks * a.chunks_per_split;
     const int nchunks = min(a.chunks_per_split, a.nchunks - t0);
     const int HoWo = a.Ho * a.Wo;
 
     // staging role: side 0 (gy, rows co) or 1 (x, rows (tap, ci)); micro-tile
-    // rows 4 mq .. 4 mq + 3, pixels 4 kq .. 4 kq + 3 of the chunk
+    // rows 4 mq .. 4 mq + 3, pixels 4 kq .. 4 kq + 3 of the chunk.  With BMW = 64 the
+    // gy tile needs only threads 0-127: waves 2-3 stage nothing (wave-uniform)
     const int side = tid >> 8, u = tid & 255, kq = u & 7, mq = u >> 3;
     const int row = 4 * mq;
+    const bool stager = side == 1 || u < 2 * BMW;
     int ci = 0, kh = 0, kw = 0;
     bool rok;
     if (side == 0) {
-        rok = m0 + row < a.M;
+        rok = stager && m0 + row < a.M;
     } else {
         const int n = n0 + row;
         rok = n < a.N;
@@ -700,6 +706,7 @@ __global__ __launch_bounds__(512, 1) void conv_x6_wgrad_kernel(ConvArgs a) {
             }
     };
     auto store = [&](int buf) {
+        if (!stager) return;
         __bf16* L = lds[buf] + (side ? 3 * PA : 0);
         const int P = side ? PB : PA;
         typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -746,6 +753,17 @@ __global__ __launch_bounds__(512, 1) void conv_x6_wgrad_kernel(ConvArgs a) {
         for (int i = 0; i < TM; ++i) tot[i] += acc[i];
     };
 
+    if (!stager) {
+        // waves 2-3 at BMW = 64: multiply only
+        __syncthreads();
+        for (int t = 0; t < nchunks; t += 2) {
+            mma(0);
+            __syncthreads();
+            if (t + 1 >= nchunks) break;
+            mma(1);
+            __syncthreads();
+        }
+    } else {
     load(0, v0);
     load(1, v1);
     split(v0);
@@ -765,6 +783,7 @@ __global__ __launch_bounds__(512, 1) void conv_x6_wgrad_kernel(ConvArgs a) {
         asm volatile("" ::: "memory");
         store(0);
         __syncthreads();
+    }
     }
 
     float* out = a.y + (size_t)ks * a.M * a.N;
@@ -902,13 +921,14 @@ ConvArgs args_of(const md2_conv_desc* d, int mode) {
     return a;
 }
 
-int resident_blocks_x6(int BN, int BMX) { return 256 * ((BN == 64 && BMX == 128) ? 2 : 1); }
+int resident_blocks_x6(int BN, int BMX) { return 256 * ((BN == 64 && BMX == 128) || BMX == 64 ? 2 : 1); }
 
 // x6 plan: BN = 128 unless N <= 64; BMX = 256 with MD2_CONV_BM256 (the caller's
-// autotune tries both); K split by the wave-quantisation model
+// autotune tries both); K split by the wave-quantisation model.  The weight-gradient
+// kernel is 128 wide, 64 or 128 rows (co) tall.
 void plan_x6(ConvArgs& a, uint32_t flags, bool wgrad = false) {
-    const int BN = (a.N <= 64 && !wgrad) ? 64 : 128;   // the weight-gradient kernel is 128 wide
-    const int BMX = (!wgrad && BN == 128 && (flags & MD2_CONV_BM256)) ? 256 : 128;
+    const int BN = (a.N <= 64 && !wgrad) ? 64 : 128;
+    const int BMX = wgrad ? (a.M <= 64 ? 64 : 128) : ((BN == 128 && (flags & MD2_CONV_BM256)) ? 256 : 128);
     const int mblocks = (a.M + BMX - 1) / BMX, nblocks = (a.N + BN - 1) / BN;
     const int base = mblocks * nblocks, res = resident_blocks_x6(BN, BMX);
     int best_s = 1;
@@ -921,7 +941,7 @@ void plan_x6(ConvArgs& a, uint32_t flags, bool wgrad = false) {
         // a chunk-round of blocks ~1.5k cycles (x BMX/128); the split reduction moves
         // (splits + 1) M x N floats at ~2.4 KB/cycle chip-wide
         const double red = splits > 1 ? (double)(splits + 1) * a.M * a.N * 4.0 / 2400.0 / 1536.0 : 0.0;
-        const double t = (double)rounds * per * (BMX / 128) + red;
+        const double t = (double)rounds * per * (BMX / 128.0) + red;
         if (t < best_t - 1e-9) {
             best_t = t;
             best_s = splits;
@@ -988,7 +1008,8 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
     const hipStream_t st = (hipStream_t)stream;
     if (use_x6(d, mode) && mode == MODE_WGRAD) {
         const dim3 grid(a.mblocks * a.nblocks * a.splits);
-        hipLaunchKernelGGL(conv_x6_wgrad_kernel, grid, dim3(512), 0, st, a);
+        if (a.bm == 64) hipLaunchKernelGGL(conv_x6_wgrad_kernel<64>, grid, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL(conv_x6_wgrad_kernel<128>, grid, dim3(512), 0, st, a);
     } else if (use_x6(d, mode)) {
         // B: the weights split into bf16 planes at the front of the workspace, or
         // already split by the caller (MD2_CONV_PRESPLIT: `weight` is the planes)
