@@ -432,9 +432,27 @@ struct X6Geo {
     static constexpr int MINB = (BN == 64 && BMX == 128) ? 2 : 1;
 };
 
+// Workgroup barrier that leaves LDS-DMA loads in flight: __syncthreads()'s fence
+// would wait for every outstanding vector-memory op (vmcnt(0)) once LDS-DMA is in
+// the kernel, draining the register prefetch of A; the DMA is ordered by explicit
+// wait_vm<> calls instead.  The "memory" clobber keeps LDS accesses on their side.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+template <int VM>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(VM >= 0 && VM < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((VM & 0xF) | ((VM >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+// 16 bytes per lane from the buffer at byte offset `voff` into LDS at lds + 16·lane
+// (lds wave-uniform; an offset past the buffer writes zeros)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, int voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+
 // A (activations, NHWC f32, im2col rows) is split while staged; B comes pre-split
-// (conv_wsplit_kernel) and is copied in 16-byte quads.  Forward and stride-1 input
-// gradient alike (ConvArgs as the f32 path builds them; b = the planes).
+// (conv_wsplit_kernel) and goes straight from memory into the LDS tile by LDS-DMA
+// (buffer_load_dwordx4 ... lds: no VGPRs, no ds_write), one chunk ahead.  Forward
+// and stride-1 input gradient alike (ConvArgs as the f32 path builds them; b = the
+// planes).
 template <int BN, int BMX>
 __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void conv_x6_kernel(ConvArgs a) {
     using G = X6Geo<BN, BMX>;
@@ -476,19 +494,23 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
             apb[j] = 0;
         }
     }
-    // B staging: quad i = tid + NT j -> plane, row, quad (k = 8 q .. 8 q + 7)
-    int bpl[BQ], brow[BQ], bq[BQ], bbase[BQ];
+    // B staging by LDS-DMA: BQ pieces per wave and chunk, each 1 KiB = 16 rows of one
+    // plane (64 B per row).  Lane l fills row 16 rb + l/4, quad slot l&3 — the slot
+    // that xidx() gives k-quad (slot ^ (row >> 2)) & 3 — so the DMA's linear lane
+    // order writes the swizzled layout.
+    constexpr int RB16 = BN / 16;
+    static_assert(3 * RB16 == BQ * (NT / 64), "one DMA piece per wave and j");
+    int bsrc[BQ], bk8[BQ], bdst[BQ];
     const __amdgpu_buffer_rsrc_t br =
         __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * 2, 0x00020000);
 #pragma unroll
     for (int j = 0; j < BQ; ++j) {
-        const int i = tid + NT * j;
-        bpl[j] = i / (BN * 4);
-        const int rem = i - bpl[j] * BN * 4;
-        brow[j] = rem >> 2;
-        bq[j] = rem & 3;
-        const int n = n0 + brow[j];
-        bbase[j] = n < a.N ? ((bpl[j] * a.N + n) * KT) * a.C + 8 * bq[j] : -1;
+        const int piece = wid + (NT / 64) * j, pl = piece / RB16, rb = piece - pl * RB16;
+        const int r = rb * 16 + (lane >> 2), q = ((lane & 3) ^ (r >> 2)) & 3;
+        const int n = n0 + r;
+        bk8[j] = 8 * q;
+        bsrc[j] = n < a.N ? ((pl * a.N + n) * KT) * a.C + 8 * q : -1;
+        bdst[j] = (3 * PA + pl * PB + rb * 16 * XBK) * 2;   // bytes into the buffer (wave-uniform)
     }
 
     f32x16 acc[TM];
@@ -498,8 +520,7 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
         for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
 
     float4 fa0[AQ], fa1[AQ];
-    uint4 qb0[BQ], qb1[BQ];
-    auto load = [&](int t, float4 (&RA)[AQ], uint4 (&RB)[BQ]) {
+    auto load = [&](int t, float4 (&RA)[AQ]) {
         const int tt = t0 + t;
         const int tap = tt / cchunks, c0 = (tt - tap * cchunks) * XBK;
         const int kh = tap / a.KW, kw = tap - kh * a.KW;
@@ -511,10 +532,17 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
             const bool ok = cok && (unsigned)(aih[j] + kh) < (unsigned)a.H && (unsigned)(aiw[j] + kw) < (unsigned)a.W;
             RA[j] = bload(ar, ok ? (apb[j] + off) * 4 : kBad);
         }
+    };
+    // B of chunk t into LDS buffer `buf` (wave-uniform skip past the last chunk)
+    auto dma = [&](int t, int buf) {
+        if (t >= nchunks) return;
+        const int tt = t0 + t;
+        const int tap = tt / cchunks, c0 = (tt - tap * cchunks) * XBK;
+        char* base = (char*)lds[buf];
 #pragma unroll
         for (int j = 0; j < BQ; ++j) {
-            const bool ok = live && bbase[j] >= 0 && c0 + 8 * bq[j] < a.C;
-            RB[j] = __builtin_bit_cast(uint4, bload(br, ok ? (bbase[j] + tap * a.C + c0) * 2 : kBad));
+            const bool ok = bsrc[j] >= 0 && c0 + bk8[j] < a.C;
+            dma16(br, base + bdst[j], ok ? (bsrc[j] + tap * a.C + c0) * 2 : kBad);
         }
     };
     bf16x4 sa[AQ][3];
@@ -522,7 +550,7 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
 #pragma unroll
         for (int j = 0; j < AQ; ++j) split3(RA[j], sa[j][0], sa[j][1], sa[j][2]);
     };
-    auto store = [&](int buf, const uint4 (&RB)[BQ]) {
+    auto store = [&](int buf) {
         __bf16* L = lds[buf];
 #pragma unroll
         for (int j = 0; j < AQ; ++j) {
@@ -530,8 +558,6 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) *(bf16x4*)(L + pl * PA + e) = sa[j][pl];
         }
-#pragma unroll
-        for (int j = 0; j < BQ; ++j) *(uint4*)(L + 3 * PA + bpl[j] * PB + xidx(brow[j], 8 * bq[j])) = RB[j];
     };
     const int lr = lane & 31, h = lane >> 5;
     auto mma = [&](int buf) {
@@ -559,28 +585,38 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
         }
     };
 
-    // chunk t+2 is fetched while chunk t is multiplied; chunk t+1 (fetched one
-    // iteration earlier) is split beside the MFMAs and stored to the other LDS buffer
-    // afterwards; one barrier per chunk.  Loads past the last chunk read zeros.
-    load(0, fa0, qb0);
-    load(1, fa1, qb1);
+    // A of chunk t+2 is fetched into registers while chunk t is multiplied; chunk t+1
+    // (fetched one iteration earlier) is split beside the MFMAs and stored to the other
+    // LDS buffer afterwards, where its B is DMA'd at the start of the iteration (that
+    // buffer was released by the previous barrier); one barrier per chunk.  The DMA is
+    // issued before the A loads, so vmcnt(AQ) before the barrier waits for the DMA
+    // alone (vector-memory loads complete in order).  A loads past the last chunk read
+    // zeros.
+    load(0, fa0);
+    load(1, fa1);
+    dma(0, 0);
     split(fa0);
-    store(0, qb0);
-    __syncthreads();
+    store(0);
+    wait_vm<0>();
+    lds_sync();
     for (int t = 0; t < nchunks; t += 2) {
-        load(t + 2, fa0, qb0);
+        dma(t + 1, 1);
+        load(t + 2, fa0);
         split(fa1);
         mma(0);
         asm volatile("" ::: "memory");
-        store(1, qb1);
-        __syncthreads();
+        store(1);
+        wait_vm<AQ>();
+        lds_sync();
         if (t + 1 >= nchunks) break;
-        load(t + 3, fa1, qb1);
+        dma(t + 2, 0);
+        load(t + 3, fa1);
         split(fa0);
         mma(1);
         asm volatile("" ::: "memory");
-        store(0, qb0);
-        __syncthreads();
+        store(0);
+        wait_vm<AQ>();
+        lds_sync();
     }
 
     float* out = a.y + (size_t)ks * a.M * a.N;
