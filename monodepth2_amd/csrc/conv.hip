@@ -394,29 +394,41 @@ __global__ __launch_bounds__(256) void conv_wsplit_kernel(const float* w, __bf16
     out[2 * n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, c) >> 16));
 }
 
-// Both layouts in one launch (md2_conv_split_weights): threads [0, n) write the
-// forward planes [3][Co][KT][Ci], threads [n, 2n) (if `dg` is non-null) the input
-// gradient's flipped/transposed [3][Ci][KT][Co], each indexed by its OUTPUT element
-// so that the 2-byte stores coalesce (the gather of w is the strided side).
-__global__ __launch_bounds__(256) void conv_wsplit2_kernel(const float* w, __bf16* fw, __bf16* dg, int Co, int KT,
-                                                           int Ci) {
-    const int n = Co * KT * Ci;
-    int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= (dg ? 2 * n : n)) return;
-    __bf16* out = fw;
-    float v;
-    if (i < n) {
-        v = w[i];
-    } else {
-        i -= n;
-        out = dg;
-        const int co = i % Co, rest = i / Co, t = rest % KT, ci = rest / KT;   // out [ci][t][co]
-        v = w[((size_t)co * KT + (KT - 1 - t)) * Ci + ci];
-    }
+// Both layouts in one launch (md2_conv_split_weights): one block per (tap, 32 co,
+// 32 ci) tile.  The tile is read once, coalesced along ci, split into the forward
+// planes [3][Co][KT][Ci] (same element order), and — if `dg` is non-null — transposed
+// through LDS into the input gradient's [3][Ci][KT][Co] with the tap flipped, so
+// those 2-byte stores coalesce along co as well.
+__device__ __forceinline__ void split_store(__bf16* out, int n, int i, float v) {
     const float a = trunc16(v), r1 = v - a, b = trunc16(r1), c = r1 - b;
     out[i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, a) >> 16));
     out[n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, b) >> 16));
     out[2 * n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, c) >> 16));
+}
+__global__ __launch_bounds__(256) void conv_wsplit_tile_kernel(const float* w, __bf16* fw, __bf16* dg, int Co,
+                                                               int KT, int Ci) {
+    __shared__ float tile[32][33];
+    const int tap = blockIdx.z, co0 = blockIdx.y * 32, ci0 = blockIdx.x * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    const int n = Co * KT * Ci;
+#pragma unroll
+    for (int r = ty; r < 32; r += 8) {
+        const int co = co0 + r, ci = ci0 + tx;
+        float v = 0.f;
+        if (co < Co && ci < Ci) {
+            const int i = (co * KT + tap) * Ci + ci;
+            v = w[i];
+            split_store(fw, n, i, v);
+        }
+        tile[r][tx] = v;
+    }
+    if (!dg) return;   // block-uniform
+    __syncthreads();
+#pragma unroll
+    for (int r = ty; r < 32; r += 8) {
+        const int ci = ci0 + r, co = co0 + tx;
+        if (ci < Ci && co < Co) split_store(dg, n, (ci * KT + (KT - 1 - tap)) * Co + co, tile[tx][r]);
+    }
 }
 
 // Tiles BMX x BN.  NT threads: 8 waves (2 x 4 / 4 x 2 / 2 x 4, wave tiles 64/128 x 32)
@@ -1107,9 +1119,8 @@ int md2_conv_split_weights(const md2_conv_desc* d, const float* weight, void* pl
     if (!valid(d) || d->in_channels % 8 || d->out_channels % 8)
         return md2_report_error(MD2_ERR_ARG, "conv_split_weights: channels % 8, pad < kernel, sizes < 2^29");
     if (!weight || !planes_fwd) return md2_report_error(MD2_ERR_ARG, "conv_split_weights: NULL operand");
-    const int n = d->out_channels * d->kernel_h * d->kernel_w * d->in_channels;
-    const int total = planes_dgrad ? 2 * n : n;
-    hipLaunchKernelGGL(conv_wsplit2_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, weight,
+    const dim3 grid((d->in_channels + 31) / 32, (d->out_channels + 31) / 32, d->kernel_h * d->kernel_w);
+    hipLaunchKernelGGL(conv_wsplit_tile_kernel, grid, dim3(256), 0, (hipStream_t)stream, weight,
                        (__bf16*)planes_fwd, (__bf16*)planes_dgrad, d->out_channels, d->kernel_h * d->kernel_w,
                        d->in_channels);
     const hipError_t e = hipGetLastError();
