@@ -60,6 +60,8 @@ struct ConvArgs {
     int a_elems, b_elems;    // sizes of the two operands (the buffer-descriptor bounds)
     int bn;                  // tile width chosen by plan()
     int bm;                  // x6 tile height (128 or 256)
+    int flatk;               // x6 fwd / dgrad with C < 32: K chunks run over the flattened
+                             // (tap, channel) index, several taps per chunk
     const float* a;          // fwd: x; dgrad: gy; wgrad: x
     const float* b;          // fwd / dgrad: weight; wgrad: gy
     float* y;                // output [M][N], or partials [splits][M][N]
@@ -433,15 +435,18 @@ __global__ __launch_bounds__(256) void conv_wsplit_tile_kernel(const float* w, _
 
 // Tiles BMX x BN.  NT threads: 8 waves (2 x 4 / 4 x 2 / 2 x 4, wave tiles 64/128 x 32)
 // whenever BN = 128 or BMX = 256, so that two waves share each SIMD and one's split
-// VALU overlaps the other's MFMAs; 128 x 64 runs 4 waves at two blocks per CU.  The
-// 256-row tile loads 1.5x the bytes of the 128-row one for 2x the MFMA work.
+// VALU overlaps the other's MFMAs; 128 x 64 and 128 x 32 (the decoder's 16/32-channel
+// convolutions, which waste 3/4 or 1/2 of a 64-wide tile) run 4 waves at two blocks
+// per CU; 128 x 16 (16 output channels) multiplies with 16x16x32 MFMAs.  The 256-row tile loads 1.5x the bytes of the 128-row one for 2x the MFMA
+// work.
 template <int BN, int BMX>
 struct X6Geo {
     static constexpr int NT = (BN == 128 || BMX == 256) ? 512 : 256;
-    static constexpr int WN = BN / 32;            // waves along N (wave tile 32 wide)
+    static constexpr int MT = BN == 16 ? 16 : 32;   // MFMA tile: 16x16x32 for 16 columns, else 32x32x16
+    static constexpr int WN = BN / MT;            // waves along N (wave tile MT wide)
     static constexpr int WM = NT / 64 / WN;       // waves along M
-    static constexpr int TM = BMX / 32 / WM;
-    static constexpr int MINB = (BN == 64 && BMX == 128) ? 2 : 1;
+    static constexpr int TM = BMX / MT / WM;      // MFMA row blocks per wave
+    static constexpr int MINB = (BN <= 64 && BMX == 128) ? 2 : 1;
 };
 
 // Workgroup barrier that leaves LDS-DMA loads in flight: __syncthreads()'s fence
@@ -470,9 +475,10 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
     using G = X6Geo<BN, BMX>;
     constexpr int NT = G::NT, TM = G::TM;
     constexpr int AQ = BMX * XBK / 4 / NT;         // f32 quads of A per thread
-    constexpr int BQ = 3 * BN * (XBK / 8) / NT;    // bf16 quads (8 values) of B per thread
+    constexpr int NW = NT / 64, PIECES = 3 * BN / 16;   // B: 1 KiB DMA pieces per chunk
+    constexpr int BQ = (PIECES + NW - 1) / NW;          // pieces per wave (the last j partial)
     constexpr int PA = BMX * XBK, PB = BN * XBK;   // bf16 elements per plane
-    static_assert(AQ * NT * 4 == BMX * XBK && BQ * NT == 3 * BN * (XBK / 8), "staging must tile the chunk");
+    static_assert(AQ * NT * 4 == BMX * XBK, "A staging must tile the chunk");
     __shared__ __bf16 lds[2][3 * (PA + PB)];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -511,13 +517,12 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
     // that xidx() gives k-quad (slot ^ (row >> 2)) & 3 — so the DMA's linear lane
     // order writes the swizzled layout.
     constexpr int RB16 = BN / 16;
-    static_assert(3 * RB16 == BQ * (NT / 64), "one DMA piece per wave and j");
     int bsrc[BQ], bk8[BQ], bdst[BQ];
     const __amdgpu_buffer_rsrc_t br =
         __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * 2, 0x00020000);
 #pragma unroll
     for (int j = 0; j < BQ; ++j) {
-        const int piece = wid + (NT / 64) * j, pl = piece / RB16, rb = piece - pl * RB16;
+        const int piece = wid + NW * j, pl = piece / RB16, rb = piece - pl * RB16;
         const int r = rb * 16 + (lane >> 2), q = ((lane & 3) ^ (r >> 2)) & 3;
         const int n = n0 + r;
         bk8[j] = 8 * q;
@@ -525,20 +530,34 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
         bdst[j] = (3 * PA + pl * PB + rb * 16 * XBK) * 2;   // bytes into the buffer (wave-uniform)
     }
 
-    f32x16 acc[TM];
+    constexpr int NACC = G::MT == 16 ? 4 : 16;
+    typedef float accv __attribute__((ext_vector_type(NACC)));
+    accv acc[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+        for (int e = 0; e < NACC; ++e) acc[i][e] = 0.f;
 
     float4 fa0[AQ], fa1[AQ];
     auto load = [&](int t, float4 (&RA)[AQ]) {
         const int tt = t0 + t;
-        const int tap = tt / cchunks, c0 = (tt - tap * cchunks) * XBK;
-        const int kh = tap / a.KW, kw = tap - kh * a.KW;
-        const int off = (kh * a.W + kw) * a.C + c0;
         const bool live = t < nchunks;
-        const bool cok = live && c0 + 4 * qa < a.C;
+        int kh, kw, off;
+        bool cok;
+        if (a.flatk) {
+            // this thread's 4 k of the chunk: one tap (C % 4 == 0), channels ci .. ci+3
+            const int k = tt * XBK + 4 * qa, tap = k / a.C, ci = k - tap * a.C;
+            kh = tap / a.KW;
+            kw = tap - kh * a.KW;
+            off = (kh * a.W + kw) * a.C + ci - 4 * qa;   // apb[] holds the + 4 qa
+            cok = live && tap < KT;
+        } else {
+            const int tap = tt / cchunks, c0 = (tt - tap * cchunks) * XBK;
+            kh = tap / a.KW;
+            kw = tap - kh * a.KW;
+            off = (kh * a.W + kw) * a.C + c0;
+            cok = live && c0 + 4 * qa < a.C;
+        }
 #pragma unroll
         for (int j = 0; j < AQ; ++j) {
             const bool ok = cok && (unsigned)(aih[j] + kh) < (unsigned)a.H && (unsigned)(aiw[j] + kw) < (unsigned)a.W;
@@ -550,11 +569,16 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
         if (t >= nchunks) return;
         const int tt = t0 + t;
         const int tap = tt / cchunks, c0 = (tt - tap * cchunks) * XBK;
+        // B rows are [tap][channel] contiguous: the chunk starts at k = tap C + c0, or
+        // at 32 tt of the flattened index
+        const int kofs = a.flatk ? tt * XBK : tap * a.C + c0;
+        const int klim = a.flatk ? KT * a.C : tap * a.C + a.C;
         char* base = (char*)lds[buf];
 #pragma unroll
         for (int j = 0; j < BQ; ++j) {
-            const bool ok = bsrc[j] >= 0 && c0 + bk8[j] < a.C;
-            dma16(br, base + bdst[j], ok ? (bsrc[j] + tap * a.C + c0) * 2 : kBad);
+            if (PIECES % NW && wid + NW * j >= PIECES) break;   // wave-uniform
+            const bool ok = bsrc[j] >= 0 && kofs + bk8[j] < klim;
+            dma16(br, base + bdst[j], ok ? (bsrc[j] + kofs) * 2 : kBad);
         }
     };
     bf16x4 sa[AQ][3];
@@ -574,25 +598,47 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
     const int lr = lane & 31, h = lane >> 5;
     auto mma = [&](int buf) {
         const __bf16* L = lds[buf];
-#pragma unroll
-        for (int s = 0; s < XBK / 16; ++s) {
+        if constexpr (G::MT == 16) {
+            // 16x16x32: lane l holds row / column l & 15, k = 8 (l >> 4) .. + 7
+            const int l16 = lane & 15, kq = lane >> 4;
             bf16x8 fb[3];
-            const int eb = xidx(wn * 32 + lr, 16 * s + 8 * h);
+            const int eb = xidx(wn * 16 + l16, 8 * kq);
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 bf16x8 fa[3];
-                const int e = xidx(wm * (TM * 32) + 32 * i + lr, 16 * s + 8 * h);
+                const int e = xidx(wm * (TM * 16) + 16 * i + l16, 8 * kq);
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(L + pl * PA + e);
-                // small terms first: x2y0, x1y1, x0y2, x1y0, x0y1, x0y0
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[2], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < XBK / 16; ++s) {
+                bf16x8 fb[3];
+                const int eb = xidx(wn * 32 + lr, 16 * s + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    bf16x8 fa[3];
+                    const int e = xidx(wm * (TM * 32) + 32 * i + lr, 16 * s + 8 * h);
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(L + pl * PA + e);
+                    // small terms first: x2y0, x1y1, x0y2, x1y0, x0y1, x0y0
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+                }
             }
         }
     };
@@ -632,15 +678,29 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
     }
 
     float* out = a.y + (size_t)ks * a.M * a.N;
-    const int n = n0 + wn * 32 + lr;
-    if (n < a.N) {
+    if constexpr (G::MT == 16) {
+        // 16x16 D: lane l holds column l & 15, rows 4 (l >> 4) .. + 3
+        const int n = n0 + wn * 16 + (lane & 15);
+        if (n < a.N) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int m = m0 + wm * (TM * 32) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
-                if (m < a.M) out[m * a.N + n] = acc[i][e];
-            }
+                for (int e = 0; e < 4; ++e) {
+                    const int m = m0 + wm * (TM * 16) + 16 * i + 4 * (lane >> 4) + e;
+                    if (m < a.M) out[m * a.N + n] = acc[i][e];
+                }
+        }
+    } else {
+        const int n = n0 + wn * 32 + lr;
+        if (n < a.N) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int m = m0 + wm * (TM * 32) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    if (m < a.M) out[m * a.N + n] = acc[i][e];
+                }
+        }
     }
 }
 
@@ -969,13 +1029,13 @@ ConvArgs args_of(const md2_conv_desc* d, int mode) {
     return a;
 }
 
-int resident_blocks_x6(int BN, int BMX) { return 256 * ((BN == 64 && BMX == 128) || BMX == 64 ? 2 : 1); }
+int resident_blocks_x6(int BN, int BMX) { return 256 * ((BN <= 64 && BMX == 128) || BMX == 64 ? 2 : 1); }
 
-// x6 plan: BN = 128 unless N <= 64; BMX = 256 with MD2_CONV_BM256 (the caller's
+// x6 plan: BN = 16 / 32 / 64 for N <= 16 / 32 / 64, else 128; BMX = 256 with MD2_CONV_BM256 (the caller's
 // autotune tries both); K split by the wave-quantisation model.  The weight-gradient
 // kernel is 128 wide, 64 or 128 rows (co) tall.
 void plan_x6(ConvArgs& a, uint32_t flags, bool wgrad = false) {
-    const int BN = (a.N <= 64 && !wgrad) ? 64 : 128;
+    const int BN = wgrad ? 128 : (a.N <= 16 ? 16 : (a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128)));
     const int BMX = wgrad ? (a.M <= 64 ? 64 : 128) : ((BN == 128 && (flags & MD2_CONV_BM256)) ? 256 : 128);
     const int mblocks = (a.M + BMX - 1) / BMX, nblocks = (a.N + BN - 1) / BN;
     const int base = mblocks * nblocks, res = resident_blocks_x6(BN, BMX);
@@ -1043,9 +1103,19 @@ size_t x6_planes_bytes(const md2_conv_desc* d) {
            ~(size_t)255;
 }
 
+// x6 fwd / dgrad on fewer than 32 GEMM channels: chunks over the flattened (tap, channel)
+// index (a 16-channel 3x3 convolution is 4.5 full chunks instead of 9 half-empty ones)
+void flat_k(ConvArgs& a, int mode) {
+    if (mode != MODE_WGRAD && a.C < XBK) {
+        a.flatk = 1;
+        a.nchunks = (a.KH * a.KW * a.C + XBK - 1) / XBK;
+    }
+}
+
 int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float* out, void* ws, void* stream,
         const char* name) {
     ConvArgs a = (mode == MODE_WGRAD && use_x6(d, mode)) ? args_x6_wgrad(d) : args_of(d, mode);
+    if (use_x6(d, mode)) flat_k(a, mode);
     if (use_x6(d, mode)) plan_x6(a, d->flags, mode == MODE_WGRAD);
     else plan(a, d->flags, min_chunks_of(mode));
     const int BN = a.bn;
@@ -1074,7 +1144,9 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
             hipLaunchKernelGGL((conv_x6_kernel<128, 256>), grid, dim3(X6Geo<128, 256>::NT), 0, st, a);
         } else {
             if (BN == 128) hipLaunchKernelGGL((conv_x6_kernel<128, 128>), grid, dim3(X6Geo<128, 128>::NT), 0, st, a);
-            else hipLaunchKernelGGL((conv_x6_kernel<64, 128>), grid, dim3(X6Geo<64, 128>::NT), 0, st, a);
+            else if (BN == 64) hipLaunchKernelGGL((conv_x6_kernel<64, 128>), grid, dim3(X6Geo<64, 128>::NT), 0, st, a);
+            else if (BN == 32) hipLaunchKernelGGL((conv_x6_kernel<32, 128>), grid, dim3(X6Geo<32, 128>::NT), 0, st, a);
+            else hipLaunchKernelGGL((conv_x6_kernel<16, 128>), grid, dim3(X6Geo<16, 128>::NT), 0, st, a);
         }
     } else if (mode == MODE_FWD) launch<MODE_FWD>(a, BN, st);
     else if (mode == MODE_DGRAD) launch<MODE_DGRAD>(a, BN, st);
@@ -1095,6 +1167,7 @@ size_t ws_bytes(const md2_conv_desc* d, int mode) {
         return a.splits > 1 ? sizeof(float) * (size_t)a.splits * a.M * a.N : 0;
     }
     if (use_x6(d, mode)) {
+        flat_k(a, mode);
         plan_x6(a, d->flags);
         return x6_planes_bytes(d) + (a.splits > 1 ? sizeof(float) * (size_t)a.splits * a.M * a.N : 0);
     }

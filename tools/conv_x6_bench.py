@@ -33,6 +33,9 @@ def main():
         if "quick" in modes:   # x6 timings only (A/B of variant builds)
             row["fwd_x6_tf"] = round(gf / timeit(lambda: fwd(x, w, s, p, X6)), 1)
             row["fwd_x6_256_tf"] = round(gf / timeit(lambda: fwd(x, w, s, p, X6 | _lib.CONV_BM256)), 1)
+            if s == 1:
+                gy = torch.randn_like(F.conv2d(x, w, None, s, p)).contiguous(memory_format=CL)
+                row["dgrad_x6_tf"] = round(gf / timeit(lambda: dgrad(gy, x, w, s, p, X6)), 1)
             print(json.dumps(row), flush=True)
             continue
         if "fwd" in modes:
