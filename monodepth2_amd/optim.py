@@ -31,20 +31,44 @@ class FusedAdam(torch.optim.Adam):
         self._table = None
         self._starts = None
         self._grads = None
+        self._params = None   # the parameter list the table was built for
         self.rebuilds = 0   # chunk-table uploads (a parameter or moment buffer moved)
 
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._key = None   # new moment buffers: rebuild the table on the next step
+
+    def _group_ok(self) -> bool:
+        if len(self.param_groups) != 1:   # one lr / betas / eps per launch
+            return False
+        g = self.param_groups[0]
+        return not (g["weight_decay"] != 0 or g["amsgrad"] or g["maximize"] or g.get("capturable")
+                    or g.get("differentiable"))
+
     def _eligible(self) -> bool:
-        for g in self.param_groups:
-            if g["weight_decay"] != 0 or g["amsgrad"] or g["maximize"] or g.get("capturable") \
-                    or g.get("differentiable"):
+        if not self._group_ok():
+            return False
+        for p in self.param_groups[0]["params"]:
+            if p.grad is None:
+                continue
+            if (not p.is_cuda or p.dtype != torch.float32 or p.grad.dtype != torch.float32 or p.grad.is_sparse
+                    or p.grad.stride() != p.stride() or not _dense(p)):
                 return False
-            for p in g["params"]:
-                if p.grad is None:
-                    continue
-                if (not p.is_cuda or p.dtype != torch.float32 or p.grad.dtype != torch.float32 or p.grad.is_sparse
-                        or p.grad.stride() != p.stride() or not _dense(p)):
-                    return False
-        return len(self.param_groups) == 1   # one lr / betas / eps per launch
+        return True
+
+    def _fast_ok(self, params) -> bool:
+        """Per-step check once the table is built for exactly these parameters: the
+        parameters' own properties (device, dtype, density) were checked at build time
+        and cannot change without a new tensor (caught by the data_ptr comparison);
+        only the gradients, new every step, are looked at."""
+        if not self._group_ok() or len(params) != len(self._params):
+            return False
+        for p, q, k in zip(params, self._params, self._key):
+            g = p.grad
+            if (p is not q or p.data_ptr() != k[0] or g.dtype != torch.float32 or g.is_sparse
+                    or g.stride() != p.stride()):
+                return False
+        return True
 
     def _state(self, p):
         st = self.state[p]
@@ -76,26 +100,31 @@ class FusedAdam(torch.optim.Adam):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        if not self._eligible():
-            return super().step()
         group = self.param_groups[0]
         params = [p for p in group["params"] if p.grad is not None]
+        fast = self._key is not None and self._fast_ok(params)
+        if not fast and not self._eligible():
+            self._key = None
+            return super().step()
         if not params:
             return loss
         states = [self._state(p) for p in params]
         # the table holds parameters and moments, which do not move; gradients (new
-        # buffers every step) travel as kernel arguments
-        key = tuple((p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), p.numel())
-                    for p, st in zip(params, states))
-        if key != self._key:
-            # (re)validate what the kernel assumes, then upload the chunk table
-            if (len({float(st["step"]) for st in states}) != 1
-                    or any(st["exp_avg"].stride() != p.stride() or st["exp_avg_sq"].stride() != p.stride()
-                           for p, st in zip(params, states))):
-                self._key = None
-                return super().step()   # mixed step counts / layouts (e.g. a loaded partial state)
-            self._build(params)
-            self._key = key
+        # buffers every step) travel as kernel arguments.  Moments only move through
+        # load_state_dict (which drops the table) or a new state (a new parameter list).
+        if not fast:
+            key = tuple((p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), p.numel())
+                        for p, st in zip(params, states))
+            if key != self._key:
+                # (re)validate what the kernel assumes, then upload the chunk table
+                if (len({float(st["step"]) for st in states}) != 1
+                        or any(st["exp_avg"].stride() != p.stride() or st["exp_avg_sq"].stride() != p.stride()
+                               for p, st in zip(params, states))):
+                    self._key = None
+                    return super().step()   # mixed step counts / layouts (e.g. a loaded partial state)
+                self._build(params)
+                self._key = key
+            self._params = list(params)
         steps = [st["step"] for st in states]
         torch._foreach_add_(steps, 1)   # CPU scalars, as torch's Adam keeps them
         step = int(steps[0])

@@ -36,6 +36,14 @@ def main():
     host = (time.perf_counter() - t) / steps
     torch.cuda.synchronize()
     print(f"host enqueue {1e3 * host:.2f} ms/step (no profiler)")
+    if os.environ.get("MD2_SERIAL_BACKWARD"):
+        # run the backward on this thread so that cProfile sees its Python code
+        torch.autograd.set_multithreading_enabled(False)
+        t = time.perf_counter()
+        for _ in range(steps):
+            tr.train_step(batch)
+        torch.cuda.synchronize()
+        print(f"serial backward: {1e3 * (time.perf_counter() - t) / steps:.2f} ms/step (incl. GPU)")
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(steps):
@@ -43,7 +51,7 @@ def main():
     pr.disable()
     torch.cuda.synchronize()
     st = pstats.Stats(pr)
-    st.sort_stats("tottime").print_stats(top)
+    st.sort_stats(os.environ.get("MD2_SORT", "tottime")).print_stats(top)
 
 
 if __name__ == "__main__":
