@@ -30,6 +30,11 @@ def main():
         w = (torch.randn(N, C, k, k, device="cuda") / (C * k * k) ** 0.5).contiguous(memory_format=CL)
         gf = 2 * B * ((H + 2 * p - k) // s + 1) * ((W + 2 * p - k) // s + 1) * N * C * k * k / 1e9
         row = {"name": name, "gflop": round(gf, 3)}
+        if "quickw" in modes:   # x6 weight-gradient timings only
+            gy = torch.randn_like(F.conv2d(x, w, None, s, p)).contiguous(memory_format=CL)
+            row["wgrad_x6_tf"] = round(gf / timeit(lambda: wgrad(gy, x, w, s, p, X6)), 1)
+            print(json.dumps(row), flush=True)
+            continue
         if "quick" in modes:   # x6 timings only (A/B of variant builds)
             row["fwd_x6_tf"] = round(gf / timeit(lambda: fwd(x, w, s, p, X6)), 1)
             row["fwd_x6_256_tf"] = round(gf / timeit(lambda: fwd(x, w, s, p, X6 | _lib.CONV_BM256)), 1)
