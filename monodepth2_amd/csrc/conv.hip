@@ -917,19 +917,38 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
     }
 }
 
-// y = Σ_split partial[split] in split order (deterministic), float4 per thread
+// y = Σ_split partial[split], deterministic: 64 float4 outputs per block, four lanes
+// per output summing every 4th split, then the four lane sums added in lane order.
+// (One thread per output walked all splits — up to ~60 in the weight gradients — as
+// one serial chain over a few dozen blocks.)
+constexpr int kRedOut = 64, kRedLanes = 256 / kRedOut;
 __global__ __launch_bounds__(256) void conv_reduce_kernel(const float4* part, float4* y, int n4, int splits) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n4) return;
-    float4 s = part[i];
-    for (int k = 1; k < splits; ++k) {
-        const float4 v = part[(size_t)k * n4 + i];
-        s.x += v.x;
-        s.y += v.y;
-        s.z += v.z;
-        s.w += v.w;
+    __shared__ float4 red[kRedLanes][kRedOut];
+    const int o = threadIdx.x % kRedOut, l = threadIdx.x / kRedOut;
+    const int i = blockIdx.x * kRedOut + o;
+    float4 s = {0.f, 0.f, 0.f, 0.f};
+    if (i < n4) {
+        for (int k = l; k < splits; k += kRedLanes) {
+            const float4 v = part[(size_t)k * n4 + i];
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
     }
-    y[i] = s;
+    red[l][o] = s;
+    __syncthreads();
+    if (l == 0 && i < n4) {
+#pragma unroll
+        for (int j = 1; j < kRedLanes; ++j) {
+            const float4 v = red[j][o];
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+        y[i] = s;
+    }
 }
 
 bool valid(const md2_conv_desc* d) {
@@ -1168,7 +1187,7 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
     else launch<MODE_WGRAD>(a, BN, st);
     if (a.splits > 1) {
         const int n4 = a.M * a.N / 4;
-        hipLaunchKernelGGL(conv_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, st, (const float4*)a.y,
+        hipLaunchKernelGGL(conv_reduce_kernel, dim3((n4 + kRedOut - 1) / kRedOut), dim3(256), 0, st, (const float4*)a.y,
                            (float4*)out, n4, a.splits);
     }
     const hipError_t e = hipGetLastError();
