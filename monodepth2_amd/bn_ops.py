@@ -56,6 +56,19 @@ def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
     return ws
 
 
+_descs: Dict[tuple, tuple] = {}
+
+
+def _desc(key: tuple):
+    """(BnDesc, workspace bytes) per (pixels, C, flags, eps, momentum, groups): built once,
+    the ~80 calls per step reuse them (the step is close to launch-bound)."""
+    hit = _descs.get(key)
+    if hit is None:
+        d = _lib.BnDesc(*key, 0)
+        hit = _descs[key] = (d, _lib.lib().md2_bn_workspace_bytes(ctypes.byref(d)))
+    return hit
+
+
 def _supported(C: int) -> bool:
     """Channel counts the kernels take: C/4 a power of two (every ResNet width)."""
     Q = C // 4
@@ -70,12 +83,13 @@ class _BNAct(torch.autograd.Function):
         B, C, H, W = x.shape
         flags = ((_lib.BN_RELU if relu else 0) | (_lib.BN_RESIDUAL if residual is not None else 0)
                  | (_lib.BN_BF16 if x.dtype == torch.bfloat16 else 0))
-        d = _lib.BnDesc(B * H * W, C, flags, eps, momentum, groups, 0)
+        key = (B * H * W, C, flags, eps, momentum, groups)
+        d, nbytes = _desc(key)
         L = _lib.lib()
-        ws = _workspace(x.device, L.md2_bn_workspace_bytes(ctypes.byref(d)))
+        ws = _workspace(x.device, nbytes)
         y = torch.empty_like(x, memory_format=_CL)
-        mean = torch.empty(groups, C, device=x.device)
-        invstd = torch.empty(groups, C, device=x.device)
+        stats = torch.empty(2, groups, C, device=x.device)   # saved mean, invstd
+        mean, invstd = stats[0], stats[1]
         stream = _lib.stream(x.device)
         rc = L.md2_bn_fwd(ctypes.byref(d), x.data_ptr(), weight.data_ptr(), bias.data_ptr(),
                           residual.data_ptr() if residual is not None else None,
@@ -84,7 +98,7 @@ class _BNAct(torch.autograd.Function):
                           y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ws.data_ptr(), stream)
         _lib.check(rc, "md2_bn_fwd")
         ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
-        ctx.desc = (B * H * W, C, flags, eps, momentum, groups, 0)
+        ctx.desc = key
         ctx.has_res = residual is not None
         if aliases:
             # views of y for its other consumers: their gradients come into this backward
@@ -100,9 +114,9 @@ class _BNAct(torch.autograd.Function):
         if not gs:
             return (None,) * 11
         gy = gs[0]
-        d = _lib.BnDesc(*ctx.desc)
+        d, nbytes = _desc(ctx.desc)
         L = _lib.lib()
-        ws = _workspace(x.device, L.md2_bn_workspace_bytes(ctypes.byref(d)))
+        ws = _workspace(x.device, nbytes)
         gx = torch.empty_like(x, memory_format=_CL)
         gr = torch.empty_like(x, memory_format=_CL) if ctx.has_res else None
         gw = torch.empty_like(weight)
