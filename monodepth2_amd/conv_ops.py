@@ -93,14 +93,19 @@ def _fwd(x, w, stride, pad, flags=0):
     return y
 
 
-def _dgrad(gy, x, w, pad, flags=0):
+def _dgrad(gy, x, w, pad, flags=0, stride=1):
     gx = torch.empty_like(x, memory_format=_CL)
-    _call("md2_conv_dgrad", x, w, 1, pad, flags, gy.data_ptr(), w.data_ptr(), gx.data_ptr(), x.device)
+    _call("md2_conv_dgrad", x, w, stride, pad, flags, gy.data_ptr(), w.data_ptr(), gx.data_ptr(), x.device)
     return gx
 
 
 def _x6_ok(x, w) -> bool:
     return x.shape[1] % 8 == 0 and w.shape[0] % 8 == 0
+
+
+def _x6_s2_ok(x, w, stride) -> bool:
+    """The x6 input gradient of a stride-2 convolution (four parity classes)."""
+    return stride == 2 and _x6_ok(x, w) and w.shape[0] >= 32
 
 
 def _split_weights(x, w, stride, pad, dgrad: bool):
@@ -126,9 +131,9 @@ def _fwd_planes(x, w, planes, stride, pad, flags):
     return y
 
 
-def _dgrad_planes(gy, x, w, planes, pad, flags):
+def _dgrad_planes(gy, x, w, planes, pad, flags, stride=1):
     gx = torch.empty_like(x, memory_format=_CL)
-    _call("md2_conv_dgrad", x, w, 1, pad, flags | PRESPLIT, gy.data_ptr(), planes.data_ptr(), gx.data_ptr(),
+    _call("md2_conv_dgrad", x, w, stride, pad, flags | PRESPLIT, gy.data_ptr(), planes.data_ptr(), gx.data_ptr(),
           x.device)
     return gx
 
@@ -203,7 +208,7 @@ class _Conv(torch.autograd.Function):
         if x6 and i < 2:
             # the x6 forward: split the weight once for it and for the input gradient
             # (one launch), the dgrad planes kept for the backward
-            pf, planes_dg = _split_weights(x, weight, stride, pad, stride == 1)
+            pf, planes_dg = _split_weights(x, weight, stride, pad, stride == 1 or _x6_s2_ok(x, weight, stride))
             y = _fwd_planes(x, weight, pf, stride, pad, _FLAGS[i])
         else:
             y = cands[i]()
@@ -228,6 +233,14 @@ class _Conv(torch.autograd.Function):
                     gx = _dgrad_planes(gy, x, w, planes_dg, p, _FLAGS[i])
                 elif i < len(cands) - 1:
                     gx = cands[i]()
+                else:
+                    mi_x = True
+            elif _x6_s2_ok(x, w, s):
+                cands = [lambda: _dgrad(gy, x, w, p, X6, 2),
+                         lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
+                i = _fastest("dgrad", ctx.key, cands)
+                if i == 0:
+                    gx = (_dgrad_planes(gy, x, w, planes_dg, p, X6, 2) if planes_dg is not None else cands[0]())
                 else:
                     mi_x = True
             else:

@@ -29,6 +29,8 @@
 
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "md2hot.h"
 
 int md2_report_error(int code, const char* msg);
@@ -60,6 +62,11 @@ struct ConvArgs {
     int a_elems, b_elems;    // sizes of the two operands (the buffer-descriptor bounds)
     int bn;                  // tile width chosen by plan()
     int bm;                  // x6 tile height (128 or 256)
+    // x6 stride-2 input gradient, one output parity class (py, px) per launch: the
+    // GEMM pixels are gx(2 oh + py, 2 ow + px) on the Ho x Wo class grid, the taps
+    // kh = kh0 + 2 th (th < nth), kw = kw0 + 2 tw (tw < ntw) read gy(oh + dy0 - th,
+    // ow + dx0 - tw); outputs scatter into the oHf x oWf image
+    int par, py, px, kh0, kw0, ntw, dy0, dx0, oHf, oWf;
     int flatk;               // x6 fwd / dgrad with C < 32: K chunks run over the flattened
                              // (tap, channel) index, several taps per chunk
     const float* a;          // fwd: x; dgrad: gy; wgrad: x
@@ -553,7 +560,14 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
         const bool live = t < nchunks;
         int kh, kw, off;
         bool cok;
-        if (a.flatk) {
+        if (a.par) {
+            const int tc = tt / cchunks, c0 = (tt - tc * cchunks) * XBK;
+            const int th = tc / a.ntw, tw = tc - th * a.ntw;
+            kh = a.dy0 - th;   // gy row / column offsets of this tap (stride 1, pad 0 grid)
+            kw = a.dx0 - tw;
+            off = (kh * a.W + kw) * a.C + c0;
+            cok = live && c0 + 4 * qa < a.C;
+        } else if (a.flatk) {
             // this thread's 4 k of the chunk: one tap (C % 4 == 0), channels ci .. ci+3
             const int k = tt * XBK + 4 * qa, tap = k / a.C, ci = k - tap * a.C;
             kh = tap / a.KW;
@@ -577,7 +591,12 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
     auto dma = [&](int t, int buf) {
         if (t >= nchunks) return;
         const int tt = t0 + t;
-        const int tap = tt / cchunks, c0 = (tt - tap * cchunks) * XBK;
+        int tap = tt / cchunks;
+        const int c0 = (tt - tap * cchunks) * XBK;
+        if (a.par) {   // the class tap's index in the flipped [Ci][KT][Co] planes
+            const int th = tap / a.ntw, tw = tap - th * a.ntw;
+            tap = (a.KH - 1 - (a.kh0 + 2 * th)) * a.KW + (a.KW - 1 - (a.kw0 + 2 * tw));
+        }
         // B rows are [tap][channel] contiguous: the chunk starts at k = tap C + c0, or
         // at 32 tt of the flattened index
         const int kofs = a.flatk ? tt * XBK : tap * a.C + c0;
@@ -687,6 +706,13 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
     }
 
     float* out = a.y + (size_t)ks * a.M * a.N;
+    // output row of GEMM pixel m: m itself, or its gx pixel for a stride-2 parity class
+    // written in place (split partials stay class-ordered; the scatter reduce places them)
+    auto orow = [&](int m) {
+        if (!a.par || a.splits > 1) return m;
+        const int hw = a.Ho * a.Wo, b = m / hw, rem = m - b * hw, oh = rem / a.Wo, ow = rem - oh * a.Wo;
+        return (b * a.oHf + 2 * oh + a.py) * a.oWf + 2 * ow + a.px;
+    };
     if constexpr (G::MT == 16) {
         // 16x16 D: lane l holds column l & 15, rows 4 (l >> 4) .. + 3
         const int n = n0 + wn * 16 + (lane & 15);
@@ -696,7 +722,7 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int m = m0 + wm * (TM * 16) + 16 * i + 4 * (lane >> 4) + e;
-                    if (m < a.M) out[m * a.N + n] = acc[i][e];
+                    if (m < a.M) out[orow(m) * a.N + n] = acc[i][e];
                 }
         }
     } else {
@@ -707,7 +733,7 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
                     const int m = m0 + wm * (TM * 32) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
-                    if (m < a.M) out[m * a.N + n] = acc[i][e];
+                    if (m < a.M) out[orow(m) * a.N + n] = acc[i][e];
                 }
         }
     }
@@ -951,6 +977,41 @@ __global__ __launch_bounds__(256) void conv_reduce_kernel(const float4* part, fl
     }
 }
 
+// conv_reduce_kernel for a stride-2 parity class: class-ordered partials [splits][M][N]
+// summed the same way, each output quad written to its gx pixel
+__global__ __launch_bounds__(256) void conv_reduce_scatter_kernel(const float4* part, float4* y, int n4, int splits,
+                                                                   int N4, int Hc, int Wc, int oHf, int oWf, int py,
+                                                                   int px) {
+    __shared__ float4 red[kRedLanes][kRedOut];
+    const int o = threadIdx.x % kRedOut, l = threadIdx.x / kRedOut;
+    const int i = blockIdx.x * kRedOut + o;
+    float4 s = {0.f, 0.f, 0.f, 0.f};
+    if (i < n4) {
+        for (int k = l; k < splits; k += kRedLanes) {
+            const float4 v = part[(size_t)k * n4 + i];
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+    }
+    red[l][o] = s;
+    __syncthreads();
+    if (l == 0 && i < n4) {
+#pragma unroll
+        for (int j = 1; j < kRedLanes; ++j) {
+            const float4 v = red[j][o];
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+        const int m = i / N4, q = i - m * N4, hw = Hc * Wc, b = m / hw, rem = m - b * hw, oh = rem / Wc,
+                  ow = rem - oh * Wc;
+        y[((size_t)(b * oHf + 2 * oh + py) * oWf + 2 * ow + px) * N4 + q] = s;
+    }
+}
+
 bool valid(const md2_conv_desc* d) {
     if (!d) return false;
     if (d->batch < 1 || d->height < 1 || d->width < 1) return false;
@@ -1146,6 +1207,90 @@ void flat_k(ConvArgs& a, int mode) {
     }
 }
 
+void launch_x6(const ConvArgs& a, hipStream_t st) {
+    const dim3 grid(a.mblocks * a.nblocks * a.splits);
+    if (a.bm == 256) hipLaunchKernelGGL((conv_x6_kernel<128, 256>), grid, dim3(X6Geo<128, 256>::NT), 0, st, a);
+    else if (a.bn == 128) hipLaunchKernelGGL((conv_x6_kernel<128, 128>), grid, dim3(X6Geo<128, 128>::NT), 0, st, a);
+    else if (a.bn == 64) hipLaunchKernelGGL((conv_x6_kernel<64, 128>), grid, dim3(X6Geo<64, 128>::NT), 0, st, a);
+    else if (a.bn == 32) hipLaunchKernelGGL((conv_x6_kernel<32, 128>), grid, dim3(X6Geo<32, 128>::NT), 0, st, a);
+    else hipLaunchKernelGGL((conv_x6_kernel<16, 128>), grid, dim3(X6Geo<16, 128>::NT), 0, st, a);
+}
+
+// Stride-2 input gradient on x6 (MD2_CONV_X6, at least 32 output channels): gx pixels
+// of one parity (py, px) receive only the taps kh ≡ py + pad, kw ≡ px + pad (mod 2),
+// each from one gy pixel — a stride-1 GEMM over that class's Ho x Wo grid, scattered
+// into gx.  Four launches (a 1x1 stride-2 convolution's odd classes have no taps: they
+// run with no chunks and write zeros).  false: the class is empty.
+bool dgrad_s2_class(const md2_conv_desc* d, int py, int px, ConvArgs& a) {
+    const Shape s = shape_of(d);
+    a = ConvArgs{};
+    a.KH = s.KH;
+    a.KW = s.KW;
+    a.B = s.B; a.H = s.Ho; a.W = s.Wo; a.C = s.N;   // GEMM input: gy
+    a.Ho = (s.H - py + 1) / 2;
+    a.Wo = (s.W - px + 1) / 2;
+    if (a.Ho < 1 || a.Wo < 1) return false;
+    a.stride = 1;
+    a.pad = 0;
+    a.N = s.C;
+    a.Cg = s.N;
+    a.M = s.B * a.Ho * a.Wo;
+    a.par = 1;
+    a.py = py;
+    a.px = px;
+    a.oHf = s.H;
+    a.oWf = s.W;
+    a.kh0 = (py + s.p) & 1;
+    a.kw0 = (px + s.p) & 1;
+    const int nth = a.kh0 < s.KH ? (s.KH - a.kh0 + 1) / 2 : 0, ntw = a.kw0 < s.KW ? (s.KW - a.kw0 + 1) / 2 : 0;
+    a.ntw = ntw > 0 ? ntw : 1;
+    a.dy0 = (py + s.p - a.kh0) / 2;
+    a.dx0 = (px + s.p - a.kw0) / 2;
+    a.a_elems = s.B * s.Ho * s.Wo * s.N;
+    a.b_elems = 3 * s.N * s.KH * s.KW * s.C;
+    const int taps = nth * ntw;
+    a.nchunks = taps > 0 ? taps * ((s.N + XBK - 1) / XBK) : 1;
+    plan_x6(a, d->flags);
+    if (taps == 0) {   // zeros: no chunks, no split
+        a.nchunks = 0;
+        a.chunks_per_split = 0;
+        a.splits = 1;
+    }
+    return true;
+}
+
+bool use_x6_s2(const md2_conv_desc* d) {
+    return d->stride == 2 && use_x6(d, MODE_DGRAD) && d->out_channels >= XBK;
+}
+
+int run_dgrad_s2(const md2_conv_desc* d, const float* gy, const float* w, float* gx, void* ws, void* stream) {
+    if (!ws) return md2_report_error(MD2_ERR_ARG, "conv_dgrad (stride 2): workspace required");
+    const hipStream_t st = (hipStream_t)stream;
+    __bf16* planes = (d->flags & MD2_CONV_PRESPLIT) ? (__bf16*)w : (__bf16*)ws;
+    if (!(d->flags & MD2_CONV_PRESPLIT)) {
+        const int nw = d->out_channels * d->kernel_h * d->kernel_w * d->in_channels;
+        hipLaunchKernelGGL(conv_wsplit_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, w, planes, d->out_channels,
+                           d->kernel_h * d->kernel_w, d->in_channels, 1);
+    }
+    for (int py = 0; py < 2; ++py)
+        for (int px = 0; px < 2; ++px) {
+            ConvArgs a;
+            if (!dgrad_s2_class(d, py, px, a)) continue;
+            a.a = gy;
+            a.b = (const float*)planes;
+            a.y = a.splits > 1 ? (float*)((char*)ws + x6_planes_bytes(d)) : gx;
+            launch_x6(a, st);
+            if (a.splits > 1) {
+                const int n4 = a.M * a.N / 4;
+                hipLaunchKernelGGL(conv_reduce_scatter_kernel, dim3((n4 + kRedOut - 1) / kRedOut), dim3(256), 0, st,
+                                   (const float4*)a.y, (float4*)gx, n4, a.splits, a.N / 4, a.Ho, a.Wo, a.oHf, a.oWf,
+                                   py, px);
+            }
+        }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
 int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float* out, void* ws, void* stream,
         const char* name) {
     ConvArgs a = (mode == MODE_WGRAD && use_x6(d, mode)) ? args_x6_wgrad(d) : args_of(d, mode);
@@ -1173,15 +1318,7 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
         if (!(d->flags & MD2_CONV_PRESPLIT))
             hipLaunchKernelGGL(conv_wsplit_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, B, planes,
                                d->out_channels, d->kernel_h * d->kernel_w, d->in_channels, mode == MODE_DGRAD ? 1 : 0);
-        const dim3 grid(a.mblocks * a.nblocks * a.splits);
-        if (a.bm == 256) {
-            hipLaunchKernelGGL((conv_x6_kernel<128, 256>), grid, dim3(X6Geo<128, 256>::NT), 0, st, a);
-        } else {
-            if (BN == 128) hipLaunchKernelGGL((conv_x6_kernel<128, 128>), grid, dim3(X6Geo<128, 128>::NT), 0, st, a);
-            else if (BN == 64) hipLaunchKernelGGL((conv_x6_kernel<64, 128>), grid, dim3(X6Geo<64, 128>::NT), 0, st, a);
-            else if (BN == 32) hipLaunchKernelGGL((conv_x6_kernel<32, 128>), grid, dim3(X6Geo<32, 128>::NT), 0, st, a);
-            else hipLaunchKernelGGL((conv_x6_kernel<16, 128>), grid, dim3(X6Geo<16, 128>::NT), 0, st, a);
-        }
+        launch_x6(a, st);
     } else if (mode == MODE_FWD) launch<MODE_FWD>(a, BN, st);
     else if (mode == MODE_DGRAD) launch<MODE_DGRAD>(a, BN, st);
     else launch<MODE_WGRAD>(a, BN, st);
@@ -1195,6 +1332,16 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
 }
 
 size_t ws_bytes(const md2_conv_desc* d, int mode) {
+    if (mode == MODE_DGRAD && use_x6_s2(d)) {
+        size_t part = 0;
+        for (int py = 0; py < 2; ++py)
+            for (int px = 0; px < 2; ++px) {
+                ConvArgs c;
+                if (dgrad_s2_class(d, py, px, c) && c.splits > 1)
+                    part = std::max(part, sizeof(float) * (size_t)c.splits * c.M * c.N);
+            }
+        return x6_planes_bytes(d) + part;
+    }
     ConvArgs a = (mode == MODE_WGRAD && use_x6(d, mode)) ? args_x6_wgrad(d) : args_of(d, mode);
     if (use_x6(d, mode) && mode == MODE_WGRAD) {
         plan_x6(a, d->flags, true);
@@ -1216,7 +1363,7 @@ extern "C" {
 size_t md2_conv_workspace_bytes(const md2_conv_desc* d) {
     if (!valid(d)) return 0;
     size_t m = ws_bytes(d, MODE_FWD);
-    if (d->stride == 1) m = m > ws_bytes(d, MODE_DGRAD) ? m : ws_bytes(d, MODE_DGRAD);
+    if (d->stride == 1 || use_x6_s2(d)) m = m > ws_bytes(d, MODE_DGRAD) ? m : ws_bytes(d, MODE_DGRAD);
     const size_t w = ws_bytes(d, MODE_WGRAD);
     return m > w ? m : w;
 }
@@ -1243,9 +1390,11 @@ int md2_conv_fwd(const md2_conv_desc* d, const float* x, const float* weight, fl
 
 int md2_conv_dgrad(const md2_conv_desc* d, const float* grad_y, const float* weight, float* grad_x,
                    void* workspace, void* stream) {
-    if (!valid(d) || d->stride != 1)
-        return md2_report_error(MD2_ERR_ARG, "conv_dgrad: stride 1, channels % 4, pad < kernel, sizes < 2^29");
+    if (!valid(d) || (d->stride != 1 && !use_x6_s2(d)))
+        return md2_report_error(MD2_ERR_ARG, "conv_dgrad: stride 1 (stride 2: MD2_CONV_X6, channels % 8, >= 32 "
+                                             "output channels), channels % 4, pad < kernel, sizes < 2^29");
     if (!grad_y || !weight || !grad_x) return md2_report_error(MD2_ERR_ARG, "conv_dgrad: NULL operand");
+    if (d->stride == 2) return run_dgrad_s2(d, grad_y, weight, grad_x, workspace, stream);
     return run(d, MODE_DGRAD, grad_y, weight, grad_x, workspace, stream, "conv_dgrad: workspace required (K split)");
 }
 

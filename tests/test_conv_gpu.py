@@ -177,7 +177,7 @@ def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
     for fl in (conv_ops.X6, conv_ops.X6 | conv_ops.BM256):
         e_x6 = _rel(conv_ops._fwd(x, w, s, p, fl).double().cpu(), ref)
         assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, (fl, e_x6, e_mi)
-    if s == 1:
+    if s == 1 or conv_ops._x6_s2_ok(x, w, s):   # stride 2: four parity-class GEMMs
         gy = torch.randn(ref.shape, device="cuda").contiguous(memory_format=CL)
         gref = torch.ops.aten.convolution_backward(gy.double().cpu(), x.double().cpu(), w.double().cpu(), None, (s, s),
                                                    (p, p), (1, 1), False, (0, 0), 1, (True, False, False))[0]
@@ -185,8 +185,8 @@ def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
                                                    (True, False, False))[0].double().cpu()
         e_mi = _rel(g_mi, gref)
         for fl in (conv_ops.X6, conv_ops.X6 | conv_ops.BM256):
-            e_x6 = _rel(conv_ops._dgrad(gy, x, w, p, fl).double().cpu(), gref)
-            assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, (fl, e_x6, e_mi)
+            e_x6 = _rel(conv_ops._dgrad(gy, x, w, p, fl, s).double().cpu(), gref)
+            assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, (fl, s, e_x6, e_mi)
     gy = torch.randn(ref.shape, device="cuda").contiguous(memory_format=CL)
     wref = torch.ops.aten.convolution_backward(gy.double().cpu(), x.double().cpu(), w.double().cpu(), None, (s, s),
                                                (p, p), (1, 1), False, (0, 0), 1, (False, True, False))[1]
@@ -209,3 +209,7 @@ def test_x6_presplit_planes_match_in_call_split():
     for fl in (conv_ops.X6, conv_ops.X6 | conv_ops.BM256):
         assert torch.equal(conv_ops._fwd_planes(x, w, pf, 1, 1, fl), conv_ops._fwd(x, w, 1, 1, fl))
         assert torch.equal(conv_ops._dgrad_planes(gy, x, w, pd, 1, fl), conv_ops._dgrad(gy, x, w, 1, fl))
+    # stride 2 (parity classes) reads the same flipped planes
+    gy2 = torch.randn(B, N, H // 2, W // 2, device="cuda").contiguous(memory_format=CL)
+    pf2, pd2 = conv_ops._split_weights(x, w, 2, 1, True)
+    assert torch.equal(conv_ops._dgrad_planes(gy2, x, w, pd2, 1, conv_ops.X6, 2), conv_ops._dgrad(gy2, x, w, 1, conv_ops.X6, 2))
