@@ -468,8 +468,10 @@ int md2_conv_split_weights(const md2_conv_desc* desc, const float* weight, void*
                            void* stream);
 int md2_conv_fwd(const md2_conv_desc* desc, const float* x, const float* weight, float* y, void* workspace,
                  void* stream);
-/* grad_x (batch, height, width, in_channels) from grad_y (batch, Ho, Wo, out_channels);
- * stride 1 only (a "full" convolution with the flipped, transposed weight) */
+/* grad_x (batch, height, width, in_channels) from grad_y (batch, Ho, Wo, out_channels):
+ * stride 1 (a "full" convolution with the flipped, transposed weight), or stride 2 with
+ * MD2_CONV_X6 and >= 32 out_channels (four output-parity classes, each a stride-1 GEMM
+ * over its taps, scattered into grad_x) */
 int md2_conv_dgrad(const md2_conv_desc* desc, const float* grad_y, const float* weight, float* grad_x,
                    void* workspace, void* stream);
 /* grad_weight (out_channels, kernel_h, kernel_w, in_channels) = channels_last layout */
