@@ -678,6 +678,10 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
     // issued before the A loads, so vmcnt(AQ) before the barrier waits for the DMA
     // alone (vector-memory loads complete in order).  A loads past the last chunk read
     // zeros.
+    // 8-wave blocks: the second-dispatched half (waves 4-7, each sharing a SIMD with
+    // one of waves 0-3) loses every VALU arbitration at equal priority; one static
+    // s_setprio for it (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+    if (NT == 512 && wid >= 4) __builtin_amdgcn_s_setprio(1);
     load(0, fa0);
     load(1, fa1);
     dma(0, 0);
@@ -897,6 +901,7 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
         for (int i = 0; i < TM; ++i) tot[i] += acc[i];
     };
 
+    if (wid >= 4) __builtin_amdgcn_s_setprio(1);   // as in conv_x6_kernel
     if (!stager) {
         // waves 2-3 at BMW = 64: multiply only
         __syncthreads();
