@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 11
+#define MD2_ABI_VERSION 12
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -477,6 +477,16 @@ int md2_conv_dgrad(const md2_conv_desc* desc, const float* grad_y, const float* 
 /* grad_weight (out_channels, kernel_h, kernel_w, in_channels) = channels_last layout */
 int md2_conv_wgrad(const md2_conv_desc* desc, const float* x, const float* grad_y, float* grad_weight,
                    void* workspace, void* stream);
+/* Direct 3x3 stride-1 convolution on the f32 VALU (csrc/direct.hip) for the
+ * DepthDecoder's 16-output-channel layers (networks/depth_decoder.py:50-65:
+ * upconv(0,0) 32->16, upconv(0,1) 16->16) and their input gradients: y (batch, Ho, Wo,
+ * out_channels) = x (batch, height, width, in_channels) correlated with
+ * wk [9][in_channels][out_channels] (tap-major; for the input gradient: the flipped
+ * weight with its channel roles swapped, pad = 2 - the forward's pad), zero padding
+ * `pad` (0..2), Ho = height + 2 pad - 2.  (in, out) channels (16,16), (32,16) or
+ * (16,32); kernel 3x3, stride 1; desc flags unused.  One thread per output pixel,
+ * exact f32 FMA chains. */
+int md2_conv_direct(const md2_conv_desc* desc, const float* x, const float* wk, float* y, void* stream);
 
 #ifdef __cplusplus
 }

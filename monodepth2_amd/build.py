@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB_NAME = "libmd2hot.so"
 LIB_PATH = os.path.join(CSRC, LIB_NAME)
-SOURCES = ["md2hot.hip", "decoder.hip", "pose.hip", "augment.hip", "bnorm.hip", "pool.hip", "adam.hip", "disphead.hip", "stem.hip", "bias_act.hip", "conv.hip", "glue.hip"]
+SOURCES = ["md2hot.hip", "decoder.hip", "pose.hip", "augment.hip", "bnorm.hip", "pool.hip", "adam.hip", "disphead.hip", "stem.hip", "bias_act.hip", "conv.hip", "direct.hip", "glue.hip"]
 ARCH = os.environ.get("MD2_OFFLOAD_ARCH", "gfx950")
 
 

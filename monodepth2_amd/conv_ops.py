@@ -41,6 +41,7 @@ ENABLED = True     # tests flip this to compare with MIOpen on the same module
 AUTOTUNE = True    # False: always the MFMA kernels (tests)
 _ws: Dict[Tuple[int, int], torch.Tensor] = {}
 _choice: Dict[tuple, int] = {}     # (op, shape) -> index of the fastest candidate
+_times: Dict[tuple, dict] = {}     # (op, shape) -> {candidate: timed ms} (tools/conv_choices.py)
 X6 = _lib.CONV_X6
 BM256 = _lib.CONV_BM256
 PRESPLIT = _lib.CONV_PRESPLIT
@@ -156,7 +157,7 @@ def _cached(op: str, key: tuple):
     return _choice.get((op,) + key)
 
 
-def _fastest(op: str, key: tuple, cands) -> int:
+def _fastest(op: str, key: tuple, cands, names=None) -> int:
     """Time every candidate once per (op, shape) (3 runs each after a warm-up,
     median) and remember the fastest; the last candidate is MIOpen, kept unless
     another beats it by >= 3 %.  Without AUTOTUNE: the first candidate.  Not while a
@@ -180,9 +181,42 @@ def _fastest(op: str, key: tuple, cands) -> int:
             e1.synchronize()
             ts.append(e0.elapsed_time(e1))
         times.append(sorted(ts)[1])
+    _times[k] = dict(zip(names or [str(i) for i in range(len(cands))], times))
     best = min(range(len(cands) - 1), key=lambda i: times[i]) if len(cands) > 1 else 0
     _choice[k] = best if times[best] < 0.97 * times[-1] else len(cands) - 1
     return _choice[k]
+
+
+_DIRECT = ((16, 16), (32, 16), (16, 32))   # (in, out) channels of md2_conv_direct
+_ddescs: Dict[tuple, object] = {}
+
+
+def _direct_ok(cin: int, cout: int, k: int, stride: int) -> bool:
+    """md2_conv_direct covers this 3x3 stride-1 convolution (the DepthDecoder's
+    16-output-channel layers, their input gradients with the roles swapped)."""
+    return k == 3 and stride == 1 and (cin, cout) in _DIRECT
+
+
+def _direct(a: torch.Tensor, wk: torch.Tensor, pad: int, cout: int) -> torch.Tensor:
+    """a (B, C, H, W) channels_last correlated with wk [3][3][C][cout], zero padding `pad`."""
+    B, C, H, W = a.shape
+    y = torch.empty(B, cout, H + 2 * pad - 2, W + 2 * pad - 2, device=a.device, memory_format=_CL)
+    k = (tuple(a.shape), cout, pad)
+    d = _ddescs.get(k)
+    if d is None:
+        d = _ddescs[k] = _lib.ConvDesc(B, H, W, C, cout, 3, 3, 1, pad, 0)
+    _lib.check(_lib.lib().md2_conv_direct(ctypes.byref(d), a.data_ptr(), wk.data_ptr(), y.data_ptr(),
+                                          _lib.stream(a.device)), "md2_conv_direct")
+    return y
+
+
+def _direct_fwd(x, w, pad):
+    return _direct(x, w.permute(2, 3, 1, 0).contiguous(), pad, w.shape[0])
+
+
+def _direct_dgrad(gy, w, pad):
+    # gx = gy correlated with the flipped weight, channel roles swapped, pad 2 - pad
+    return _direct(gy, w.flip(2, 3).permute(2, 3, 0, 1).contiguous(), 2 - pad, w.shape[1])
 
 
 def _fits(cin: int, cout: int) -> bool:
@@ -199,11 +233,14 @@ class _Conv(torch.autograd.Function):
         cands = None
         i = _cached("fwd", ctx.key)
         if i is None or not (x6 and i < 2):
+            direct = _direct_ok(weight.shape[1], weight.shape[0], weight.shape[2], stride)
             cands = ([lambda: _fwd(x, weight, stride, pad, X6), lambda: _fwd(x, weight, stride, pad, X6 | BM256)]
-                     if x6 else []) + \
-                [lambda: _fwd(x, weight, stride, pad), lambda: F.conv2d(x, weight, None, stride, pad)]
+                     if x6 else []) + [lambda: _fwd(x, weight, stride, pad)] + \
+                ([lambda: _direct_fwd(x, weight, pad)] if direct else []) + \
+                [lambda: F.conv2d(x, weight, None, stride, pad)]
+            names = (["x6", "x6_256"] if x6 else []) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"]
             if i is None:
-                i = _fastest("fwd", ctx.key, cands)
+                i = _fastest("fwd", ctx.key, cands, names)
         planes_dg = None
         if x6 and i < 2:
             # the x6 forward: split the weight once for it and for the input gradient
@@ -226,9 +263,12 @@ class _Conv(torch.autograd.Function):
         if need_x:
             if s == 1:
                 x6 = _x6_ok(x, w)
+                direct = _direct_ok(w.shape[0], w.shape[1], w.shape[2], s)
                 cands = ([lambda: _dgrad(gy, x, w, p, X6), lambda: _dgrad(gy, x, w, p, X6 | BM256)] if x6 else []) + \
-                    [lambda: _dgrad(gy, x, w, p), lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
-                i = _fastest("dgrad", ctx.key, cands)
+                    [lambda: _dgrad(gy, x, w, p)] + ([lambda: _direct_dgrad(gy, w, p)] if direct else []) + \
+                    [lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
+                names = (["x6", "x6_256"] if x6 else []) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"]
+                i = _fastest("dgrad", ctx.key, cands, names)
                 if x6 and i < 2 and planes_dg is not None:
                     gx = _dgrad_planes(gy, x, w, planes_dg, p, _FLAGS[i])
                 elif i < len(cands) - 1:
@@ -238,7 +278,7 @@ class _Conv(torch.autograd.Function):
             elif _x6_s2_ok(x, w, s):
                 cands = [lambda: _dgrad(gy, x, w, p, X6, 2),
                          lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
-                i = _fastest("dgrad", ctx.key, cands)
+                i = _fastest("dgrad", ctx.key, cands, ["x6_s2", "miopen"])
                 if i == 0:
                     gx = (_dgrad_planes(gy, x, w, planes_dg, p, X6, 2) if planes_dg is not None else cands[0]())
                 else:
@@ -248,7 +288,7 @@ class _Conv(torch.autograd.Function):
         if need_w:
             cands = ([lambda: _wgrad(gy, x, w, s, p, X6)] if _x6_ok(x, w) else []) + \
                 [lambda: _wgrad(gy, x, w, s, p), lambda: _miopen_bwd(gy, x, w, s, p, (False, True, False))[1]]
-            i = _fastest("wgrad", ctx.key, cands)
+            i = _fastest("wgrad", ctx.key, cands, (["x6"] if _x6_ok(x, w) else []) + ["f32mfma", "miopen"])
             if i < len(cands) - 1:
                 gw = cands[i]()
             else:

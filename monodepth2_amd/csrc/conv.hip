@@ -1277,10 +1277,23 @@ int run_dgrad_s2(const md2_conv_desc* d, const float* gy, const float* w, float*
         hipLaunchKernelGGL(conv_wsplit_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, w, planes, d->out_channels,
                            d->kernel_h * d->kernel_w, d->in_channels, 1);
     }
+    // classes without taps (a 1x1 stride-2 convolution's three odd ones) are zeros:
+    // one memset of grad_x instead of a GEMM launch per class that multiplies nothing
+    bool tapless = false;
     for (int py = 0; py < 2; ++py)
         for (int px = 0; px < 2; ++px) {
             ConvArgs a;
-            if (!dgrad_s2_class(d, py, px, a)) continue;
+            if (dgrad_s2_class(d, py, px, a) && a.nchunks == 0) tapless = true;
+        }
+    if (tapless) {
+        const hipError_t me = hipMemsetAsync(gx, 0, sizeof(float) * (size_t)d->batch * d->height * d->width *
+                                                        d->in_channels, st);
+        if (me != hipSuccess) return md2_report_error(MD2_ERR_HIP, hipGetErrorString(me));
+    }
+    for (int py = 0; py < 2; ++py)
+        for (int px = 0; px < 2; ++px) {
+            ConvArgs a;
+            if (!dgrad_s2_class(d, py, px, a) || a.nchunks == 0) continue;
             a.a = gy;
             a.b = (const float*)planes;
             a.y = a.splits > 1 ? (float*)((char*)ws + x6_planes_bytes(d)) : gx;

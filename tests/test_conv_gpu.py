@@ -213,3 +213,30 @@ def test_x6_presplit_planes_match_in_call_split():
     gy2 = torch.randn(B, N, H // 2, W // 2, device="cuda").contiguous(memory_format=CL)
     pf2, pd2 = conv_ops._split_weights(x, w, 2, 1, True)
     assert torch.equal(conv_ops._dgrad_planes(gy2, x, w, pd2, 1, conv_ops.X6, 2), conv_ops._dgrad(gy2, x, w, 1, conv_ops.X6, 2))
+
+
+@pytest.mark.parametrize("B,C,N,p,H,W", [(2, 16, 16, 0, 20, 34), (2, 32, 16, 0, 12, 18), (2, 16, 32, 1, 9, 13),
+                                         (1, 16, 16, 1, 7, 9), (3, 32, 16, 2, 5, 6)])
+def test_direct_conv_matches_miopen(B, C, N, p, H, W):
+    """md2_conv_direct (f32 VALU, one thread per output pixel) for the DepthDecoder's
+    16-output-channel layers: forward and input gradient vs MIOpen fp32 (the two are
+    f32 FMA chains in different orders)."""
+    torch.manual_seed(B * 10 + C + N + p)
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    w = (torch.randn(N, C, 3, 3, device="cuda") / (9 * C) ** 0.5).contiguous(memory_format=CL)
+    y = conv_ops._direct_fwd(x, w, p)
+    yr = F.conv2d(x, w, padding=p)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=CL)
+    assert _rel(y, yr) < 2e-5
+    gy = torch.randn_like(yr).contiguous(memory_format=CL)
+    gx = conv_ops._direct_dgrad(gy, w, p)
+    gxr = torch.ops.aten.convolution_backward(gy, x, w, None, (1, 1), (p, p), (1, 1), False, (0, 0), 1,
+                                              (True, False, False))[0]
+    assert gx.shape == x.shape
+    assert _rel(gx, gxr) < 1e-4
+
+
+def test_direct_conv_rejects_other_shapes():
+    d = _lib.ConvDesc(1, 8, 8, 64, 16, 3, 3, 1, 1, 0)   # 64 input channels: not a direct shape
+    x = torch.zeros(1, 8, 8, 64, device="cuda")
+    assert _lib.lib().md2_conv_direct(ctypes.byref(d), x.data_ptr(), x.data_ptr(), x.data_ptr(), None) != 0
