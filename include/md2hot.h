@@ -487,6 +487,13 @@ int md2_conv_wgrad(const md2_conv_desc* desc, const float* x, const float* grad_
  * (16,32); kernel 3x3, stride 1; desc flags unused.  One thread per output pixel,
  * exact f32 FMA chains. */
 int md2_conv_direct(const md2_conv_desc* desc, const float* x, const float* wk, float* y, void* stream);
+/* Weight gradient of the same layers on the f32 VALU: grad_weight (out_channels, 3, 3,
+ * in_channels) = sum over output pixels of grad_y x the input's tap; (in, out) channels
+ * (16,16) or (32,16), stride 1, pad 0..2.  Per-block partial rows in `workspace`
+ * (md2_conv_wgrad_direct_workspace_bytes), summed in block order (deterministic). */
+size_t md2_conv_wgrad_direct_workspace_bytes(const md2_conv_desc* desc);
+int md2_conv_wgrad_direct(const md2_conv_desc* desc, const float* x, const float* grad_y, float* grad_weight,
+                          void* workspace, void* stream);
 
 #ifdef __cplusplus
 }

@@ -63,7 +63,8 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_stem_wgrad_workspace_bytes", "md2_stem_wgrad", "md2_bias_act_fwd", "md2_bias_act_bwd",
            "md2_bias_act_workspace_bytes", "md2_maxpool3s2_bwd_add", "md2_bn_bwd_multi",
            "md2_conv_fwd", "md2_conv_workspace_bytes", "md2_conv_split_weights",
-           "md2_conv_dgrad", "md2_conv_wgrad", "md2_conv_direct"]
+           "md2_conv_dgrad", "md2_conv_wgrad", "md2_conv_direct", "md2_conv_wgrad_direct",
+           "md2_conv_wgrad_direct_workspace_bytes"]
 
 PAD_ELU = 1 << 0
 PAD_UPSAMPLE = 1 << 1
@@ -162,6 +163,10 @@ def _declare(L):
     L.md2_conv_split_weights.restype = ctypes.c_int
     L.md2_conv_direct.restype = ctypes.c_int
     L.md2_conv_direct.argtypes = [ctypes.POINTER(ConvDesc)] + [_vp] * 4
+    L.md2_conv_wgrad_direct.restype = ctypes.c_int
+    L.md2_conv_wgrad_direct.argtypes = [ctypes.POINTER(ConvDesc)] + [_vp] * 5
+    L.md2_conv_wgrad_direct_workspace_bytes.restype = ctypes.c_size_t
+    L.md2_conv_wgrad_direct_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc)]
     L.md2_conv_split_weights.argtypes = [ctypes.POINTER(ConvDesc)] + [_vp] * 4
     L.md2_conv_workspace_bytes.restype = ctypes.c_size_t
     L.md2_conv_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc)]

@@ -210,6 +210,18 @@ def _direct(a: torch.Tensor, wk: torch.Tensor, pad: int, cout: int) -> torch.Ten
     return y
 
 
+def _direct_wgrad(gy, x, w, pad):
+    """md2_conv_wgrad_direct: the weight gradient of a (16|32) -> 16 3x3 convolution."""
+    N, C = w.shape[0], w.shape[1]
+    gw = torch.empty_like(w, memory_format=_CL)
+    d = _desc(x, w, 1, pad)
+    nbytes = _lib.lib().md2_conv_wgrad_direct_workspace_bytes(ctypes.byref(d))
+    ws = _workspace(x.device, nbytes)
+    _lib.check(_lib.lib().md2_conv_wgrad_direct(ctypes.byref(d), x.data_ptr(), gy.data_ptr(), gw.data_ptr(),
+                                                ws.data_ptr(), _lib.stream(x.device)), "md2_conv_wgrad_direct")
+    return gw
+
+
 def _direct_fwd(x, w, pad):
     return _direct(x, w.permute(2, 3, 1, 0).contiguous(), pad, w.shape[0])
 
@@ -286,9 +298,12 @@ class _Conv(torch.autograd.Function):
             else:
                 mi_x = True
         if need_w:
-            cands = ([lambda: _wgrad(gy, x, w, s, p, X6)] if _x6_ok(x, w) else []) + \
-                [lambda: _wgrad(gy, x, w, s, p), lambda: _miopen_bwd(gy, x, w, s, p, (False, True, False))[1]]
-            i = _fastest("wgrad", ctx.key, cands, (["x6"] if _x6_ok(x, w) else []) + ["f32mfma", "miopen"])
+            direct = _direct_ok(w.shape[1], w.shape[0], w.shape[2], s) and w.shape[0] == 16
+            cands = ([lambda: _wgrad(gy, x, w, s, p, X6)] if _x6_ok(x, w) else []) + [lambda: _wgrad(gy, x, w, s, p)] + \
+                ([lambda: _direct_wgrad(gy, x, w, p)] if direct else []) + \
+                [lambda: _miopen_bwd(gy, x, w, s, p, (False, True, False))[1]]
+            i = _fastest("wgrad", ctx.key, cands,
+                         (["x6"] if _x6_ok(x, w) else []) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"])
             if i < len(cands) - 1:
                 gw = cands[i]()
             else:

@@ -69,6 +69,122 @@ __global__ __launch_bounds__(kThreads) void conv3_direct_kernel(const float* __r
     for (int o = 0; o < COUT / 4; ++o) yp[o] = float4{acc[4 * o], acc[4 * o + 1], acc[4 * o + 2], acc[4 * o + 3]};
 }
 
+
+// Weight gradient of the same layers: gw[co][tap][ci] = sum_p gy[p][co] x[p + tap][ci]
+// over every output pixel p.  A block walks chunks of 64 consecutive pixels: the chunk's
+// gy rows and each pixel's nine tap rows of x (zero outside the image) are staged in
+// LDS; a thread owns a (4 co x 4 ci) quad pair over all 9 taps (144 accumulators) and
+// a residue class of the chunk's pixels (G = 256 / pairs groups), so per pixel it
+// reads one gy quad and nine x quads for 144 FMAs.  The groups' sums are combined in
+// LDS in a fixed order, one partial row [COUT][9][CIN] per block; conv3_wgrad_reduce
+// adds the blocks' rows in block order (deterministic, no atomics).
+constexpr int kWChunk = 64;
+
+template <int CIN, int COUT>
+__global__ __launch_bounds__(kThreads) void conv3_wgrad_direct_kernel(const float* __restrict__ x,
+                                                                      const float* __restrict__ gy,
+                                                                      float* __restrict__ part, int B, int H, int W,
+                                                                      int Ho, int Wo, int pad, int chunks_per_block) {
+    constexpr int IQ = CIN / 4, OQ = COUT / 4, PAIRS = IQ * OQ, G = kThreads / PAIRS;
+    constexpr int NOUT = COUT * 9 * CIN;
+    static_assert(kThreads % PAIRS == 0 && kThreads == 4 * kWChunk && IQ % 4 == 0 && OQ <= 4, "thread roles");
+    __shared__ float4 sx[kWChunk][9][IQ];
+    __shared__ float4 sg[kWChunk][OQ];
+    __shared__ float red[G][PAIRS * 16];
+    const int tid = threadIdx.x, g = tid / PAIRS, u = tid - g * PAIRS, oq = u / IQ, iq = u - oq * IQ;
+    const int P = B * Ho * Wo;
+    float acc[9][4][4];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[t][a][c] = 0.f;
+    // staging role: chunk pixel t % 64 (one pixel decomposition per chunk) and quads
+    // j + 4 k of its [tap][quad] rows, j = t / 64 (tap = 4k / IQ and quad j + 4k % IQ
+    // are compile-time in k); the next chunk's loads are issued into registers before
+    // this chunk's FMAs, so their latency hides behind them
+    constexpr int NK = 9 * IQ / 4;
+    const int spp = tid % kWChunk, sj = tid / kWChunk;
+    float4 rx[NK], rg;
+    const int c0 = blockIdx.x * chunks_per_block;
+    const int cend = min(c0 + chunks_per_block, (P + kWChunk - 1) / kWChunk);
+    auto fetch = [&](int ch) {
+        const int p = ch * kWChunk + spp;
+        const bool live = ch < cend && p < P;
+        int b = 0, oh = 0, ow = 0;
+        if (live) {
+            b = p / (Ho * Wo);
+            const int rem = p - b * Ho * Wo;
+            oh = rem / Wo;
+            ow = rem - oh * Wo;
+        }
+        rg = (live && sj < OQ) ? ((const float4*)gy)[(size_t)p * OQ + sj] : float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int tap = 4 * k / IQ, q = sj + (4 * k) % IQ;
+            const int ih = oh + tap / 3 - pad, iw = ow + tap % 3 - pad;
+            rx[k] = (live && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+                        ? ((const float4*)x)[((size_t)(b * H + ih) * W + iw) * IQ + q]
+                        : float4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    fetch(c0);
+    for (int ch = c0; ch < cend; ++ch) {
+        if (sj < OQ) sg[spp][sj] = rg;
+#pragma unroll
+        for (int k = 0; k < NK; ++k) sx[spp][4 * k / IQ][sj + (4 * k) % IQ] = rx[k];
+        __syncthreads();
+        fetch(ch + 1);
+        for (int pp = g; pp < kWChunk; pp += G) {
+            const float4 gv = sg[pp][oq];
+            const float ga[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const float4 xv = sx[pp][t][iq];
+                const float xa[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[t][a][c] = fmaf(ga[a], xa[c], acc[t][a][c]);
+            }
+        }
+        __syncthreads();
+    }
+    // combine the G groups per tap in a fixed order, one partial row per block
+    float* out = part + (size_t)blockIdx.x * NOUT;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) red[g][u * 16 + a * 4 + c] = acc[t][a][c];
+        __syncthreads();
+        for (int i = tid; i < PAIRS * 16; i += kThreads) {
+            float sum = 0.f;
+            for (int k = 0; k < G; ++k) sum += red[k][i];
+            const int uu = i / 16, a = (i / 4) % 4, c = i % 4, oo = uu / IQ, ii = uu - oo * IQ;
+            out[((4 * oo + a) * 9 + t) * CIN + 4 * ii + c] = sum;
+        }
+        __syncthreads();
+    }
+}
+
+// gw[i] = sum over blocks (in block order) of part[blk][i]: 4 lanes per output
+// (every 4th block), lane sums added in lane order
+__global__ __launch_bounds__(kThreads) void conv3_wgrad_reduce_kernel(const float* __restrict__ part,
+                                                                      float* __restrict__ gw, int n, int nblk) {
+    __shared__ float red[4][kThreads / 4];
+    const int o = threadIdx.x % (kThreads / 4), l = threadIdx.x / (kThreads / 4);
+    const int i = blockIdx.x * (kThreads / 4) + o;
+    float s = 0.f;
+    if (i < n)
+        for (int k = l; k < nblk; k += 4) s += part[(size_t)k * n + i];
+    red[l][o] = s;
+    __syncthreads();
+    if (l == 0 && i < n) gw[i] = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
+}
+
 }  // namespace
 
 extern "C" {
@@ -97,6 +213,44 @@ int md2_conv_direct(const md2_conv_desc* d, const float* x, const float* wk, flo
                            d->width, Ho, Wo, d->pad);
     else
         return md2_report_error(MD2_ERR_ARG, "conv_direct: (in, out) channels (16,16), (32,16) or (16,32)");
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
+
+constexpr int kWBlocks = 512;   // partial rows of the weight gradient
+
+size_t md2_conv_wgrad_direct_workspace_bytes(const md2_conv_desc* d) {
+    return d ? sizeof(float) * (size_t)kWBlocks * d->out_channels * 9 * d->in_channels : 0;
+}
+
+int md2_conv_wgrad_direct(const md2_conv_desc* d, const float* x, const float* grad_y, float* grad_weight,
+                          void* workspace, void* stream) {
+    if (!d || !x || !grad_y || !grad_weight || !workspace)
+        return md2_report_error(MD2_ERR_ARG, "conv_wgrad_direct: NULL operand or workspace");
+    if (d->kernel_h != 3 || d->kernel_w != 3 || d->stride != 1 || d->pad < 0 || d->pad > 2 || d->batch < 1)
+        return md2_report_error(MD2_ERR_ARG, "conv_wgrad_direct: 3x3, stride 1, pad 0..2");
+    const int Ho = d->height + 2 * d->pad - 2, Wo = d->width + 2 * d->pad - 2;
+    if (Ho < 1 || Wo < 1) return md2_report_error(MD2_ERR_ARG, "conv_wgrad_direct: empty output");
+    const long long P = (long long)d->batch * Ho * Wo;
+    if (P * 32 >= (1ll << 31) || (long long)d->batch * d->height * d->width * 32 >= (1ll << 31))
+        return md2_report_error(MD2_ERR_ARG, "conv_wgrad_direct: tensors of < 2^26 pixels");
+    const int chunks = (int)((P + kWChunk - 1) / kWChunk);
+    const int per = (chunks + kWBlocks - 1) / kWBlocks;
+    const int nblk = (chunks + per - 1) / per;
+    const hipStream_t st = (hipStream_t)stream;
+    float* part = (float*)workspace;
+    const int ci = d->in_channels, co = d->out_channels, n = co * 9 * ci;
+    if (ci == 16 && co == 16)
+        hipLaunchKernelGGL((conv3_wgrad_direct_kernel<16, 16>), dim3(nblk), dim3(kThreads), 0, st, x, grad_y, part,
+                           d->batch, d->height, d->width, Ho, Wo, d->pad, per);
+    else if (ci == 32 && co == 16)
+        hipLaunchKernelGGL((conv3_wgrad_direct_kernel<32, 16>), dim3(nblk), dim3(kThreads), 0, st, x, grad_y, part,
+                           d->batch, d->height, d->width, Ho, Wo, d->pad, per);
+    else
+        return md2_report_error(MD2_ERR_ARG, "conv_wgrad_direct: (in, out) channels (16,16) or (32,16)");
+    hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3((n + kThreads / 4 - 1) / (kThreads / 4)), dim3(kThreads), 0,
+                       st, part, grad_weight, n, nblk);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }

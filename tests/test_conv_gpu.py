@@ -240,3 +240,21 @@ def test_direct_conv_rejects_other_shapes():
     d = _lib.ConvDesc(1, 8, 8, 64, 16, 3, 3, 1, 1, 0)   # 64 input channels: not a direct shape
     x = torch.zeros(1, 8, 8, 64, device="cuda")
     assert _lib.lib().md2_conv_direct(ctypes.byref(d), x.data_ptr(), x.data_ptr(), x.data_ptr(), None) != 0
+
+
+@pytest.mark.parametrize("B,C,p,H,W", [(2, 16, 0, 20, 34), (2, 32, 0, 12, 18), (1, 16, 1, 7, 9), (3, 32, 2, 5, 6),
+                                       (4, 16, 0, 66, 70)])
+def test_direct_wgrad_matches_miopen(B, C, p, H, W):
+    """md2_conv_wgrad_direct (per-block partial rows summed in block order) vs MIOpen's
+    fp32 weight gradient; bitwise reproducible run to run."""
+    torch.manual_seed(B * 10 + C + p + H)
+    N = 16
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    w = (torch.randn(N, C, 3, 3, device="cuda") / (9 * C) ** 0.5).contiguous(memory_format=CL)
+    gy = torch.randn_like(F.conv2d(x, w, padding=p)).contiguous(memory_format=CL)
+    gw = conv_ops._direct_wgrad(gy, x, w, p)
+    gwr = torch.ops.aten.convolution_backward(gy, x, w, None, (1, 1), (p, p), (1, 1), False, (0, 0), 1,
+                                              (False, True, False))[1]
+    assert gw.shape == w.shape and gw.is_contiguous(memory_format=CL)
+    assert _rel(gw, gwr) < 1e-4
+    assert torch.equal(gw, conv_ops._direct_wgrad(gy, x, w, p))

@@ -23,5 +23,8 @@ for name, C, N, H, W in [("dec.8 32->16", 32, 16, 98, 322), ("dec.9 16->16", 16,
          "fwd x6": timeit(lambda: conv_ops._fwd(x, w, 1, 0, conv_ops.X6)),
          "dgrad direct": timeit(lambda: conv_ops._direct(gy, wkd, 2, C)),
          "dgrad miopen": timeit(lambda: conv_ops._miopen_bwd(gy, x, w, 1, 0, (True, False, False))[0]),
-         "dgrad x6": timeit(lambda: conv_ops._dgrad(gy, x, w, 0, conv_ops.X6))}
+         "dgrad x6": timeit(lambda: conv_ops._dgrad(gy, x, w, 0, conv_ops.X6)),
+         "wgrad direct": timeit(lambda: conv_ops._direct_wgrad(gy, x, w, 0)),
+         "wgrad miopen": timeit(lambda: conv_ops._miopen_bwd(gy, x, w, 1, 0, (False, True, False))[1]),
+         "wgrad x6": timeit(lambda: conv_ops._wgrad(gy, x, w, 1, 0, conv_ops.X6))}
     print(name, "  ".join(f"{k} {1e3 * v:.1f} us ({gf / v:.0f} TF)" for k, v in r.items()), flush=True)
