@@ -32,11 +32,44 @@ class FusedAdam(torch.optim.Adam):
         self._starts = None
         self._grads = None
         self._params = None   # the parameter list the table was built for
+        self._step_t = None   # on the fast path every state's "step" is this one CPU tensor
         self.rebuilds = 0   # chunk-table uploads (a parameter or moment buffer moved)
+
+    def state_dict(self):
+        """torch's layout, each parameter with its own step tensor (a reference Adam
+        loading adam.pth increments them one by one)."""
+        sd = super().state_dict()
+        if self._step_t is not None:
+            sd["state"] = {k: ({**v, "step": v["step"].clone()} if v.get("step") is self._step_t else v)
+                           for k, v in sd["state"].items()}
+        return sd
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         self._key = None   # new moment buffers: rebuild the table on the next step
+        self._step_t = None
+        # a state_dict saved from the fast path carries one step tensor under every
+        # parameter: give each state its own, as torch's Adam increments them one by one
+        seen = set()
+        for st in self.state.values():
+            t = st.get("step")
+            if t is None:
+                continue
+            if id(t) in seen:
+                st["step"] = t.clone()
+            else:
+                seen.add(id(t))
+
+    def _unshare_steps(self):
+        """Before torch's own step (which increments each state's "step" in place):
+        give every state its own step tensor again."""
+        if self._step_t is None:
+            return
+        for p in self.param_groups[0]["params"] if len(self.param_groups) == 1 else []:
+            st = self.state.get(p)
+            if st and st.get("step") is self._step_t:
+                st["step"] = self._step_t.clone()
+        self._step_t = None
 
     def _group_ok(self) -> bool:
         if len(self.param_groups) != 1:   # one lr / betas / eps per launch
@@ -105,6 +138,7 @@ class FusedAdam(torch.optim.Adam):
         fast = self._key is not None and self._fast_ok(params)
         if not fast and not self._eligible():
             self._key = None
+            self._unshare_steps()
             return super().step()
         if not params:
             return loss
@@ -121,13 +155,20 @@ class FusedAdam(torch.optim.Adam):
                         or any(st["exp_avg"].stride() != p.stride() or st["exp_avg_sq"].stride() != p.stride()
                                for p, st in zip(params, states))):
                     self._key = None
+                    self._unshare_steps()
                     return super().step()   # mixed step counts / layouts (e.g. a loaded partial state)
                 self._build(params)
                 self._key = key
             self._params = list(params)
-        steps = [st["step"] for st in states]
-        torch._foreach_add_(steps, 1)   # CPU scalars, as torch's Adam keeps them
-        step = int(steps[0])
+        # the step counters (CPU scalars, as torch's Adam keeps them; all equal here) are
+        # one shared tensor: one increment per step instead of a foreach over every
+        # parameter (~0.4 ms of host time per step)
+        if self._step_t is None or any(st["step"] is not self._step_t for st in states):
+            self._step_t = states[0]["step"].clone()
+            for st in states:
+                st["step"] = self._step_t
+        self._step_t += 1
+        step = int(self._step_t)
         b1, b2 = group["betas"]
         lr = group["lr"]
         lr = float(lr) if not torch.is_tensor(lr) else float(lr.item())

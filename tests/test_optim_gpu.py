@@ -71,3 +71,26 @@ def test_fused_adam_state_dict_interchanges_with_torch_adam():
         torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
     sd = oa.state_dict()
     assert set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"} and sd["state"][0]["step"].device.type == "cpu"
+
+
+def test_fused_adam_shared_step_roundtrips_through_torch_adam():
+    """The fast path keeps one step tensor for every state; its state_dict loaded into
+    torch's Adam (or back into FusedAdam) still steps each parameter once."""
+    pa, pb = _params(3), _params(3)
+    oa = FusedAdam(pa, lr=1e-3)
+    for _ in range(3):
+        for p in pa:
+            p.grad = torch.ones_like(p)
+        oa.step()
+    sd = oa.state_dict()
+    assert all(float(s["step"]) == 3.0 for s in sd["state"].values())
+    ob = torch.optim.Adam(pb, lr=1e-3)
+    ob.load_state_dict(copy.deepcopy(sd))
+    for p in pb:
+        p.grad = torch.ones_like(p)
+    ob.step()
+    assert all(float(s["step"]) == 4.0 for s in ob.state.values())
+    oc = FusedAdam(_params(3), lr=1e-3)
+    oc.load_state_dict(sd)   # in memory: the step tensors arrive aliased
+    steps = [s["step"] for s in oc.state.values()]
+    assert len({id(t) for t in steps}) == len(steps)
