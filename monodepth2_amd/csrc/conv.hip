@@ -27,6 +27,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include <stdint.h>
 
 #include <algorithm>
@@ -1126,6 +1128,15 @@ ConvArgs args_of(const md2_conv_desc* d, int mode) {
 
 int resident_blocks_x6(int BN, int BMX) { return 256 * ((BN <= 64 && BMX == 128) || BMX == 64 ? 2 : 1); }
 
+// fixed cost of a K split's reduction launch in chunk-rounds (A/B knob MD2_X6_SPLIT_COST)
+double split_launch_cost() {
+    static const double c = [] {
+        const char* e = getenv("MD2_X6_SPLIT_COST");
+        return e ? atof(e) : 0.0;
+    }();
+    return c;
+}
+
 // x6 plan: BN = 16 / 32 / 64 for N <= 16 / 32 / 64, else 128; BMX = 256 with MD2_CONV_BM256 (the caller's
 // autotune tries both); K split by the wave-quantisation model.  The weight-gradient
 // kernel is 128 wide, 64 or 128 rows (co) tall.
@@ -1143,7 +1154,8 @@ void plan_x6(ConvArgs& a, uint32_t flags, bool wgrad = false) {
         const int rounds = (base * splits + res - 1) / res;
         // a chunk-round of blocks ~1.5k cycles (x BMX/128); the split reduction moves
         // (splits + 1) M x N floats at ~2.4 KB/cycle chip-wide
-        const double red = splits > 1 ? (double)(splits + 1) * a.M * a.N * 4.0 / 2400.0 / 1536.0 : 0.0;
+        const double red = splits > 1 ? (double)(splits + 1) * a.M * a.N * 4.0 / 2400.0 / 1536.0 + split_launch_cost()
+                                      : 0.0;
         const double t = (double)rounds * per * (BMX / 128.0) + red;
         if (t < best_t - 1e-9) {
             best_t = t;
