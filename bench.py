@@ -14,10 +14,18 @@ GPU, each with its own 12-image shard (weak scaling), DDP gradient all-reduce ov
 RCCL.  Rank 0 prints ONE JSON line.
 
 Extra fields:
-  roofline      — the dominant HIP kernel (photo_bwd_kernel), HIP-event timed on
-                  its launch stream during the timed steps; algorithmic bytes per
-                  launch = B * 4*H*W*(3 + 3S + 1.328125 + 1 + 4) (DESIGN.md §5);
-                  traffic from profiles/<round>/pmc_traffic.json when present.
+  roofline      — the fused hot path (md2_photometric_fwd + md2_photometric_bwd: every
+                  kernel of it), HIP-event timed on its launch stream during the timed
+                  steps (first kernel's start to last kernel's end of each call).
+                  Algorithmic work per step from monodepth2_amd/roofline.py (SURVEY.md
+                  §8(d)): bytes = B * 4 N (3 S + 6.640625), flops = B * N * the pinned
+                  per-pixel census; both fractions are reported (HBM vs 8 TB/s, VALU vs
+                  the 157.3 TF FP32 vector peak) and the larger, binding one is the
+                  headline.  traffic = HBM bytes per step measured IN THIS RUN by two
+                  rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; FETCH x2 per
+                  MI355X_MICROARCH.md) over tools/hot_bench.py at the same shape
+                  (rank 0, N=1; --pmc 0 skips them).  `photo_bwd` details the
+                  dominant single kernel.
   cpu_baseline  — rank 0, N=1: the same training step on the host cores with the
                   oracle hot path (oracle/md2_oracle.py, op-for-op restatement of
                   the reference), a bounded sample of steps at batch 4 (configs[0]).
@@ -47,24 +55,60 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "training images/sec at 640x192 mono, 1/2/4/8 GPUs; loss delta vs ref"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, HBM3E spec
 F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, dense f32 matrix (= f32 vector) peak
+F32_VALU_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, "Peak FP32 (vector)"
 BF16_MFMA_PEAK_TFLOPS = 2500.0 # dense bf16; the split-bf16 convs issue 6 bf16 products per f32 product
-VALU_ISSUE_PEAK = 256 * 4 * 0.5 * 2.4e9   # wave-instructions/s: 256 CU x 4 SIMD x 1 per 2 clk x 2.4 GHz
-ROUND = "r02"
+ROUND = "r03"
 
 
-def photo_bwd_bytes(B, H, W, S, nscales=4):
-    """Algorithmic HBM bytes of one photo_bwd_kernel launch: read target + S sources
-    (3 ch fp32), the disparity pyramid (fp32), the per-scale selection maps (u8);
-    write the per-scale full-resolution dL/ddisp (fp32)."""
-    N = H * W
-    pyr = sum(1.0 / 4 ** s for s in range(nscales))
-    return B * N * (4 * 3 * (1 + S) + 4 * pyr + 1 * nscales + 4 * nscales)
+HOT_KERNELS = "pack_src8|photo_|smooth_fwd|finalize_fwd|disp_grad_kernel|grad_T_kernel"
 
 
-def photo_fwd_bytes(B, H, W, S, nscales=4):
-    N = H * W
-    pyr = sum(1.0 / 4 ** s for s in range(nscales))
-    return B * N * (4 * 3 * (1 + S) + 4 * pyr + 1 * nscales)
+def pmc_traffic(args, S, timeout=150):
+    """HBM bytes per hot-path step (forward + backward), measured now: two rocprofv3
+    --pmc passes (FETCH_SIZE, WRITE_SIZE: one pass cannot hold both) over
+    tools/hot_bench.py at the bench's shape, averaged per dispatch per kernel and
+    summed over the hot path's kernels.  FETCH_SIZE x2 (gfx950 under-reports wide
+    reads by half, MI355X_MICROARCH.md §HBM), KB -> bytes.  Runs in child processes
+    while this one waits (no GPU work of its own in flight)."""
+    import csv
+    import glob
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not found"
+    per = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="md2pmc_", dir="/tmp")
+        cmd = [exe, "--pmc", counter, "--kernel-include-regex", HOT_KERNELS, "-d", d, "-o", "pmc",
+               "--output-format", "csv", "--", sys.executable, os.path.join(REPO, "tools", "hot_bench.py"),
+               "--batch", str(args.batch), "--height", str(args.height), "--width", str(args.width),
+               "--src", str(S), "--iters", "6", "--eight-bit"]
+        env = dict(os.environ, TMPDIR="/tmp")
+        p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env, start_new_session=True)
+        try:
+            _, err = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.communicate()
+            return None, f"rocprofv3 --pmc {counter} timed out"
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if p.returncode != 0 or not files:
+            return None, f"rocprofv3 --pmc {counter} rc={p.returncode}: {err.decode(errors='replace')[-300:]}"
+        vals = {}
+        for f in files:
+            for r in csv.DictReader(open(f)):
+                if r["Counter_Name"] == counter:
+                    name = r["Kernel_Name"].split("(")[0].split("::")[-1].split("<")[0]
+                    vals.setdefault(name, []).append(float(r["Counter_Value"]))
+        per[counter] = {k: sum(v) / len(v) for k, v in vals.items()}
+        shutil.rmtree(d, ignore_errors=True)
+    kernels = sorted(set(per["FETCH_SIZE"]) | set(per["WRITE_SIZE"]))
+    by_kernel = {k: int(1024 * (2 * per["FETCH_SIZE"].get(k, 0.0) + per["WRITE_SIZE"].get(k, 0.0)))
+                 for k in kernels}
+    return by_kernel, None
 
 
 _T0 = time.perf_counter()
@@ -88,11 +132,14 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--pmc", type=int, default=1, help="measure the hot path's HBM traffic with rocprofv3 "
+                    "PMC passes in this run (rank 0, N=1)")
     ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen exhaustive find per conv shape")
     ap.add_argument("--channels-last", type=int, default=1, help="NHWC convolutions (1/0)")
     ap.add_argument("--pose-last", type=int, default=0,
                     help="1: pose network forward enqueued after the depth network (its backward first)")
     ap.add_argument("--graph", type=int, default=0, help="capture the whole step in a hipGraph (1/0)")
+    ap.add_argument("--pose-stream", type=int, default=1, help="pose network on its own HIP stream (1/0)")
     ap.add_argument("--miopen-find", type=str, default="fast", help="MIOPEN_FIND_MODE (fast|normal|...)")
     ap.add_argument("--amp", type=str, default="none", choices=["none", "bf16"],
                     help="bf16 autocast for the networks (config C5); the photometric loss stays fp32")
@@ -108,7 +155,8 @@ def make_trainer(args, device, rank, world):
     opt = default_options(batch_size=args.batch, height=args.height, width=args.width,
                           num_layers=args.num_layers, weights_init="scratch", use_stereo=args.stereo,
                           frame_ids=[0, -1, 1], log_dir="/tmp/md2_bench",
-                          channels_last=bool(args.channels_last), hip_graph=bool(args.graph), amp=args.amp)
+                          channels_last=bool(args.channels_last), hip_graph=bool(args.graph), amp=args.amp,
+                          pose_streams=args.pose_stream)
     tr = Trainer(opt, device=device, rank=rank, world_size=world)
     tr.pose_last = bool(args.pose_last)
     return tr
@@ -154,7 +202,7 @@ def time_hot_kernels(trainer, batch, n=10):
         loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=1)
         loss[hot.num_scales].backward()
     torch.cuda.synchronize()
-    with _lib.KernelTimer(max_launches=2 * n + 4) as kt:
+    with _lib.KernelTimer(max_launches=4 * n + 8) as kt:
         for i in range(n):
             loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=2 + i)
             loss[hot.num_scales].backward()
@@ -300,6 +348,10 @@ def main():
         trainer.train_step(next_batch())
         torch.cuda.synchronize()
         log(f"warmup step {i}: {1e3 * (time.perf_counter() - t):.1f} ms")
+        if trainer.graph is not None and not args.gpu_augment:
+            # the resident batch IS the captured step's input buffers (no per-replay copy)
+            static = trainer.static_inputs
+            next_batch = lambda: static   # noqa: E731
     stop_hb.set()
     torch.cuda.synchronize()
     # host enqueue rate: how long the CPU takes to issue 3 steps right after a sync
@@ -313,7 +365,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    with _lib.KernelTimer(max_launches=4 * args.steps + 8) as kt:
+    with _lib.KernelTimer(max_launches=8 * args.steps + 16) as kt:
         t0 = time.perf_counter()
         for _ in range(args.steps):
             _, losses = trainer.train_step(next_batch())
@@ -336,29 +388,42 @@ def main():
         B, H, W = args.batch, args.height, args.width
         bwd_ms = kt.bwd_ms / max(kt.n_bwd, 1)
         fwd_ms = kt.fwd_ms / max(kt.n_fwd, 1)
-        alg = photo_bwd_bytes(B, H, W, S)
-        achieved = alg / (bwd_ms * 1e-3) / 1e9
-        traffic, pipe = None, None
-        pmc = os.path.join(REPO, "profiles", ROUND, "pmc_traffic.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                pm = json.load(f)
-            traffic = pm.get("photo_bwd_kernel_bytes_per_launch")
-            # what actually binds the kernel (HBM is not it): the vector-memory pipeline of
-            # its bilinear gathers (texture data unit busy) and VALU issue, from the
-            # committed PMC passes of the same build (rocprofv3, profiles/<round>/)
-            pipe = {"td_busy_frac": pm.get("photo_bwd_td_busy_frac"),
-                    "ta_busy_frac": pm.get("photo_bwd_ta_busy_frac"),
-                    "valu_issue_frac": pm.get("photo_bwd_valu_issue_frac"),
-                    "source": f"profiles/{ROUND}/pmc_traffic.json"}
-        roof = {"bound": "hbm", "kernel": "photo_bwd_kernel", "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic, "algorithmic_bytes_per_launch": int(alg),
-                "avg_launch_ms": round(bwd_ms, 5), "launches": kt.n_bwd,
-                "fwd_kernel_avg_ms": round(fwd_ms, 5),
-                "fwd_kernel_gbs": round(photo_fwd_bytes(B, H, W, S) / (fwd_ms * 1e-3) / 1e9, 2),
-                "binding_pipeline": pipe}
-        log(f"timed: {1e3 * dt / args.steps:.2f} ms/step, photo_bwd {bwd_ms:.3f} ms, photo_fwd {fwd_ms:.3f} ms, "
+        fcall = kt.fwd_call_ms / max(kt.n_fwd_call, 1)
+        bcall = kt.bwd_call_ms / max(kt.n_bwd_call, 1)
+        hot_ms = fcall + bcall
+        from monodepth2_amd.roofline import hot_path_census
+        cen = hot_path_census(H, W, S)
+        step_bytes, step_flops = B * cen.bytes, B * cen.flops
+        gbs = step_bytes / (hot_ms * 1e-3) / 1e9
+        tfs = step_flops / (hot_ms * 1e-3) / 1e12
+        hbm_frac, valu_frac = gbs / HBM_PEAK_GBS, tfs / F32_VALU_PEAK_TFLOPS
+        traffic, pmc_note, pmc_kernels = None, "skipped (--pmc 0 or N>1)", None
+        if args.pmc and world == 1:
+            pmc_kernels, err = pmc_traffic(args, S)
+            if pmc_kernels is not None:
+                traffic = sum(pmc_kernels.values())
+                pmc_note = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in this run over tools/hot_bench.py "
+                            "at this shape; 2*FETCH+WRITE (KB->B) per step, summed over the hot path's kernels")
+            else:
+                pmc_note = err
+            log(f"pmc traffic: {traffic} B/step ({pmc_note[:80]})")
+        head = ("valu", tfs, F32_VALU_PEAK_TFLOPS, "TFLOP/s", valu_frac) if valu_frac >= hbm_frac else \
+            ("hbm", gbs, HBM_PEAK_GBS, "GB/s", hbm_frac)
+        roof = {"bound": head[0], "kernel": "hot path: md2_photometric_fwd + md2_photometric_bwd (all their kernels)",
+                "achieved": round(head[1], 3), "peak": head[2], "unit": head[3], "frac": round(head[4], 5),
+                "traffic": traffic,
+                "algorithmic_bytes_per_step": int(step_bytes), "algorithmic_flops_per_step": int(step_flops),
+                "census": {"bytes_per_px": cen.bytes / (H * W), "fwd_flops_per_px": cen.fwd_flops / (H * W),
+                           "bwd_flops_per_px": cen.bwd_flops / (H * W), "source": "monodepth2_amd/roofline.py"},
+                "hbm": {"achieved_gbs": round(gbs, 2), "peak": HBM_PEAK_GBS, "frac": round(hbm_frac, 5)},
+                "valu": {"achieved_tflops": round(tfs, 3), "peak": F32_VALU_PEAK_TFLOPS, "frac": round(valu_frac, 5)},
+                "avg_ms_per_step": round(hot_ms, 5), "fwd_call_ms": round(fcall, 5), "bwd_call_ms": round(bcall, 5),
+                "calls": kt.n_bwd_call, "traffic_source": pmc_note, "traffic_by_kernel": pmc_kernels,
+                "photo_bwd": {"avg_launch_ms": round(bwd_ms, 5), "launches": kt.n_bwd,
+                              "share_of_hot_path": round(bwd_ms / hot_ms, 3) if hot_ms else None},
+                "photo_fwd_kernels_ms": round(fwd_ms, 5)}
+        log(f"timed: {1e3 * dt / args.steps:.2f} ms/step, hot path {hot_ms:.3f} ms (fwd {fcall:.3f}, bwd {bcall:.3f};"
+            f" photo_bwd {bwd_ms:.3f}), {tfs:.2f} TF = {valu_frac:.3f} of VALU peak, {gbs:.0f} GB/s, "
             f"adam table uploads {getattr(trainer.model_optimizer, 'rebuilds', '-')}")
         conv_roof = conv_mfma_roofline(device)
         log(f"conv_x6: {conv_roof['achieved']} TFLOP/s ({conv_roof['frac']} of the f32 matrix peak)")

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 12
+#define MD2_ABI_VERSION 13
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -160,6 +160,11 @@ int md2_tiebreak_noise(const md2_desc* desc, const uint64_t* seed_ptr, int scale
  */
 int md2_timing_begin(int max_launches);
 int md2_timing_end(double* fwd_ms, int* n_fwd, double* bwd_ms, int* n_bwd);
+/* After md2_timing_end: the summed durations of whole md2_photometric_fwd calls (first
+ * kernel's start to the finalize kernel's end) and md2_photometric_bwd calls (photo_bwd
+ * start to grad_T end) in that window — every kernel of the hot path, for its roofline.
+ * Each whole call takes a slot of max_launches besides its kernel slot. */
+int md2_timing_calls(double* fwd_ms, int* n_fwd, double* bwd_ms, int* n_bwd);
 
 /*
  * DepthDecoder block fusion: the input of every decoder
@@ -295,6 +300,14 @@ typedef struct md2_adam_chunk {
  * pointers (same layout as their parameters). */
 int md2_adam_step(const md2_adam_chunk* table, const int* chunk_start, int nparams, const float* const* grads,
                   double lr, double beta1, double beta2, double eps, int step, void* stream);
+/* The same step with the step counter and lr on the device (hipGraph-capturable, the
+ * `capturable=True` form of torch.optim.Adam): *step (fp32, the value torch keeps in
+ * state["step"]) is incremented first, the bias corrections are formed in double from
+ * it and *lr (fp64, the param group's lr tensor that StepLR fills); `hyper` is 2 fp32
+ * of device scratch. */
+int md2_adam_step_dev(const md2_adam_chunk* table, const int* chunk_start, int nparams, const float* const* grads,
+                      const double* lr, double beta1, double beta2, double eps, float* step, float* hyper,
+                      void* stream);
 
 /*
  * Fused pose producer: transformation_from_parameters

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -55,8 +55,8 @@ _lib = None
 
 EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_select_bytes",
            "md2_photometric_fwd", "md2_photometric_bwd", "md2_generate_images", "md2_tiebreak_noise",
-           "md2_timing_begin", "md2_timing_end", "md2_decoder_pad_fwd", "md2_decoder_pad_bwd",
-           "md2_decoder_pad_workspace_bytes", "md2_adam_step", "md2_encoder_input",
+           "md2_timing_begin", "md2_timing_end", "md2_timing_calls", "md2_decoder_pad_fwd", "md2_decoder_pad_bwd",
+           "md2_decoder_pad_workspace_bytes", "md2_adam_step", "md2_adam_step_dev", "md2_encoder_input",
            "md2_pose_fwd", "md2_pose_bwd", "md2_aug_plan_create", "md2_aug_plan_destroy", "md2_aug_run",
            "md2_bn_workspace_bytes", "md2_bn_fwd", "md2_bn_bwd", "md2_maxpool3s2_fwd", "md2_maxpool3s2_bwd",
            "md2_disp_head_workspace_bytes", "md2_disp_head_fwd", "md2_disp_head_bwd",
@@ -208,6 +208,9 @@ def _declare(L):
     L.md2_adam_step.restype = ctypes.c_int
     L.md2_adam_step.argtypes = [_vp, _vp, ctypes.c_int, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                 ctypes.c_double, ctypes.c_int, _vp]
+    L.md2_adam_step_dev.restype = ctypes.c_int
+    L.md2_adam_step_dev.argtypes = [_vp, _vp, ctypes.c_int, _vp, _vp, ctypes.c_double, ctypes.c_double,
+                                    ctypes.c_double, _vp, _vp, _vp]
     L.md2_decoder_pad_workspace_bytes.restype = ctypes.c_size_t
     L.md2_decoder_pad_workspace_bytes.argtypes = [ctypes.POINTER(PadDesc)]
     L.md2_pose_fwd.restype = ctypes.c_int
@@ -236,6 +239,9 @@ def _declare(L):
     L.md2_maxpool3s2_bwd_add.argtypes = [ctypes.POINTER(PoolDesc)] + [_vp] * 5
     L.md2_timing_begin.restype = ctypes.c_int
     L.md2_timing_begin.argtypes = [ctypes.c_int]
+    L.md2_timing_calls.restype = ctypes.c_int
+    L.md2_timing_calls.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
     L.md2_timing_end.restype = ctypes.c_int
     L.md2_timing_end.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
@@ -293,4 +299,7 @@ class KernelTimer:
         check(lib().md2_timing_end(ctypes.byref(f), ctypes.byref(nf), ctypes.byref(b), ctypes.byref(nb)),
               "md2_timing_end")
         self.fwd_ms, self.n_fwd, self.bwd_ms, self.n_bwd = f.value, nf.value, b.value, nb.value
+        check(lib().md2_timing_calls(ctypes.byref(f), ctypes.byref(nf), ctypes.byref(b), ctypes.byref(nb)),
+              "md2_timing_calls")
+        self.fwd_call_ms, self.n_fwd_call, self.bwd_call_ms, self.n_bwd_call = f.value, nf.value, b.value, nb.value
         return False

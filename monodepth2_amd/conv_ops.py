@@ -28,6 +28,7 @@ networks/decoders.py (DepthDecoder convs on the reflection-padded inputs).
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, Tuple
 
 import torch
@@ -150,6 +151,55 @@ def _miopen_bwd(gy, x, w, stride, pad, mask):
                                                mask)
 
 
+_pinned: Dict[tuple, str] = {}    # (op, shape) -> candidate name from a loaded table
+
+
+def _key_of(row) -> tuple:
+    return (row["op"], tuple(row["x"]), tuple(row["w"]), int(row["stride"]), int(row["pad"]))
+
+
+def load_choices(path: str) -> int:
+    """Pin the per-shape choice to a table (tools/conv_choices.py output, e.g.
+    monodepth2_amd/conv_choices.json): every shape listed runs the candidate named
+    in its "kept" field instead of being timed, so the kernels — and with them the
+    rounding — are the same in every process and on every rank (bitwise
+    reproducible training).  Shapes not in the table are still timed.  Returns
+    the number of pinned entries.  `MD2_CONV_CHOICES=<path>` does this at import."""
+    import json
+    with open(path) as f:
+        rows = json.load(f)["rows"]
+    for row in rows:
+        _pinned[_key_of(row)] = row["kept"]
+    _choice.clear()
+    return len(rows)
+
+
+def save_choices(path: str) -> int:
+    """Write the choices made so far (timed or pinned) as a table load_choices reads."""
+    import json
+    rows = []
+    for k, i in sorted(_choice.items()):
+        names = _names.get(k)
+        if names is None:
+            continue
+        op, xs, ws, st, pd = k
+        rows.append({"op": op, "x": list(xs), "w": list(ws), "stride": st, "pad": pd, "kept": names[i],
+                     "ms": _times.get(k, {})})
+    with open(path, "w") as f:
+        json.dump({"rows": rows}, f, indent=1)
+    return len(rows)
+
+
+def clear_choices():
+    _choice.clear()
+    _pinned.clear()
+    _times.clear()
+    _names.clear()
+
+
+_names: Dict[tuple, list] = {}    # (op, shape) -> candidate names, in candidate order
+
+
 def _cached(op: str, key: tuple):
     """The remembered choice for (op, shape), 0 without AUTOTUNE, None if not timed yet."""
     if not AUTOTUNE:
@@ -167,6 +217,14 @@ def _fastest(op: str, key: tuple, cands, names=None) -> int:
         return 0
     if k in _choice:
         return _choice[k]
+    names = list(names or [str(i) for i in range(len(cands))])
+    _names[k] = names
+    pin = _pinned.get(k)
+    if pin is not None:
+        if pin not in names:
+            raise RuntimeError(f"pinned conv choice {pin!r} for {k} is not a candidate here ({names})")
+        _choice[k] = names.index(pin)
+        return _choice[k]
     if torch.cuda.is_current_stream_capturing():
         return len(cands) - 1
     times = []
@@ -181,7 +239,7 @@ def _fastest(op: str, key: tuple, cands, names=None) -> int:
             e1.synchronize()
             ts.append(e0.elapsed_time(e1))
         times.append(sorted(ts)[1])
-    _times[k] = dict(zip(names or [str(i) for i in range(len(cands))], times))
+    _times[k] = dict(zip(names, times))
     best = min(range(len(cands) - 1), key=lambda i: times[i]) if len(cands) > 1 else 0
     _choice[k] = best if times[best] < 0.97 * times[-1] else len(cands) - 1
     return _choice[k]
@@ -315,18 +373,29 @@ class _Conv(torch.autograd.Function):
         return gx, gw, None, None
 
 
-def _shape_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
+def _sizes_ok(x: torch.Tensor, weight: torch.Tensor, stride: int, pad: int) -> bool:
+    """csrc/conv.hip valid(): input, output and weight each < 2^29 elements."""
+    B, _, H, W = x.shape
+    Co, _, kh, kw = weight.shape
+    ho = (H + 2 * pad - kh) // stride + 1
+    wo = (W + 2 * pad - kw) // stride + 1
+    return (ho >= 1 and wo >= 1 and x.numel() < 2 ** 29 and B * ho * wo * Co < 2 ** 29
+            and weight.numel() < 2 ** 29)
+
+
+def _shape_ok(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad: int = 0) -> bool:
     return (ENABLED and x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.float32 and x.dim() == 4
             and weight.shape[2] == weight.shape[3] and _fits(weight.shape[1], weight.shape[0])
             and x.is_contiguous(memory_format=_CL) and weight.is_contiguous(memory_format=_CL)
-            and not torch.is_autocast_enabled() and x.numel() < 2 ** 29)
+            and not torch.is_autocast_enabled() and stride >= 1 and 0 <= pad < weight.shape[2]
+            and _sizes_ok(x, weight, stride, pad))
 
 
 def supports(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     k, s, p = conv.kernel_size, conv.stride, conv.padding
     return (conv.bias is None and conv.groups == 1 and tuple(conv.dilation) == (1, 1)
             and conv.padding_mode == "zeros" and k[0] == k[1] and s[0] == s[1] and p[0] == p[1] and p[0] < k[0]
-            and _shape_ok(x, conv.weight))
+            and _shape_ok(x, conv.weight, s[0], p[0]))
 
 
 def conv2d(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
@@ -339,6 +408,10 @@ def conv2d(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
 def conv2d_w(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad: int = 0) -> torch.Tensor:
     """F.conv2d(x, weight, None, stride, pad) for a bare weight (decoder convs whose
     bias is folded elsewhere), on the MFMA kernels when the shape fits."""
-    if _shape_ok(x, weight) and pad < weight.shape[2]:
+    if _shape_ok(x, weight, stride, pad):
         return _Conv.apply(x, weight, stride, pad)
     return F.conv2d(x, weight, None, stride, pad)
+
+
+if os.environ.get("MD2_CONV_CHOICES"):
+    load_choices(os.environ["MD2_CONV_CHOICES"])

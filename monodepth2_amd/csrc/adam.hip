@@ -37,9 +37,29 @@ struct GradPtrs {
     const float* g[kMaxParams];
 };
 
+// Capturable form (hipGraph replays): the step counter and lr live on the device.  One
+// thread advances the step and forms the bias corrections in double (as the host path
+// does with the Python doubles), written as the two fp32 factors the update uses.
+__global__ void adam_hyper_kernel(float* __restrict__ step, const double* __restrict__ lr, double b1, double b2,
+                                  float* __restrict__ hyper) {
+    if (threadIdx.x != 0) return;
+    const float s = *step + 1.0f;
+    *step = s;
+    const double bc1 = 1.0 - pow(b1, (double)s);
+    const double bc2 = 1.0 - pow(b2, (double)s);
+    hyper[0] = (float)(*lr / bc1);
+    hyper[1] = (float)sqrt(bc2);
+}
+
+template <bool DEV>
 __global__ __launch_bounds__(kThreads) void adam_kernel(const md2_adam_chunk* __restrict__ table, int first_param,
                                                         GradPtrs grads, float b1, float b2, float c1, float c2,
-                                                        float step_size, float bc2_sqrt, float eps) {
+                                                        float step_size, float bc2_sqrt, float eps,
+                                                        const float* __restrict__ hyper) {
+    if (DEV) {
+        step_size = hyper[0];
+        bc2_sqrt = hyper[1];
+    }
     const md2_adam_chunk c = table[blockIdx.x];
     const long long n = c.n;
     const float* gp = grads.g[c.param - first_param] + c.off;
@@ -82,9 +102,28 @@ int md2_adam_step(const md2_adam_chunk* table, const int* chunk_start, int npara
         for (int k = k0; k < k1; ++k) gp.g[k - k0] = grads[k];
         const int c0 = chunk_start[k0], c1 = chunk_start[k1];
         if (c1 <= c0) continue;
-        hipLaunchKernelGGL(adam_kernel, dim3(c1 - c0), dim3(kThreads), 0, (hipStream_t)stream, table + c0, k0, gp,
-                           (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2),
-                           (float)(lr / bc1), (float)sqrt(bc2), (float)eps);
+        hipLaunchKernelGGL(adam_kernel<false>, dim3(c1 - c0), dim3(kThreads), 0, (hipStream_t)stream, table + c0, k0,
+                           gp, (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2),
+                           (float)(lr / bc1), (float)sqrt(bc2), (float)eps, (const float*)nullptr);
+    }
+    return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
+}
+
+int md2_adam_step_dev(const md2_adam_chunk* table, const int* chunk_start, int nparams, const float* const* grads,
+                      const double* lr, double beta1, double beta2, double eps, float* step, float* hyper,
+                      void* stream) {
+    if (!table || !chunk_start || !grads || nparams < 0 || !lr || !step || !hyper || !(eps > 0.0))
+        return MD2_ERR_ARG;
+    hipLaunchKernelGGL(adam_hyper_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step, lr, beta1, beta2, hyper);
+    for (int k0 = 0; k0 < nparams; k0 += kMaxParams) {
+        const int k1 = k0 + kMaxParams < nparams ? k0 + kMaxParams : nparams;
+        GradPtrs gp = {};
+        for (int k = k0; k < k1; ++k) gp.g[k - k0] = grads[k];
+        const int c0 = chunk_start[k0], c1 = chunk_start[k1];
+        if (c1 <= c0) continue;
+        hipLaunchKernelGGL(adam_kernel<true>, dim3(c1 - c0), dim3(kThreads), 0, (hipStream_t)stream, table + c0, k0,
+                           gp, (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), 0.f, 1.f,
+                           (float)eps, (const float*)hyper);
     }
     return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
 }

@@ -445,11 +445,8 @@ struct PhotoArgs {
     // predictive mask (MD2_PREDICTIVE_MASK): per local scale (B,S,h,w)
     const float* mask[MD2_MAX_SCALES];
     float* gmask[MD2_MAX_SCALES];
-    // split forward: identity losses [S][B][h][w], reprojection losses per local scale
-    // [S][B][h][w], combine blocks per image
+    // identity losses [S][B][h][w] (forward, written once, read by every scale's waves)
     float* ident;
-    float* rep[MD2_MAX_SCALES];
-    int cblk;
     // 8-bit copies of the source frames (B,h,w) RGBx and per (frame, image) flags
     // "every colour is exactly k/255" (null: fp32 planes only)
     const uint32_t* src8[MD2_MAX_SRC];
@@ -474,20 +471,18 @@ __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int 
 }
 
 // ----------------------------------------------------------------------------
-// Forward: three launches (instead of one wave doing every (scale, frame) of a
-// 4-row item, the round-1 design).
-//   photo_ident_kernel   identity losses of every source frame, once per step
-//                        (scale-invariant, trainer.py:432-439)
-//   photo_reproj_kernel  one wave per (image, 16-row block, strip, scale, frame):
-//                        warp + SSIM/L1 per pixel -> loss plane (trainer.py:426-430)
-//   photo_combine_kernel per pixel: identity + noise vs reprojection candidates,
-//                        first-index argmin (trainer.py:466-482), automask code,
-//                        fixed-order block partial sums of the per-pixel minimum
-// A 16-row item evaluates 18 rows (1.125x) where the fused 4-row item evaluated 6
-// (1.5x), and the identity pass is no longer repeated per item; the loss planes
-// (8 x 5.9 MB at B=12) stay L2/Infinity-cache resident between the launches.
+// Forward: two launches.
+//   photo_ident_kernel    identity losses of every source frame, once per step
+//                         (scale-invariant, trainer.py:432-439) -> identity planes
+//   photo_fwdloss_kernel  one wave per (image, 16-row block, strip, scale): window
+//                         depths once, then per frame warp + SSIM/L1 (trainer.py:
+//                         426-430) folded straight into the per-pixel minimum over the
+//                         identity (+ noise) and reprojection candidates (466-482),
+//                         automask code, one partial sum per wave
+// A 16-row item evaluates 18 rows (1.125x).  Round 2 wrote every reprojection loss
+// as a plane (47 MB at B=12) and re-read it in a third launch; those planes are gone.
 // ----------------------------------------------------------------------------
-constexpr int kRowsP = 16;   // output rows per item of the split forward passes
+constexpr int kRowsP = 16;   // output rows per item of the forward passes
 
 // one evaluated window row of the forward walk
 struct FRow {
@@ -586,163 +581,148 @@ __global__ __launch_bounds__(kBlock) void photo_ident_kernel(PhotoArgs a) {
     });
 }
 
-template <int NS, bool SSIM_ON, bool MASK>
-__global__ __launch_bounds__(kBlock) void photo_reproj_kernel(PhotoArgs a) {
-    __shared__ float dep_all[kWavesPerBlock][kRowsP + 2][kWave];
-    const int lane = threadIdx.x & (kWave - 1);
-    float (*dep)[kWave] = dep_all[threadIdx.x >> 6];
-    const int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
-    const int wv = __builtin_amdgcn_readfirstlane(blk * kWavesPerBlock + (threadIdx.x >> 6));
-    if (wv >= a.B * a.wpi * a.nsc * NS) return;
-    // item order: frame fastest, then scale, so the waves sharing a strip's target and
-    // source rows run together on one XCD
-    const int f = wv % NS, ls = (wv / NS) % a.nsc;
-    const FItem it = fitem(a, wv / (NS * a.nsc), lane);
-    const int h = a.h, w = a.w, HW = h * w;
-    WarpCtx ctx;
-    make_ctx(a, ls, f, it.b, ctx);
-#pragma unroll
-    for (int k = 0; k < kRowsP + 2; ++k) dep[k][lane] = depth_at(ctx, reflect_clamp(it.r0 - 1 + k, h), it.cc);
-    float* out = a.rep[ls] + ((size_t)f * a.B + it.b) * HW;
-    const float* pmask = MASK ? a.mask[ls] + ((size_t)it.b * NS + f) * HW : nullptr;
-    auto emit = [&](int i, float v) {
-        const int r = it.r0 + i;
-        if (it.colok && r < h) {
-            if (MASK) v *= pmask[r * w + it.c];  // trainer.py:455
-            out[r * w + it.c] = v;
-        }
-    };
-    const float* tgt = a.tgt + (size_t)it.b * 3 * HW;
-    if (ctx.src8)   // wave-uniform: this image's sources are 8-bit exact
-        loss_rows<SSIM_ON, true, true>(ctx, tgt, dep, it.r0, it.cc, lane, emit);
-    else
-        loss_rows<SSIM_ON, true, false>(ctx, tgt, dep, it.r0, it.cc, lane, emit);
+// The reprojection losses of every source frame at one scale and the per-pixel
+// minimum over cat(identity + 1e-5 noise, reprojection) (trainer.py:426-482) in one
+// wave per (image, 16-row block, 62-column strip, scale): the window depths are staged
+// once in LDS and shared by the frames; for each frame in order the wave walks the
+// rows and folds every pixel's loss into its running minimum (LDS, one column per
+// lane), so no loss plane goes to memory.  Candidate order and tie rule as torch.min
+// over the concatenation: identity candidates first, then frame by frame, a strictly
+// smaller value replaces the minimum (the first index wins ties).  One partial sum of
+// the minima per wave, folded in wave order by finalize_fwd_kernel (deterministic).
+// LDS per wave (dynamic, fwdloss_lds_bytes): window depths [kRowsP+2][64], running
+// minimum [kRowsP][64], argmin code [kRowsP][64] bytes, and with avg_reprojection the
+// running sum of the frames' losses [kRowsP][64] (9.7 KB, 13.8 KB with avg: 4 / 2
+// blocks per CU)
+__host__ __device__ constexpr int fwdloss_wave_floats(bool avg) { return (kRowsP + 2 + kRowsP + (avg ? kRowsP : 0)) * kWave; }
+__host__ __device__ constexpr size_t fwdloss_lds_bytes(bool avg) {
+    return (size_t)kWavesPerBlock * (fwdloss_wave_floats(avg) * sizeof(float) + kRowsP * kWave);
 }
 
-// Four consecutive pixels of one image per thread, every local scale (the identity
-// losses are read once for all scales); blocks cover kCombinePix pixels of an image.
-// Candidate order and tie rule as torch.min over cat(identity + noise, reprojection)
-// (first index wins, trainer.py:471-482).  One partial sum of the per-pixel minimum
-// per (scale, block), folded in a fixed order (deterministic).
-constexpr int kCombinePix = 4 * kBlock;
-
-template <int NS>
-__global__ __launch_bounds__(kBlock) void photo_combine_kernel(PhotoArgs a) {
-    __shared__ float red[MD2_MAX_SCALES][kWavesPerBlock];
-    const int b = blockIdx.x / a.cblk, cb = blockIdx.x - b * a.cblk;
-    const int HW = a.h * a.w;
-    const int p0 = cb * kCombinePix + 4 * threadIdx.x;
-    const bool automask = !(a.flags & MD2_NO_AUTOMASK);
+template <int NS, bool SSIM_ON, bool MASK>
+__global__ __launch_bounds__(kBlock) void photo_fwdloss_kernel(PhotoArgs a) {
+    extern __shared__ float fwd_smem[];
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
     const bool avg = (a.flags & MD2_AVG_REPROJECTION) != 0;
+    float* wbase = fwd_smem + wid * fwdloss_wave_floats(avg);
+    float (*dep)[kWave] = (float (*)[kWave])wbase;
+    float (*best)[kWave] = (float (*)[kWave])(wbase + (kRowsP + 2) * kWave);
+    float (*acc)[kWave] = (float (*)[kWave])(wbase + (2 * kRowsP + 2) * kWave);   // avg only
+    uint8_t (*code)[kWave] = (uint8_t (*)[kWave])((uint8_t*)(fwd_smem + kWavesPerBlock * fwdloss_wave_floats(avg))
+                                                 + wid * kRowsP * kWave);
+    const int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int wv = __builtin_amdgcn_readfirstlane(blk * kWavesPerBlock + wid);
+    if (wv >= a.B * a.wpi * a.nsc) return;
+    // item order: scale fastest, so the waves sharing a strip's rows run together
+    const int ls = wv % a.nsc;
+    const int item = wv / a.nsc;
+    const FItem it = fitem(a, item, lane);
+    const int h = a.h, w = a.w, HW = h * w;
+    const bool automask = !(a.flags & MD2_NO_AUTOMASK);
     const int C = avg ? 1 : NS;
-    const uint64_t seed = a.seed_ptr ? (a.seed ^ (*a.seed_ptr * 0x9E3779B97F4A7C15ULL)) : a.seed;
-    const bool vec = (HW & 3) == 0 && p0 + 3 < HW;
-    const int npx = p0 >= HW ? 0 : min(4, HW - p0);
-    float id[NS][4];
-    if (automask) {
-#pragma unroll
-        for (int f = 0; f < NS; ++f) {
-            const float* src = a.ident + ((size_t)f * a.B + b) * HW;
-            if (vec) {
-                const float4 v = *(const float4*)(src + p0);
-                id[f][0] = v.x, id[f][1] = v.y, id[f][2] = v.z, id[f][3] = v.w;
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) id[f][i] = i < npx ? src[p0 + i] : 0.f;
-            }
-        }
-    }
-    for (int ls = 0; ls < a.nsc; ++ls) {
-        float rp[NS][4];
-#pragma unroll
-        for (int f = 0; f < NS; ++f) {
-            const float* src = a.rep[ls] + ((size_t)f * a.B + b) * HW;
-            if (vec) {
-                const float4 v = *(const float4*)(src + p0);
-                rp[f][0] = v.x, rp[f][1] = v.y, rp[f][2] = v.z, rp[f][3] = v.w;
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) rp[f][i] = i < npx ? src[p0 + i] : 0.f;
-            }
-        }
-        const float* nz = a.noise[ls];
+    // identity candidates + tie-break noise (trainer.py:466-471)
+    {
+        const uint64_t seed = a.seed_ptr ? (a.seed ^ (*a.seed_ptr * 0x9E3779B97F4A7C15ULL)) : a.seed;
         const uint32_t key = noise_key(seed, a.gscale[ls]);
-        float lsum = 0.f;
-        uint32_t codes = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int p = p0 + i;
-            float best = INFINITY;
-            int code = 0;
-            if (automask) {
+        const float* nz = a.noise[ls];
+#pragma unroll 1
+        for (int i = 0; i < kRowsP; ++i) {
+            const int r = it.r0 + i;
+            float bv = INFINITY;
+            int bc = 0;
+            if (automask && it.colok && r < h) {
+                const int p = r * w + it.c;
                 float nv[NS];
                 if (nz) {
 #pragma unroll
-                    for (int ch = 0; ch < NS; ++ch) nv[ch] = ch < C && i < npx ? nz[((size_t)b * C + ch) * HW + p] : 0.f;
+                    for (int ch = 0; ch < NS; ++ch) nv[ch] = ch < C ? nz[((size_t)it.b * C + ch) * HW + p] : 0.f;
                 } else {
 #pragma unroll
                     for (int j = 0; 2 * j < NS; ++j) {
-                        const float2 n2 = noise_pair(key, (uint32_t)(b * HW + p), j);
+                        const float2 n2 = noise_pair(key, (uint32_t)(it.b * HW + p), j);
                         nv[2 * j] = n2.x;
                         if (2 * j + 1 < NS) nv[2 * j + 1] = n2.y;
                     }
                 }
+                float id[NS];
+#pragma unroll
+                for (int f = 0; f < NS; ++f) id[f] = a.ident[((size_t)f * a.B + it.b) * HW + p];
                 for (int ch = 0; ch < C; ++ch) {
                     float v;
                     if (avg) {
                         v = 0.f;
 #pragma unroll
-                        for (int f = 0; f < NS; ++f) v += id[f][i];
+                        for (int f = 0; f < NS; ++f) v += id[f];
                         v = v / (float)NS;
                     } else {
-                        v = id[ch][i];
+                        v = id[ch];
                     }
                     v = v + nv[ch] * 1e-5f;
-                    if (v < best) {
-                        best = v;
-                        code = ch;
+                    if (v < bv) {
+                        bv = v;
+                        bc = ch;
                     }
                 }
             }
-            float accum = 0.f;
+            best[i][lane] = bv;
+            code[i][lane] = (uint8_t)bc;
+            if (avg) acc[i][lane] = 0.f;
+        }
+    }
+    WarpCtx ctx;
+    make_ctx(a, ls, 0, it.b, ctx);
 #pragma unroll
-            for (int f = 0; f < NS; ++f) {
-                const float v = rp[f][i];
-                if (avg) {
-                    accum += v;
-                } else if (v < best) {
-                    best = v;
-                    code = (automask ? NS : 0) + f;
-                }
-            }
+    for (int k = 0; k < kRowsP + 2; ++k) dep[k][lane] = depth_at(ctx, reflect_clamp(it.r0 - 1 + k, h), it.cc);
+    const float* tgt = a.tgt + (size_t)it.b * 3 * HW;
+#pragma unroll 1
+    for (int f = 0; f < NS; ++f) {
+        if (f > 0) {   // the frame's source and pose; the depths are shared
+            ctx.src = a.src[f] + (size_t)it.b * 3 * HW;
+            ctx.src8 = (a.src8[f] && a.exact[f * a.B + it.b]) ? a.src8[f] + (size_t)it.b * HW : nullptr;
+            load_cam(ctx.cm, a.K + it.b * 16, a.iK + it.b * 16, a.T[ls] + ((size_t)f * a.B + it.b) * 16);
+        }
+        const float* pmask = MASK ? a.mask[ls] + ((size_t)it.b * NS + f) * HW : nullptr;
+        const int fcode = (automask ? NS : 0) + f;
+        auto emit = [&](int i, float v) {
+            const int r = it.r0 + i;
+            if (MASK && it.colok && r < h) v *= pmask[r * w + it.c];  // trainer.py:455
             if (avg) {
-                const float ra = accum / (float)NS;
-                if (automask) {
-                    if (ra < best) {
-                        best = ra;
-                        code = 1;
-                    }
-                } else {
-                    best = ra;
-                }
+                acc[i][lane] += v;
+            } else if (v < best[i][lane]) {
+                best[i][lane] = v;
+                code[i][lane] = (uint8_t)fcode;
             }
-            if (i < npx) lsum += best;
-            codes |= (uint32_t)code << (8 * i);
-        }
-        uint8_t* sel = a.sel[ls] + (size_t)b * HW;
-        if (vec) {
-            *(uint32_t*)(sel + p0) = codes;
-        } else {
-            for (int i = 0; i < npx; ++i) sel[p0 + i] = (uint8_t)(codes >> (8 * i));
-        }
-        const float t = wave_sum(lsum);
-        if ((threadIdx.x & 63) == 0) red[ls][threadIdx.x >> 6] = t;
+        };
+        if (ctx.src8)   // wave-uniform: this image's sources are 8-bit exact
+            loss_rows<SSIM_ON, true, true>(ctx, tgt, dep, it.r0, it.cc, lane, emit);
+        else
+            loss_rows<SSIM_ON, true, false>(ctx, tgt, dep, it.r0, it.cc, lane, emit);
     }
-    __syncthreads();
-    if (threadIdx.x < a.nsc) {
-        const int ls = threadIdx.x;
-        a.photo_part[ls][(size_t)b * a.cblk + cb] = ((red[ls][0] + red[ls][1]) + red[ls][2]) + red[ls][3];
+    float lsum = 0.f;
+    uint8_t* sel = a.sel[ls] + (size_t)it.b * HW;
+#pragma unroll 1
+    for (int i = 0; i < kRowsP; ++i) {
+        const int r = it.r0 + i;
+        float bv = best[i][lane];
+        int bc = code[i][lane];
+        if (avg) {
+            const float ra = acc[i][lane] / (float)NS;
+            if (automask) {
+                if (ra < bv) {
+                    bv = ra;
+                    bc = 1;
+                }
+            } else {
+                bv = ra;
+            }
+        }
+        if (it.colok && r < h) {
+            lsum += bv;
+            sel[r * w + it.c] = (uint8_t)bc;
+        }
     }
+    const float t = wave_sum(lsum);
+    if (lane == 0) a.photo_part[ls][item] = t;   // item = (b * rowblocks + rb) * strips + st
 }
 
 // 8-bit source copies: every source colour x with x == RN(k/255) for k = rint(255 x)
@@ -1467,20 +1447,25 @@ struct Timing {
     std::mutex mu;
     bool on = false;
     int cap = 0, used = 0;
-    std::vector<hipEvent_t> ev;   // pairs: [2*i] start, [2*i+1] stop
-    std::vector<int> kind;        // 0 fwd, 1 bwd
+    std::vector<hipEvent_t> ev;     // pairs: [2*i] start, [2*i+1] stop (owned)
+    std::vector<hipEvent_t> start;  // the start event slot i measures from (ev[2*i] or another slot's)
+    std::vector<int> kind;          // 0 fwd photo kernels, 1 photo_bwd, 2 whole fwd call, 3 whole bwd call
+    double call_ms[2] = {0.0, 0.0}; // kinds 2, 3 of the last md2_timing_end
+    int call_n[2] = {0, 0};
 };
 Timing g_timing;
 
 // Reserve a timing slot (or -1).  The events are stamped by hipExtLaunchKernelGGL on
 // the kernel dispatch itself, so they measure the kernel, not the queue around it.
-int timing_slot(int kind, hipEvent_t* start, hipEvent_t* stop) {
+// shared_start: measure from that (already reserved) start event instead of the slot's own.
+int timing_slot(int kind, hipEvent_t* start, hipEvent_t* stop, hipEvent_t shared_start = nullptr) {
     std::lock_guard<std::mutex> lk(g_timing.mu);
     *start = *stop = nullptr;
     if (!g_timing.on || g_timing.used >= g_timing.cap) return -1;
     const int i = g_timing.used++;
     g_timing.kind[i] = kind;
-    *start = g_timing.ev[2 * i];
+    g_timing.start[i] = shared_start ? shared_start : g_timing.ev[2 * i];
+    *start = g_timing.start[i];
     *stop = g_timing.ev[2 * i + 1];
     return i;
 }
@@ -1501,8 +1486,7 @@ struct Layout {
     int fstrips[MD2_MAX_SCALES], frows[MD2_MAX_SCALES], fwpi[MD2_MAX_SCALES];
     int bstrips[MD2_MAX_SCALES], brows[MD2_MAX_SCALES], bwpi[MD2_MAX_SCALES];
     int chunks[MD2_MAX_SCALES];
-    int cblk[MD2_MAX_SCALES];                        // combine blocks per image (split forward)
-    size_t rep_off[MD2_MAX_SCALES], ident_off, src8_off, exact_off;
+    size_t ident_off, src8_off, exact_off;
     size_t photo_off[MD2_MAX_SCALES], dP_off[MD2_MAX_SCALES], smooth_off[MD2_MAX_SCALES];
     size_t dfull_off[MD2_MAX_SCALES], stats_off, total;
     size_t sel_off[MD2_MAX_SCALES], sel_total;
@@ -1541,15 +1525,12 @@ int make_layout(const md2_desc* d, Layout& L) {
         L.fstrips[s] = (L.lw[s] + kFwdCols - 1) / kFwdCols;
         L.frows[s] = (L.lh[s] + kRowsP - 1) / kRowsP;
         L.fwpi[s] = L.fstrips[s] * L.frows[s];
-        L.cblk[s] = (L.lh[s] * L.lw[s] + kCombinePix - 1) / kCombinePix;
         L.bstrips[s] = (L.lw[s] + kBwdCols - 1) / kBwdCols;
         L.brows[s] = (L.lh[s] + kRowsB - 1) / kRowsB;
         L.bwpi[s] = L.bstrips[s] * L.brows[s];
         L.chunks[s] = (L.hs[s] * L.ws[s] + kSmoothChunk - 1) / kSmoothChunk;
         L.photo_off[s] = off;
-        off = align256(off + sizeof(float) * (size_t)L.B * L.cblk[s]);
-        L.rep_off[s] = off;
-        off = align256(off + sizeof(float) * (size_t)L.S * L.B * L.lh[s] * L.lw[s]);
+        off = align256(off + sizeof(float) * (size_t)L.B * L.fwpi[s]);   // one partial per forward wave
         L.dP_off[s] = off;
         off = align256(off + sizeof(float) * (size_t)L.S * L.B * L.bwpi[s] * 12);
         L.smooth_off[s] = off;
@@ -1641,10 +1622,8 @@ void photo_args(const md2_desc* d, const md2_tensors* t, const Layout& L, int s_
         a.dP_part[ls] = (float*)(ws + L.dP_off[s]);
         a.mask[ls] = t->mask ? t->mask + L.mask_off[s] : nullptr;
         a.gmask[ls] = grad_mask ? grad_mask + L.mask_off[s] : nullptr;
-        a.rep[ls] = ws ? (float*)(ws + L.rep_off[s]) : nullptr;
     }
     a.ident = ws ? (float*)(ws + L.ident_off) : nullptr;
-    a.cblk = L.cblk[s_begin];
     if (ws && !L.v1) {
         for (int f = 0; f < L.S; ++f)
             a.src8[f] = (const uint32_t*)(ws + L.src8_off) + (size_t)f * L.B * L.lh[0] * L.lw[0];
@@ -1660,10 +1639,10 @@ void launch_fwd_t(const PhotoArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t 
         const int blocks = (a.B * a.wpi * NS + kWavesPerBlock - 1) / kWavesPerBlock;
         hipExtLaunchKernelGGL((photo_ident_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, e0, nullptr, 0, a);
     }
-    const int rblocks = (a.B * a.wpi * a.nsc * NS + kWavesPerBlock - 1) / kWavesPerBlock;
-    hipExtLaunchKernelGGL((photo_reproj_kernel<NS, SSIM, MASK>), dim3(rblocks), dim3(kBlock), 0, st,
-                          automask ? nullptr : e0, nullptr, 0, a);
-    hipExtLaunchKernelGGL((photo_combine_kernel<NS>), dim3(a.B * a.cblk), dim3(kBlock), 0, st, nullptr, e1, 0, a);
+    const int rblocks = (a.B * a.wpi * a.nsc + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipExtLaunchKernelGGL((photo_fwdloss_kernel<NS, SSIM, MASK>), dim3(rblocks), dim3(kBlock),
+                          fwdloss_lds_bytes((a.flags & MD2_AVG_REPROJECTION) != 0), st, automask ? nullptr : e0, e1,
+                          0, a);
 }
 // number of workgroups that can be resident at once for a kernel (cached per
 // kernel and device); the persistent-loop kernels launch exactly that many
@@ -1757,6 +1736,7 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
     hipStream_t st = (hipStream_t)stream;
     uint8_t* ws = (uint8_t*)workspace;
     PhotoArgs a;
+    hipEvent_t c0 = nullptr, c1 = nullptr;
     if (L.v1) {  // one launch per scale (each at its own resolution); not timed
         for (int s = 0; s < L.nscales; ++s) {
             photo_args(d, t, L, s, s + 1, false, ws, select_out, a);
@@ -1775,7 +1755,8 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
         if (hipMemsetAsync(pk.exact, 0x01, sizeof(int) * (size_t)L.S * L.B, st) != hipSuccess)
             return fail(MD2_ERR_HIP, "hipMemsetAsync failed");
         const int per_img = (pk.HW + 4 * kBlock - 1) / (4 * kBlock);
-        hipLaunchKernelGGL(pack_src8_kernel, dim3(L.S * L.B * per_img), dim3(kBlock), 0, st, pk);
+        timing_slot(2, &c0, &c1);   // the whole call: pack .. finalize
+        hipExtLaunchKernelGGL(pack_src8_kernel, dim3(L.S * L.B * per_img), dim3(kBlock), 0, st, c0, nullptr, 0, pk);
         hipEvent_t e0, e1;
         timing_slot(0, &e0, &e1);
         photo_args(d, t, L, 0, L.nscales, false, ws, select_out, a);
@@ -1812,7 +1793,7 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
         fa.hs[s] = L.hs[s];
         fa.ws[s] = L.ws[s];
         fa.chunks[s] = L.chunks[s];
-        fa.nphoto[s] = L.B * L.cblk[s];
+        fa.nphoto[s] = L.B * L.fwpi[s];
         fa.photo_part[s] = (const float*)(ws + L.photo_off[s]);
         fa.smooth_part[s] = (const float*)(ws + L.smooth_off[s]);
     }
@@ -1820,7 +1801,10 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
     fa.smoothness = d->disparity_smoothness;
     fa.loss_out = loss_out;
     if (L.B > kBlock) return fail(MD2_ERR_ARG, "batch > %d not supported by the finalize kernel", kBlock);
-    hipLaunchKernelGGL(finalize_fwd_kernel, dim3(1), dim3(kWave * kFinWaves), 0, st, fa);
+    if (c1)
+        hipExtLaunchKernelGGL(finalize_fwd_kernel, dim3(1), dim3(kWave * kFinWaves), 0, st, nullptr, c1, 0, fa);
+    else
+        hipLaunchKernelGGL(finalize_fwd_kernel, dim3(1), dim3(kWave * kFinWaves), 0, st, fa);
     return hip_check("finalize_fwd_kernel");
 }
 
@@ -1839,6 +1823,7 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
     hipStream_t st = (hipStream_t)stream;
     uint8_t* ws = (uint8_t*)workspace;
     PhotoArgs a;
+    hipEvent_t c0 = nullptr, c1 = nullptr;
     if (L.v1) {
         for (int s = 0; s < L.nscales; ++s) {
             photo_args(d, t, L, s, s + 1, true, ws, (uint8_t*)select, a, grad_mask);
@@ -1848,6 +1833,7 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
     } else {
         hipEvent_t e0, e1;
         timing_slot(1, &e0, &e1);
+        timing_slot(3, &c0, &c1, e0);   // the whole call: photo_bwd .. grad_T
         photo_args(d, t, L, 0, L.nscales, true, ws, (uint8_t*)select, a, grad_mask);
         a.grad_loss = grad_loss;
         launch_photo(a, true, st, e0, e1);
@@ -1893,7 +1879,10 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
     }
     ta.grad_T = grad_T;
     const int nT = ta.per_scale ? L.nscales : 1;
-    hipLaunchKernelGGL(grad_T_kernel, dim3(nT * L.S * L.B), dim3(kBlock), 0, st, ta);
+    if (c1)
+        hipExtLaunchKernelGGL(grad_T_kernel, dim3(nT * L.S * L.B), dim3(kBlock), 0, st, nullptr, c1, 0, ta);
+    else
+        hipLaunchKernelGGL(grad_T_kernel, dim3(nT * L.S * L.B), dim3(kBlock), 0, st, ta);
     return hip_check("grad_T_kernel");
 }
 
@@ -1944,6 +1933,7 @@ int md2_timing_begin(int max_launches) {
     if (max_launches < 1) return fail(MD2_ERR_ARG, "max_launches must be >= 1");
     for (hipEvent_t e : g_timing.ev) (void)hipEventDestroy(e);
     g_timing.ev.assign(2 * (size_t)max_launches, nullptr);
+    g_timing.start.assign(max_launches, nullptr);
     g_timing.kind.assign(max_launches, 0);
     for (auto& e : g_timing.ev)
         if (hipEventCreate(&e) != hipSuccess) return fail(MD2_ERR_HIP, "hipEventCreate failed");
@@ -1957,21 +1947,34 @@ int md2_timing_end(double* fwd_ms, int* n_fwd, double* bwd_ms, int* n_bwd) {
     std::lock_guard<std::mutex> lk(g_timing.mu);
     if (!g_timing.on) return fail(MD2_ERR_ARG, "md2_timing_begin was not called");
     g_timing.on = false;
-    double tot[2] = {0.0, 0.0};
-    int cnt[2] = {0, 0};
+    double tot[4] = {0.0, 0.0, 0.0, 0.0};
+    int cnt[4] = {0, 0, 0, 0};
     for (int i = 0; i < g_timing.used; ++i) {
         if (hipEventSynchronize(g_timing.ev[2 * i + 1]) != hipSuccess)
             return fail(MD2_ERR_HIP, "hipEventSynchronize failed");
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, g_timing.ev[2 * i], g_timing.ev[2 * i + 1]) != hipSuccess)
+        if (hipEventElapsedTime(&ms, g_timing.start[i], g_timing.ev[2 * i + 1]) != hipSuccess)
             return fail(MD2_ERR_HIP, "hipEventElapsedTime failed");
         tot[g_timing.kind[i]] += ms;
         cnt[g_timing.kind[i]] += 1;
     }
+    g_timing.call_ms[0] = tot[2];
+    g_timing.call_ms[1] = tot[3];
+    g_timing.call_n[0] = cnt[2];
+    g_timing.call_n[1] = cnt[3];
     if (fwd_ms) *fwd_ms = tot[0];
     if (n_fwd) *n_fwd = cnt[0];
     if (bwd_ms) *bwd_ms = tot[1];
     if (n_bwd) *n_bwd = cnt[1];
+    return MD2_OK;
+}
+
+int md2_timing_calls(double* fwd_ms, int* n_fwd, double* bwd_ms, int* n_bwd) {
+    std::lock_guard<std::mutex> lk(g_timing.mu);
+    if (fwd_ms) *fwd_ms = g_timing.call_ms[0];
+    if (n_fwd) *n_fwd = g_timing.call_n[0];
+    if (bwd_ms) *bwd_ms = g_timing.call_ms[1];
+    if (n_bwd) *n_bwd = g_timing.call_n[1];
     return MD2_OK;
 }
 

@@ -24,9 +24,19 @@ CHUNK = 1 << 16   # elements per table entry (one block)
 
 
 class FusedAdam(torch.optim.Adam):
+    """capturable=True: the hipGraph form (torch's `capturable` semantics) — the lr is
+    a device fp64 tensor (StepLR fills it in place, so replays see the decay), the
+    step counters are device tensors advanced by the kernel launch itself
+    (md2_adam_step_dev), so the whole step can be captured and replayed."""
 
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
-        super().__init__(params, lr=lr, betas=betas, eps=eps)
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, capturable: bool = False):
+        params = list(params)
+        if capturable and not torch.is_tensor(lr):
+            first = params[0]["params"][0] if isinstance(params[0], dict) else params[0]
+            lr = torch.tensor(float(lr), dtype=torch.float64, device=first.device)
+        super().__init__(params, lr=lr, betas=betas, eps=eps, capturable=capturable)
+        self.capturable = capturable
+        self._hyper = None   # device scratch of the capturable launch (step size, sqrt(bc2))
         self._key = None
         self._table = None
         self._starts = None
@@ -37,17 +47,34 @@ class FusedAdam(torch.optim.Adam):
 
     def state_dict(self):
         """torch's layout, each parameter with its own step tensor (a reference Adam
-        loading adam.pth increments them one by one)."""
+        loading adam.pth increments them one by one).  The capturable form saves what a
+        plain torch.optim.Adam saves (float lr, CPU step tensors, capturable False), so
+        adam.pth stays interchangeable with the reference's."""
         sd = super().state_dict()
-        if self._step_t is not None:
-            sd["state"] = {k: ({**v, "step": v["step"].clone()} if v.get("step") is self._step_t else v)
+        if self._step_t is not None or self.capturable:
+            sd["state"] = {k: ({**v, "step": v["step"].detach().clone().cpu()} if "step" in v else v)
                            for k, v in sd["state"].items()}
+        if self.capturable:
+            sd["param_groups"] = [{**g, "lr": float(g["lr"]), "capturable": False, "fused": None}
+                                  for g in sd["param_groups"]]
         return sd
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         self._key = None   # new moment buffers: rebuild the table on the next step
         self._step_t = None
+        if self.capturable:
+            # torch takes the saved groups' hyper-parameters (a reference adam.pth has a
+            # float lr and capturable False): back to the device lr and device steps
+            for g in self.param_groups:
+                dev = g["params"][0].device
+                g["lr"] = torch.tensor(float(g["lr"]), dtype=torch.float64, device=dev)
+                g["capturable"] = True
+                g["fused"] = None
+                for p in g["params"]:
+                    st = self.state.get(p)
+                    if st and torch.is_tensor(st.get("step")):
+                        st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
         # a state_dict saved from the fast path carries one step tensor under every
         # parameter: give each state its own, as torch's Adam increments them one by one
         seen = set()
@@ -65,9 +92,8 @@ class FusedAdam(torch.optim.Adam):
         give every state its own step tensor again."""
         if self._step_t is None:
             return
-        for p in self.param_groups[0]["params"] if len(self.param_groups) == 1 else []:
-            st = self.state.get(p)
-            if st and st.get("step") is self._step_t:
+        for st in self.state.values():   # every group (add_param_group may have run since)
+            if st.get("step") is self._step_t:
                 st["step"] = self._step_t.clone()
         self._step_t = None
 
@@ -75,8 +101,12 @@ class FusedAdam(torch.optim.Adam):
         if len(self.param_groups) != 1:   # one lr / betas / eps per launch
             return False
         g = self.param_groups[0]
-        return not (g["weight_decay"] != 0 or g["amsgrad"] or g["maximize"] or g.get("capturable")
-                    or g.get("differentiable"))
+        if bool(g.get("capturable")) != self.capturable:
+            return False
+        if self.capturable and not (torch.is_tensor(g["lr"]) and g["lr"].dtype == torch.float64
+                                    and g["lr"].is_cuda):
+            return False
+        return not (g["weight_decay"] != 0 or g["amsgrad"] or g["maximize"] or g.get("differentiable"))
 
     def _eligible(self) -> bool:
         if not self._group_ok():
@@ -106,7 +136,8 @@ class FusedAdam(torch.optim.Adam):
     def _state(self, p):
         st = self.state[p]
         if len(st) == 0:
-            st["step"] = torch.tensor(0.0)
+            st["step"] = (torch.zeros((), dtype=torch.float32, device=p.device) if self.capturable
+                          else torch.tensor(0.0))
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
         return st
@@ -150,6 +181,9 @@ class FusedAdam(torch.optim.Adam):
             key = tuple((p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), p.numel())
                         for p, st in zip(params, states))
             if key != self._key:
+                if torch.cuda.is_current_stream_capturing():
+                    raise RuntimeError("FusedAdam: the parameter set changed during hipGraph capture "
+                                       "(run an eager step first)")
                 # (re)validate what the kernel assumes, then upload the chunk table
                 if (len({float(st["step"]) for st in states}) != 1
                         or any(st["exp_avg"].stride() != p.stride() or st["exp_avg_sq"].stride() != p.stride()
@@ -167,13 +201,30 @@ class FusedAdam(torch.optim.Adam):
             self._step_t = states[0]["step"].clone()
             for st in states:
                 st["step"] = self._step_t
-        self._step_t += 1
-        step = int(self._step_t)
+        if not fast:
+            # a parameter without a gradient this step keeps its own counter (torch's
+            # Adam leaves its step alone)
+            live = {id(st) for st in states}
+            for st in self.state.values():
+                if id(st) not in live and st.get("step") is self._step_t:
+                    st["step"] = self._step_t.clone()
         b1, b2 = group["betas"]
-        lr = group["lr"]
-        lr = float(lr) if not torch.is_tensor(lr) else float(lr.item())
         for k, p in enumerate(params):
             self._grads[k] = p.grad.data_ptr()
+        if self.capturable:
+            # the kernel launch advances the device step counter itself
+            if self._hyper is None:
+                self._hyper = torch.empty(2, dtype=torch.float32, device=params[0].device)
+            rc = _lib.lib().md2_adam_step_dev(self._table.data_ptr(), self._starts, len(params), self._grads,
+                                              group["lr"].data_ptr(), float(b1), float(b2), float(group["eps"]),
+                                              self._step_t.data_ptr(), self._hyper.data_ptr(),
+                                              _lib.stream(params[0].device))
+            _lib.check(rc, "md2_adam_step_dev")
+            return loss
+        self._step_t += 1
+        step = int(self._step_t)
+        lr = group["lr"]
+        lr = float(lr) if not torch.is_tensor(lr) else float(lr.item())
         rc = _lib.lib().md2_adam_step(self._table.data_ptr(), self._starts, len(params), self._grads, lr,
                                       float(b1), float(b2), float(group["eps"]), step,
                                       _lib.stream(params[0].device))

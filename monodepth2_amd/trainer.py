@@ -152,22 +152,24 @@ class Trainer:
         streams = ([torch.cuda.current_stream(self.device), self._pose_stream]
                    if self._pose_stream is not None else None)
         self.ddp = wrap_ddp(self.nets, self.device, streams) if (world_size > 1 and sync == "ddp") else None
+        # one GPU needs no buckets: under capture the gradients are allocated (and
+        # freed) in the graph's private pool like every other tensor, at the same
+        # addresses on every replay, and autograd hands each producer's output over
+        # instead of adding it into a pre-zeroed bucket (~150 add launches per step)
         self.flat_sync = FlatGradSync(self.nets.named_parameters(), world_size) \
-            if (sync == "flat" or self.use_graph) else None
+            if (world_size > 1 and (sync == "flat" or self.use_graph)) else None
         self.graph = None
         self.seed_tensor = None
 
         # Adam (trainer.py:102): one HIP launch per step over every parameter (optim.py);
-        # under hipGraph torch's capturable fused Adam (device-side step counters)
-        if self.device.type == "cuda" and not self.use_graph:
-            self.model_optimizer = FusedAdam(self.parameters_to_train, self.opt.learning_rate)
+        # under hipGraph its capturable form: the lr is a device tensor that StepLR
+        # updates in place (lr_scheduler._update_param_group_val -> fill_), so replays
+        # see the decay, and the step counter lives on the device
+        if self.device.type == "cuda":
+            self.model_optimizer = FusedAdam(self.parameters_to_train, self.opt.learning_rate,
+                                             capturable=self.use_graph)
         else:
-            # under capture the lr is a device tensor: StepLR updates it in place
-            # (lr_scheduler._update_param_group_val -> fill_), so replays see the decay
-            lr = (torch.tensor(float(self.opt.learning_rate), device=self.device)
-                  if self.use_graph else self.opt.learning_rate)
-            self.model_optimizer = optim.Adam(self.parameters_to_train, lr,
-                                              capturable=self.use_graph, fused=self.device.type == "cuda")
+            self.model_optimizer = optim.Adam(self.parameters_to_train, self.opt.learning_rate)
         self.model_lr_scheduler = optim.lr_scheduler.StepLR(self.model_optimizer, self.opt.scheduler_step_size, 0.1)
         if self.opt.load_weights_folder is not None:
             self.load_model()
@@ -475,8 +477,13 @@ class Trainer:
         torch.cuda.current_stream(self.device).wait_stream(side)
         self._restore_training_state(snap)
         self.graph = torch.cuda.CUDAGraph()
+        dot = os.environ.get("MD2_GRAPH_DOT")
+        if dot:
+            self.graph.enable_debug_mode()
         with torch.cuda.graph(self.graph):
             self.static_outputs, self.static_losses = self._step_body(self.static_inputs)
+        if dot:
+            self.graph.debug_dump(dot)
 
     def _training_state(self):
         """Copies of every tensor a training step advances (see _capture)."""

@@ -57,6 +57,10 @@ CASES = {
     "full_stereo_b2_192x640": (2, 192, 640, [0, -1, 1, "s"], {}, 0.01, False),
     "predictive_mask_b2_32x64": (2, 32, 64, [0, -1, 1],
                                  {"disable_automasking": True, "predictive_mask": True}, 0.05, True),
+    # BASELINE configs[1] (C2): the bench's own shape, B=12 at 640x192 — losses, gradient
+    # checksums and identity-selection means only (the full planes would be ~8 MB)
+    # (8-bit colours, as the loader and the bench deliver them)
+    "c2_mono_b12_192x640": (12, 192, 640, [0, -1, 1], {"eight_bit": True}, 0.01, False, True),
 }
 
 
@@ -90,10 +94,11 @@ def import_reference(ref):
 
 
 def run_case(ref_trainer, ref_layers, name, spec, seed=0):
-    B, H, W, frame_ids, flags, pose_scale, keep_full = spec
+    B, H, W, frame_ids, flags, pose_scale, keep_full = spec[:7]
+    checksums_only = len(spec) > 7 and spec[7]
     scales = [0, 1, 2, 3]
     S = len(frame_ids) - 1
-    inputs = synthetic_batch(B, H, W, frame_ids, 4, seed=seed)
+    inputs = synthetic_batch(B, H, W, frame_ids, 4, seed=seed, eight_bit=flags.get("eight_bit", False))
     hp = synthetic_hotpath(B, H, W, num_src=S, seed=seed, pose_scale=pose_scale)
     disps = {s: hp["disps"][s].clone().requires_grad_(True) for s in scales}
     temporal = [f for f in frame_ids[1:] if f != "s"]
@@ -142,7 +147,20 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
         drawn.append(n.clone())
         return n
 
+    # the per-pixel argmin of trainer.py:478 (torch.min(combined, dim=1)), recorded as the
+    # reference computes it: the tests compare gradients away from pixels whose argmin
+    # differs (an fp32 near-tie re-routes that pixel's gradient)
+    argmins = []
+    real_min = torch.min
+
+    def recording_min(*a, **k):
+        r = real_min(*a, **k)
+        if k.get("dim") == 1 or (len(a) > 1 and a[1] == 1):
+            argmins.append(r[1].clone())
+        return r
+
     ref_trainer.torch.randn = fake_randn
+    ref_trainer.torch.min = recording_min
     real_cuda = torch.Tensor.cuda
     torch.Tensor.cuda = lambda t, *a, **k: t     # trainer.py:458 calls .cuda(); CPU-only here
     try:
@@ -150,6 +168,7 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
         losses = ref_trainer.Trainer.compute_losses(self, inputs, outputs)
     finally:
         ref_trainer.torch.randn = real_randn
+        ref_trainer.torch.min = real_min
         torch.Tensor.cuda = real_cuda
     losses["loss"].backward()
 
@@ -158,8 +177,12 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
            "flags": np.array(sorted(k for k, v in flags.items() if v))}
     for s in scales:
         rec[f"loss_{s}"] = losses[f"loss/{s}"].detach().numpy()
-        rec[f"grad_disp_{s}"] = disps[s].grad.numpy()
+        if not checksums_only:
+            rec[f"grad_disp_{s}"] = disps[s].grad.numpy()
     rec["loss"] = losses["loss"].detach().numpy()
+    if len(argmins) == len(scales):
+        for s, idx in zip(scales, argmins):
+            rec[f"argmin_{s}"] = idx.numpy().astype(np.uint8)
     rec["grad_axisangle"] = axis.grad.numpy()
     rec["grad_translation"] = trans.grad.numpy()
     for s, m in masks.items():
@@ -196,6 +219,9 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
             g = disps[s].grad
             rec[f"grad_disp_sum_{s}"] = g.double().sum().numpy()
             rec[f"grad_disp_abs_{s}"] = g.double().abs().sum().numpy()
+            rec[f"grad_disp_sq_{s}"] = g.double().square().sum().numpy()
+            # per-image abs sums: a gradient routed to the wrong image shows up here
+            rec[f"grad_disp_abs_img_{s}"] = g.double().abs().sum((1, 2, 3)).numpy()
             if not opt.disable_automasking:
                 rec[f"identity_selection_mean_{s}"] = outputs[f"identity_selection/{s}"].double().mean().numpy()
     return rec

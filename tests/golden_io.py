@@ -31,6 +31,7 @@ class Case:
         self.frame_ids = [parse_frame(str(f)) for f in z["frame_ids"]]
         self.flags = set(str(f) for f in z["flags"])
         self.full = "disp_0" in z.files
+        self.checksums_only = "grad_disp_0" not in z.files   # large cases: scalars + checksums
         self.scales = [0, 1, 2, 3]
         self.temporal = [f for f in self.frame_ids[1:] if f != "s"]
         if self.full:
@@ -60,7 +61,8 @@ class Case:
     def _regenerate(self):
         z = self.z
         seed = int(z["seed"])
-        self.inputs = synthetic_batch(self.B, self.H, self.W, self.frame_ids, 4, seed=seed)
+        self.inputs = synthetic_batch(self.B, self.H, self.W, self.frame_ids, 4, seed=seed,
+                                      eight_bit="eight_bit" in self.flags)
         hp = synthetic_hotpath(self.B, self.H, self.W, num_src=self.S, seed=seed,
                                pose_scale=float(z["pose_scale"]))
         self.disps = {s: hp["disps"][s] for s in self.scales}

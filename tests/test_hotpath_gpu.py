@@ -1,42 +1,30 @@
 """GPU parity: the HIP hot path (through the C ABI) against the reference's golden
-vectors (tests/golden/*.npz, captured from /root/reference by make_golden.py) and
-against the oracle on the same seeded inputs.
+vectors (tests/golden/*.npz, captured from /root/reference by make_golden.py, which
+also records the reference's own per-pixel argmin of trainer.py:478) and against the
+oracle on the same inputs.  fp32 throughout; north_star asks loss delta < 1e-4.
 
-Two tiers (fp32; north_star asks loss delta < 1e-4):
+Bars are fixed numbers, set per case at about 3x what tools/parity_measure.py
+measured on MI355X (profiles/r03/parity_measured.json), never recomputed at run time:
 
-1. against the reference's golden vectors:
-   * losses: |delta| <= 2e-6 per scale and total;
-   * warped colours / samples / depth: abs 2e-5 / 2e-5 / rel 1e-5;
-   * per-pixel argmin (identity_selection): at most max(2, 1e-4 * pixels) flips
-     per scale.  A flip happens only where two candidates tie to within fp32
-     rounding (gaps of 3e-8..6e-7 observed, tools/parity_report.py) and it
-     re-routes that pixel's gradient, so:
-   * gradients: relative L2 error <= 2e-2 per tensor.
-2. against the oracle on the same inputs with the argmin PINNED to the HIP
-   selection (oracle `selection=`), which isolates the gradient math from the
-   tie flips: losses <= 2e-6; >= 99 % of gradient pixels within
-   1e-4*max|ref| + 1e-3*|ref| and relative L2 <= 1e-2.  The remaining pixels are
-   where a sample coordinate lies within fp32 rounding of an integer (the bilinear
-   derivative is discontinuous there, so the two implementations pick different
-   cells) or where SSIM's clamp at 0 ties; measured: 0-10 pixels per tensor,
-   typical relative L2 1e-5 (small cases) to 4e-3 (the coarsest scale at
-   640x192, where one pixel aggregates 256 full-resolution gradients).
-   Sample-grid coordinates of near-singular projections (points behind or at the
-   camera plane, |value| up to 3e5) are compared at 1e-2 relative beyond |100|.
-
-At full size (640x192, 1024x320, mono+stereo) more samples land within rounding of
-a cell boundary and the coarse-scale gradients aggregate them, so the fixed bars
-are widened to what the reference's OWN formulation drifts on a second fp32
-platform: the same ATen ops run on PyTorch-ROCm (`run_oracle(device="cuda")`,
-a yardstick only) against the CPU goldens / CPU oracle.  The HIP path must stay
-within 3x that drift (relative L2) and 0.5 % of it (fraction of pixels in
-tolerance); against the goldens (argmin not pinned) the disparity pixels whose
-gradient footprint touches an argmin flip are left out (flip_footprint), the flips
-themselves bounded as above.  Measured (tools/parity_platforms.py), pinned:
-stereo 640x192 scale 2 rel-L2 HIP 1.4e-2 vs ATen-GPU 2.0e-2, scale 3 1.2e-2 vs
-6.0e-3; 1024x320 scale 3 in-tolerance HIP 98.6 % vs ATen-GPU 98.8 %.  Argmin flips
-per scale vs the CPU reference: HIP 4-58, ATen-GPU 2-43 (out of 245,760-655,360
-pixels).
+* losses: |delta| <= 2e-6 per scale and total (measured <= 9.5e-7);
+* warped colours / samples / depth (small cases): abs 2e-5 / 2e-5 / rel 1e-5;
+* argmin flips (HIP selection vs the reference's argmin): at most max(2, 1e-4 *
+  pixels) per scale.  A flip happens only where two candidates tie to within fp32
+  rounding (gaps of 3e-8..6e-7, tools/parity_report.py) and re-routes that pixel's
+  gradient, so gradients are compared outside its footprint (`flip_footprint`);
+* tier 1 (vs the goldens, outside the flip footprint), small cases: relative L2 of
+  dL/ddisp_s <= 1e-4 (measured 2e-6 .. 2.2e-5);
+* tier 2 (vs the oracle with the argmin PINNED to the HIP selection): relative L2
+  <= 1e-4 (measured <= 2e-5) on the small cases;
+* full size (640x192 B=2 and B=12, 1024x320, mono+stereo): a handful of pixels per
+  image have a sample coordinate within fp32 rounding of an integer, where the
+  bilinear derivative is discontinuous (the two implementations pick different
+  cells); every coarse-scale pixel aggregating one of them inherits the jump.  There
+  the bar is on the relative L2 with the largest 0.1 % of the per-pixel differences
+  left out (`trimmed_rel_l2`), per case and scale (FULL_T1 / FULL_T2), together with
+  >= 98.5 % .. 99.9 % of pixels within 1e-4 max|ref| + 1e-3 |ref|;
+* pose gradients (dL/daxisangle, dL/dtranslation, which sum over every pixel
+  including the flipped ones): tier 2 <= 1e-4 small, 5e-3 full.
 """
 import numpy as np
 import pytest
@@ -73,6 +61,55 @@ def rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
+def trimmed_rel_l2(g, r, frac=1e-3):
+    """relative L2 with the ceil(frac * n) largest absolute differences left out"""
+    g = np.asarray(g, np.float64).ravel()
+    r = np.asarray(r, np.float64).ravel()
+    d = np.abs(g - r)
+    n = int(np.ceil(frac * d.size))
+    keep = np.ones(d.size, bool)
+    if n:
+        keep[np.argpartition(d, -n)[-n:]] = False
+    return rel_l2(g[keep], r[keep])
+
+
+def in_tol(g, r):
+    return float((np.abs(g - r) <= 1e-4 * np.abs(r).max() + 1e-3 * np.abs(r)).mean())
+
+
+SMALL_BAR = 1e-4          # tier 1 and tier 2 relative L2, small cases
+# the one cell-flip pixel of stereo_b2_64x128 lands in the 8x16 scale 3 (measured 9.6e-4)
+SMALL_T2_OVERRIDE = {("stereo_b2_64x128", 3): 3e-3}
+# per-scale bars on trimmed_rel_l2, 3x measured: tier 1 (vs goldens outside the flip
+# footprint; C2: vs the oracle, its golden holds checksums) and tier 2 (pinned oracle)
+FULL_T1 = {"full_mono_b2_192x640": (2e-4, 2.5e-4, 3e-4, 1.6e-3),
+           "full_mono_b2_320x1024": (2.5e-4, 3e-4, 2e-3, 7e-3),
+           "full_stereo_b2_192x640": (2e-4, 2e-4, 4.5e-4, 4.5e-3),
+           "c2_mono_b12_192x640": (2.5e-4, 1e-3, 6e-3, 1.2e-2)}
+FULL_T2 = {"full_mono_b2_192x640": (2e-4, 2.5e-4, 3e-4, 2e-3),
+           "full_mono_b2_320x1024": (3e-4, 3.5e-4, 3.2e-3, 9.5e-3),
+           "full_stereo_b2_192x640": (2e-4, 2.5e-4, 3e-4, 6e-3),
+           "c2_mono_b12_192x640": (2.5e-4, 3.2e-4, 1.5e-3, 6.5e-3)}
+# fraction of pixels within 1e-4 max|ref| + 1e-3 |ref| (measured >= 0.9857 at 1024x320 s3)
+# (bar = 1 - 3x the measured out-of-tolerance fraction)
+FULL_IN_TOL = (0.9998, 0.996, 0.987, 0.955)
+# C2 gradient checksums vs the reference's, relative (3x measured): sum |g|, sum g^2,
+# and sum |g| per image
+CHECKSUM_BAR = {"abs": (1e-4, 1e-4, 4e-4, 7e-4), "sq": (2e-4, 1e-4, 4.5e-4, 1.2e-3)}
+CHECKSUM_IMG_BAR = (6e-4, 1.1e-3, 2.2e-3, 4e-3)
+
+
+def golden_flips(case, out, s):
+    """HIP argmin != the reference's recorded argmin (None when the golden has none)"""
+    if f"argmin_{s}" not in case.z.files:
+        return None
+    return out["select"][s] != case.expected(f"argmin_{s}")
+
+
+def footprint_scale(case, s):
+    return 0 if "v1_multiscale" in case.flags else s
+
+
 @pytest.mark.parametrize("name", case_names())
 def test_hip_matches_reference(name):
     case = Case(name)
@@ -102,38 +139,47 @@ def test_hip_matches_reference(name):
                 C = 1 if cfg.avg_reprojection else cfg.num_src
                 m = float((out["select"][s] > C - 1).mean())
                 assert abs(m - float(case.expected(f"identity_selection_mean_{s}"))) < 1e-3
-    if case.full is False and "disable_automasking" not in case.flags:
-        # full size: compare away from the argmin flips (each re-routes a pixel's
-        # gradient to another candidate); the flips themselves are bounded above
+    if case.checksums_only:
+        # configs[1]'s shape (B=12, 640x192): the golden holds gradient checksums, the
+        # per-pixel comparison is against the oracle on the regenerated inputs
+        for s in range(4):
+            g = out["grad_disp"][s].astype(np.float64)
+            for key, v in (("abs", np.abs(g).sum()), ("sq", np.square(g).sum())):
+                want = float(case.expected(f"grad_disp_{key}_{s}"))
+                assert abs(v - want) <= CHECKSUM_BAR[key][s] * abs(want), (s, key, v, want)
+            img = np.abs(g).sum((1, 2, 3))
+            want = case.expected(f"grad_disp_abs_img_{s}")
+            assert np.all(np.abs(img - want) <= CHECKSUM_IMG_BAR[s] * want), (s, img, want)
         cpu = run_oracle(case)
-        aten = run_oracle(case, device="cuda")
-        C = 1 if cfg.avg_reprojection else cfg.num_src
         for s in range(4):
-            ref_sel = cpu["outputs"][f"identity_selection/{s}"].cpu().numpy() > 0.5
-            ident_flips = (out["select"][s] > C - 1) != ref_sel
-            assert ident_flips.sum() <= max(2, 1e-4 * ident_flips.size), (s, int(ident_flips.sum()))
-            # any argmin difference (also between two reprojection candidates)
-            flips = out["select"][s] != cpu["outputs"][f"argmin/{s}"].cpu().numpy()
+            flips = golden_flips(case, out, s)
+            assert flips.sum() <= max(2, 1e-4 * flips.size), (s, int(flips.sum()))
             keep = ~flip_footprint(flips, s)
-            want = case.expected(f"grad_disp_{s}")
+            e = trimmed_rel_l2(out["grad_disp"][s][keep], cpu["grad_disp"][s][keep])
+            assert e <= FULL_T1[name][s], (s, e)
+        return
+    for s in range(4):
+        want = case.expected(f"grad_disp_{s}")
+        flips = golden_flips(case, out, s)
+        keep = np.ones(want.shape, bool)
+        if flips is not None:
+            assert flips.sum() <= max(2, 1e-4 * flips.size), (s, int(flips.sum()))
+            keep = ~flip_footprint(flips, footprint_scale(case, s))
+        if case.full:
             e = rel_l2(out["grad_disp"][s][keep], want[keep])
-            # the reference's own drift on this machine: the same ATen ops on the GPU,
-            # and on this host's CPU (its vector kernels need not sum in the order of
-            # the machine that wrote the goldens)
-            drift = max(rel_l2(aten["grad_disp"][s][keep], want[keep]),
-                        rel_l2(cpu["grad_disp"][s][keep], want[keep]))
-            bar = max(2e-2, 3 * drift)
-            assert e <= bar, (s, e, bar)
-    else:
-        for s in range(4):
-            e = rel_l2(out["grad_disp"][s], case.expected(f"grad_disp_{s}"))
-            assert e <= 2e-2, (s, e)
-    assert rel_l2(out["grad_axis"], case.expected("grad_axisangle")) <= 2e-2
-    assert rel_l2(out["grad_trans"], case.expected("grad_translation")) <= 2e-2
+            assert e <= SMALL_BAR, (s, e)
+        else:
+            e = trimmed_rel_l2(out["grad_disp"][s][keep], want[keep])
+            assert e <= FULL_T1[name][s], (s, e)
+    # pose gradients sum over every pixel, flipped ones included (measured: small cases
+    # <= 1.6e-4, stereo / full size <= 1.7e-3)
+    pose_bar = 5e-3 if (not case.full or name.startswith("stereo")) else 5e-4
+    assert rel_l2(out["grad_axis"], case.expected("grad_axisangle")) <= pose_bar
+    assert rel_l2(out["grad_trans"], case.expected("grad_translation")) <= pose_bar
     for i, f in enumerate(case.temporal):
-        assert rel_l2(out["grad_T"][case.frame_ids[1:].index(f)], case.expected(f"grad_T_{f}")) <= 2e-2
+        assert rel_l2(out["grad_T"][case.frame_ids[1:].index(f)], case.expected(f"grad_T_{f}")) <= pose_bar
     for s, g in out.get("grad_mask", {}).items():
-        assert rel_l2(g, case.expected(f"grad_mask_{s}")) <= 2e-2, (s, rel_l2(g, case.expected(f"grad_mask_{s}")))
+        assert rel_l2(g, case.expected(f"grad_mask_{s}")) <= SMALL_BAR, (s, rel_l2(g, case.expected(f"grad_mask_{s}")))
 
 
 @pytest.mark.parametrize("name", case_names())
@@ -142,26 +188,23 @@ def test_hip_gradients_match_oracle_pinned_selection(name):
     cfg, out = run_hip(case)
     sel = None if cfg.disable_automasking and cfg.avg_reprojection else out["select"]
     ref = run_oracle(case, selection=sel)
-    aten = run_oracle(case, selection=sel, device="cuda") if case.full is False else None
     for s in range(5):
         assert abs(out["loss"][s] - ref["loss"][s]) <= 2e-6, (s, out["loss"][s], ref["loss"][s])
-
-    def in_tol(g, r):
-        return float((np.abs(g - r) <= 1e-4 * np.abs(r).max() + 1e-3 * np.abs(r)).mean())
-
+    small = name not in FULL_T2
     for s in range(4):
         g, r = out["grad_disp"][s], ref["grad_disp"][s]
-        frac_bar, rel_bar = 0.99, 1e-2
-        if aten is not None:
-            a = aten["grad_disp"][s]
-            frac_bar = min(frac_bar, in_tol(a, r) - 0.005)
-            rel_bar = max(rel_bar, 3 * rel_l2(a, r))
-        assert in_tol(g, r) >= frac_bar, (s, in_tol(g, r), frac_bar)
-        assert rel_l2(g, r) <= rel_bar, (s, rel_l2(g, r), rel_bar)
-    assert rel_l2(out["grad_axis"], ref["grad_axis"]) <= 1e-2
-    assert rel_l2(out["grad_trans"], ref["grad_trans"]) <= 1e-2
+        if small:
+            e = rel_l2(g, r)
+            assert e <= SMALL_T2_OVERRIDE.get((name, s), SMALL_BAR), (s, e)
+        else:
+            e = trimmed_rel_l2(g, r)
+            assert e <= FULL_T2[name][s], (s, e)
+            assert in_tol(g, r) >= FULL_IN_TOL[s], (s, in_tol(g, r))
+    pose_bar = (6e-4 if name.startswith("stereo") else SMALL_BAR) if small else 5e-3
+    assert rel_l2(out["grad_axis"], ref["grad_axis"]) <= pose_bar
+    assert rel_l2(out["grad_trans"], ref["grad_trans"]) <= pose_bar
     for s, g in out.get("grad_mask", {}).items():
-        assert rel_l2(g, ref["grad_mask"][s]) <= 1e-2, s
+        assert rel_l2(g, ref["grad_mask"][s]) <= SMALL_BAR, s
 
 
 def test_hip_deterministic():
@@ -220,10 +263,11 @@ def test_eight_bit_sources_match_oracle(name):
         assert abs(out["loss"][s] - ref["loss"][s]) <= 2e-6, (s, out["loss"][s], ref["loss"][s])
     for s in range(4):
         g, r = out["grad_disp"][s], ref["grad_disp"][s]
-        assert float((np.abs(g - r) <= 1e-4 * np.abs(r).max() + 1e-3 * np.abs(r)).mean()) >= 0.99, s
-        assert rel_l2(g, r) <= 1e-2, (s, rel_l2(g, r))
-    assert rel_l2(out["grad_axis"], ref["grad_axis"]) <= 1e-2
-    assert rel_l2(out["grad_trans"], ref["grad_trans"]) <= 1e-2
+        e = rel_l2(g, r)
+        assert e <= SMALL_T2_OVERRIDE.get((name, s), SMALL_BAR), (s, e)
+    pose_bar = 6e-4 if name.startswith("stereo") else SMALL_BAR
+    assert rel_l2(out["grad_axis"], ref["grad_axis"]) <= pose_bar
+    assert rel_l2(out["grad_trans"], ref["grad_trans"]) <= pose_bar
     # the warped colours the 8-bit gathers produce (generate_images reads fp32) agree
     # through the loss: an unpinned run selects the same candidates up to near-ties
     ref_free = run_oracle(case)

@@ -283,3 +283,118 @@ def test_encoder_input_matches_eager():
     fo = [torch.rand(2, 3, 15, 23, device="cuda", generator=g) for _ in range(2)]
     xo = enc.prepare([[fo[0], fo[1]]])
     assert torch.equal(xo, (torch.cat(fo, 1) - 0.45) / 0.225)
+
+
+def _replay_vs_eager(tr, batch):
+    """Snapshot the training state, replay the captured step, restore, run the same
+    step eagerly; returns (graph loss, eager loss, worst param diff, step delta)."""
+    torch.cuda.synchronize()
+    opt_state = [{k: v.detach().clone() for k, v in st.items()} for st in tr.model_optimizer.state.values()]
+    params0, bufs0 = _graph_state(tr)
+    seed0 = tr.seed_tensor.clone()
+    _, lg = tr.train_step(batch)
+    torch.cuda.synchronize()
+    loss_g = float(lg["loss"])
+    params_g, _ = _graph_state(tr)
+    with torch.no_grad():
+        for p, v in zip(tr.nets.parameters(), params0):
+            p.copy_(v)
+        for b, v in zip(tr.nets.buffers(), bufs0):
+            b.copy_(v)
+        for st, saved in zip(tr.model_optimizer.state.values(), opt_state):
+            for k, v in saved.items():
+                st[k].copy_(v)
+        tr.seed_tensor.copy_(seed0)
+    _, le = tr._step_body(tr.static_inputs)
+    torch.cuda.synchronize()
+    delta = max(float((a - b).abs().max()) for a, b in zip(params_g, params0))
+    worst = max(float((a - b).abs().max()) for a, b in zip(params_g, tr.nets.parameters()))
+    return loss_g, float(le["loss"]), worst, delta
+
+
+def test_hip_graph_bf16_full_resolution_step():
+    """Config C5's step (BASELINE configs[4]: bf16 autocast on the networks, the
+    photometric loss in fp32, the whole step captured in one hipGraph) at the full
+    640x192 resolution: a replay equals the same step run eagerly from the same state,
+    and the replay's loss equals the CPU oracle (reference formulation,
+    trainer.py:341-496) on the replay's own network outputs within 1e-5."""
+    from oracle.md2_oracle import HotPathOptions, hot_path
+    from monodepth2_amd.trainer import Trainer
+    Hf, Wf, Bf = 192, 640, 2
+    torch.manual_seed(0)
+    tr = Trainer(default_options(batch_size=Bf, height=Hf, width=Wf, weights_init="scratch", log_dir="/tmp/md2_test",
+                                 frame_ids=[0, -1, 1], amp="bf16", hip_graph=True), device=torch.device("cuda", 0))
+    batch = synthetic_batch(Bf, Hf, Wf, tr.opt.frame_ids, 4, seed=3, device="cuda", eight_bit=True)
+    gen = torch.Generator().manual_seed(7)
+    noise = {s: torch.randn(*tr.hot.noise_shape(s), generator=gen) for s in range(4)}
+    tr.noise_override = {s: n.cuda() for s, n in noise.items()}
+    tr.train_step(batch)       # warm-up + capture + first replay
+    tr.train_step(batch)
+    loss_g, loss_e, worst, delta = _replay_vs_eager(tr, batch)
+    assert abs(loss_g - loss_e) < 1e-6, (loss_g, loss_e)
+    assert delta > 0 and worst < 1e-3 * delta + 1e-9, (worst, delta)
+    # the replay's own outputs through the oracle
+    _, lg = tr.train_step(batch)
+    torch.cuda.synchronize()
+    out = tr.static_outputs
+    disps = {s: out[("disp", s)].detach().float().cpu() for s in range(4)}
+    T = tr._stacked_T(tr.static_inputs, out).detach().cpu()
+    cpu = {k: v.cpu() for k, v in tr.static_inputs.items()}
+    ref, _ = hot_path(HotPathOptions(height=Hf, width=Wf, frame_ids=[0, -1, 1]), disps, cpu,
+                      {f: T[i] for i, f in enumerate(tr.src_frames)}, noise=noise, keep_images=False)
+    assert abs(float(lg["loss"]) - float(ref["loss"])) < 1e-5, (float(lg["loss"]), float(ref["loss"]))
+
+
+def test_hip_graph_resume_keeps_device_lr(tmp_path):
+    """Resuming a hip_graph run from a checkpoint (trainer.py:605-630 load_model, incl.
+    adam.pth): the optimizer keeps its capturable form (device lr, device steps), the
+    saved adam.pth has the reference's plain layout (float lr, CPU step tensors), and
+    after the capture StepLR's decay still reaches the replays."""
+    tr, batch = make("mono", log_dir=str(tmp_path), hip_graph=True)
+    tr.train_step(batch)
+    tr.train_step(batch)
+    folder = tr.save_model()
+    sd = torch.load(os.path.join(folder, "adam.pth"), weights_only=True)
+    assert all(isinstance(g["lr"], float) and not g["capturable"] for g in sd["param_groups"])
+    assert all(v["step"].device.type == "cpu" and float(v["step"]) == 2.0 for v in sd["state"].values())
+    tr2, batch2 = make("mono", log_dir=str(tmp_path), hip_graph=True, load_weights_folder=folder)
+    g = tr2.model_optimizer.param_groups[0]
+    assert torch.is_tensor(g["lr"]) and g["lr"].is_cuda and g["capturable"]
+    assert all(st["step"].is_cuda for st in tr2.model_optimizer.state.values())
+    tr2.train_step(batch2)
+    tr2.train_step(batch2)
+    assert {float(st["step"]) for st in tr2.model_optimizer.state.values()} == {4.0}
+    lr0 = float(g["lr"])
+    for _ in range(tr2.opt.scheduler_step_size):
+        tr2.model_lr_scheduler.step()
+    assert abs(float(tr2.model_optimizer.param_groups[0]["lr"]) - 0.1 * lr0) < 1e-15
+    loss_g, loss_e, worst, delta = _replay_vs_eager(tr2, batch2)
+    assert abs(loss_g - loss_e) < 1e-6
+    assert delta > 0 and worst < 1e-3 * delta + 1e-9, (worst, delta)
+
+
+def test_resnet50_1024x320_losses_match_oracle():
+    """Config C4's shape (BASELINE configs[3]: mono 1024x320, ResNet-50, 8 images per
+    GPU): the trainer's fused losses on its own network outputs equal the oracle's
+    (reference formulation, trainer.py:407-496) within 1e-5 per scale and total."""
+    from oracle.md2_oracle import HotPathOptions, hot_path
+    from monodepth2_amd.trainer import Trainer
+    Hc, Wc, Bc = 320, 1024, 8
+    torch.manual_seed(0)
+    tr = Trainer(default_options(batch_size=Bc, height=Hc, width=Wc, num_layers=50, weights_init="scratch",
+                                 log_dir="/tmp/md2_test", frame_ids=[0, -1, 1]), device=torch.device("cuda", 0))
+    batch = synthetic_batch(Bc, Hc, Wc, tr.opt.frame_ids, 4, seed=11, device="cuda", eight_bit=True)
+    tr.train_step(batch)            # one real step first: the outputs below are a trained state's
+    gen = torch.Generator().manual_seed(9)
+    noise = {s: torch.randn(*tr.hot.noise_shape(s), generator=gen) for s in range(4)}
+    tr.noise_override = {s: n.cuda() for s, n in noise.items()}
+    with torch.no_grad():
+        outputs = tr.nets(tr, batch)
+        losses = tr.compute_losses(batch, outputs)
+    T = tr._stacked_T(batch, outputs).cpu()
+    ref, _ = hot_path(HotPathOptions(height=Hc, width=Wc, frame_ids=[0, -1, 1]),
+                      {s: outputs[("disp", s)].cpu() for s in range(4)}, {k: v.cpu() for k, v in batch.items()},
+                      {f: T[i] for i, f in enumerate(tr.src_frames)}, noise=noise, keep_images=False)
+    for s in range(4):
+        assert abs(float(losses[f"loss/{s}"]) - float(ref[f"loss/{s}"])) < 1e-5, s
+    assert abs(float(losses["loss"]) - float(ref["loss"])) < 1e-5
