@@ -65,13 +65,15 @@ HOT_KERNELS = "pack_src8|photo_|smooth_fwd|finalize_fwd|disp_grad_kernel|grad_T_
 
 def pmc_traffic(args, S, timeout=150):
     """HBM bytes per hot-path step (forward + backward), measured now: two rocprofv3
-    --pmc passes (FETCH_SIZE, WRITE_SIZE: one pass cannot hold both) over
-    tools/hot_bench.py at the bench's shape, averaged per dispatch per kernel and
+    --pmc passes (FETCH_SIZE, WRITE_SIZE: one pass cannot hold both) over a short run
+    of this same training step (bench.py --steps 3 at the same shape, so the caches
+    hold what they hold in the timed steps), averaged per dispatch per kernel and
     summed over the hot path's kernels.  FETCH_SIZE x2 (gfx950 under-reports wide
     reads by half, MI355X_MICROARCH.md §HBM), KB -> bytes.  Runs in child processes
     while this one waits (no GPU work of its own in flight)."""
     import csv
     import glob
+    import re
     import shutil
     import signal
     import subprocess
@@ -83,9 +85,11 @@ def pmc_traffic(args, S, timeout=150):
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="md2pmc_", dir="/tmp")
         cmd = [exe, "--pmc", counter, "--kernel-include-regex", HOT_KERNELS, "-d", d, "-o", "pmc",
-               "--output-format", "csv", "--", sys.executable, os.path.join(REPO, "tools", "hot_bench.py"),
+               "--output-format", "csv", "--", sys.executable, os.path.join(REPO, "bench.py"),
                "--batch", str(args.batch), "--height", str(args.height), "--width", str(args.width),
-               "--src", str(S), "--iters", "6", "--eight-bit"]
+               "--num_layers", str(args.num_layers), "--amp", args.amp, "--steps", "3", "--warmup", "2",
+               "--no-cpu-baseline", "--no-parity", "--pmc", "0", "--no-conv-roofline"] + \
+              (["--stereo"] if args.stereo else [])
         env = dict(os.environ, TMPDIR="/tmp")
         p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env, start_new_session=True)
         try:
@@ -101,7 +105,7 @@ def pmc_traffic(args, S, timeout=150):
         for f in files:
             for r in csv.DictReader(open(f)):
                 if r["Counter_Name"] == counter:
-                    name = r["Kernel_Name"].split("(")[0].split("::")[-1].split("<")[0]
+                    name = re.sub(r"\(anonymous namespace\)::|^void ", "", r["Kernel_Name"]).split("(")[0].split("<")[0]
                     vals.setdefault(name, []).append(float(r["Counter_Value"]))
         per[counter] = {k: sum(v) / len(v) for k, v in vals.items()}
         shutil.rmtree(d, ignore_errors=True)
@@ -132,6 +136,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-conv-roofline", action="store_true")
     ap.add_argument("--pmc", type=int, default=1, help="measure the hot path's HBM traffic with rocprofv3 "
                     "PMC passes in this run (rank 0, N=1)")
     ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen exhaustive find per conv shape")
@@ -402,8 +407,9 @@ def main():
             pmc_kernels, err = pmc_traffic(args, S)
             if pmc_kernels is not None:
                 traffic = sum(pmc_kernels.values())
-                pmc_note = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in this run over tools/hot_bench.py "
-                            "at this shape; 2*FETCH+WRITE (KB->B) per step, summed over the hot path's kernels")
+                pmc_note = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in this run over a 3-step run of this "
+                            "training step (bench.py --steps 3); 2*FETCH+WRITE (KB->B) per dispatch, summed over "
+                            "the hot path's kernels")
             else:
                 pmc_note = err
             log(f"pmc traffic: {traffic} B/step ({pmc_note[:80]})")
@@ -425,8 +431,10 @@ def main():
         log(f"timed: {1e3 * dt / args.steps:.2f} ms/step, hot path {hot_ms:.3f} ms (fwd {fcall:.3f}, bwd {bcall:.3f};"
             f" photo_bwd {bwd_ms:.3f}), {tfs:.2f} TF = {valu_frac:.3f} of VALU peak, {gbs:.0f} GB/s, "
             f"adam table uploads {getattr(trainer.model_optimizer, 'rebuilds', '-')}")
-        conv_roof = conv_mfma_roofline(device)
-        log(f"conv_x6: {conv_roof['achieved']} TFLOP/s ({conv_roof['frac']} of the f32 matrix peak)")
+        conv_roof = None
+        if not args.no_conv_roofline:
+            conv_roof = conv_mfma_roofline(device)
+            log(f"conv_x6: {conv_roof['achieved']} TFLOP/s ({conv_roof['frac']} of the f32 matrix peak)")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args)

@@ -1,7 +1,7 @@
 """Turn gpurun_out/<round>/ rocprofv3 CSVs into the committed summaries under profiles/<round>/:
   kernel_stats.csv       (copy of the --stats summary of the bench command)
   hot_kernels.json       per hot-path kernel: calls, avg ns, PMC averages per dispatch
-  pmc_traffic.json       photo_bwd/photo_fwd HBM bytes per launch (bench.py reads it)
+  pmc_traffic.json       the hot path per step: summed kernel time, HBM bytes, roofline fractions
 
 HBM bytes per MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KB; on gfx950
 FETCH_SIZE reads 1/2 of the bytes of wide coalesced streaming reads, so the corrected
@@ -19,6 +19,7 @@ import shutil
 import sys
 
 VALU_ISSUE_PER_S = 256 * 4 * 0.5 * 2.4e9   # wave-instructions/s (SIMD32 issues a wave64 op per 2 clk)
+HOT = ("pack_src8", "photo_", "smooth_fwd", "finalize_fwd", "disp_grad_kernel", "grad_T_kernel")
 
 
 def short(n):
@@ -38,8 +39,7 @@ def main():
     res = {}
     for r in rows:
         k = short(r["Name"])
-        if any(t in k for t in ("photo_", "pack_src8", "disp_grad", "smooth_fwd", "grad_T", "finalize_fwd", "conv_x6",
-                                "conv_wsplit")):
+        if k.startswith(HOT) or any(t in k for t in ("conv_x6", "conv_wsplit")):
             res.setdefault(k, {}).update(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
                                          share_of_gpu_time=float(r["TotalDurationNs"]) / total)
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -68,23 +68,31 @@ def main():
         if "TCC_HIT_sum" in d:
             d["l2_hit_rate"] = d["TCC_HIT_sum"] / max(1.0, d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
     json.dump(res, open(os.path.join(dst, "hot_kernels.json"), "w"), indent=1, sort_keys=True)
+    # the whole hot path (bench.py's roofline): every kernel of md2_photometric_fwd /
+    # _bwd runs once per call; per step = the sum of their average durations and HBM bytes
+    sys.path.insert(0, os.getcwd())
+    from monodepth2_amd.roofline import hot_path_census
+    hot = [k for k in res if k.startswith(HOT)]
+    step_ns = sum(res[k]["avg_ns"] for k in hot if "avg_ns" in res[k])
+    step_traffic = sum(res[k].get("hbm_traffic_bytes", 0.0) for k in hot)
+    B, H, W, S = 12, 192, 640, 2
+    cen = hot_path_census(H, W, S)
+    tf = B * cen.flops / (step_ns * 1e-9) / 1e12
+    gbs = B * cen.bytes / (step_ns * 1e-9) / 1e9
     bwd = next(v for k, v in res.items() if k.startswith("photo_bwd"))
-    # the forward is three launches (identity, reprojection, combine); its main kernel
-    # is the reprojection pass, the byte total sums the three
-    fwd = dict(next(v for k, v in res.items() if k.startswith("photo_reproj")))
-    fwd["hbm_traffic_bytes"] = sum(v.get("hbm_traffic_bytes", 0.0) for k, v in res.items()
-                                   if k.startswith(("photo_ident", "photo_reproj", "photo_combine")))
-    traffic = {"photo_bwd_kernel_bytes_per_launch": bwd.get("hbm_traffic_bytes"),
-               "photo_fwd_kernel_bytes_per_launch": fwd.get("hbm_traffic_bytes"),
-               "photo_bwd_valu_issue_frac": bwd.get("valu_issue_frac"),
-               "photo_fwd_valu_issue_frac": fwd.get("valu_issue_frac"),
-               "photo_bwd_td_busy_frac": bwd.get("td_busy_frac"),
-               "photo_fwd_td_busy_frac": fwd.get("td_busy_frac"),
-               "photo_bwd_ta_busy_frac": bwd.get("ta_busy_frac"),
-               "photo_fwd_ta_busy_frac": fwd.get("ta_busy_frac"),
+    traffic = {"hot_path_kernels": sorted(hot),
+               "hot_path_ns_per_step_rocprof": step_ns,
+               "hot_path_traffic_bytes_per_step": step_traffic,
+               "algorithmic_bytes_per_step": B * cen.bytes,
+               "algorithmic_flops_per_step": B * cen.flops,
+               "valu_frac_from_rocprof": tf / 157.3,
+               "hbm_frac_from_rocprof": gbs / 8000.0,
                "photo_bwd_avg_ns_rocprof": bwd.get("avg_ns"),
-               "photo_fwd_avg_ns_rocprof": fwd.get("avg_ns"),
-               "note": "traffic = 2*FETCH_SIZE + WRITE_SIZE (KB->B) per launch, separate --pmc passes"}
+               "photo_bwd_valu_issue_frac": bwd.get("valu_issue_frac"),
+               "photo_bwd_td_busy_frac": bwd.get("td_busy_frac"),
+               "note": "configs[1] shape (B=12, 640x192, S=2); traffic = 2*FETCH_SIZE + WRITE_SIZE (KB->B) per "
+                       "launch from separate --pmc passes, summed over the hot path's kernels; fractions = "
+                       "monodepth2_amd/roofline.py census / the summed rocprof average durations"}
     json.dump(traffic, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(traffic, indent=1))
     for k, d in sorted(res.items()):
