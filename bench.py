@@ -185,7 +185,7 @@ def loss_delta_vs_oracle(trainer, batch):
     camT = {f: T[i].cpu() for i, f in enumerate(trainer.src_frames)}
     opt = HotPathOptions(height=hot.height, width=hot.width, frame_ids=trainer.opt.frame_ids)
     with torch.no_grad():
-        ref, _ = hot_path(opt, {s: d.cpu() for s, d in enumerate(disps)}, cpu_inputs, camT, noise=noise,
+        ref, _ = hot_path(opt, {s: d.float().cpu() for s, d in enumerate(disps)}, cpu_inputs, camT, noise=noise,
                           keep_images=False)
     return abs(float(loss[hot.num_scales]) - float(ref["loss"]))
 

@@ -15,7 +15,8 @@
  * binds; INTEGRATION.md shows the binding.
  *
  * Conventions
- *  - Every tensor is fp32, contiguous NCHW, device memory owned by the caller
+ *  - Every tensor is fp32 (disparities: fp32 or bf16, md2_desc.disp_dtype),
+ *    contiguous NCHW, device memory owned by the caller
  *    (PyTorch's caching allocator).  The library never allocates outside
  *    md2_aug_plan_create: scratch lives in `workspace` (md2_workspace_bytes) and
  *    must be the SAME buffer for a forward and its backward (the forward leaves
@@ -53,6 +54,11 @@ extern "C" {
 #define MD2_T_PER_SCALE      (1u << 4) /* a cam_T_cam per scale (posecnn, trainer.py:366-375) */
 #define MD2_PREDICTIVE_MASK  (1u << 5) /* --predictive_mask     trainer.py:447-459 (needs NO_AUTOMASK) */
 
+/* md2_desc.disp_dtype: the disparities (and the gradients written for them) as fp32,
+ * or bf16 as the depth decoder emits them under bf16 autocast (config C5), read as is */
+#define MD2_DTYPE_F32  0u
+#define MD2_DTYPE_BF16 1u
+
 typedef struct md2_desc {
     int32_t batch;               /* B: images per rank (opt.batch_size)                  */
     int32_t height, width;       /* opt.height / opt.width (full resolution)             */
@@ -61,7 +67,7 @@ typedef struct md2_desc {
     uint32_t flags;              /* MD2_* above                                          */
     float min_depth, max_depth;  /* opt.min_depth / opt.max_depth                        */
     float disparity_smoothness;  /* opt.disparity_smoothness                             */
-    uint32_t reserved;
+    uint32_t disp_dtype;         /* MD2_DTYPE_*: element type of disp[] and grad_disp[]  */
     uint64_t seed;               /* tie-break noise seed when tensors.noise == NULL      */
 } md2_desc;
 

@@ -35,7 +35,7 @@ class Desc(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int32), ("height", ctypes.c_int32), ("width", ctypes.c_int32),
                 ("num_src", ctypes.c_int32), ("num_scales", ctypes.c_int32), ("flags", ctypes.c_uint32),
                 ("min_depth", ctypes.c_float), ("max_depth", ctypes.c_float),
-                ("disparity_smoothness", ctypes.c_float), ("reserved", ctypes.c_uint32),
+                ("disparity_smoothness", ctypes.c_float), ("disp_dtype", ctypes.c_uint32),
                 ("seed", ctypes.c_uint64)]
 
 
@@ -66,6 +66,8 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_conv_dgrad", "md2_conv_wgrad", "md2_conv_direct", "md2_conv_wgrad_direct",
            "md2_conv_wgrad_direct_workspace_bytes"]
 
+DTYPE_F32 = 0    # md2_desc.disp_dtype
+DTYPE_BF16 = 1
 PAD_ELU = 1 << 0
 PAD_UPSAMPLE = 1 << 1
 PAD_NHWC = 1 << 2

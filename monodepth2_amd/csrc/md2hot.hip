@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "md2hot.h"
+#include "md2_bf16.h"
 
 namespace {
 
@@ -109,6 +110,18 @@ __device__ __forceinline__ float2_a4 ldf2(const float* base, int idx) {
 }
 __device__ __forceinline__ uint8_t ldb(const uint8_t* base, int idx) { return base[(uint32_t)idx]; }
 
+// Disparities come as fp32 or bf16 (md2_desc.disp_dtype: the depth decoder's output
+// under bf16 autocast, read as is instead of cast up in a separate pass; bf16 -> fp32
+// is exact, so the arithmetic is the fp32 path's).  Pointers stay `const float*`;
+// element offsets are scaled by the element size here.
+__device__ __forceinline__ const float* disp_off(const float* base, size_t elems, bool bf16) {
+    return (const float*)((const char*)base + (elems << (bf16 ? 1 : 2)));
+}
+__device__ __forceinline__ float ldd(const float* base, int idx, bool bf16) {
+    if (bf16) return md2::bf2f(*(const uint16_t*)((const char*)base + ((uint32_t)idx << 1)));
+    return ldf(base, idx);
+}
+
 // x / 3 correctly rounded (the channel mean of trainer.py:396-397 divides by 3), in
 // three VALU ops instead of the IEEE division sequence: q = x * RN(1/3), one exact
 // fma residual, one fma correction (Markstein)
@@ -171,7 +184,8 @@ __device__ __forceinline__ void load_cam(Cam& cm, const float* K, const float* i
 
 // everything a warp of one (image, frame, scale) needs
 struct WarpCtx {
-    const float* disp;  // (dh, dw) disparity of this image at its native scale
+    const float* disp;  // (dh, dw) disparity of this image at its native scale (fp32 or bf16)
+    bool dbf16;
     int dh, dw, upsh;   // upsample factor 2^upsh to the loss resolution
     const float* src;   // (3, h, w) source colours at the loss resolution
     const uint32_t* src8;  // the same colours as 8-bit RGBx per pixel (k/255 exact), or null
@@ -183,7 +197,7 @@ struct WarpCtx {
 
 // bilinear upsample, align_corners=False (ATen area_pixel_compute_source_index)
 __device__ __forceinline__ float disp_at(const WarpCtx& c, int y, int x) {
-    if (c.upsh == 0) return ldf(c.disp, y * c.dw + x);
+    if (c.upsh == 0) return ldd(c.disp, y * c.dw + x, c.dbf16);
     const float sc = 1.0f / (float)(1 << c.upsh);
     const float sy = fmaxf(((float)y + 0.5f) * sc - 0.5f, 0.f);
     const float sx = fmaxf(((float)x + 0.5f) * sc - 0.5f, 0.f);
@@ -194,7 +208,13 @@ __device__ __forceinline__ float disp_at(const WarpCtx& c, int y, int x) {
     const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
     // (x0, x1) as one pair load; at the right border the pair starts one column left
     const int xa = xin ? x0 : x0 - 1;
-    const float2_a4 t = ldf2(c.disp, y0 * c.dw + xa), u = ldf2(c.disp, y1 * c.dw + xa);
+    float2_a4 t, u;
+    if (c.dbf16) {
+        t.x = ldd(c.disp, y0 * c.dw + xa, true), t.y = ldd(c.disp, y0 * c.dw + xa + 1, true);
+        u.x = ldd(c.disp, y1 * c.dw + xa, true), u.y = ldd(c.disp, y1 * c.dw + xa + 1, true);
+    } else {
+        t = ldf2(c.disp, y0 * c.dw + xa), u = ldf2(c.disp, y1 * c.dw + xa);
+    }
     const float t0 = xin ? t.x : t.y, u0 = xin ? u.x : u.y;
     return ly0 * (lx0 * t0 + lx1 * t.y) + ly1 * (lx0 * u0 + lx1 * u.y);
 }
@@ -436,11 +456,13 @@ struct PhotoArgs {
     const uint64_t* seed_ptr;               // optional device-side seed (graph replay)
     float min_disp, range;
     uint32_t flags;
+    int disp_bf16;                          // disp[] elements are bf16 (md2_desc.disp_dtype)
     float* photo_part[MD2_MAX_SCALES];      // fwd: per local scale [B*wpi]
     uint8_t* sel[MD2_MAX_SCALES];           // per local scale (B,h,w)
     // backward only
     const float* grad_loss;                 // (num_scales + 1)
-    float* dfull[MD2_MAX_SCALES];           // per local scale (B,h,w)
+    float* dfull[MD2_MAX_SCALES];           // per local scale (B,h,w), scales without upsample
+    float* upart[MD2_MAX_SCALES];           // per local scale [B][rowblocks][strips][NR][NC], upsampled scales
     float* dP_part[MD2_MAX_SCALES];         // per local scale [S][B*wpi][12]
     // predictive mask (MD2_PREDICTIVE_MASK): per local scale (B,S,h,w)
     const float* mask[MD2_MAX_SCALES];
@@ -458,7 +480,8 @@ __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int 
     c.dh = a.dh[ls];
     c.dw = a.dw[ls];
     c.upsh = a.upsh[ls];
-    c.disp = a.disp[ls] + (size_t)b * c.dh * c.dw;
+    c.dbf16 = a.disp_bf16 != 0;
+    c.disp = disp_off(a.disp[ls], (size_t)b * c.dh * c.dw, c.dbf16);
     c.src = a.src[f] + (size_t)b * 3 * HW;
     c.src8 = (a.src8[f] && a.exact[f * a.B + b]) ? a.src8[f] + (size_t)b * HW : nullptr;
     c.h = a.h;
@@ -784,6 +807,32 @@ __global__ __launch_bounds__(kBlock) void pack_src8_kernel(PackArgs a) {
 // ----------------------------------------------------------------------------
 // backward: SSIM/L1 adjoint -> grid_sample backward -> projection chain
 // ----------------------------------------------------------------------------
+// ---- adjoint of the bilinear upsample (trainer.py:350-351), item by item -------------
+// A backward item (60 columns x kRowsB rows of one scale's full-resolution grid) folds
+// its dL/d(upsampled disp) straight into the native-resolution pixels it touches: a
+// partial grid of NR x NC native pixels starting at (ilo, jlo), written once per item.
+// disp_grad_kernel then sums the <= 2 x 2 partials of the items whose pixels reach a
+// native pixel (the footprint of a native pixel spans 2^(s+1) <= 16 full-resolution
+// rows / columns, less than an item), in a fixed order.  This replaces a full-resolution
+// dL/d(upsampled disp) plane per scale written here and gathered with a 2^(s+1) x
+// 2^(s+1) footprint per native pixel there (~170 MB of L2 traffic per step at B=12).
+__host__ __device__ __forceinline__ int up_nc(int upsh) { return (kBwdCols + (1 << upsh) - 1) / (1 << upsh) + 2; }
+__host__ __device__ __forceinline__ int up_nr(int upsh) { return (kRowsB + (1 << upsh) - 1) / (1 << upsh) + 2; }
+// weight of low-res index i in the upsample of full-res index y (factor 2^sh)
+__device__ __forceinline__ float up_weight(int y, int i, int n_in, float sc) {
+    const float sy = fmaxf(((float)y + 0.5f) * sc - 0.5f, 0.f);
+    const int y0 = min((int)sy, n_in - 1);
+    const int y1 = y0 + (y0 < n_in - 1 ? 1 : 0);
+    const float l1 = fminf(fmaxf(sy - (float)y0, 0.f), 1.f);
+    return (y0 == i ? 1.f - l1 : 0.f) + (y1 == i ? l1 : 0.f);
+}
+// lower source index of full-resolution index x (ATen area_pixel_compute_source_index,
+// align_corners=False, as disp_at / up_weight)
+__device__ __forceinline__ int up_src0(int x, int n_in, float sc) {
+    const float sx = fmaxf(((float)x + 0.5f) * sc - 0.5f, 0.f);
+    return min((int)sx, n_in - 1);
+}
+
 struct Coef {  // horizontally folded SSIM adjoint of one row, 3 channels
     float A[3], B[3], C[3];
     float g;     // per-pixel loss weight at this row (centre lane)
@@ -872,7 +921,7 @@ struct BwdFrame {
 template <int NS, bool SSIM_ON, bool MASK, bool U8>
 __device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, RowS& cur, const RowS& m1, const RowS& m2,
                                          Coef& cnew, const Coef& cm2, const Coef& cm3, float (&dP)[12],
-                                         float* dfull, float (*ddacc)[kWave], int lane) {
+                                         float (*ddacc)[kWave], int lane) {
     constexpr float kThird = 1.0f / 3.0f;
     const float l1w = SSIM_ON ? 0.15f : 1.0f;
     const int h = F.ctx.h, w = F.ctx.w, HW = h * w;
@@ -955,9 +1004,8 @@ __device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, RowS& cur, co
         dP[i * 4 + 3] += dc[i];
     }
     const float dd = (dc[0] * k2.u[0] + dc[1] * k2.u[1] + dc[2] * k2.u[2]) * k2.dd;
-    // frames accumulate in LDS; dfull is written once per item
-    if (NS == 1) dfull[q * w + F.c] = dd;
-    else if (F.f == 0) ddacc[q - F.r0][lane] = dd;
+    // frames accumulate in LDS; the item's result leaves once (bwd_item)
+    if (F.f == 0) ddacc[q - F.r0][lane] = dd;
     else ddacc[q - F.r0][lane] += dd;
 }
 
@@ -967,8 +1015,7 @@ __device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, RowS& cur, co
 // One source frame of a backward item: the row walk and its dL/dP partial.  U8:
 // this (frame, image)'s gathers read the 8-bit copy (wave-uniform choice).
 template <int NS, bool SSIM_ON, bool MASK, bool U8>
-__device__ __forceinline__ void bwd_frame_walk(const BwdFrame& F, float* dfull, float (*ddacc)[kWave], float* dst,
-                                            int lane) {
+__device__ __forceinline__ void bwd_frame_walk(const BwdFrame& F, float (*ddacc)[kWave], float* dst, int lane) {
     float dP[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) dP[j] = 0.f;
@@ -980,12 +1027,12 @@ __device__ __forceinline__ void bwd_frame_walk(const BwdFrame& F, float* dfull, 
     int k = 0;
 #pragma unroll 1
     for (; k + 3 <= kSteps; k += 3) {
-        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, dfull, ddacc, lane);
-        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, dfull, ddacc, lane);
-        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 2, S2, S1, S0, C1, C0, C2, dP, dfull, ddacc, lane);
+        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
+        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
+        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 2, S2, S1, S0, C1, C0, C2, dP, ddacc, lane);
     }
-    if (kSteps % 3 >= 1) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, dfull, ddacc, lane);
-    if (kSteps % 3 >= 2) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, dfull, ddacc, lane);
+    if (kSteps % 3 >= 1) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
+    if (kSteps % 3 >= 2) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
     // one 12-float partial of dL/dP per (item, frame)
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
@@ -1016,7 +1063,6 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
     const int gsc = a.gscale[ls];
     F.gscale = (a.grad_loss[gsc] + a.grad_loss[a.num_scales] / (float)a.num_scales) / ((float)a.B * (float)HW);
     F.sel = a.sel[ls] + (size_t)b * HW;
-    float* dfull = a.dfull[ls] + (size_t)b * HW;
     const int item_in_scale = b * a.wpi + rb * a.strips + st;
     F.pmask = MASK ? a.mask[ls] : nullptr;
     F.pgmask = MASK ? a.gmask[ls] : nullptr;
@@ -1032,13 +1078,67 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
         make_ctx(a, ls, f, b, F.ctx);
         float* dst = a.dP_part[ls] + ((size_t)f * a.B * a.wpi + item_in_scale) * 12;
         if (F.ctx.src8)
-            bwd_frame_walk<NS, SSIM_ON, MASK, true>(F, dfull, ddacc, dst, lane);
+            bwd_frame_walk<NS, SSIM_ON, MASK, true>(F, ddacc, dst, lane);
         else
-            bwd_frame_walk<NS, SSIM_ON, MASK, false>(F, dfull, ddacc, dst, lane);
+            bwd_frame_walk<NS, SSIM_ON, MASK, false>(F, ddacc, dst, lane);
     }
-    if (NS > 1 && F.colok) {
-        for (int i = 0; i < kRowsB && F.r0 + i < h; ++i) dfull[(F.r0 + i) * w + F.c] = ddacc[i][lane];
+    const int upsh = a.upsh[ls];
+#ifdef MD2_NO_FOLD   // timing experiments only: results are wrong
+    if (upsh != 0) return;
+#endif
+    if (upsh == 0) {   // no upsample: dL/d(disp) at this resolution, written once
+        float* dfull = a.dfull[ls] + (size_t)b * HW;
+        if (F.colok)
+            for (int i = 0; i < kRowsB && F.r0 + i < h; ++i) dfull[(F.r0 + i) * w + F.c] = ddacc[i][lane];
+        return;
     }
+    // fold into the native pixels: horizontal adjoint of the item's rows into R (LDS,
+    // the item's depth rows are no longer needed), then vertical into the partial grid
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int kf = 1 << upsh, half = kf >> 1;
+    const float sc = 1.0f / (float)kf;
+    const int dh = a.dh[ls], dw = a.dw[ls];
+    const int NC = up_nc(upsh), NR = up_nr(upsh);
+    const int X0 = st * kBwdCols, X1 = min(X0 + kBwdCols, w), Y0 = F.r0, Y1 = min(F.r0 + kRowsB, h);
+    const int jlo = up_src0(X0, dw, sc), ilo = up_src0(Y0, dh, sc);
+    float* R = &dep[0][0];   // [kRowsB][NC]
+    // lanes 0 .. G*NC-1 own native column jc = lane % NC and every G-th row; the column's
+    // taps (<= 2^(s+1) full-resolution columns of this item) and weights once per item
+    const int G = kWave / NC, gi = lane / NC, jc = lane - gi * NC, j = jlo + jc;
+    const bool jlive = gi < G && j < dw;
+    const int xa = max(X0, kf * (j - 1) + half), xb = jlive ? min(X1, kf * (j + 1) + half) : xa;
+    float wx[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) wx[t] = (xa + t < xb) ? up_weight(xa + t, j, dw, sc) : 0.f;
+    const int nt = xb - xa;
+    for (int yi = gi; yi < kRowsB; yi += G) {
+        if (!jlive) break;
+        float sum = 0.f;
+        if (Y0 + yi < Y1) {
+            const float* drow = &ddacc[yi][xa - X0 + 2];
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+                if (t < nt) sum += wx[t] * drow[t];
+        }
+        R[yi * NC + jc] = sum;
+    }
+    float* part = a.upart[ls] + (size_t)item_in_scale * NR * NC;
+    if (gi < G) {
+        for (int ic = gi; ic < NR; ic += G) {
+            const int i = ilo + ic;
+            float sum = 0.f;
+            if (i < dh) {
+                const int ya = max(Y0, kf * (i - 1) + half), yb = min(Y1, kf * (i + 1) + half);
+                for (int y = ya; y < yb; ++y) sum += up_weight(y, i, dh, sc) * R[(y - Y0) * NC + jc];
+            }
+            part[ic * NC + jc] = sum;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Resident waves walk the (image, row block, strip, scale) items; each XCD owns a
@@ -1078,6 +1178,7 @@ struct SmoothArgs {
     const float* disp[MD2_MAX_SCALES];
     const float* img[MD2_MAX_SCALES];   // target colour at the native scale
     float* part[MD2_MAX_SCALES];        // [B][chunks][3]
+    int disp_bf16;
 };
 
 __device__ __forceinline__ float edge_weight(const float* img, int HW, int o0, int o1) {
@@ -1111,16 +1212,17 @@ __global__ __launch_bounds__(kBlock) void smooth_fwd_kernel(SmoothArgs a) {
     const int local = blockIdx.x - a.block_base[s];
     const int b = local / a.chunks[s], chunk = local - b * a.chunks[s];
     const int hs = a.hs[s], ws = a.ws[s], HW = hs * ws;
-    const float* d = a.disp[s] + (size_t)b * HW;
+    const bool bf = a.disp_bf16 != 0;
+    const float* d = disp_off(a.disp[s], (size_t)b * HW, bf);
     const float* img = a.img[s] + (size_t)b * 3 * HW;
     float sd = 0.f, sx = 0.f, sy = 0.f;
     const int p0 = chunk * kSmoothChunk;
     for (int p = p0 + threadIdx.x; p < min(p0 + kSmoothChunk, HW); p += kBlock) {
         const int i = p / ws, j = p - i * ws;
-        const float v = d[p];
+        const float v = ldd(d, p, bf);
         sd += v;
-        if (j + 1 < ws) sx += fabsf(v - d[p + 1]) * edge_weight(img, HW, p, p + 1);
-        if (i + 1 < hs) sy += fabsf(v - d[p + ws]) * edge_weight(img, HW, p, p + ws);
+        if (j + 1 < ws) sx += fabsf(v - ldd(d, p + 1, bf)) * edge_weight(img, HW, p, p + 1);
+        if (i + 1 < hs) sy += fabsf(v - ldd(d, p + ws, bf)) * edge_weight(img, HW, p, p + ws);
     }
     block_sum3(sd, sx, sy);
     if (threadIdx.x == 0) {
@@ -1243,69 +1345,60 @@ struct DispGradArgs {
     int hs[MD2_MAX_SCALES], ws[MD2_MAX_SCALES];   // native resolution of each scale
     int lh[MD2_MAX_SCALES], lw[MD2_MAX_SCALES];   // loss resolution (= (hs<<upsh, ws<<upsh))
     int upsh[MD2_MAX_SCALES];
+    int strips[MD2_MAX_SCALES], rowblocks[MD2_MAX_SCALES];   // backward item grid per image
     int block_base[MD2_MAX_SCALES + 1];           // first block of each scale (one launch)
     int bpr[MD2_MAX_SCALES];                      // blocks per native row
-    const float* dfull[MD2_MAX_SCALES];           // (B, lh, lw) dL/d(upsampled disp)
+    const float* dfull[MD2_MAX_SCALES];           // upsh == 0: (B, lh, lw) dL/d(disp)
+    const float* upart[MD2_MAX_SCALES];           // upsh > 0: per-item partial grids (bwd_item)
     const float* disp[MD2_MAX_SCALES];            // (B, 1, hs, ws)
     const float* img[MD2_MAX_SCALES];             // (B, 3, hs, ws) target colour at this scale
     const float* stats;                           // [scale][B][4]
     const float* grad_loss;
     float smoothness;
-    float* out[MD2_MAX_SCALES];                   // (B, 1, hs, ws)
+    float* out[MD2_MAX_SCALES];                   // (B, 1, hs, ws), fp32 or bf16 as disp
+    int disp_bf16;
 };
 
-// threads per native pixel of a scale: one per row of its upsample footprint
-// (2^(upsh+1) full-resolution rows, capped at 16), so the coarse scales still fill
-// the chip; the row sums are combined by a fixed butterfly (deterministic)
-__host__ __device__ __forceinline__ int disp_grad_group(int upsh) { return upsh == 0 ? 1 : min(2 << upsh, 16); }
-
-// weight of low-res index i in the upsample of full-res index y (factor 2^sh)
-__device__ __forceinline__ float up_weight(int y, int i, int n_in, float sc) {
-    const float sy = fmaxf(((float)y + 0.5f) * sc - 0.5f, 0.f);
-    const int y0 = min((int)sy, n_in - 1);
-    const int y1 = y0 + (y0 < n_in - 1 ? 1 : 0);
-    const float l1 = fminf(fmaxf(sy - (float)y0, 0.f), 1.f);
-    return (y0 == i ? 1.f - l1 : 0.f) + (y1 == i ? l1 : 0.f);
-}
-
-// Blocks own whole native rows: block_base[s] + (b·hs + i)·bpr[s] + chunk, threads over
-// (column j, footprint slot g) of the row — the (scale, image, row) decode is uniform
-// (scalar) per block and j / g are shifts, so no per-thread integer division.
+// One thread per native pixel; blocks own whole native rows: block_base[s] +
+// (b·hs + i)·bpr[s] + chunk (the (scale, image, row) decode is uniform per block).
+// Upsampled scales: the sum of the <= 2 x 2 backward items' partials that reach this
+// pixel (row blocks, then strips, ascending: fixed order); plus the smoothness gradient.
 __global__ __launch_bounds__(kBlock) void disp_grad_kernel(DispGradArgs a) {
     int s = 0;
     while (s + 1 < a.num_scales && (int)blockIdx.x >= a.block_base[s + 1]) ++s;
     const int sh = a.upsh[s];
-    const int tsh = sh == 0 ? 0 : min(sh + 1, 4), T = 1 << tsh;   // = disp_grad_group(sh)
     const int hs = a.hs[s], ws = a.ws[s], lh = a.lh[s], lw = a.lw[s], HWs = hs * ws;
     const int rb = (int)blockIdx.x - a.block_base[s], bpr = a.bpr[s];
     const int row = rb / bpr, chunk = rb - row * bpr;
     const int b = row / hs, i = row - b * hs;
-    const int t = chunk * kBlock + threadIdx.x;
-    const int jj = t >> tsh, g = t & (T - 1);
-    const bool live = jj < ws;
-    const int j = live ? jj : ws - 1;
+    const int j = chunk * kBlock + threadIdx.x;
+    if (j >= ws) return;
     const int p = i * ws + j;
-    const float* df = a.dfull[s] + (size_t)b * lh * lw;
     float acc = 0.f;
-    if (a.upsh[s] == 0) {
-        if (live) acc = df[i * lw + j];
+    if (sh == 0) {
+        acc = a.dfull[s][(size_t)b * lh * lw + i * lw + j];
     } else {
-        const int k = 1 << a.upsh[s], half = k >> 1;
-        const float sc = 1.0f / (float)k;
-        const int ylo = max(0, k * (i - 1) + half), yhi = min(lh, k * (i + 1) + half);
-        const int xlo = max(0, k * (j - 1) + half), xhi = min(lw, k * (j + 1) + half);
-        if (live) {
-            for (int y = ylo + g; y < yhi; y += T) {
-                const float wy = up_weight(y, i, hs, sc);
-                if (wy == 0.f) continue;
-                float row_sum = 0.f;
-                for (int x = xlo; x < xhi; ++x) row_sum += up_weight(x, j, ws, sc) * df[y * lw + x];
-                acc += wy * row_sum;
+        const int kf = 1 << sh, half = kf >> 1;
+        const float sc = 1.0f / (float)kf;
+        const int NC = up_nc(sh), NR = up_nr(sh);
+        const int strips = a.strips[s], rowblocks = a.rowblocks[s];
+        // the full-resolution footprint of (i, j) (a superset of the weight-carrying rows /
+        // columns) and the items holding it
+        const int yf0 = max(0, kf * (i - 1) + half), yf1 = min(lh, kf * (i + 1) + half);
+        const int xf0 = max(0, kf * (j - 1) + half), xf1 = min(lw, kf * (j + 1) + half);
+        const int rb0 = yf0 / kRowsB, rb1 = (yf1 - 1) / kRowsB;
+        const int st0 = xf0 / kBwdCols, st1 = (xf1 - 1) / kBwdCols;
+        const float* base = a.upart[s] + (size_t)b * rowblocks * strips * NR * NC;
+        for (int r = rb0; r <= rb1; ++r) {
+            const int ic = i - up_src0(r * kRowsB, hs, sc);
+            if (ic < 0 || ic >= NR) continue;
+            for (int t = st0; t <= st1; ++t) {
+                const int jc = j - up_src0(t * kBwdCols, ws, sc);
+                if (jc < 0 || jc >= NC) continue;
+                acc += base[((size_t)r * strips + t) * NR * NC + ic * NC + jc];
             }
         }
-        for (int o = 1; o < T; o <<= 1) acc += __shfl_xor(acc, o, kWave);   // T divides 64
     }
-    if (!live || g != 0) return;
     // smoothness gradient on disp / (mean + 1e-7)
     const float gl = a.grad_loss[s] + a.grad_loss[a.num_scales] / (float)a.num_scales;
     const float* st = a.stats + ((size_t)s * a.B + b) * 4;
@@ -1313,16 +1406,20 @@ __global__ __launch_bounds__(kBlock) void disp_grad_kernel(DispGradArgs a) {
     const float wsm = gl * a.smoothness / (float)(1 << s);
     const float ax = wsm / ((float)a.B * hs * (ws - 1)) / m;
     const float ay = wsm / ((float)a.B * (hs - 1) * ws) / m;
-    const float* d = a.disp[s] + (size_t)b * HWs;
+    const bool bf = a.disp_bf16 != 0;
+    const float* d = disp_off(a.disp[s], (size_t)b * HWs, bf);
     const float* img = a.img[s] + (size_t)b * 3 * HWs;
-    const float v = d[p];
+    const float v = ldd(d, p, bf);
     float sg = 0.f;
-    if (j + 1 < ws) sg += ax * signf(v - d[p + 1]) * edge_weight(img, HWs, p, p + 1);
-    if (j > 0) sg -= ax * signf(d[p - 1] - v) * edge_weight(img, HWs, p - 1, p);
-    if (i + 1 < hs) sg += ay * signf(v - d[p + ws]) * edge_weight(img, HWs, p, p + ws);
-    if (i > 0) sg -= ay * signf(d[p - ws] - v) * edge_weight(img, HWs, p - ws, p);
+    if (j + 1 < ws) sg += ax * signf(v - ldd(d, p + 1, bf)) * edge_weight(img, HWs, p, p + 1);
+    if (j > 0) sg -= ax * signf(ldd(d, p - 1, bf) - v) * edge_weight(img, HWs, p - 1, p);
+    if (i + 1 < hs) sg += ay * signf(v - ldd(d, p + ws, bf)) * edge_weight(img, HWs, p, p + ws);
+    if (i > 0) sg -= ay * signf(ldd(d, p - ws, bf) - v) * edge_weight(img, HWs, p - ws, p);
     sg -= (ax * st[1] + ay * st[2]) / (m * (float)HWs);
-    a.out[s][(size_t)b * HWs + p] = acc + sg;
+    // the gradient in the disparity's own dtype (bf16: round to nearest even, as the
+    // cast-up's autograd backward would)
+    if (bf) ((uint16_t*)a.out[s])[(size_t)b * HWs + p] = (uint16_t)md2::f2bf(acc + sg);
+    else a.out[s][(size_t)b * HWs + p] = acc + sg;
 }
 
 // ----------------------------------------------------------------------------
@@ -1511,6 +1608,8 @@ int make_layout(const md2_desc* d, Layout& L) {
         return fail(MD2_ERR_ARG, "coarsest scale must be at least 4x4");
     if (!(d->min_depth > 0.f) || !(d->max_depth > d->min_depth))
         return fail(MD2_ERR_ARG, "need 0 < min_depth < max_depth");
+    if (d->disp_dtype != MD2_DTYPE_F32 && d->disp_dtype != MD2_DTYPE_BF16)
+        return fail(MD2_ERR_ARG, "disp_dtype must be MD2_DTYPE_F32 or MD2_DTYPE_BF16 (got %u)", d->disp_dtype);
     L.nscales = d->num_scales;
     L.S = d->num_src;
     L.B = d->batch;
@@ -1535,8 +1634,10 @@ int make_layout(const md2_desc* d, Layout& L) {
         off = align256(off + sizeof(float) * (size_t)L.S * L.B * L.bwpi[s] * 12);
         L.smooth_off[s] = off;
         off = align256(off + sizeof(float) * (size_t)L.B * L.chunks[s] * 3);
-        L.dfull_off[s] = off;
-        off = align256(off + sizeof(float) * (size_t)L.B * L.lh[s] * L.lw[s]);
+        L.dfull_off[s] = off;   // upsampled scales: the backward items' partial grids instead
+        const int upsh = L.v1 ? 0 : s;
+        off = align256(off + sizeof(float) * (upsh == 0 ? (size_t)L.B * L.lh[s] * L.lw[s]
+                                                         : (size_t)L.B * L.bwpi[s] * up_nr(upsh) * up_nc(upsh)));
         L.sel_off[s] = soff;
         soff += (size_t)L.B * L.lh[s] * L.lw[s];
         L.noise_off[s] = noff;
@@ -1603,6 +1704,7 @@ void photo_args(const md2_desc* d, const md2_tensors* t, const Layout& L, int s_
     a.iK = t->inv_K[cs];
     a.seed = d->seed;
     a.seed_ptr = t->seed_ptr;
+    a.disp_bf16 = d->disp_dtype == MD2_DTYPE_BF16;
     a.min_disp = 1.0f / d->max_depth;
     a.range = 1.0f / d->min_depth - 1.0f / d->max_depth;
     a.flags = d->flags;
@@ -1619,6 +1721,7 @@ void photo_args(const md2_desc* d, const md2_tensors* t, const Layout& L, int s_
         a.photo_part[ls] = (float*)(ws + L.photo_off[s]);
         a.sel[ls] = sel ? sel + L.sel_off[s] : nullptr;
         a.dfull[ls] = (float*)(ws + L.dfull_off[s]);
+        a.upart[ls] = (float*)(ws + L.dfull_off[s]);
         a.dP_part[ls] = (float*)(ws + L.dP_off[s]);
         a.mask[ls] = t->mask ? t->mask + L.mask_off[s] : nullptr;
         a.gmask[ls] = grad_mask ? grad_mask + L.mask_off[s] : nullptr;
@@ -1780,6 +1883,7 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
         sa.part[s] = (float*)(ws + L.smooth_off[s]);
     }
     sa.block_base[L.nscales] = blocks;
+    sa.disp_bf16 = d->disp_dtype == MD2_DTYPE_BF16;
     hipLaunchKernelGGL(smooth_fwd_kernel, dim3(blocks), dim3(kBlock), 0, st, sa);
     if ((rc = hip_check("smooth_fwd_kernel"))) return rc;
 
@@ -1847,6 +1951,7 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
     g.stats = (const float*)(ws + L.stats_off);
     g.grad_loss = grad_loss;
     g.smoothness = d->disparity_smoothness;
+    g.disp_bf16 = d->disp_dtype == MD2_DTYPE_BF16;
     int gblocks = 0;
     for (int s = 0; s < L.nscales; ++s) {   // all scales in one launch
         g.hs[s] = L.hs[s];
@@ -1855,11 +1960,14 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
         g.lw[s] = L.lw[s];
         g.upsh[s] = L.v1 ? 0 : s;
         g.dfull[s] = (const float*)(ws + L.dfull_off[s]);
+        g.upart[s] = (const float*)(ws + L.dfull_off[s]);
+        g.strips[s] = L.bstrips[s];
+        g.rowblocks[s] = L.brows[s];
         g.disp[s] = t->disp[s];
         g.img[s] = t->color[s][0];
         g.out[s] = grad_disp[s];
         g.block_base[s] = gblocks;
-        g.bpr[s] = (L.ws[s] * disp_grad_group(g.upsh[s]) + kBlock - 1) / kBlock;
+        g.bpr[s] = (L.ws[s] + kBlock - 1) / kBlock;
         gblocks += L.B * L.hs[s] * g.bpr[s];
     }
     g.block_base[L.nscales] = gblocks;

@@ -53,30 +53,60 @@ def ignored_parameters(module: nn.Module):
             or n.endswith("encoder.fc.bias")]
 
 
-def _stream_synced_allreduce(state, bucket):
-    """DDP comm hook for a backward that runs on several HIP streams (the trainer's
-    pose network has its own): a bucket's gradients may be written by any of them,
-    and DDP's reducer only orders the all-reduce after the stream that completes the
-    bucket.  Wait for every stream first, then the default mean all-reduce."""
+class GradReadyEvents:
+    """Per-parameter "gradient final" events for a backward that runs on several HIP
+    streams (the trainer's pose network has its own).  A post-accumulate-grad hook
+    records an event on the stream that produced the gradient (the current stream
+    inside the hook is the autograd node's), so a consumer can wait for exactly the
+    gradients it reads instead of for everything queued on every stream."""
+
+    def __init__(self, params):
+        self.events = {}
+        self.handles = []
+        for p in params:
+            if p.requires_grad:
+                self.handles.append(p.register_post_accumulate_grad_hook(self._ready))
+
+    def _ready(self, p):
+        if p.is_cuda:
+            ev = self.events.get(p)
+            if ev is None:
+                ev = self.events[p] = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(p.device))
+
+    def wait(self, params, stream):
+        for p in params:
+            ev = self.events.get(p)
+            if ev is not None:
+                stream.wait_event(ev)
+
+
+def _event_synced_allreduce(state, bucket):
+    """DDP comm hook: the bucket's all-reduce waits for the ready events of ITS
+    parameters' gradients (GradReadyEvents), not for whole streams, so the depth
+    network's buckets go out while the pose stream is still busy."""
     from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
-    cur = torch.cuda.current_stream()
-    for s in state["streams"]:
-        if s.cuda_stream != cur.cuda_stream:
-            cur.wait_stream(s)
+    state["events"].wait(bucket.parameters(), torch.cuda.current_stream())
     return default_hooks.allreduce_hook(state["group"], bucket)
 
 
 def wrap_ddp(module: nn.Module, device: torch.device, streams=None):
     """DDP over the networks.  `streams`: every HIP stream the backward writes
-    gradients on (more than one -> the synchronising comm hook above)."""
+    gradients on (more than one -> the per-bucket event comm hook above)."""
     from torch.nn.parallel import DistributedDataParallel as DDP
     DDP._set_params_and_buffers_to_ignore_for_model(module, ignored_parameters(module))
+    events = None
+    if streams and len(streams) > 1:
+        # registered BEFORE DDP's own autograd hooks, so a parameter's event is recorded
+        # before DDP can find its bucket ready and call the comm hook
+        events = GradReadyEvents(module.parameters())
     kw = dict(broadcast_buffers=False, bucket_cap_mb=BUCKET_CAP_MB, gradient_as_bucket_view=True)
     if device.type == "cuda":
         kw.update(device_ids=[device.index], output_device=device.index)
     ddp = DDP(module, **kw)
-    if streams and len(streams) > 1:
-        ddp.register_comm_hook({"group": None, "streams": list(streams)}, _stream_synced_allreduce)
+    if events is not None:
+        ddp.register_comm_hook({"group": None, "events": events}, _event_synced_allreduce)
+        ddp._md2_grad_events = events
     return ddp
 
 
@@ -93,20 +123,32 @@ def shard(batch: Dict, rank: int, world: int) -> Dict:
 
 
 class FlatGradSync:
-    """Gradient averaging over flat buckets, graph-capturable.
+    """Gradient averaging over flat buckets, graph-capturable, overlapped with the
+    backward.
 
-    Every trainable parameter's `.grad` is a view into one of a few flat fp32
-    buckets (BUCKET_CAP_MB each).  After the backward pass `sync()` issues one
-    all-reduce (ReduceOp.AVG on RCCL) per bucket; `zero()` clears the buckets
-    with one memset each.  Unlike DDP's autograd hooks this is plain stream
-    work, so it can sit inside a captured hipGraph of the whole training step.
+    Parameters are bucketed in reverse registration order (the order the backward
+    finishes them, as DDP).  `zero()` drops the gradients (autograd then hands each
+    producer's output over instead of adding it into a zeroed buffer); a post-
+    accumulate-grad hook per parameter notes the gradient and the stream it was
+    produced on, and when a bucket's last gradient is final the bucket goes out at
+    once: the communication stream waits for the producing streams, copies the
+    gradients into the flat buffer (one multi-tensor copy), and all-reduces it
+    (ReduceOp.AVG on RCCL) — while the backward of the earlier layers continues.
+    `sync()` sends any bucket still pending (parameters that got no gradient this step
+    count as zero), makes the current stream wait for the communication stream, and
+    points every `.grad` at its averaged view.  All of it is stream work ordered by
+    events, so it can sit inside a captured hipGraph of the whole training step.
     Parameters that never get a gradient (the encoders' fc heads) are left out.
-    """
+    `overlap=False`: the round-2 form (views of pre-zeroed buckets, one all-reduce per
+    bucket after the backward), kept for comparison."""
 
-    def __init__(self, named_params, world: int, group=None, bucket_cap_mb: int = BUCKET_CAP_MB):
-        self.world, self.group = world, group
+    def __init__(self, named_params, world: int, group=None, bucket_cap_mb: int = BUCKET_CAP_MB,
+                 overlap: bool = True):
+        self.world, self.group, self.overlap = world, group, overlap
         params = [(n, p) for n, p in named_params if p.requires_grad and not (
             n.endswith("encoder.fc.weight") or n.endswith("encoder.fc.bias"))]
+        if overlap:
+            params = params[::-1]
         cap = bucket_cap_mb * (1 << 20) // 4
         self.buckets = []
         cur, size = [], 0
@@ -118,23 +160,95 @@ class FlatGradSync:
             size += p.numel()
         if cur:
             self.buckets.append(cur)
-        self.flat = []
-        for plist in self.buckets:
+        self.flat, self.views = [], []
+        self.where = {}
+        for bi, plist in enumerate(self.buckets):
             buf = torch.zeros(sum(p.numel() for p in plist), dtype=torch.float32, device=plist[0].device)
-            off = 0
+            views, off = [], 0
             for p in plist:
-                # the grad view keeps the parameter's strides (channels_last conv weights):
-                # the gradient layout contract of autograd and the fused Adam kernel
-                p.grad = buf[off:off + p.numel()].as_strided(p.size(), p.stride())
+                # the view keeps the parameter's strides (channels_last conv weights): the
+                # gradient layout contract of autograd and the fused Adam kernel
+                views.append(buf[off:off + p.numel()].as_strided(p.size(), p.stride()))
+                self.where[p] = (bi, len(views) - 1)
                 off += p.numel()
             self.flat.append(buf)
+            self.views.append(views)
+        if not overlap:
+            for plist, views in zip(self.buckets, self.views):
+                for p, v in zip(plist, views):
+                    p.grad = v
+            return
+        cuda = self.flat and self.flat[0].is_cuda
+        self.comm = torch.cuda.Stream(self.flat[0].device) if cuda else None
+        self.pending = [dict() for _ in self.buckets]   # bucket -> {param: (grad, stream)}
+        self.sent = [False] * len(self.buckets)
+        self.handles = [p.register_post_accumulate_grad_hook(self._ready) for plist in self.buckets for p in plist]
+        self.works = []
 
     def zero(self):
-        for buf in self.flat:
-            buf.zero_()
+        if not self.overlap:
+            for buf in self.flat:
+                buf.zero_()
+            return
+        for plist in self.buckets:
+            for p in plist:
+                p.grad = None
+        self.pending = [dict() for _ in self.buckets]
+        self.sent = [False] * len(self.buckets)
+        self.works = []
+
+    def _ready(self, p):
+        bi, _ = self.where[p]
+        if self.sent[bi]:
+            return
+        stream = torch.cuda.current_stream(p.device) if p.is_cuda else None
+        self.pending[bi][p] = (p.grad, stream)
+        if len(self.pending[bi]) == len(self.buckets[bi]):
+            self._send(bi)
+
+    def _send(self, bi):
+        self.sent[bi] = True
+        got = self.pending[bi]
+        views = [v for p, v in zip(self.buckets[bi], self.views[bi]) if p in got]
+        grads = [got[p][0] for p in self.buckets[bi] if p in got]
+        missing = [v for p, v in zip(self.buckets[bi], self.views[bi]) if p not in got]
+        buf = self.flat[bi]
+        if self.comm is not None:
+            for stream in {s for _, s in got.values() if s is not None}:
+                self.comm.wait_stream(stream)
+            with torch.cuda.stream(self.comm):
+                self._fill(views, grads, missing)
+                for g in grads:   # the producers' buffers stay alive until the copy ran
+                    g.record_stream(self.comm)
+                if self.world > 1:
+                    dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.group)
+        else:
+            self._fill(views, grads, missing)
+            if self.world > 1:
+                self.works.append(dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
+
+    @staticmethod
+    def _fill(views, grads, missing):
+        if views:
+            torch._foreach_copy_(views, grads)
+        for v in missing:   # no gradient this step: it counts as zero, like a zeroed bucket
+            v.zero_()
 
     def sync(self):
-        if self.world <= 1:
+        if not self.overlap:
+            if self.world <= 1:
+                return
+            for buf in self.flat:
+                dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.group)
             return
-        for buf in self.flat:
-            dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.group)
+        for bi in range(len(self.buckets)):
+            if not self.sent[bi]:
+                self._send(bi)
+        if self.comm is not None:
+            torch.cuda.current_stream(self.flat[0].device).wait_stream(self.comm)
+        for w in self.works:   # CPU (gloo): the asynchronous all-reduces
+            w.wait()
+        for plist, views in zip(self.buckets, self.views):
+            for p, v in zip(plist, views):
+                p.grad = v
+

@@ -54,9 +54,10 @@ class HotPathConfig:
         f |= _lib.PREDICTIVE_MASK if self.predictive_mask else 0
         return f
 
-    def desc(self, seed: int = 0) -> _lib.Desc:
+    def desc(self, seed: int = 0, disp_dtype: torch.dtype = torch.float32) -> _lib.Desc:
+        dt = _lib.DTYPE_BF16 if disp_dtype == torch.bfloat16 else _lib.DTYPE_F32
         return _lib.Desc(self.batch, self.height, self.width, self.num_src, self.num_scales, self.flags,
-                         self.min_depth, self.max_depth, self.disparity_smoothness, 0, seed & (2 ** 64 - 1))
+                         self.min_depth, self.max_depth, self.disparity_smoothness, dt, seed & (2 ** 64 - 1))
 
     def loss_res(self, s: int):
         if self.v1_multiscale:
@@ -75,13 +76,13 @@ def _stream_ptr(device: torch.device) -> int:
     return _lib.stream(device)
 
 
-def _require(t: torch.Tensor, name: str, shape, device):
+def _require(t: torch.Tensor, name: str, shape, device, dtypes=(torch.float32,)):
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name} must be a tensor")
     if t.device != device:
         raise ValueError(f"{name} is on {t.device}, expected {device}")
-    if t.dtype != torch.float32:
-        raise ValueError(f"{name} must be float32 (got {t.dtype})")
+    if t.dtype not in dtypes:
+        raise ValueError(f"{name} must be {' or '.join(str(d) for d in dtypes)} (got {t.dtype})")
     if tuple(t.shape) != tuple(shape):
         raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
 
@@ -154,7 +155,7 @@ class _PhotometricLoss(torch.autograd.Function):
     def forward(ctx, cfg: HotPathConfig, ops: Operands, seed: int, T: torch.Tensor, mask, *disps: torch.Tensor):
         L = _lib.lib()
         dev = T.device
-        desc = cfg.desc(seed)
+        desc = cfg.desc(seed, disps[0].dtype)
         st = ops.struct(disps, T, mask)
         ws = torch.empty(L.md2_workspace_bytes(ctypes.byref(desc)), dtype=torch.uint8, device=dev)
         sel = torch.empty(L.md2_select_bytes(ctypes.byref(desc)), dtype=torch.uint8, device=dev)
@@ -178,9 +179,9 @@ class _PhotometricLoss(torch.autograd.Function):
         if grad_loss is None:
             grad_loss = torch.zeros(cfg.num_scales + 1, dtype=torch.float32, device=dev)
         grad_loss = grad_loss.contiguous().float()
-        desc = cfg.desc(ctx.seed)
+        desc = cfg.desc(ctx.seed, disps[0].dtype)
         st = ctx.ops.struct(disps, T, mask)
-        gdisp = [torch.empty_like(d) for d in disps]
+        gdisp = [torch.empty_like(d) for d in disps]   # the disparities' dtype (bf16 written by the kernel)
         gT = torch.empty_like(T)
         gmask = torch.empty_like(mask) if mask is not None else None
         arr = (ctypes.c_void_p * _lib.MAX_SCALES)(*([g.data_ptr() for g in gdisp]
@@ -216,7 +217,11 @@ def photometric_loss(cfg: HotPathConfig, disps: Sequence[torch.Tensor], colors, 
         raise ValueError(f"expected {cfg.num_scales} disparity maps, got {len(disps)}")
     disps = [d.contiguous() for d in disps]
     for s, d in enumerate(disps):
-        _require(d, f"disp[{s}]", (B, 1, H >> s, W >> s), dev)
+        # fp32, or bf16 as the decoder emits them under bf16 autocast (read as is,
+        # md2_desc.disp_dtype); every scale in the same dtype
+        _require(d, f"disp[{s}]", (B, 1, H >> s, W >> s), dev, (torch.float32, torch.bfloat16))
+        if d.dtype != disps[0].dtype:
+            raise ValueError(f"disp[{s}] is {d.dtype}, disp[0] {disps[0].dtype}: one dtype for every scale")
     tshape = (cfg.num_scales, S, B, 4, 4) if cfg.t_per_scale else (S, B, 4, 4)
     _require(T, "T", tshape, dev)
     ops = Operands(cfg, colors, K, inv_K, noise, dev, seed_tensor)
@@ -271,7 +276,7 @@ def generate_images(cfg: HotPathConfig, disps, colors, K, inv_K, T, want_depth=T
     disps = [d.contiguous() for d in disps]
     ops = Operands(cfg, colors, K, inv_K, None, dev)
     st = ops.struct(disps, T.contiguous())
-    desc = cfg.desc()
+    desc = cfg.desc(0, disps[0].dtype)
     S = cfg.num_src
     depth, sample, color = {}, {}, {}
     dptr = (ctypes.c_void_p * _lib.MAX_SCALES)()

@@ -49,10 +49,14 @@ def _sec_to_hm_str(t):
     return "{:02d}h{:02d}m{:02d}s".format(t, m, s)
 
 
-def _to_fp32(outputs):
-    """Network outputs (nested dicts of tensors) as fp32 (--amp bf16)."""
+def _to_fp32(outputs, keep_disp: bool = True):
+    """Network outputs (nested dicts of tensors) as fp32 (--amp bf16).  The depth
+    decoder's disparities stay as they are: the fused hot path reads bf16 disparities
+    directly (md2_desc.disp_dtype) and returns their gradients in bf16, which is what
+    a cast up and its backward would give, without the two extra passes."""
     if isinstance(outputs, dict):
-        return {k: _to_fp32(v) for k, v in outputs.items()}
+        return {k: (v if (keep_disp and isinstance(k, tuple) and len(k) == 2 and k[0] == "disp")
+                    else _to_fp32(v, keep_disp=False)) for k, v in outputs.items()}
     if torch.is_tensor(outputs) and outputs.is_floating_point() and outputs.dtype != torch.float32:
         return outputs.float()
     return outputs
@@ -363,7 +367,7 @@ class Trainer:
             return torch.stack(Ts, 0)
         per_scale = []
         for s in range(self.num_scales):
-            disp = outputs[("disp", s)]
+            disp = outputs[("disp", s)].float()
             if not self.opt.v1_multiscale:
                 disp = F.interpolate(disp, [self.opt.height, self.opt.width], mode="bilinear", align_corners=False)
             scaled, _ = disp_to_depth(disp, self.opt.min_depth, self.opt.max_depth)

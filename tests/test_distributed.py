@@ -89,11 +89,14 @@ def _worker(rank, world, port, mode, out_dir):
         loss = loss_fn(model, inputs)
         loss.backward()
     else:
-        sync = FlatGradSync(nets.named_parameters(), world)
-        sync.zero()
-        loss = loss_fn(nets, inputs)
-        loss.backward()
-        sync.sync()
+        # "flat": buckets sent from the backward's hooks as they complete (overlapped);
+        # "flat_post": the round-2 form (zeroed buckets, all-reduce after the backward)
+        sync = FlatGradSync(nets.named_parameters(), world, overlap=(mode == "flat"))
+        for _ in range(2):   # a second step re-arms the hooks and buckets
+            sync.zero()
+            loss = loss_fn(nets, inputs)
+            loss.backward()
+            sync.sync()
     grads = {n: (p.grad.clone() if p.grad is not None else None) for n, p in nets.named_parameters()}
     torch.save(grads, os.path.join(out_dir, f"{mode}_{rank}.pt"))
     dist.barrier()
@@ -118,7 +121,7 @@ def ref_grads():
     return _reference_grads()
 
 
-@pytest.mark.parametrize("mode", ["ddp", "flat"])
+@pytest.mark.parametrize("mode", ["ddp", "flat", "flat_post"])
 def test_gradient_average_matches_single_process(mode, ref_grads, tmp_path):
     port = _free_port()
     mp.spawn(_worker, args=(2, port, mode, str(tmp_path)), nprocs=2, join=True)
@@ -144,3 +147,20 @@ def test_shard_slices_batched_tensors():
     assert torch.equal(s1[("color", 0, 0)], batch[("color", 0, 0)][B_PER_RANK:])
     assert torch.equal(s1[("K", 2)], batch[("K", 2)][B_PER_RANK:])
     assert s1[("color", -1, 3)].shape[0] == B_PER_RANK
+
+
+def test_overlapped_buckets_equal_post_backward_sync(tmp_path):
+    """The overlapped FlatGradSync (buckets all-reduced from the backward's hooks)
+    gives bit for bit the gradients of the post-backward sync."""
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, "flat", str(tmp_path)), nprocs=2, join=True)
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, "flat_post", str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        a = torch.load(os.path.join(tmp_path, f"flat_{r}.pt"), weights_only=True)
+        b = torch.load(os.path.join(tmp_path, f"flat_post_{r}.pt"), weights_only=True)
+        for n in a:
+            if a[n] is None or b[n] is None:
+                assert (a[n] is None or float(a[n].abs().sum()) == 0) and (b[n] is None or float(b[n].abs().sum()) == 0)
+                continue
+            assert torch.equal(a[n], b[n]), n

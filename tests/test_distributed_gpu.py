@@ -22,6 +22,47 @@ def _free_port():
     return p
 
 
+def _rank_flat(rank, world, port):
+    """FlatGradSync with the buckets sent from the backward's hooks on a communication
+    stream (the graph-mode sync, run eagerly: gloo is not capturable): every rank's
+    synced gradients equal the mean of the ranks' local gradients."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from monodepth2_amd.data import synthetic_batch
+        from monodepth2_amd.options import default_options
+        from monodepth2_amd.trainer import Trainer
+        dev = torch.device("cuda", 0)
+        torch.manual_seed(0)
+        tr = Trainer(default_options(batch_size=2, height=64, width=128, weights_init="scratch", grad_sync="flat",
+                                     log_dir="/tmp/md2_ddp_gpu"), device=dev, rank=rank, world_size=world)
+        assert tr.ddp is None and tr.flat_sync is not None and tr.flat_sync.overlap
+        tr.set_train()
+        batch = synthetic_batch(2, 64, 128, tr.opt.frame_ids, 4, seed=10 + rank, device=dev)
+        named = [(n, p) for n, p in tr.nets.named_parameters() if p.requires_grad and "fc." not in n]
+        tr.flat_sync.zero()
+        _, losses = tr.process_batch(batch)
+        local = torch.autograd.grad(losses["loss"], [p for _, p in named], allow_unused=True)
+        tr.flat_sync.zero()
+        _, losses = tr.process_batch(batch)
+        losses["loss"].backward()
+        tr.flat_sync.sync()
+        torch.cuda.synchronize()
+        checked = 0
+        for (n, p), lg in zip(named, local):
+            if lg is None:
+                continue
+            mean = lg.clone()
+            dist.all_reduce(mean)
+            mean /= world
+            err = float((p.grad - mean).norm() / (mean.norm() + 1e-12))
+            assert err < 1e-5, (n, err)
+            checked += 1
+        assert checked > 100
+    finally:
+        dist.destroy_process_group()
+
+
 def _rank(rank, world, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -70,3 +111,7 @@ def _rank(rank, world, port):
 
 def test_ddp_with_pose_stream_averages_gradients():
     mp.spawn(_rank, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def test_flat_overlapped_sync_averages_gradients():
+    mp.spawn(_rank_flat, args=(2, _free_port()), nprocs=2, join=True)

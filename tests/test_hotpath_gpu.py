@@ -279,3 +279,43 @@ def test_eight_bit_sources_match_oracle(name):
         flips = int(((out["select"][s] > C - 1)
                      != (ref_free["outputs"][f"identity_selection/{s}"].cpu().numpy() > 0.5)).sum())
         assert flips <= max(2, 1e-4 * out["select"][s].size), (s, flips)
+
+
+@pytest.mark.parametrize("name", ["mono_b2_64x128", "stereo_b2_64x128"])
+def test_bf16_disparities_read_directly(name):
+    """md2_desc.disp_dtype = bf16 (the depth decoder's output under bf16 autocast, C5):
+    the kernels read the bf16 disparities as is.  bf16 -> fp32 is exact, so the losses
+    and the selection equal those of the same values cast up to fp32, bit for bit, and
+    the gradients the kernel writes in bf16 are the fp32 path's rounded to nearest even
+    (what the cast-up's autograd backward returns)."""
+    from monodepth2_amd.hotpath import photometric_loss
+    from hotpath_case import case_config, case_operands
+    from monodepth2_amd.layers import transformation_from_parameters
+    case = Case(name)
+    cfg = case_config(case)
+    colors, K, inv_K, noise = case_operands(case, "cuda")
+    base = [case.disps[s].cuda().to(torch.bfloat16) for s in range(4)]
+    Ts = []
+    ti = 0
+    for f in case.frame_ids[1:]:
+        if f == "s":
+            Ts.append(case.inputs["stereo_T"].cuda())
+        else:
+            Ts.append(transformation_from_parameters(case.axisangle[ti].cuda(), case.translation[ti].cuda(),
+                                                     invert=(f < 0)))
+            ti += 1
+    T = torch.stack(Ts).detach()
+    out = {}
+    for dt in (torch.bfloat16, torch.float32):
+        d = [b.detach().to(dt).clone().requires_grad_(True) for b in base]
+        Tg = T.clone().requires_grad_(True)
+        loss, sel = photometric_loss(cfg, d, colors, K, inv_K, Tg, noise=noise)
+        loss[4].backward()
+        out[dt] = (loss.detach().cpu(), sel.cpu(), [x.grad for x in d], Tg.grad.cpu())
+    lb, sb, gb, tb = out[torch.bfloat16]
+    lf, sf, gf, tf = out[torch.float32]
+    assert torch.equal(lb, lf) and torch.equal(sb, sf)
+    for s in range(4):
+        assert gb[s].dtype == torch.bfloat16
+        assert torch.equal(gb[s], gf[s].to(torch.bfloat16)), s
+    assert torch.equal(tb, tf)

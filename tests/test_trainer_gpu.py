@@ -75,7 +75,7 @@ def test_losses_match_oracle_on_same_outputs(name):
                          no_ssim=o.no_ssim, avg_reprojection=o.avg_reprojection,
                          disable_automasking=o.disable_automasking, predictive_mask=o.predictive_mask)
     cpu = {k: v.cpu() for k, v in batch.items()}
-    disps = {s: outputs[("disp", s)].cpu() for s in range(4)}
+    disps = {s: outputs[("disp", s)].float().cpu() for s in range(4)}
     masks = {s: outputs["predictive_mask"][("disp", s)].cpu() for s in range(4)} if o.predictive_mask else None
     if o.pose_model_type == "posecnn":
         T = tr._stacked_T(batch, outputs).cpu()
