@@ -112,6 +112,7 @@ CONV_TILE_N128 = 1 << 4
 CONV_X6 = 1 << 5
 CONV_BM256 = 1 << 6
 CONV_PRESPLIT = 1 << 7
+CONV_PATCH = 1 << 8
 
 
 class ConvDesc(ctypes.Structure):

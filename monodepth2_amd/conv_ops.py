@@ -46,7 +46,19 @@ _times: Dict[tuple, dict] = {}     # (op, shape) -> {candidate: timed ms} (tools
 X6 = _lib.CONV_X6
 BM256 = _lib.CONV_BM256
 PRESPLIT = _lib.CONV_PRESPLIT
+PATCH = _lib.CONV_PATCH
 _FLAGS = (X6, X6 | BM256)    # the x6 candidates, in candidate order
+_PFLAGS = (X6 | PATCH, X6 | PATCH | BM256)   # + the patch-staged ones where the shape fits
+_XNAMES = ("x6", "x6_256", "x6p", "x6p_256")
+
+
+def _x6_flags(gemm_c: int, k: int, stride: int, n_out: int):
+    """The x6 flag variants for a forward / stride-1 input gradient whose GEMM reads
+    gemm_c channels: the patch kernel needs 3x3, stride 1, gemm_c % 32 == 0 and more
+    than 16 GEMM columns (csrc/conv.hip use_x6p)."""
+    if k == 3 and stride == 1 and gemm_c % 32 == 0 and n_out > 16:
+        return _FLAGS + _PFLAGS
+    return _FLAGS
 
 
 def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
@@ -300,23 +312,24 @@ class _Conv(torch.autograd.Function):
         ctx.stride, ctx.pad = stride, pad
         ctx.key = (tuple(x.shape), tuple(weight.shape), stride, pad)
         x6 = _x6_ok(x, weight)
+        xf = _x6_flags(x.shape[1], weight.shape[2], stride, weight.shape[0]) if x6 else ()
         cands = None
         i = _cached("fwd", ctx.key)
-        if i is None or not (x6 and i < 2):
+        if i is None or not (x6 and i < len(xf)):
             direct = _direct_ok(weight.shape[1], weight.shape[0], weight.shape[2], stride)
-            cands = ([lambda: _fwd(x, weight, stride, pad, X6), lambda: _fwd(x, weight, stride, pad, X6 | BM256)]
-                     if x6 else []) + [lambda: _fwd(x, weight, stride, pad)] + \
+            cands = [(lambda f=f: _fwd(x, weight, stride, pad, f)) for f in xf] + \
+                [lambda: _fwd(x, weight, stride, pad)] + \
                 ([lambda: _direct_fwd(x, weight, pad)] if direct else []) + \
                 [lambda: F.conv2d(x, weight, None, stride, pad)]
-            names = (["x6", "x6_256"] if x6 else []) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"]
+            names = list(_XNAMES[:len(xf)]) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"]
             if i is None:
                 i = _fastest("fwd", ctx.key, cands, names)
         planes_dg = None
-        if x6 and i < 2:
+        if x6 and i < len(xf):
             # the x6 forward: split the weight once for it and for the input gradient
             # (one launch), the dgrad planes kept for the backward
             pf, planes_dg = _split_weights(x, weight, stride, pad, stride == 1 or _x6_s2_ok(x, weight, stride))
-            y = _fwd_planes(x, weight, pf, stride, pad, _FLAGS[i])
+            y = _fwd_planes(x, weight, pf, stride, pad, xf[i])
         else:
             y = cands[i]()
         ctx.save_for_backward(x, weight, planes_dg)
@@ -333,14 +346,16 @@ class _Conv(torch.autograd.Function):
         if need_x:
             if s == 1:
                 x6 = _x6_ok(x, w)
+                # the input gradient's GEMM reads gy: out_channels channels, in_channels columns
+                xf = _x6_flags(w.shape[0], w.shape[2], 1, w.shape[1]) if x6 else ()
                 direct = _direct_ok(w.shape[0], w.shape[1], w.shape[2], s)
-                cands = ([lambda: _dgrad(gy, x, w, p, X6), lambda: _dgrad(gy, x, w, p, X6 | BM256)] if x6 else []) + \
+                cands = [(lambda f=f: _dgrad(gy, x, w, p, f)) for f in xf] + \
                     [lambda: _dgrad(gy, x, w, p)] + ([lambda: _direct_dgrad(gy, w, p)] if direct else []) + \
                     [lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
-                names = (["x6", "x6_256"] if x6 else []) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"]
+                names = list(_XNAMES[:len(xf)]) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"]
                 i = _fastest("dgrad", ctx.key, cands, names)
-                if x6 and i < 2 and planes_dg is not None:
-                    gx = _dgrad_planes(gy, x, w, planes_dg, p, _FLAGS[i])
+                if x6 and i < len(xf) and planes_dg is not None:
+                    gx = _dgrad_planes(gy, x, w, planes_dg, p, xf[i])
                 elif i < len(cands) - 1:
                     gx = cands[i]()
                 else:

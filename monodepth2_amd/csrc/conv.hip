@@ -71,6 +71,7 @@ struct ConvArgs {
     int par, py, px, kh0, kw0, ntw, dy0, dx0, oHf, oWf;
     int flatk;               // x6 fwd / dgrad with C < 32: K chunks run over the flattened
                              // (tap, channel) index, several taps per chunk
+    int ptr, ptc;            // patch kernel (conv_x6p_kernel): output tiles per image, rows / columns
     const float* a;          // fwd: x; dgrad: gy; wgrad: x
     const float* b;          // fwd / dgrad: weight; wgrad: gy
     float* y;                // output [M][N], or partials [splits][M][N]
@@ -745,6 +746,179 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
     }
 }
 
+// Patch-staged split-bf16 3x3 stride-1 convolution (forward, and the stride-1 input
+// gradient as the "full" convolution of gy with the flipped planes).  conv_x6_kernel
+// stages its A tile per (tap, 32 channels) chunk: every activation is fetched, split and
+// written to LDS nine times, once per tap.  Here a block owns a TR x TC rectangle of
+// output pixels of one image; for every 32-channel chunk it stages the (TR+2) x (TC+2)
+// input patch ONCE (one global fetch, one split, one LDS write per activation), and the
+// nine taps read it at row / column offsets — the A fragment of tap (kh, kw) for output
+// pixel (r, c) is patch pixel (r + kh, c + kw), the same [pixel][32 k] swizzled rows as
+// conv_x6_kernel's tile, conflict-free at any offset (16-lane groups hit 16 distinct
+// bank quads).  B (the weight planes of one tap) goes in by LDS-DMA, double-buffered
+// across taps; one barrier per tap.  The next chunk's patch is fetched into registers
+// behind tap 0's MFMAs and split / stored after tap 8.  A tiles of 128 or 256 pixels
+// as TR x TC with TC in {16, 32, 64} chosen per shape (the least padding); outputs
+// outside the image are not stored.  K splits run over channel chunks.
+template <int BN, int BMX, int TC>
+__global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvArgs a) {
+    using G = X6Geo<BN, BMX>;
+    static_assert(G::MT == 32, "patch kernel: 32x32x16 MFMA tiles");
+    constexpr int NT = G::NT, TM = G::TM;
+    constexpr int TR = BMX / TC, PW = TC + 2, PH = TR + 2, PP = PH * PW;
+    constexpr int AQP = (PP * 8 + NT - 1) / NT;          // f32 quads of the patch per thread
+    constexpr int NW = NT / 64, PIECES = 3 * BN / 16;
+    constexpr int BQ = (PIECES + NW - 1) / NW;
+    constexpr int PA = PP * XBK, PB = BN * XBK;          // bf16 elements per plane
+    __shared__ __bf16 lds[3 * PA + 2 * 3 * PB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / G::WN, wn = wid % G::WN;
+    int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int nb = blk % a.nblocks;
+    blk /= a.nblocks;
+    const int mb = blk % a.mblocks, ks = blk / a.mblocks;
+    const int per_img = a.ptr * a.ptc;
+    const int b = mb / per_img, trc = mb - b * per_img, tr = trc / a.ptc, tc = trc - tr * a.ptc;
+    const int oh0 = tr * TR, ow0 = tc * TC, n0 = nb * BN;
+    const int t0 = ks * a.chunks_per_split;
+    const int nchunks = min(a.chunks_per_split, a.nchunks - t0);   // 32-channel chunks
+    constexpr int KT = 9;
+
+    // A: patch float4 f = tid + NT j -> pixel f / 8 (row-major PH x PW), channel quad f % 8
+    int aofs[AQP];
+    const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * 4, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < AQP; ++j) {
+        const int f = tid + NT * j, pix = f >> 3, q = f & 7;
+        const int pr = pix / PW, pc = pix - pr * PW;
+        const int ih = oh0 + pr - a.pad, iw = ow0 + pc - a.pad;
+        const bool ok = f < PP * 8 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        aofs[j] = ok ? ((b * a.H + ih) * a.W + iw) * a.C + 4 * q : -1;
+    }
+    // B: as conv_x6_kernel (1 KiB LDS-DMA pieces, swizzle-ordered lanes)
+    constexpr int RB16 = BN / 16;
+    int bsrc[BQ], bk8[BQ], bdst[BQ];
+    const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * 2, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < BQ; ++j) {
+        const int piece = wid + NW * j, pl = piece / RB16, rb = piece - pl * RB16;
+        const int r = rb * 16 + (lane >> 2), q = ((lane & 3) ^ (r >> 2)) & 3;
+        const int n = n0 + r;
+        bk8[j] = 8 * q;
+        bsrc[j] = n < a.N ? ((pl * a.N + n) * KT) * a.C + 8 * q : -1;
+        bdst[j] = (3 * PA + pl * PB + rb * 16 * XBK) * 2;
+    }
+    f32x16 acc[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+
+    float4 RA[AQP];
+    auto load = [&](int t) {   // the patch of channel chunk t (zeros outside the image)
+        const int c0 = (t0 + t) * XBK;
+#pragma unroll
+        for (int j = 0; j < AQP; ++j) RA[j] = bload(ar, aofs[j] >= 0 ? (aofs[j] + c0) * 4 : kBad);
+    };
+    auto store_patch = [&]() {
+#pragma unroll
+        for (int j = 0; j < AQP; ++j) {
+            const int f = tid + NT * j;
+            if (PP * 8 % NT && f >= PP * 8) break;
+            bf16x4 p0, p1, p2;
+            split3(RA[j], p0, p1, p2);
+            const int e = xidx(f >> 3, 4 * (f & 7));
+            *(bf16x4*)(lds + e) = p0;
+            *(bf16x4*)(lds + PA + e) = p1;
+            *(bf16x4*)(lds + 2 * PA + e) = p2;
+        }
+    };
+    auto dma = [&](int t, int tap, int buf) {   // B of (chunk t, tap) into buffer buf
+        const int kofs = tap * a.C + (t0 + t) * XBK, klim = tap * a.C + a.C;
+        char* base = (char*)lds + buf * 3 * PB * 2;
+#pragma unroll
+        for (int j = 0; j < BQ; ++j) {
+            if (PIECES % NW && wid + NW * j >= PIECES) break;   // wave-uniform
+            const bool ok = bsrc[j] >= 0 && kofs + bk8[j] < klim;
+            dma16(br, base + bdst[j], ok ? (bsrc[j] + kofs) * 2 : kBad);
+        }
+    };
+    const int lr = lane & 31, h = lane >> 5;
+    int abase[TM];   // this lane's patch pixel at tap (0, 0), per row fragment
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int ml = wm * (TM * 32) + 32 * i + lr, r = ml / TC, c = ml - r * TC;
+        abase[i] = r * PW + c;
+    }
+    auto mma = [&](int buf, int tap) {
+        const __bf16* LB = lds + 3 * PA + buf * 3 * PB;
+        const int th = tap / 3, toff = th * PW + (tap - 3 * th);
+#pragma unroll
+        for (int s = 0; s < XBK / 16; ++s) {
+            bf16x8 fb[3];
+            const int eb = xidx(wn * 32 + lr, 16 * s + 8 * h);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(LB + pl * PB + eb);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                bf16x8 fa[3];
+                const int e = xidx(abase[i] + toff, 16 * s + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(lds + pl * PA + e);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+            }
+        }
+    };
+
+    if (NT == 512 && wid >= 4) __builtin_amdgcn_s_setprio(1);   // as conv_x6_kernel
+    if (nchunks > 0) {
+        load(0);
+        dma(0, 0, 0);
+        store_patch();
+        wait_vm<0>();
+        lds_sync();
+    }
+    int buf = 0;
+    for (int t = 0; t < nchunks; ++t) {
+        for (int tap = 0; tap < KT; ++tap) {
+            const bool more = tap + 1 < KT || t + 1 < nchunks;
+            if (more) dma(tap + 1 < KT ? t : t + 1, tap + 1 < KT ? tap + 1 : 0, buf ^ 1);
+            // the next patch behind tap 0 (issued after the DMA: waiting for the DMA at the
+            // end of this tap leaves these loads in flight)
+            if (tap == 0 && t + 1 < nchunks) load(t + 1);
+            mma(buf, tap);
+            asm volatile("" ::: "memory");
+            if (tap == 0 && t + 1 < nchunks) wait_vm<AQP>();
+            else wait_vm<0>();
+            lds_sync();
+            buf ^= 1;
+        }
+        if (t + 1 < nchunks) {   // every wave is past tap 8: the patch can be replaced
+            store_patch();
+            lds_sync();
+        }
+    }
+
+    float* out = a.y + (size_t)ks * a.M * a.N;
+    const int n = n0 + wn * 32 + lr;
+    if (n < a.N) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int ml = wm * (TM * 32) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+                const int r = ml / TC, c = ml - r * TC, oh = oh0 + r, ow = ow0 + c;
+                if (oh < a.Ho && ow < a.Wo) out[((size_t)(b * a.Ho + oh) * a.Wo + ow) * a.N + n] = acc[i][e];
+            }
+    }
+}
+
 // Split-bf16 weight gradient: gw[co][tap][ci] = Σ_p gy[p][co] · x[p + tap][ci] as a
 // GEMM with rows m = co, columns n = (tap, ci), K = output pixels.  Both operands are
 // stored k-row in HBM (channels contiguous per pixel), the MFMA wants 8 consecutive k
@@ -1233,6 +1407,77 @@ void launch_x6(const ConvArgs& a, hipStream_t st) {
     else hipLaunchKernelGGL((conv_x6_kernel<16, 128>), grid, dim3(X6Geo<16, 128>::NT), 0, st, a);
 }
 
+// Patch kernel (MD2_CONV_X6 | MD2_CONV_PATCH): 3x3 stride-1 forward / input gradient with
+// the GEMM's channel count a multiple of 32 and more than 16 output channels
+bool use_x6p(const md2_conv_desc* d, int mode, const ConvArgs& a) {
+    return (d->flags & MD2_CONV_PATCH) && use_x6(d, mode) && mode != MODE_WGRAD && a.KH == 3 && a.KW == 3 &&
+           a.stride == 1 && a.C % XBK == 0 && a.N > 16 && !a.flatk;
+}
+
+// TC (tile columns) with the least padded area; K split over 32-channel chunks by the
+// wave-quantisation model of plan_x6 (a chunk here is nine taps)
+void plan_x6p(ConvArgs& a, uint32_t flags) {
+    const int BN = a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128);
+    const int BMX = (BN == 128 && (flags & MD2_CONV_BM256)) ? 256 : 128;
+    // least padded output area; among equals the smallest patch (the least halo per tile)
+    int best_tc = 64;
+    long long best_cost = -1;
+    for (int TC = 64; TC >= 16; TC /= 2) {
+        const int TR = BMX / TC;
+        const long long area = (long long)((a.Ho + TR - 1) / TR) * TR * ((a.Wo + TC - 1) / TC) * TC;
+        const long long cost = area * 4096 + (TR + 2) * (TC + 2);
+        if (best_cost < 0 || cost < best_cost) {
+            best_cost = cost;
+            best_tc = TC;
+        }
+    }
+    const int TR = BMX / best_tc;
+    a.ptr = (a.Ho + TR - 1) / TR;
+    a.ptc = (a.Wo + best_tc - 1) / best_tc;
+    a.nchunks = a.C / XBK;
+    const int mblocks = a.B * a.ptr * a.ptc, nblocks = (a.N + BN - 1) / BN;
+    const int base = mblocks * nblocks, res = BN == 128 ? 256 : 512;   // blocks per CU: 1 (BN 128) / 2
+    int best_s = 1;
+    double best_t = 1e30;
+    const int smax = (flags & MD2_CONV_NO_SPLIT) ? 1 : a.nchunks;
+    for (int sp = 1; sp <= smax && sp <= 64; ++sp) {
+        const int per = (a.nchunks + sp - 1) / sp;
+        const int splits = (a.nchunks + per - 1) / per;
+        const int rounds = (base * splits + res - 1) / res;
+        const double red = splits > 1 ? (double)(splits + 1) * a.M * a.N * 4.0 / 2400.0 / 1536.0 + split_launch_cost()
+                                      : 0.0;
+        const double t = (double)rounds * per * 9.0 * (BMX / 128.0) + red;
+        if (t < best_t - 1e-9) {
+            best_t = t;
+            best_s = splits;
+        }
+    }
+    a.bm = BMX;
+    a.bn = BN;
+    a.mblocks = mblocks;
+    a.nblocks = nblocks;
+    a.chunks_per_split = (a.nchunks + best_s - 1) / best_s;
+    a.splits = (a.nchunks + a.chunks_per_split - 1) / a.chunks_per_split;
+    a.flatk = best_tc;   // carried to launch_x6p (the kernel itself does not read flatk)
+}
+
+template <int BN, int BMX>
+void launch_x6p_tc(const ConvArgs& a, hipStream_t st) {
+    const dim3 grid(a.mblocks * a.nblocks * a.splits), block(X6Geo<BN, BMX>::NT);
+    ConvArgs b = a;
+    b.flatk = 0;
+    if (a.flatk == 64) hipLaunchKernelGGL((conv_x6p_kernel<BN, BMX, 64>), grid, block, 0, st, b);
+    else if (a.flatk == 32) hipLaunchKernelGGL((conv_x6p_kernel<BN, BMX, 32>), grid, block, 0, st, b);
+    else hipLaunchKernelGGL((conv_x6p_kernel<BN, BMX, 16>), grid, block, 0, st, b);
+}
+
+void launch_x6p(const ConvArgs& a, hipStream_t st) {
+    if (a.bm == 256) launch_x6p_tc<128, 256>(a, st);
+    else if (a.bn == 128) launch_x6p_tc<128, 128>(a, st);
+    else if (a.bn == 64) launch_x6p_tc<64, 128>(a, st);
+    else launch_x6p_tc<32, 128>(a, st);
+}
+
 // Stride-2 input gradient on x6 (MD2_CONV_X6, at least 32 output channels): gx pixels
 // of one parity (py, px) receive only the taps kh ≡ py + pad, kw ≡ px + pad (mod 2),
 // each from one gy pixel — a stride-1 GEMM over that class's Ho x Wo grid, scattered
@@ -1325,7 +1570,9 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
         const char* name) {
     ConvArgs a = (mode == MODE_WGRAD && use_x6(d, mode)) ? args_x6_wgrad(d) : args_of(d, mode);
     if (use_x6(d, mode)) flat_k(a, mode);
-    if (use_x6(d, mode)) plan_x6(a, d->flags, mode == MODE_WGRAD);
+    const bool patch = use_x6p(d, mode, a);
+    if (patch) plan_x6p(a, d->flags);
+    else if (use_x6(d, mode)) plan_x6(a, d->flags, mode == MODE_WGRAD);
     else plan(a, d->flags, min_chunks_of(mode));
     const int BN = a.bn;
     a.a = A;
@@ -1348,7 +1595,8 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
         if (!(d->flags & MD2_CONV_PRESPLIT))
             hipLaunchKernelGGL(conv_wsplit_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, B, planes,
                                d->out_channels, d->kernel_h * d->kernel_w, d->in_channels, mode == MODE_DGRAD ? 1 : 0);
-        launch_x6(a, st);
+        if (patch) launch_x6p(a, st);
+        else launch_x6(a, st);
     } else if (mode == MODE_FWD) launch<MODE_FWD>(a, BN, st);
     else if (mode == MODE_DGRAD) launch<MODE_DGRAD>(a, BN, st);
     else launch<MODE_WGRAD>(a, BN, st);
@@ -1379,7 +1627,8 @@ size_t ws_bytes(const md2_conv_desc* d, int mode) {
     }
     if (use_x6(d, mode)) {
         flat_k(a, mode);
-        plan_x6(a, d->flags);
+        if (use_x6p(d, mode, a)) plan_x6p(a, d->flags);
+        else plan_x6(a, d->flags);
         return x6_planes_bytes(d) + (a.splits > 1 ? sizeof(float) * (size_t)a.splits * a.M * a.N : 0);
     }
     plan(a, d->flags, min_chunks_of(mode));

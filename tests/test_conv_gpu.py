@@ -162,6 +162,12 @@ def test_conv_abi_dgrad_wgrad(B, C, N, k, s, p, H, W):
         assert _rel(gx, gx_ref) < 1e-4
 
 
+# x6 variants: 128 / 256-row tiles, and the patch-staged kernel (which run() uses only
+# where the shape fits it: 3x3, stride 1, GEMM channels % 32 — elsewhere the flag is inert)
+XFLAGS = (conv_ops.X6, conv_ops.X6 | conv_ops.BM256, conv_ops.X6 | conv_ops.PATCH,
+          conv_ops.X6 | conv_ops.PATCH | conv_ops.BM256)
+
+
 @pytest.mark.parametrize("B,C,N,k,s,p,H,W", [sh for sh in SHAPES if sh[1] % 8 == 0 and sh[2] % 8 == 0])
 def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
     """The split-bf16 path (MD2_CONV_X6: exact three-plane split, six bf16 MFMA
@@ -174,7 +180,7 @@ def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
     ref = F.conv2d(x.double().cpu(), w.double().cpu(), None, s, p)
     y_mi = F.conv2d(x, w, None, s, p).double().cpu()
     e_mi = _rel(y_mi, ref)
-    for fl in (conv_ops.X6, conv_ops.X6 | conv_ops.BM256):
+    for fl in XFLAGS:
         e_x6 = _rel(conv_ops._fwd(x, w, s, p, fl).double().cpu(), ref)
         assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, (fl, e_x6, e_mi)
     if s == 1 or conv_ops._x6_s2_ok(x, w, s):   # stride 2: four parity-class GEMMs
@@ -184,7 +190,7 @@ def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
         g_mi = torch.ops.aten.convolution_backward(gy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
                                                    (True, False, False))[0].double().cpu()
         e_mi = _rel(g_mi, gref)
-        for fl in (conv_ops.X6, conv_ops.X6 | conv_ops.BM256):
+        for fl in XFLAGS:
             e_x6 = _rel(conv_ops._dgrad(gy, x, w, p, fl, s).double().cpu(), gref)
             assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, (fl, s, e_x6, e_mi)
     gy = torch.randn(ref.shape, device="cuda").contiguous(memory_format=CL)
@@ -258,3 +264,44 @@ def test_direct_wgrad_matches_miopen(B, C, p, H, W):
     assert gw.shape == w.shape and gw.is_contiguous(memory_format=CL)
     assert _rel(gw, gwr) < 1e-4
     assert torch.equal(gw, conv_ops._direct_wgrad(gy, x, w, p))
+
+
+PATCH_SHAPES = [  # (B, Cin, Cout, pad, H, W): tile-column choices 64 / 32 / 16, odd tails, K splits
+    (2, 64, 64, 1, 24, 80),     # layer-1-like width: 16-column tiles
+    (2, 128, 128, 1, 12, 40),   # 64-column tiles with a 24-column tail
+    (1, 96, 64, 0, 18, 34),     # decoder conv on a pre-padded input (pad 0; input gradient pad 2)
+    (2, 256, 256, 1, 6, 10),    # deep layer: K split over channel chunks
+    (3, 32, 32, 1, 7, 9),       # one channel chunk, 32 output columns, odd sizes
+    (2, 64, 128, 1, 48, 160),   # wide: 64-column tiles
+    (2, 512, 64, 1, 5, 7),      # many chunks, tiny image
+]
+
+
+@pytest.mark.parametrize("B,C,N,p,H,W", PATCH_SHAPES)
+def test_x6_patch_kernel_is_f32_class(B, C, N, p, H, W):
+    """The patch-staged split-bf16 kernel (MD2_CONV_PATCH: one input patch per 32
+    channels for all nine taps) on forward and stride-1 input gradient against fp64:
+    f32-class like the per-tap x6 kernel, and within 2e-6 of it."""
+    torch.manual_seed(31 + C + N + H + W)
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    w = (torch.randn(N, C, 3, 3, device="cuda") / (C * 9) ** 0.5).contiguous(memory_format=CL)
+    ref = F.conv2d(x.double().cpu(), w.double().cpu(), None, 1, p)
+    e_mi = _rel(F.conv2d(x, w, None, 1, p).double().cpu(), ref)
+    gy = torch.randn(ref.shape, device="cuda").contiguous(memory_format=CL)
+    gref = torch.ops.aten.convolution_backward(gy.double().cpu(), x.double().cpu(), w.double().cpu(), None, (1, 1),
+                                               (p, p), (1, 1), False, (0, 0), 1, (True, False, False))[0]
+    g_mi = torch.ops.aten.convolution_backward(gy, x, w, None, (1, 1), (p, p), (1, 1), False, (0, 0), 1,
+                                               (True, False, False))[0].double().cpu()
+    eg_mi = _rel(g_mi, gref)
+    base_y = conv_ops._fwd(x, w, 1, p, conv_ops.X6).double().cpu()
+    base_g = conv_ops._dgrad(gy, x, w, p, conv_ops.X6).double().cpu()
+    for fl in (conv_ops.X6 | conv_ops.PATCH, conv_ops.X6 | conv_ops.PATCH | conv_ops.BM256):
+        y = conv_ops._fwd(x, w, 1, p, fl).double().cpu()
+        e = _rel(y, ref)
+        assert e < max(3 * e_mi, 1e-7) and e < 2e-6, (fl, e, e_mi)
+        assert _rel(y, base_y) < 2e-6
+        g = conv_ops._dgrad(gy, x, w, p, fl).double().cpu()
+        e = _rel(g, gref)
+        assert e < max(3 * eg_mi, 1e-7) and e < 2e-6, (fl, e, eg_mi)
+        assert _rel(g, base_g) < 2e-6
+        assert torch.equal(conv_ops._fwd(x, w, 1, p, fl), conv_ops._fwd(x, w, 1, p, fl))   # deterministic
