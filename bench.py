@@ -88,7 +88,7 @@ def pmc_traffic(args, S, timeout=150):
                "--output-format", "csv", "--", sys.executable, os.path.join(REPO, "bench.py"),
                "--batch", str(args.batch), "--height", str(args.height), "--width", str(args.width),
                "--num_layers", str(args.num_layers), "--amp", args.amp, "--steps", "3", "--warmup", "2",
-               "--no-cpu-baseline", "--no-parity", "--pmc", "0", "--no-conv-roofline"] + \
+               "--no-cpu-baseline", "--no-parity", "--pmc", "0", "--no-conv-roofline", "--graph", "0"] + \
               (["--stereo"] if args.stereo else [])
         env = dict(os.environ, TMPDIR="/tmp")
         p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env, start_new_session=True)
@@ -143,7 +143,9 @@ def parse():
     ap.add_argument("--channels-last", type=int, default=1, help="NHWC convolutions (1/0)")
     ap.add_argument("--pose-last", type=int, default=0,
                     help="1: pose network forward enqueued after the depth network (its backward first)")
-    ap.add_argument("--graph", type=int, default=0, help="capture the whole step in a hipGraph (1/0)")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture the whole step in a hipGraph (1/0; default: 1 on one GPU, where the captured "
+                         "step is at or below eager and immune to a slow host, 0 with N > 1)")
     ap.add_argument("--pose-stream", type=int, default=1, help="pose network on its own HIP stream (1/0)")
     ap.add_argument("--miopen-find", type=str, default="fast", help="MIOPEN_FIND_MODE (fast|normal|...)")
     ap.add_argument("--amp", type=str, default="none", choices=["none", "bf16"],
@@ -324,6 +326,8 @@ def main():
     _lib.lib()
     log(f"world={world} device={torch.cuda.get_device_name(device)}")
 
+    if args.graph < 0:
+        args.graph = 1 if world == 1 else 0
     trainer = make_trainer(args, device, rank, world)
     frame_ids = trainer.opt.frame_ids
     # colours as the reference's loader delivers them: uint8 frames through to_tensor,
@@ -452,7 +456,8 @@ def main():
                                           else "")
                                        + (" + GPU input pipeline from 375x1242 uint8" if args.gpu_augment else ""),
                            "global_batch": B * world, "height": H, "width": W, "frame_ids": [str(f) for f in frame_ids],
-                           "parallelism": f"dp{world}"},
+                           "parallelism": f"dp{world}",
+                           "step": "hipgraph replay" if trainer.graph is not None else "eager"},
                 "roofline": roof, "conv_roofline": conv_roof, "cpu_baseline": cpu,
                 "loss_delta_vs_oracle": delta, "final_loss": round(final_loss, 6),
                 "host_enqueue_ms_per_step": round(host_ms, 3)}

@@ -372,11 +372,16 @@ class _Conv(torch.autograd.Function):
                 mi_x = True
         if need_w:
             direct = _direct_ok(w.shape[1], w.shape[0], w.shape[2], s) and w.shape[0] == 16
-            cands = ([lambda: _wgrad(gy, x, w, s, p, X6)] if _x6_ok(x, w) else []) + [lambda: _wgrad(gy, x, w, s, p)] + \
+            x6 = _x6_ok(x, w)
+            # the patch-staged weight gradient: 3x3, stride 1 (csrc/conv.hip use_x6pw)
+            pw = x6 and w.shape[2] == 3 and w.shape[3] == 3 and s == 1
+            cands = ([lambda: _wgrad(gy, x, w, s, p, X6)] if x6 else []) + \
+                ([lambda: _wgrad(gy, x, w, s, p, X6 | PATCH)] if pw else []) + [lambda: _wgrad(gy, x, w, s, p)] + \
                 ([lambda: _direct_wgrad(gy, x, w, p)] if direct else []) + \
                 [lambda: _miopen_bwd(gy, x, w, s, p, (False, True, False))[1]]
             i = _fastest("wgrad", ctx.key, cands,
-                         (["x6"] if _x6_ok(x, w) else []) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"])
+                         (["x6"] if x6 else []) + (["x6pw"] if pw else []) + ["f32mfma"] +
+                         (["direct"] if direct else []) + ["miopen"])
             if i < len(cands) - 1:
                 gw = cands[i]()
             else:

@@ -1124,18 +1124,245 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
     }
 }
 
+// xidx with rows r and r ^ 1 swapped in every odd row quad: the same ds_read_b128
+// banks as xidx (a fragment group's rows map onto the same row set), and an 8-byte
+// store of row 4 q + j by the 16 lanes of two quads (q, q + 1) then lands on both
+// 16-bank halves (row parity differs) instead of two-way on one
+__device__ __forceinline__ int xidx2(int r, int k) { return xidx(r ^ ((r >> 2) & 1), k); }
+
+// Patch-staged split-bf16 weight gradient (MD2_CONV_X6 | MD2_CONV_PATCH; 3x3, stride 1).
+// conv_x6_wgrad_kernel stages x once per (tap, ci) column, so every activation is
+// fetched and split nine times.  Here a K chunk is one 32-pixel segment of one output
+// row: its three input rows x 34 columns x 32 channels are fetched and split ONCE and
+// written as nine [32 ci][32 k] tiles — input row kh, columns shifted by kw, i.e. the B
+// operand of tap (kh, kw), 16-byte aligned for the fragment reads.  Block tile: BMW
+// output channels (rows, A = gy) x 9 taps x 32 input channels; nine waves, wave w
+// multiplies tap w (TM = BMW / 32 row fragments).  Staging: waves 0-2 the x rows (a
+// lane loads 6 pixels x 4 channels to fill the three shifted copies of 4 positions),
+// waves 3-4 (3 at BMW = 32) the gy tile; LDS double-buffered, one barrier per chunk.
+// K splits run over the chunks; output and partials as conv_x6_wgrad_kernel.
+// ConvArgs: M = Co, N = 9 Ci, C = Ci, Cg = Co, nblocks = 32-channel groups of Ci,
+// ptc = 32-column segments per output row, nchunks = B Ho ptc.
+template <int BMW>
+__global__ __launch_bounds__(576, 1) void conv_x6pw_kernel(ConvArgs a) {
+    constexpr int TM = BMW / 32;
+    constexpr int PA = BMW * XBK, PT = 32 * XBK;   // bf16 per A plane / per B tile plane
+    constexpr int BUF = 3 * PA + 27 * PT;
+    static_assert(BMW == 32 || BMW == 64, "wgrad patch row tile");
+    __shared__ __bf16 lds[2 * BUF];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int cb = blk % a.nblocks;
+    blk /= a.nblocks;
+    const int mb = blk % a.mblocks, ks = blk / a.mblocks;
+    const int m0 = mb * BMW, c0 = cb * XBK;
+    const int t0 = ks * a.chunks_per_split;
+    const int nchunks = min(a.chunks_per_split, a.nchunks - t0);
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+    // staging roles by wave (the x rows on waves 0-2, the gy tile on 3-4; measured 4 %
+    // faster than keeping the three waves that share a SIMD, 0 / 4 / 8, free of staging)
+    const int rr = wid, g = lane & 7, q = lane >> 3;        // x: input row rr, columns 4g .., channels 4q ..
+    const int u = tid - 192, kq = u & 7, mq = u >> 3;       // gy: pixels 4kq .., channels 4mq ..
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * 4, 0x00020000);
+
+    // the loader's chunk position (b, oh, seg), advanced one chunk at a time
+    int pc = t0, pseg, poh, pb;
+    {
+        const int r = pc / a.ptc;
+        pseg = pc - r * a.ptc;
+        pb = r / a.Ho;
+        poh = r - pb * a.Ho;
+    }
+    auto advance = [&]() {
+        ++pc;
+        if (++pseg == a.ptc) {
+            pseg = 0;
+            if (++poh == a.Ho) {
+                poh = 0;
+                ++pb;
+            }
+        }
+    };
+    float4 V[6];
+    // loads of the loader's chunk (zeros past the split's last chunk: no branch)
+    auto load_x = [&]() {
+        const int ih = poh - a.pad + rr, iw0 = pseg * 32 - a.pad + 4 * g;
+        const bool rok = pc < t0 + nchunks && c0 + 4 * q < a.C && (unsigned)ih < (unsigned)a.H;
+        const int base = ((pb * a.H + ih) * a.W) * a.C + c0 + 4 * q;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const int iw = iw0 + i;
+            V[i] = bload(xr, rok && (unsigned)iw < (unsigned)a.W ? (base + iw * a.C) * 4 : kBad);
+        }
+    };
+    auto load_g = [&]() {
+        const int ow0 = pseg * 32 + 4 * kq;
+        const bool ok = pc < t0 + nchunks && m0 + 4 * mq < a.M;
+        const int base = ((pb * a.Ho + poh) * a.Wo) * a.Cg + m0 + 4 * mq;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) V[i] = bload(gr, ok && ow0 + i < a.Wo ? (base + (ow0 + i) * a.Cg) * 4 : kBad);
+    };
+    auto store_x = [&](__bf16* L) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float c[3][6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const float x = j == 0 ? V[i].x : (j == 1 ? V[i].y : (j == 2 ? V[i].z : V[i].w));
+                const float a0 = trunc16(x), r1 = x - a0, a1 = trunc16(r1);
+                c[0][i] = a0;
+                c[1][i] = a1;
+                c[2][i] = r1 - a1;
+            }
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                uint32_t w[5];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) w[k] = hi16x2(c[pl][k], c[pl][k + 1]);
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) {
+                    u32x2 v;
+                    v.x = w[kw];
+                    v.y = w[kw + 2];
+                    *(u32x2*)(L + 3 * PA + ((kw * 3 + rr) * 3 + pl) * PT + xidx2(4 * q + j, 4 * g)) = v;
+                }
+            }
+        }
+    };
+    auto store_g = [&](__bf16* L) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float c[3][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float x = j == 0 ? V[i].x : (j == 1 ? V[i].y : (j == 2 ? V[i].z : V[i].w));
+                const float a0 = trunc16(x), r1 = x - a0, a1 = trunc16(r1);
+                c[0][i] = a0;
+                c[1][i] = a1;
+                c[2][i] = r1 - a1;
+            }
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                u32x2 v;
+                v.x = hi16x2(c[pl][0], c[pl][1]);
+                v.y = hi16x2(c[pl][2], c[pl][3]);
+                *(u32x2*)(L + pl * PA + xidx2(4 * mq + j, 4 * kq)) = v;
+            }
+        }
+    };
+
+    const int lr = lane & 31, h = lane >> 5;
+    const int kh = wid / 3, kw = wid - 3 * kh;
+    // one accumulator per row fragment over the whole split: plan_x6pw caps a split at
+    // kX6pwMaxChunks chunks (2048 pixels), short enough for the MFMA's f32 accumulation
+    f32x16 acc[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    const int boff = 3 * PA + (kw * 3 + kh) * 3 * PT;
+    auto mma = [&](const __bf16* L) {
+#pragma unroll
+        for (int s = 0; s < XBK / 16; ++s) {
+            bf16x8 fb[3];
+            const int eb = boff + xidx2(lr, 16 * s + 8 * h);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + pl * PT + eb);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                bf16x8 fa[3];
+                const int e = xidx2(32 * i + lr, 16 * s + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(L + pl * PA + e);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+            }
+        }
+    };
+
+    // One loop per staging role (wave-uniform), so that a step — multiply the chunk in
+    // one buffer, split / store the next one (in registers) into the other, fetch the
+    // one after — is one basic block the scheduler can interleave (MFMA shadows hide
+    // the split VALU).  Every role runs the same number of barriers.
+    auto run = [&](auto role_c) {
+        constexpr int ROLE = decltype(role_c)::value;   // 0: x rows, 1: gy, 2: multiply only
+        auto load = [&]() {
+            if constexpr (ROLE == 0) load_x();
+            else if constexpr (ROLE == 1) load_g();
+        };
+        auto store = [&](__bf16* L) {
+            if constexpr (ROLE == 0) store_x(L);
+            else if constexpr (ROLE == 1) store_g(L);
+        };
+        load();                 // chunk 0
+        store(lds);
+        advance();
+        load();                 // chunk 1
+        lds_sync();
+        int t = 0;
+        for (; t + 2 < nchunks; t += 2) {
+            mma(lds);
+            store(lds + BUF);   // chunk t + 1
+            advance();
+            load();             // chunk t + 2
+            lds_sync();
+            mma(lds + BUF);
+            store(lds);         // chunk t + 2
+            advance();
+            load();             // chunk t + 3 (zeros past the end)
+            lds_sync();
+        }
+        if (t + 1 < nchunks) {
+            mma(lds);
+            store(lds + BUF);
+            lds_sync();
+            mma(lds + BUF);
+        } else if (t < nchunks) {
+            mma(lds);
+        }
+    };
+    if (wid < 3) run(std::integral_constant<int, 0>());
+    else if (tid < 192 + 2 * BMW) run(std::integral_constant<int, 1>());
+    else run(std::integral_constant<int, 2>());
+
+    float* out = a.y + (size_t)ks * a.M * a.N;
+    const int ci = c0 + lr;
+    if (ci < a.C) {
+        const int n = (kh * 3 + kw) * a.C + ci;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int m = m0 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (m < a.M) out[m * a.N + n] = acc[i][e];
+            }
+    }
+}
+
 // y = Σ_split partial[split], deterministic: 64 float4 outputs per block, four lanes
 // per output summing every 4th split, then the four lane sums added in lane order.
 // (One thread per output walked all splits — up to ~60 in the weight gradients — as
 // one serial chain over a few dozen blocks.)
 constexpr int kRedOut = 64, kRedLanes = 256 / kRedOut;
+// OUT outputs per block, 256 / OUT lanes each: 64 for wide partials with few splits,
+// 16 (sixteen lanes, each every 16th split) for the weight gradients' narrow ones with
+// many splits, which at 64 per block ran a few dozen blocks of long serial chains
+template <int OUT>
 __global__ __launch_bounds__(256) void conv_reduce_kernel(const float4* part, float4* y, int n4, int splits) {
-    __shared__ float4 red[kRedLanes][kRedOut];
-    const int o = threadIdx.x % kRedOut, l = threadIdx.x / kRedOut;
-    const int i = blockIdx.x * kRedOut + o;
+    constexpr int LANES = 256 / OUT;
+    __shared__ float4 red[LANES][OUT];
+    const int o = threadIdx.x % OUT, l = threadIdx.x / OUT;
+    const int i = blockIdx.x * OUT + o;
     float4 s = {0.f, 0.f, 0.f, 0.f};
     if (i < n4) {
-        for (int k = l; k < splits; k += kRedLanes) {
+#pragma unroll 4
+        for (int k = l; k < splits; k += LANES) {
             const float4 v = part[(size_t)k * n4 + i];
             s.x += v.x;
             s.y += v.y;
@@ -1147,7 +1374,7 @@ __global__ __launch_bounds__(256) void conv_reduce_kernel(const float4* part, fl
     __syncthreads();
     if (l == 0 && i < n4) {
 #pragma unroll
-        for (int j = 1; j < kRedLanes; ++j) {
+        for (int j = 1; j < LANES; ++j) {
             const float4 v = red[j][o];
             s.x += v.x;
             s.y += v.y;
@@ -1156,6 +1383,14 @@ __global__ __launch_bounds__(256) void conv_reduce_kernel(const float4* part, fl
         }
         y[i] = s;
     }
+}
+
+void launch_reduce(const float4* part, float4* y, int n4, int splits, hipStream_t st) {
+    if (splits >= 16 && (n4 + kRedOut - 1) / kRedOut < 512)
+        hipLaunchKernelGGL(conv_reduce_kernel<16>, dim3((n4 + 15) / 16), dim3(256), 0, st, part, y, n4, splits);
+    else
+        hipLaunchKernelGGL(conv_reduce_kernel<kRedOut>, dim3((n4 + kRedOut - 1) / kRedOut), dim3(256), 0, st, part, y,
+                           n4, splits);
 }
 
 // conv_reduce_kernel for a stride-2 parity class: class-ordered partials [splits][M][N]
@@ -1478,6 +1713,48 @@ void launch_x6p(const ConvArgs& a, hipStream_t st) {
     else launch_x6p_tc<32, 128>(a, st);
 }
 
+// Patch weight gradient (MD2_CONV_X6 | MD2_CONV_PATCH): 3x3 stride 1, any Ci % 8 (the
+// last 32-channel group zero-filled), Co % 8
+bool use_x6pw(const md2_conv_desc* d) {
+    return (d->flags & MD2_CONV_PATCH) && use_x6(d, MODE_WGRAD) && d->kernel_h == 3 && d->kernel_w == 3 &&
+           d->stride == 1;
+}
+
+// rows BMW = 32 for Co <= 32 else 64; one block per CU (135 KB LDS); K split by the
+// wave-quantisation model of plan_x6 (a chunk-round ~1.7k cycles)
+constexpr int kX6pwMaxChunks = 64;
+
+void plan_x6pw(ConvArgs& a, uint32_t flags) {
+    const int BMW = a.M <= 32 ? 32 : 64;
+    a.ptc = (a.Wo + 31) / 32;
+    a.nchunks = a.B * a.Ho * a.ptc;
+    const int smin = (a.nchunks + kX6pwMaxChunks - 1) / kX6pwMaxChunks;
+    const int mblocks = (a.M + BMW - 1) / BMW, nblocks = (a.C + XBK - 1) / XBK;
+    const int base = mblocks * nblocks, res = 256;
+    int best_s = 1;
+    double best_t = 1e30;
+    const int smax = std::max(1, a.nchunks / 4);
+    // candidates: no split, and the largest split count that fills k rounds of CUs
+    for (int k = 0; k <= 8; ++k) {
+        const int sp = std::max(smin, std::min(smax, k == 0 ? 1 : std::max(1, k * res / base)));
+        const int per = (a.nchunks + sp - 1) / sp;
+        const int splits = (a.nchunks + per - 1) / per;
+        const int rounds = (base * splits + res - 1) / res;
+        const double red = splits > 1 ? (double)(splits + 1) * a.M * a.N * 4.0 / 2400.0 / 1700.0 + split_launch_cost()
+                                      : 0.0;
+        const double t = (double)rounds * per + red;
+        if (t < best_t - 1e-9) {
+            best_t = t;
+            best_s = splits;
+        }
+    }
+    a.bm = BMW;
+    a.mblocks = mblocks;
+    a.nblocks = nblocks;
+    a.chunks_per_split = (a.nchunks + best_s - 1) / best_s;
+    a.splits = (a.nchunks + a.chunks_per_split - 1) / a.chunks_per_split;
+}
+
 // Stride-2 input gradient on x6 (MD2_CONV_X6, at least 32 output channels): gx pixels
 // of one parity (py, px) receive only the taps kh ≡ py + pad, kw ≡ px + pad (mod 2),
 // each from one gy pixel — a stride-1 GEMM over that class's Ho x Wo grid, scattered
@@ -1571,7 +1848,9 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
     ConvArgs a = (mode == MODE_WGRAD && use_x6(d, mode)) ? args_x6_wgrad(d) : args_of(d, mode);
     if (use_x6(d, mode)) flat_k(a, mode);
     const bool patch = use_x6p(d, mode, a);
+    const bool patch_w = mode == MODE_WGRAD && use_x6pw(d);
     if (patch) plan_x6p(a, d->flags);
+    else if (patch_w) plan_x6pw(a, d->flags);
     else if (use_x6(d, mode)) plan_x6(a, d->flags, mode == MODE_WGRAD);
     else plan(a, d->flags, min_chunks_of(mode));
     const int BN = a.bn;
@@ -1580,7 +1859,11 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
     if ((a.splits > 1 || (use_x6(d, mode) && mode != MODE_WGRAD)) && !ws) return md2_report_error(MD2_ERR_ARG, name);
     a.y = a.splits > 1 ? (float*)ws : out;
     const hipStream_t st = (hipStream_t)stream;
-    if (use_x6(d, mode) && mode == MODE_WGRAD) {
+    if (patch_w) {
+        const dim3 grid(a.mblocks * a.nblocks * a.splits);
+        if (a.bm == 64) hipLaunchKernelGGL(conv_x6pw_kernel<64>, grid, dim3(576), 0, st, a);
+        else hipLaunchKernelGGL(conv_x6pw_kernel<32>, grid, dim3(576), 0, st, a);
+    } else if (use_x6(d, mode) && mode == MODE_WGRAD) {
         const dim3 grid(a.mblocks * a.nblocks * a.splits);
         if (a.bm == 64) hipLaunchKernelGGL(conv_x6_wgrad_kernel<64>, grid, dim3(512), 0, st, a);
         else hipLaunchKernelGGL(conv_x6_wgrad_kernel<128>, grid, dim3(512), 0, st, a);
@@ -1602,8 +1885,7 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
     else launch<MODE_WGRAD>(a, BN, st);
     if (a.splits > 1) {
         const int n4 = a.M * a.N / 4;
-        hipLaunchKernelGGL(conv_reduce_kernel, dim3((n4 + kRedOut - 1) / kRedOut), dim3(256), 0, st, (const float4*)a.y,
-                           (float4*)out, n4, a.splits);
+        launch_reduce((const float4*)a.y, (float4*)out, n4, a.splits, st);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
@@ -1621,6 +1903,10 @@ size_t ws_bytes(const md2_conv_desc* d, int mode) {
         return x6_planes_bytes(d) + part;
     }
     ConvArgs a = (mode == MODE_WGRAD && use_x6(d, mode)) ? args_x6_wgrad(d) : args_of(d, mode);
+    if (mode == MODE_WGRAD && use_x6pw(d)) {
+        plan_x6pw(a, d->flags);
+        return a.splits > 1 ? sizeof(float) * (size_t)a.splits * a.M * a.N : 0;
+    }
     if (use_x6(d, mode) && mode == MODE_WGRAD) {
         plan_x6(a, d->flags, true);
         return a.splits > 1 ? sizeof(float) * (size_t)a.splits * a.M * a.N : 0;

@@ -305,3 +305,37 @@ def test_x6_patch_kernel_is_f32_class(B, C, N, p, H, W):
         assert e < max(3 * eg_mi, 1e-7) and e < 2e-6, (fl, e, eg_mi)
         assert _rel(g, base_g) < 2e-6
         assert torch.equal(conv_ops._fwd(x, w, 1, p, fl), conv_ops._fwd(x, w, 1, p, fl))   # deterministic
+
+
+PATCH_W_SHAPES = [  # (B, Cin, Cout, pad, H, W): segment tails, partial channel groups, Co 16 / 24 / 32 / 128
+    (2, 64, 64, 1, 24, 80),     # 80 columns: two full 32-column segments and a 16-column tail
+    (1, 96, 32, 0, 18, 34),     # decoder conv on a pre-padded input, Co 32 (32-row tile)
+    (2, 16, 16, 1, 20, 70),     # 16 input channels: half a channel group, Co 16
+    (3, 32, 32, 2, 7, 9),       # pad 2, one short segment
+    (2, 128, 128, 1, 12, 40),   # two row blocks x four channel groups
+    (2, 40, 24, 1, 9, 33),      # 40 channels (8 in the second group), Co 24, a 1-column tail
+    (4, 64, 64, 1, 48, 160),    # layer-1 shape: many chunks, K split
+]
+
+
+@pytest.mark.parametrize("B,C,N,p,H,W", PATCH_W_SHAPES)
+def test_x6_patch_wgrad_is_f32_class(B, C, N, p, H, W):
+    """The patch-staged split-bf16 weight gradient (MD2_CONV_PATCH on md2_conv_wgrad:
+    one fetch and split of three input rows per 32-pixel segment, nine shifted tiles)
+    against fp64: f32-class like the per-tap x6 kernel and within 2e-6 of it;
+    deterministic."""
+    torch.manual_seed(41 + C + N + H + W)
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    w = (torch.randn(N, C, 3, 3, device="cuda") / (C * 9) ** 0.5).contiguous(memory_format=CL)
+    gy = torch.randn(F.conv2d(x, w, None, 1, p).shape, device="cuda").contiguous(memory_format=CL)
+    wref = torch.ops.aten.convolution_backward(gy.double().cpu(), x.double().cpu(), w.double().cpu(), None, (1, 1),
+                                               (p, p), (1, 1), False, (0, 0), 1, (False, True, False))[1]
+    w_mi = torch.ops.aten.convolution_backward(gy, x, w, None, (1, 1), (p, p), (1, 1), False, (0, 0), 1,
+                                               (False, True, False))[1].double().cpu()
+    e_mi = _rel(w_mi, wref)
+    fl = conv_ops.X6 | conv_ops.PATCH
+    gw = conv_ops._wgrad(gy, x, w, 1, p, fl)
+    e = _rel(gw.double().cpu(), wref)
+    assert e < max(3 * e_mi, 1e-7) and e < 2e-6, (e, e_mi)
+    assert _rel(gw.double().cpu(), conv_ops._wgrad(gy, x, w, 1, p, conv_ops.X6).double().cpu()) < 2e-6
+    assert torch.equal(gw, conv_ops._wgrad(gy, x, w, 1, p, fl))

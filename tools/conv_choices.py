@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("out", nargs="?", default=None)
     args = ap.parse_args()
-    sys.argv = [sys.argv[0], "--batch", str(args.batch)]
+    sys.argv = [sys.argv[0], "--batch", str(args.batch), "--graph", "0"]
     import bench
     from monodepth2_amd.data import synthetic_batch
     bargs = bench.parse()
