@@ -131,6 +131,13 @@ __device__ __forceinline__ float div3(float x) {
     return fmaf(fmaf(-3.0f, q, x), c, q);
 }
 
+// k / 255 correctly rounded for integer k in 0..255 (3 ops; the 8-bit copies' decode)
+__device__ __forceinline__ float div255(float k) {
+    const float c = 1.0f / 255.0f;
+    const float q = k * c;
+    return fmaf(fmaf(-255.0f, q, k), c, q);
+}
+
 __device__ __forceinline__ float signf(float v) { return (v > 0.f) ? 1.f : ((v < 0.f) ? -1.f : 0.f); }
 
 // Tie-break noise of the forward (trainer.py:468 draws N(0,1) * 1e-5 per
@@ -497,13 +504,16 @@ __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int 
 // Forward: two launches.
 //   photo_ident_kernel    identity losses of every source frame, once per step
 //                         (scale-invariant, trainer.py:432-439) -> identity planes
-//   photo_fwdloss_kernel  one wave per (image, 16-row block, strip, scale): window
-//                         depths once, then per frame warp + SSIM/L1 (trainer.py:
-//                         426-430) folded straight into the per-pixel minimum over the
-//                         identity (+ noise) and reprojection candidates (466-482),
-//                         automask code, one partial sum per wave
+//   photo_fwdall_kernel   one wave per (image, 16-row block, strip, scale): window
+//                         depths once, then one walk down the rows evaluating every
+//                         frame's warp + SSIM/L1 (trainer.py:426-430) with the target's
+//                         terms shared, each output row reduced at once to the minimum
+//                         over the identity (+ noise) and reprojection candidates
+//                         (466-482), automask code, one partial sum per wave
 // A 16-row item evaluates 18 rows (1.125x).  Round 2 wrote every reprojection loss
-// as a plane (47 MB at B=12) and re-read it in a third launch; those planes are gone.
+// as a plane (47 MB at B=12) and re-read it in a third launch; those planes are gone,
+// and since round 3 the frames no longer walk the rows one after the other through a
+// running minimum in LDS (137 -> 124 us at B=12).
 // ----------------------------------------------------------------------------
 constexpr int kRowsP = 16;   // output rows per item of the forward passes
 
@@ -604,132 +614,182 @@ __global__ __launch_bounds__(kBlock) void photo_ident_kernel(PhotoArgs a) {
     });
 }
 
-// The reprojection losses of every source frame at one scale and the per-pixel
-// minimum over cat(identity + 1e-5 noise, reprojection) (trainer.py:426-482) in one
-// wave per (image, 16-row block, 62-column strip, scale): the window depths are staged
-// once in LDS and shared by the frames; for each frame in order the wave walks the
-// rows and folds every pixel's loss into its running minimum (LDS, one column per
-// lane), so no loss plane goes to memory.  Candidate order and tie rule as torch.min
-// over the concatenation: identity candidates first, then frame by frame, a strictly
-// smaller value replaces the minimum (the first index wins ties).  One partial sum of
-// the minima per wave, folded in wave order by finalize_fwd_kernel (deterministic).
-// LDS per wave (dynamic, fwdloss_lds_bytes): window depths [kRowsP+2][64], running
-// minimum [kRowsP][64], argmin code [kRowsP][64] bytes, and with avg_reprojection the
-// running sum of the frames' losses [kRowsP][64] (9.7 KB, 13.8 KB with avg: 4 / 2
-// blocks per CU)
-__host__ __device__ constexpr int fwdloss_wave_floats(bool avg) { return (kRowsP + 2 + kRowsP + (avg ? kRowsP : 0)) * kWave; }
-__host__ __device__ constexpr size_t fwdloss_lds_bytes(bool avg) {
-    return (size_t)kWavesPerBlock * (fwdloss_wave_floats(avg) * sizeof(float) + kRowsP * kWave);
+// ----------------------------------------------------------------------------
+// All-frames forward walk (photo_fwdall_kernel): one pass down the window rows per
+// (image, 16-row block, strip, scale) item evaluating every source frame at each row.
+// Per row the target's colours, their horizontal sums and the camera ray are formed
+// once (not once per frame), the frames' gathers of a row are in flight together, and
+// each output row's candidates — identity (+ noise), then the frames in order — are
+// reduced to the minimum at once, so no running minimum goes through LDS.
+// Arithmetic per frame as frow_eval / ssim_from_sums (the same expressions).
+// ----------------------------------------------------------------------------
+template <int NS>
+struct FRowA {
+    float y[3], hy[3], hyy[3];                          // target colour, 3-tap sums of y, y^2
+    float x[NS][3], hx[NS][3], hxx[NS][3], hxy[NS][3];  // per frame: warped colour, sums of x, x^2, x*y
+};
+
+template <int NS, bool SSIM_ON, bool U8>
+__device__ __forceinline__ void frowa_eval(const WarpCtx (&c)[NS], const float* tgt, float depth, int rr, int cc,
+                                           FRowA<NS>& o) {
+    const int HW = c[0].h * c[0].w;
+    const float fx = (float)cc, fy = (float)rr;
+    float ray[3], pt[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        ray[i] = c[0].cm.iK[i * 3 + 0] * fx + c[0].cm.iK[i * 3 + 1] * fy + c[0].cm.iK[i * 3 + 2];
+        pt[i] = depth * ray[i];
+    }
+    float yl[3], yr[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        o.y[ch] = ldf(tgt, ch * HW + rr * c[0].w + cc);
+        if (SSIM_ON) {
+            yl[ch] = shfl_prev(o.y[ch]);
+            yr[ch] = shfl_next(o.y[ch]);
+            o.hy[ch] = yl[ch] + o.y[ch] + yr[ch];
+            o.hyy[ch] = yl[ch] * yl[ch] + o.y[ch] * o.y[ch] + yr[ch] * yr[ch];
+        }
+    }
+#pragma unroll
+    for (int f = 0; f < NS; ++f) {
+        FastSample s;
+        s.depth = depth;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            s.ray[i] = ray[i];
+            s.pt[i] = pt[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            s.cam[i] = c[f].cm.P[i * 4 + 0] * s.pt[0] + c[f].cm.P[i * 4 + 1] * s.pt[1] +
+                       c[f].cm.P[i * 4 + 2] * s.pt[2] + c[f].cm.P[i * 4 + 3];
+        s.inv_den = rcpf(s.cam[2] + 1e-7f);
+        s.px = s.cam[0] * s.inv_den;
+        s.py = s.cam[1] * s.inv_den;
+        const float ix = s.px * c[f].sx - 0.5f, iy = s.py * c[f].sy - 0.5f;
+        const float xmax = (float)(c[f].w - 1), ymax = (float)(c[f].h - 1);
+        const float ixc = fminf(fmaxf(ix, 0.f), xmax), iyc = fminf(fmaxf(iy, 0.f), ymax);
+        const float fx0 = floorf(ixc), fy0 = floorf(iyc);
+        s.x0 = (int)fx0;
+        s.y0 = (int)fy0;
+        s.tx = ixc - fx0;
+        s.ty = iyc - fy0;
+        Corners v;
+        gather<U8>(c[f], s, v);
+        interp<U8>(s, v, o.x[f]);
+        if (SSIM_ON) {
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                const float x = o.x[f][ch], xl = shfl_prev(x), xr = shfl_next(x);
+                o.hx[f][ch] = xl + x + xr;
+                o.hxx[f][ch] = xl * xl + x * x + xr * xr;
+                o.hxy[f][ch] = xl * yl[ch] + x * o.y[ch] + xr * yr[ch];
+            }
+        }
+    }
 }
 
-template <int NS, bool SSIM_ON, bool MASK>
-__global__ __launch_bounds__(kBlock) void photo_fwdloss_kernel(PhotoArgs a) {
-    extern __shared__ float fwd_smem[];
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
-    const bool avg = (a.flags & MD2_AVG_REPROJECTION) != 0;
-    float* wbase = fwd_smem + wid * fwdloss_wave_floats(avg);
-    float (*dep)[kWave] = (float (*)[kWave])wbase;
-    float (*best)[kWave] = (float (*)[kWave])(wbase + (kRowsP + 2) * kWave);
-    float (*acc)[kWave] = (float (*)[kWave])(wbase + (2 * kRowsP + 2) * kWave);   // avg only
-    uint8_t (*code)[kWave] = (uint8_t (*)[kWave])((uint8_t*)(fwd_smem + kWavesPerBlock * fwdloss_wave_floats(avg))
-                                                 + wid * kRowsP * kWave);
-    const int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
-    const int wv = __builtin_amdgcn_readfirstlane(blk * kWavesPerBlock + wid);
-    if (wv >= a.B * a.wpi * a.nsc) return;
-    // item order: scale fastest, so the waves sharing a strip's rows run together
-    const int ls = wv % a.nsc;
-    const int item = wv / a.nsc;
-    const FItem it = fitem(a, item, lane);
+// reprojection loss of frame f at the middle row of (A, B, C) (as frow_loss)
+template <int NS, bool SSIM_ON>
+__device__ __forceinline__ void frowa_losses(const FRowA<NS>& A, const FRowA<NS>& B, const FRowA<NS>& C,
+                                             float (&loss)[NS]) {
+    float my[3], sy[3];
+    if (SSIM_ON) {
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            my[ch] = (A.hy[ch] + B.hy[ch] + C.hy[ch]) * kInv9;
+            sy[ch] = (A.hyy[ch] + B.hyy[ch] + C.hyy[ch]) * kInv9 - my[ch] * my[ch];
+        }
+    }
+#pragma unroll
+    for (int f = 0; f < NS; ++f) {
+        float ss = 0.f, l1 = 0.f;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            if (SSIM_ON) {
+                const float mx = (A.hx[f][ch] + B.hx[f][ch] + C.hx[f][ch]) * kInv9;
+                const float sx = (A.hxx[f][ch] + B.hxx[f][ch] + C.hxx[f][ch]) * kInv9 - mx * mx;
+                const float sxy = (A.hxy[f][ch] + B.hxy[f][ch] + C.hxy[f][ch]) * kInv9 - mx * my[ch];
+                const float n = (2.f * mx * my[ch] + kC1) * (2.f * sxy + kC2);
+                const float d = (mx * mx + my[ch] * my[ch] + kC1) * (sx + sy[ch] + kC2);
+                ss += fminf(fmaxf((1.f - n * rcpf(d)) * 0.5f, 0.f), 1.f);
+            }
+            l1 += fabsf(B.y[ch] - B.x[f][ch]);
+        }
+        loss[f] = SSIM_ON ? 0.85f * div3(ss) + 0.15f * div3(l1) : div3(l1);
+    }
+}
+
+template <int NS, bool SSIM_ON, bool MASK, bool U8>
+__device__ __forceinline__ float fwdall_walk(const PhotoArgs& a, const WarpCtx (&ctx)[NS], const FItem& it, int ls,
+                                             const float (*dep)[kWave], int lane) {
     const int h = a.h, w = a.w, HW = h * w;
     const bool automask = !(a.flags & MD2_NO_AUTOMASK);
+    const bool avg = (a.flags & MD2_AVG_REPROJECTION) != 0;
     const int C = avg ? 1 : NS;
-    // identity candidates + tie-break noise (trainer.py:466-471)
-    {
-        const uint64_t seed = a.seed_ptr ? (a.seed ^ (*a.seed_ptr * 0x9E3779B97F4A7C15ULL)) : a.seed;
-        const uint32_t key = noise_key(seed, a.gscale[ls]);
-        const float* nz = a.noise[ls];
-#pragma unroll 1
-        for (int i = 0; i < kRowsP; ++i) {
-            const int r = it.r0 + i;
-            float bv = INFINITY;
-            int bc = 0;
-            if (automask && it.colok && r < h) {
-                const int p = r * w + it.c;
-                float nv[NS];
-                if (nz) {
-#pragma unroll
-                    for (int ch = 0; ch < NS; ++ch) nv[ch] = ch < C ? nz[((size_t)it.b * C + ch) * HW + p] : 0.f;
-                } else {
-#pragma unroll
-                    for (int j = 0; 2 * j < NS; ++j) {
-                        const float2 n2 = noise_pair(key, (uint32_t)(it.b * HW + p), j);
-                        nv[2 * j] = n2.x;
-                        if (2 * j + 1 < NS) nv[2 * j + 1] = n2.y;
-                    }
-                }
-                float id[NS];
-#pragma unroll
-                for (int f = 0; f < NS; ++f) id[f] = a.ident[((size_t)f * a.B + it.b) * HW + p];
-                for (int ch = 0; ch < C; ++ch) {
-                    float v;
-                    if (avg) {
-                        v = 0.f;
-#pragma unroll
-                        for (int f = 0; f < NS; ++f) v += id[f];
-                        v = v / (float)NS;
-                    } else {
-                        v = id[ch];
-                    }
-                    v = v + nv[ch] * 1e-5f;
-                    if (v < bv) {
-                        bv = v;
-                        bc = ch;
-                    }
-                }
-            }
-            best[i][lane] = bv;
-            code[i][lane] = (uint8_t)bc;
-            if (avg) acc[i][lane] = 0.f;
-        }
-    }
-    WarpCtx ctx;
-    make_ctx(a, ls, 0, it.b, ctx);
-#pragma unroll
-    for (int k = 0; k < kRowsP + 2; ++k) dep[k][lane] = depth_at(ctx, reflect_clamp(it.r0 - 1 + k, h), it.cc);
+    const uint64_t seed = a.seed_ptr ? (a.seed ^ (*a.seed_ptr * 0x9E3779B97F4A7C15ULL)) : a.seed;
+    const uint32_t key = noise_key(seed, a.gscale[ls]);
+    const float* nz = a.noise[ls];
     const float* tgt = a.tgt + (size_t)it.b * 3 * HW;
-#pragma unroll 1
-    for (int f = 0; f < NS; ++f) {
-        if (f > 0) {   // the frame's source and pose; the depths are shared
-            ctx.src = a.src[f] + (size_t)it.b * 3 * HW;
-            ctx.src8 = (a.src8[f] && a.exact[f * a.B + it.b]) ? a.src8[f] + (size_t)it.b * HW : nullptr;
-            load_cam(ctx.cm, a.K + it.b * 16, a.iK + it.b * 16, a.T[ls] + ((size_t)f * a.B + it.b) * 16);
-        }
-        const float* pmask = MASK ? a.mask[ls] + ((size_t)it.b * NS + f) * HW : nullptr;
-        const int fcode = (automask ? NS : 0) + f;
-        auto emit = [&](int i, float v) {
-            const int r = it.r0 + i;
-            if (MASK && it.colok && r < h) v *= pmask[r * w + it.c];  // trainer.py:455
-            if (avg) {
-                acc[i][lane] += v;
-            } else if (v < best[i][lane]) {
-                best[i][lane] = v;
-                code[i][lane] = (uint8_t)fcode;
-            }
-        };
-        if (ctx.src8)   // wave-uniform: this image's sources are 8-bit exact
-            loss_rows<SSIM_ON, true, true>(ctx, tgt, dep, it.r0, it.cc, lane, emit);
-        else
-            loss_rows<SSIM_ON, true, false>(ctx, tgt, dep, it.r0, it.cc, lane, emit);
-    }
-    float lsum = 0.f;
     uint8_t* sel = a.sel[ls] + (size_t)it.b * HW;
-#pragma unroll 1
-    for (int i = 0; i < kRowsP; ++i) {
+    float lsum = 0.f;
+    // output row i = window row k - 2 from rows (k-2, k-1, k)
+    auto out_row = [&](int i, const FRowA<NS>& A, const FRowA<NS>& B, const FRowA<NS>& Cr) {
+        float lf[NS];
+        frowa_losses<NS, SSIM_ON>(A, B, Cr, lf);
         const int r = it.r0 + i;
-        float bv = best[i][lane];
-        int bc = code[i][lane];
+        if (!(it.colok && r < h)) return;
+        const int p = r * w + it.c;
+        float bv = INFINITY;
+        int bc = 0;
+        if (automask) {   // identity candidates + tie-break noise (trainer.py:466-471)
+            float nv[NS];
+            if (nz) {
+#pragma unroll
+                for (int ch = 0; ch < NS; ++ch) nv[ch] = ch < C ? nz[((size_t)it.b * C + ch) * HW + p] : 0.f;
+            } else {
+#pragma unroll
+                for (int j = 0; 2 * j < NS; ++j) {
+                    const float2 n2 = noise_pair(key, (uint32_t)(it.b * HW + p), j);
+                    nv[2 * j] = n2.x;
+                    if (2 * j + 1 < NS) nv[2 * j + 1] = n2.y;
+                }
+            }
+            float id[NS];
+#pragma unroll
+            for (int f = 0; f < NS; ++f) id[f] = a.ident[((size_t)f * a.B + it.b) * HW + p];
+            for (int ch = 0; ch < C; ++ch) {
+                float v;
+                if (avg) {
+                    v = 0.f;
+#pragma unroll
+                    for (int f = 0; f < NS; ++f) v += id[f];
+                    v = v / (float)NS;
+                } else {
+                    v = id[ch];
+                }
+                v = v + nv[ch] * 1e-5f;
+                if (v < bv) {
+                    bv = v;
+                    bc = ch;
+                }
+            }
+        }
+        float accv = 0.f;
+#pragma unroll
+        for (int f = 0; f < NS; ++f) {
+            float v = lf[f];
+            if (MASK) v *= a.mask[ls][((size_t)it.b * NS + f) * HW + p];   // trainer.py:455
+            if (avg) {
+                accv += v;
+            } else if (v < bv) {
+                bv = v;
+                bc = (automask ? NS : 0) + f;
+            }
+        }
         if (avg) {
-            const float ra = acc[i][lane] / (float)NS;
+            const float ra = accv / (float)NS;
             if (automask) {
                 if (ra < bv) {
                     bv = ra;
@@ -739,13 +799,48 @@ __global__ __launch_bounds__(kBlock) void photo_fwdloss_kernel(PhotoArgs a) {
                 bv = ra;
             }
         }
-        if (it.colok && r < h) {
-            lsum += bv;
-            sel[r * w + it.c] = (uint8_t)bc;
-        }
+        lsum += bv;
+        sel[p] = (uint8_t)bc;
+    };
+    FRowA<NS> R0, R1, R2;
+    static_assert((kRowsP + 2) % 3 == 0, "window rows must be a multiple of 3");
+#pragma unroll 1
+    for (int k = 0; k < kRowsP + 2; k += 3) {
+        frowa_eval<NS, SSIM_ON, U8>(ctx, tgt, dep[k][lane], reflect_clamp(it.r0 - 1 + k, h), it.cc, R0);
+        if (k >= 2) out_row(k - 2, R1, R2, R0);
+        frowa_eval<NS, SSIM_ON, U8>(ctx, tgt, dep[k + 1][lane], reflect_clamp(it.r0 + k, h), it.cc, R1);
+        if (k >= 1) out_row(k - 1, R2, R0, R1);
+        frowa_eval<NS, SSIM_ON, U8>(ctx, tgt, dep[k + 2][lane], reflect_clamp(it.r0 + 1 + k, h), it.cc, R2);
+        out_row(k, R0, R1, R2);
     }
+    return lsum;
+}
+
+template <int NS, bool SSIM_ON, bool MASK>
+__global__ __launch_bounds__(kBlock) void photo_fwdall_kernel(PhotoArgs a) {
+    __shared__ float dep_s[kWavesPerBlock][kRowsP + 2][kWave];
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
+    float (*dep)[kWave] = dep_s[wid];
+    const int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int wv = __builtin_amdgcn_readfirstlane(blk * kWavesPerBlock + wid);
+    if (wv >= a.B * a.wpi * a.nsc) return;
+    const int ls = wv % a.nsc;   // scale fastest: the waves sharing a strip's rows run together
+    const int item = wv / a.nsc;
+    const FItem it = fitem(a, item, lane);
+    WarpCtx ctx[NS];
+    bool u8 = true;
+#pragma unroll
+    for (int f = 0; f < NS; ++f) {
+        make_ctx(a, ls, f, it.b, ctx[f]);
+        u8 = u8 && ctx[f].src8 != nullptr;
+    }
+#pragma unroll
+    for (int k = 0; k < kRowsP + 2; ++k) dep[k][lane] = depth_at(ctx[0], reflect_clamp(it.r0 - 1 + k, a.h), it.cc);
+    // every frame's sources 8-bit exact (wave-uniform), else all frames on the fp32 planes
+    const float lsum = u8 ? fwdall_walk<NS, SSIM_ON, MASK, true>(a, ctx, it, ls, dep, lane)
+                          : fwdall_walk<NS, SSIM_ON, MASK, false>(a, ctx, it, ls, dep, lane);
     const float t = wave_sum(lsum);
-    if (lane == 0) a.photo_part[ls][item] = t;   // item = (b * rowblocks + rb) * strips + st
+    if (lane == 0) a.photo_part[ls][item] = t;
 }
 
 // 8-bit source copies: every source colour x with x == RN(k/255) for k = rint(255 x)
@@ -758,12 +853,6 @@ struct PackArgs {
     uint32_t* out;                   // [S][B][HW]
     int* exact;                      // [S][B], preset to nonzero
 };
-
-__device__ __forceinline__ float div255(float k) {
-    const float c = 1.0f / 255.0f;
-    const float q = k * c;
-    return fmaf(fmaf(-255.0f, q, k), c, q);
-}
 
 __global__ __launch_bounds__(kBlock) void pack_src8_kernel(PackArgs a) {
     const int per_img = (a.HW + 4 * kBlock - 1) / (4 * kBlock);
@@ -1743,9 +1832,8 @@ void launch_fwd_t(const PhotoArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t 
         hipExtLaunchKernelGGL((photo_ident_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, e0, nullptr, 0, a);
     }
     const int rblocks = (a.B * a.wpi * a.nsc + kWavesPerBlock - 1) / kWavesPerBlock;
-    hipExtLaunchKernelGGL((photo_fwdloss_kernel<NS, SSIM, MASK>), dim3(rblocks), dim3(kBlock),
-                          fwdloss_lds_bytes((a.flags & MD2_AVG_REPROJECTION) != 0), st, automask ? nullptr : e0, e1,
-                          0, a);
+    hipExtLaunchKernelGGL((photo_fwdall_kernel<NS, SSIM, MASK>), dim3(rblocks), dim3(kBlock), 0, st,
+                          automask ? nullptr : e0, e1, 0, a);
 }
 // number of workgroups that can be resident at once for a kernel (cached per
 // kernel and device); the persistent-loop kernels launch exactly that many
