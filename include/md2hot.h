@@ -471,9 +471,13 @@ int md2_maxpool3s2_bwd_add(const md2_pool_desc* desc, const uint32_t* idx, const
 #define MD2_CONV_X6        (1u << 5) /* split-bf16 (3 planes, 6 products) f32-class MFMA path */
 #define MD2_CONV_BM256     (1u << 6) /* x6 forward / input grad: 256 x 128 tiles (N > 64)     */
 #define MD2_CONV_PRESPLIT  (1u << 7) /* x6: `weight` holds md2_conv_split_weights planes      */
-#define MD2_CONV_PATCH     (1u << 8) /* x6 3x3 stride-1 fwd / dgrad, channels % 32 == 0: the
-                                        input patch of a pixel rectangle staged once for all
-                                        nine taps (conv_x6p_kernel)                         */
+#define MD2_CONV_PATCH     (1u << 8) /* x6 3x3 stride 1: fwd / dgrad (GEMM channels % 32) with
+                                        the input patch of a pixel rectangle staged once for
+                                        all nine taps (conv_x6p_kernel); the weight gradient
+                                        with three input rows per 32-pixel segment staged
+                                        once for the nine taps (conv_x6pw_kernel)           */
+#define MD2_CONV_S2_ONE    (1u << 9) /* x6 stride-2 input gradient: the four parity classes
+                                        in one launch, no K split                           */
 
 typedef struct md2_conv_desc {
     int32_t batch, height, width, in_channels; /* input */

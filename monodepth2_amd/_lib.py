@@ -113,6 +113,7 @@ CONV_X6 = 1 << 5
 CONV_BM256 = 1 << 6
 CONV_PRESPLIT = 1 << 7
 CONV_PATCH = 1 << 8
+CONV_S2_ONE = 1 << 9
 
 
 class ConvDesc(ctypes.Structure):

@@ -47,18 +47,23 @@ X6 = _lib.CONV_X6
 BM256 = _lib.CONV_BM256
 PRESPLIT = _lib.CONV_PRESPLIT
 PATCH = _lib.CONV_PATCH
-_FLAGS = (X6, X6 | BM256)    # the x6 candidates, in candidate order
-_PFLAGS = (X6 | PATCH, X6 | PATCH | BM256)   # + the patch-staged ones where the shape fits
-_XNAMES = ("x6", "x6_256", "x6p", "x6p_256")
+S2_ONE = _lib.CONV_S2_ONE
+NO_SPLIT = _lib.CONV_NO_SPLIT
+# the x6 candidates, in candidate order: 128 / 256-row tiles, each with the planner's K
+# split and without one (the split's partials round trip is timed, not modelled)
+_FLAGS = (X6, X6 | BM256, X6 | NO_SPLIT, X6 | BM256 | NO_SPLIT)
+_PFLAGS = (X6 | PATCH, X6 | PATCH | BM256, X6 | PATCH | NO_SPLIT, X6 | PATCH | BM256 | NO_SPLIT)
+_NAMES_X6 = ("x6", "x6_256", "x6_ns", "x6_256_ns")
+_NAMES_X6P = ("x6p", "x6p_256", "x6p_ns", "x6p_256_ns")
 
 
 def _x6_flags(gemm_c: int, k: int, stride: int, n_out: int):
     """The x6 flag variants for a forward / stride-1 input gradient whose GEMM reads
-    gemm_c channels: the patch kernel needs 3x3, stride 1, gemm_c % 32 == 0 and more
-    than 16 GEMM columns (csrc/conv.hip use_x6p)."""
+    gemm_c channels, and their candidate names: the patch kernel needs 3x3, stride 1,
+    gemm_c % 32 == 0 and more than 16 GEMM columns (csrc/conv.hip use_x6p)."""
     if k == 3 and stride == 1 and gemm_c % 32 == 0 and n_out > 16:
-        return _FLAGS + _PFLAGS
-    return _FLAGS
+        return _FLAGS + _PFLAGS, _NAMES_X6 + _NAMES_X6P
+    return _FLAGS, _NAMES_X6
 
 
 def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
@@ -312,7 +317,7 @@ class _Conv(torch.autograd.Function):
         ctx.stride, ctx.pad = stride, pad
         ctx.key = (tuple(x.shape), tuple(weight.shape), stride, pad)
         x6 = _x6_ok(x, weight)
-        xf = _x6_flags(x.shape[1], weight.shape[2], stride, weight.shape[0]) if x6 else ()
+        xf, xn = _x6_flags(x.shape[1], weight.shape[2], stride, weight.shape[0]) if x6 else ((), ())
         cands = None
         i = _cached("fwd", ctx.key)
         if i is None or not (x6 and i < len(xf)):
@@ -321,7 +326,7 @@ class _Conv(torch.autograd.Function):
                 [lambda: _fwd(x, weight, stride, pad)] + \
                 ([lambda: _direct_fwd(x, weight, pad)] if direct else []) + \
                 [lambda: F.conv2d(x, weight, None, stride, pad)]
-            names = list(_XNAMES[:len(xf)]) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"]
+            names = list(xn) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"]
             if i is None:
                 i = _fastest("fwd", ctx.key, cands, names)
         planes_dg = None
@@ -347,12 +352,12 @@ class _Conv(torch.autograd.Function):
             if s == 1:
                 x6 = _x6_ok(x, w)
                 # the input gradient's GEMM reads gy: out_channels channels, in_channels columns
-                xf = _x6_flags(w.shape[0], w.shape[2], 1, w.shape[1]) if x6 else ()
+                xf, xn = _x6_flags(w.shape[0], w.shape[2], 1, w.shape[1]) if x6 else ((), ())
                 direct = _direct_ok(w.shape[0], w.shape[1], w.shape[2], s)
                 cands = [(lambda f=f: _dgrad(gy, x, w, p, f)) for f in xf] + \
                     [lambda: _dgrad(gy, x, w, p)] + ([lambda: _direct_dgrad(gy, w, p)] if direct else []) + \
                     [lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
-                names = list(_XNAMES[:len(xf)]) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"]
+                names = list(xn) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"]
                 i = _fastest("dgrad", ctx.key, cands, names)
                 if x6 and i < len(xf) and planes_dg is not None:
                     gx = _dgrad_planes(gy, x, w, planes_dg, p, xf[i])
@@ -361,11 +366,13 @@ class _Conv(torch.autograd.Function):
                 else:
                     mi_x = True
             elif _x6_s2_ok(x, w, s):
-                cands = [lambda: _dgrad(gy, x, w, p, X6, 2),
-                         lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
-                i = _fastest("dgrad", ctx.key, cands, ["x6_s2", "miopen"])
-                if i == 0:
-                    gx = (_dgrad_planes(gy, x, w, planes_dg, p, X6, 2) if planes_dg is not None else cands[0]())
+                # per-class launches (K split) / the four classes in one launch
+                sf = (X6, X6 | S2_ONE)
+                cands = [(lambda f=f: _dgrad(gy, x, w, p, f, 2)) for f in sf] + \
+                    [lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
+                i = _fastest("dgrad", ctx.key, cands, ["x6_s2", "x6_s2one", "miopen"])
+                if i < len(sf):
+                    gx = (_dgrad_planes(gy, x, w, planes_dg, p, sf[i], 2) if planes_dg is not None else cands[i]())
                 else:
                     mi_x = True
             else:

@@ -131,28 +131,36 @@ __global__ void __launch_bounds__(kThreads) bn_stats_kernel(const void* __restri
     }
 }
 
-// One block per channel: fixed-order double sums of its G partial pairs (strided
-// over the block, then an LDS tree).  Returns the sums in thread 0.
+// One block per channel: fixed-order double sums of its G partial pairs — thread t
+// sums rows t, t + 256, ... in order, a fixed xor butterfly per wave, then the four wave
+// sums in wave order (one barrier; an 8-level LDS tree cost ~1.5 us of the ~6 us
+// launch, and a single wave per channel had too few loads in flight).  Returns the
+// sums in thread 0.
 __device__ bool channel_sums(Work w, int rows, int r0, int G, int C, int c, double& a, double& b) {
-    __shared__ double red[2][kThreads];
+    __shared__ double red[2][kThreads / 64];
     a = 0.0;
     b = 0.0;
     for (int g = threadIdx.x; g < G; g += kThreads) {
         a += w.part[(size_t)(r0 + g) * C + c];
         b += w.part[((size_t)rows + r0 + g) * C + c];
     }
-    red[0][threadIdx.x] = a;
-    red[1][threadIdx.x] = b;
-    __syncthreads();
-    for (int half = kThreads / 2; half > 0; half /= 2) {
-        if (threadIdx.x < half) {
-            red[0][threadIdx.x] += red[0][threadIdx.x + half];
-            red[1][threadIdx.x] += red[1][threadIdx.x + half];
-        }
-        __syncthreads();
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        b += __shfl_xor(b, o, 64);
     }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = a;
+        red[1][threadIdx.x >> 6] = b;
+    }
+    __syncthreads();
     a = red[0][0];
     b = red[1][0];
+#pragma unroll
+    for (int i = 1; i < kThreads / 64; ++i) {
+        a += red[0][i];
+        b += red[1][i];
+    }
     __syncthreads();   // red is reused by the next group
     return threadIdx.x == 0;
 }

@@ -72,6 +72,11 @@ struct ConvArgs {
     int flatk;               // x6 fwd / dgrad with C < 32: K chunks run over the flattened
                              // (tap, channel) index, several taps per chunk
     int ptr, ptc;            // patch kernel (conv_x6p_kernel): output tiles per image, rows / columns
+    // conv_x6_kernel over several stride-2 parity classes in one launch (ncls > 0): the
+    // blocks of class c start at cls_blk[c]; per class the fields above it replaces
+    int ncls;
+    int cls_blk[4], cls_py[4], cls_px[4], cls_kh0[4], cls_kw0[4], cls_ntw[4], cls_dy0[4], cls_dx0[4], cls_Ho[4],
+        cls_Wo[4], cls_nchunks[4];
     const float* a;          // fwd: x; dgrad: gy; wgrad: x
     const float* b;          // fwd / dgrad: weight; wgrad: gy
     float* y;                // output [M][N], or partials [splits][M][N]
@@ -490,7 +495,7 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, int v
 // and stride-1 input gradient alike (ConvArgs as the f32 path builds them; b = the
 // planes).
 template <int BN, int BMX>
-__global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void conv_x6_kernel(ConvArgs a) {
+__global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void conv_x6_kernel(ConvArgs a_) {
     using G = X6Geo<BN, BMX>;
     constexpr int NT = G::NT, TM = G::TM;
     constexpr int AQ = BMX * XBK / 4 / NT;         // f32 quads of A per thread
@@ -503,6 +508,30 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / G::WN, wn = wid % G::WN;
     int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    ConvArgs a = a_;
+    if (a.ncls > 0) {   // this block's parity class (constant-index selects: no scratch array)
+        int c = 0;
+#pragma unroll
+        for (int i = 1; i < 4; ++i) c += (i < a.ncls && blk >= a.cls_blk[i]) ? 1 : 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (i == c) {
+                blk -= a.cls_blk[i];
+                a.py = a.cls_py[i];
+                a.px = a.cls_px[i];
+                a.kh0 = a.cls_kh0[i];
+                a.kw0 = a.cls_kw0[i];
+                a.ntw = a.cls_ntw[i];
+                a.dy0 = a.cls_dy0[i];
+                a.dx0 = a.cls_dx0[i];
+                a.Ho = a.cls_Ho[i];
+                a.Wo = a.cls_Wo[i];
+                a.nchunks = a.cls_nchunks[i];
+            }
+        a.M = a.B * a.Ho * a.Wo;
+        a.mblocks = (a.M + BMX - 1) / BMX;
+        a.chunks_per_split = a.nchunks;
+    }
     const int nb = blk % a.nblocks;
     blk /= a.nblocks;
     const int mb = blk % a.mblocks, ks = blk / a.mblocks;
@@ -1760,7 +1789,7 @@ void plan_x6pw(ConvArgs& a, uint32_t flags) {
 // each from one gy pixel — a stride-1 GEMM over that class's Ho x Wo grid, scattered
 // into gx.  Four launches (a 1x1 stride-2 convolution's odd classes have no taps: they
 // run with no chunks and write zeros).  false: the class is empty.
-bool dgrad_s2_class(const md2_conv_desc* d, int py, int px, ConvArgs& a) {
+bool dgrad_s2_class(const md2_conv_desc* d, int py, int px, ConvArgs& a, uint32_t extra_flags = 0) {
     const Shape s = shape_of(d);
     a = ConvArgs{};
     a.KH = s.KH;
@@ -1789,7 +1818,7 @@ bool dgrad_s2_class(const md2_conv_desc* d, int py, int px, ConvArgs& a) {
     a.b_elems = 3 * s.N * s.KH * s.KW * s.C;
     const int taps = nth * ntw;
     a.nchunks = taps > 0 ? taps * ((s.N + XBK - 1) / XBK) : 1;
-    plan_x6(a, d->flags);
+    plan_x6(a, d->flags | extra_flags);
     if (taps == 0) {   // zeros: no chunks, no split
         a.nchunks = 0;
         a.chunks_per_split = 0;
@@ -1824,6 +1853,44 @@ int run_dgrad_s2(const md2_conv_desc* d, const float* gy, const float* w, float*
                                                         d->in_channels, st);
         if (me != hipSuccess) return md2_report_error(MD2_ERR_HIP, hipGetErrorString(me));
     }
+    if (d->flags & MD2_CONV_S2_ONE) {
+        // one launch over the classes with taps, heaviest class first, no K split
+        ConvArgs m;
+        int nc = 0, blocks = 0;
+        int order[4] = {0, 1, 2, 3}, taps[4] = {0, 0, 0, 0};
+        ConvArgs cl[4];
+        for (int c = 0; c < 4; ++c)
+            if (dgrad_s2_class(d, c >> 1, c & 1, cl[c], MD2_CONV_NO_SPLIT)) taps[c] = cl[c].nchunks;
+        std::sort(order, order + 4, [&](int x, int y) { return taps[x] > taps[y] || (taps[x] == taps[y] && x < y); });
+        for (int k = 0; k < 4; ++k) {
+            const int c = order[k];
+            if (taps[c] == 0) continue;
+            const ConvArgs& a = cl[c];
+            if (nc == 0) m = a;
+            m.cls_blk[nc] = blocks;
+            m.cls_py[nc] = a.py;
+            m.cls_px[nc] = a.px;
+            m.cls_kh0[nc] = a.kh0;
+            m.cls_kw0[nc] = a.kw0;
+            m.cls_ntw[nc] = a.ntw;
+            m.cls_dy0[nc] = a.dy0;
+            m.cls_dx0[nc] = a.dx0;
+            m.cls_Ho[nc] = a.Ho;
+            m.cls_Wo[nc] = a.Wo;
+            m.cls_nchunks[nc] = a.nchunks;
+            blocks += a.mblocks * a.nblocks;
+            ++nc;
+        }
+        if (nc > 0) {
+            m.ncls = nc;
+            m.splits = 1;
+            m.mblocks = blocks / m.nblocks;   // launch_x6: grid = mblocks * nblocks * splits
+            m.a = gy;
+            m.b = (const float*)planes;
+            m.y = gx;
+            launch_x6(m, st);
+        }
+    } else {
     for (int py = 0; py < 2; ++py)
         for (int px = 0; px < 2; ++px) {
             ConvArgs a;
@@ -1839,6 +1906,7 @@ int run_dgrad_s2(const md2_conv_desc* d, const float* gy, const float* w, float*
                                    py, px);
             }
         }
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }

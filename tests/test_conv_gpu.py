@@ -24,6 +24,8 @@ SHAPES = [  # (B, Cin, Cout, k, stride, pad, H, W)
     (2, 512, 512, 3, 1, 1, 3, 5),      # layer4 at 96x320: K split, M tail
     (2, 96, 64, 3, 1, 0, 18, 34),      # decoder conv on a padded input (pad 0), C = 3 chunks
     (1, 32, 64, 3, 1, 1, 7, 9),        # odd sizes, M not a tile multiple
+    (2, 64, 128, 3, 2, 1, 23, 39),     # stride 2 on odd sizes: unequal parity classes
+    (2, 64, 128, 1, 2, 0, 23, 39),     # 1x1 stride 2 on odd sizes: three tapless classes
 ]
 
 
@@ -162,10 +164,12 @@ def test_conv_abi_dgrad_wgrad(B, C, N, k, s, p, H, W):
         assert _rel(gx, gx_ref) < 1e-4
 
 
-# x6 variants: 128 / 256-row tiles, and the patch-staged kernel (which run() uses only
-# where the shape fits it: 3x3, stride 1, GEMM channels % 32 — elsewhere the flag is inert)
+# x6 variants: 128 / 256-row tiles, the patch-staged kernel (which run() uses only where
+# the shape fits it: 3x3, stride 1, GEMM channels % 32 — elsewhere the flag is inert) and
+# the one-launch stride-2 input gradient (inert at stride 1)
 XFLAGS = (conv_ops.X6, conv_ops.X6 | conv_ops.BM256, conv_ops.X6 | conv_ops.PATCH,
-          conv_ops.X6 | conv_ops.PATCH | conv_ops.BM256)
+          conv_ops.X6 | conv_ops.PATCH | conv_ops.BM256, conv_ops.X6 | conv_ops.S2_ONE,
+          conv_ops.X6 | conv_ops.S2_ONE | conv_ops.BM256)
 
 
 @pytest.mark.parametrize("B,C,N,k,s,p,H,W", [sh for sh in SHAPES if sh[1] % 8 == 0 and sh[2] % 8 == 0])
