@@ -1,23 +1,32 @@
 // stem.hip — weight gradient of the ResNet stem convolution (conv1: 7x7, stride 2,
 // padding 3, C -> 64, no bias; networks/resnet_encoder.py -> torchvision conv1) on
-// gfx950 f32 MFMA.
+// split-bf16 MFMA (f32-class: three exact bf16 planes per operand, six products,
+// f32 accumulation — the scheme of conv.hip's x6 kernels).
 //
 // The stem's input is data (the normalised frames), so its backward is the weight
 // gradient alone: dW[co][ky][kx][ci] = Σ_p dy[p][co] · x[p's 7x7 window][ky][kx][ci]
-// over every output pixel p — a GEMM with M = 64 output channels, N = 49·C window
-// taps, and the reduction over B·Ho·Wo pixels (368k at B=12, 192x640).  MIOpen runs it
-// at 41 TFLOP/s (C=3) / 71 TFLOP/s (C=6, the pose encoder's frame pair); here:
-//   * v_mfma_f32_32x32x2_f32 (exact f32 fma chains), K = 2 pixels per instruction:
-//     lane l feeds dy[pixel 2q + l/32][co tile + l%32] as A and the window tap
-//     x[pixel 2q + l/32][tap tile + l%32] as B, gathered straight from the NHWC input
-//     (taps of one window row are C·7 contiguous floats; zero outside the image);
-//   * blocks walk 64-pixel output row segments, staging the window rows and dy in LDS
-//     (double-buffered); a wave owns both 32-channel tiles × 5 tap tiles (160
-//     accumulators) for its pixel pairs; the 8 waves of a block are summed in LDS in wave order,
-//     blocks write partials, a second launch sums them in block order — deterministic,
-//     no atomics.
-// Layouts: x (B,H,W,C) and dy (B,Ho,Wo,64) channels_last fp32; dW in the weight's own
-// memory format (channels_last [co][ky][kx][ci] or contiguous [co][ci][ky][kx]).
+// over every output pixel p — a GEMM with M = 64 output channels, N = 49·C window taps
+// and K = B·Ho·Wo output pixels (368k at B=12, 192x640).  MIOpen's backward-weights
+// kernel (igemm_wrw) runs it in ~125 / ~430 us at the step's shapes (C = 3, B = 12 /
+// C = 6, B = 24; 192x640); this one in ~100 / ~413 us with its split reduction.  Its
+// phases (fetch, build, multiply) do not overlap within a block — the next step for
+// it is producer waves that build chunk t+1 while the multiplying waves run chunk t.
+//
+// Here the channels go in groups of three (one frame; the pose encoder's pair is two
+// groups, blockIdx.y) padded to four, and K in chunks of one 32-pixel segment of one
+// output row.  Per chunk a block stages the 7 input rows x 69 columns x 3 channels
+// under the segment ONCE (fp32, coalesced row runs, one LDS buffer per chunk), and
+// builds from them the seven B tiles — kernel row kh: rows (kx, ci) = 4 kx + ci, 32
+// pixels, x[2 oh - 3 + kh][2 ow - 3 + kx][ci] — split into bf16 planes in LDS, beside
+// the dy tile (64 co x 32 pixels, split on the way in).  Wave kh (7 waves) multiplies
+// its kernel row: 64 x 32 outputs per chunk, 2 x 6 MFMAs per 16 pixels.  The next
+// chunk's rows and dy are fetched into registers behind the current chunk's build /
+// MFMAs; two barriers per chunk; two blocks per CU.  Blocks take contiguous chunk
+// ranges (K splits) and write fp32 partials [group][split][64][147]; a second launch
+// sums them in split order into dW in the weight's memory format — deterministic,
+// no atomics.
+// Layouts: x (B,H,W,C) and dy (B,Ho,Wo,64) channels_last fp32; dW channels_last
+// [co][ky][kx][ci] (MD2_STEM_WEIGHT_CL) or contiguous [co][ci][ky][kx].
 
 #include <hip/hip_runtime.h>
 
@@ -30,226 +39,299 @@ int md2_report_error(int code, const char* msg);
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kWaves = 8;       // waves per block
-constexpr int kThreads = 64 * kWaves;
-constexpr int kNTW = 5;         // 32-wide tap tiles per wave
-constexpr int kNB = 32 * kNTW;  // taps per tap group (160)
 constexpr int kCo = 64;
-constexpr int kBlocks = 256;    // blocks per tap group: one per CU
-constexpr int kPartStride = kCo * kNB + 64;   // floats per block partial (padded)
+constexpr int kWaves = 7;               // one per kernel row
+constexpr int kThreads = 64 * kWaves;
+constexpr int kSeg = 32;                // output pixels per chunk (one output row segment)
+constexpr int kRawW = 2 * kSeg + 5;     // input columns under a segment
+constexpr int kCG = 3;                  // channels per group (one frame)
+constexpr int kRaw = 7 * kCG * 2 * 36;   // floats per staged chunk ([kh][ci][parity][36])
+constexpr int kXBK = 32;
+constexpr int kPA = kCo * kXBK;         // bf16 per dy plane (64 co x 32 pixels)
+constexpr int kPT = 32 * kXBK;          // bf16 per B tile plane (32 rows x 32 pixels)
+constexpr int kOut = 49 * kCG;          // outputs per output channel per group
+constexpr int kBlocksPerCU = 2;
+constexpr int kMaxChunks = 64;          // chunks per K split at most
 
 struct StemArgs {
     int B, C, H, W, Ho, Wo;
     int w_cl;
+    int nseg, nchunks, splits, cps;     // segments per output row, chunks, K splits, chunks per split
     const float* x;
     const float* gy;
-    float* part;   // [tap group][block][64][160]
-    const float* zeros;   // 64 zero floats (the workspace tail): DMA source outside the image
+    float* part;                        // [group][split][64][147]
     float* gw;
 };
 
-// Blocks walk segments of kSeg consecutive output pixels of one output row.  Per
-// segment the 7 input rows under it (2·kSeg+5 columns, zero outside the image) and
-// its dy rows are staged in LDS by LDS-DMA (global_load_lds_dword: no staging
-// registers), three buffers deep: segment s+2 is in flight while s is computed, so the
-// MFMAs do not wait on HBM latency.  The MFMA operands come from LDS with no per-lane
-// bounds checks or pixel decoding.  Wave w takes pixel pairs w, w+8, ... of the
-// segment with all 2×kNTW tiles of its tap group.
-constexpr int kSeg = 64;
-constexpr int kSW = 2 * kSeg + 5;   // staged input columns
-constexpr int kDyS = 65;            // dy row stride in LDS (pair halves on different banks)
-constexpr int kBufs = 3;
-
-template <int C>
-struct StemLds {
-    static constexpr int RW = kSW * C;                     // floats per staged input row
-    static constexpr int RI = (RW + 63) / 64;              // DMA instructions per row
-    static constexpr int XI = 7 * RI;                      // ... per segment's input rows
-    static constexpr int NXI = (XI + kWaves - 1) / kWaves; // per wave (padded with dummies)
-    static constexpr int K = NXI + kSeg / kWaves;          // DMA instructions per wave per segment
-    static constexpr int RWP = RI * 64;                    // LDS row stride (whole DMA rows)
-    static constexpr int XS = 7 * RWP;
-    static constexpr int DS = kSeg * kDyS;
-    static constexpr int BUF = XS + DS;
-    static constexpr int TOTAL = kBufs * BUF + 64;         // + the dummies' landing row
-};
-
-// s_waitcnt vmcnt(VM) (expcnt / lgkmcnt unconstrained), gfx9 encoding
-template <int VM>
-__device__ __forceinline__ void wait_vm() {
-    static_assert(VM >= 0 && VM < 64, "vmcnt");
-    __builtin_amdgcn_s_waitcnt((VM & 0xF) | ((VM >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+// Exact three-way split by truncation (conv.hip): x == x0 + x1 + x2, each a bf16
+__device__ __forceinline__ float trunc16(float x) {
+    return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, x) & 0xFFFF0000u);
 }
+__device__ __forceinline__ uint32_t hi16x2(float lo, float hi) {
+    return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo), 0x07060302u);
+}
+// [rows][32 k] bf16 planes with 16-byte quads XOR-swizzled by (row >> 2) & 3 and rows
+// r, r ^ 1 swapped in odd row quads (conv.hip xidx2): conflict-free fragment reads
+// and conflict-free 8-byte stores from lanes covering two adjacent rows
+__device__ __forceinline__ int xidx2(int r, int k) {
+    r ^= (r >> 2) & 1;
+    return r * kXBK + ((((k >> 3) ^ (r >> 2)) & 3) << 3) + (k & 7);
+}
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Workgroup barrier that leaves the LDS-DMA prefetches in flight: __syncthreads()'s
-// workgroup fence waits for every outstanding vector-memory op (vmcnt(0)), which would
-// drain the pipeline each segment.  The wait_vm<> calls order the DMA explicitly; the
-// "memory" clobber keeps the compiler from moving LDS accesses across the barrier.
-__device__ __forceinline__ void block_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
+// two 7-wave blocks per CU put four waves on two of the SIMDs: <= 128 VGPRs
 template <int C>
-__global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(StemArgs a) {
-    using L = StemLds<C>;
-    constexpr int KC = 49 * C;
-    static_assert(2 * L::K < 64, "in-flight DMA count exceeds vmcnt");
-    __shared__ float lds[L::TOTAL > kCo * kNB ? L::TOTAL : kCo * kNB];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int col = lane & 31, half = lane >> 5;
-    const int ng = blockIdx.y;
-    const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
-    int toff[kNTW];
-    bool tv[kNTW];
-#pragma unroll
-    for (int t = 0; t < kNTW; ++t) {
-        const int n = (ng * kNTW + t) * 32 + col;
-        tv[t] = n < KC;
-        const int nn = tv[t] ? n : 0;
-        const int ky = nn / (7 * C), r = nn - ky * 7 * C, kx = r / C, ci = r - kx * C;
-        toff[t] = ky * L::RWP + kx * C + ci;
-    }
-    f32x16 acc[2][kNTW];
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int t = 0; t < kNTW; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[m][t][r] = 0.f;
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void stem_x6_wgrad_kernel(StemArgs a) {
+    __shared__ float raw[2][kRaw];   // [kh][ci][column parity][36]: x[2oh-3+kh][iw0 + 2m + parity][3cg+ci]
+    __shared__ __bf16 At[3 * kPA];
+    __shared__ __bf16 Bt[7 * 3 * kPT];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int ks = blockIdx.x, cg = blockIdx.y;
+    const int t0 = ks * a.cps;
+    const int n = min(a.cps, a.nchunks - t0);
+    const int H = a.H, W = a.W;
+    constexpr int runq = (kRawW * C + 3) / 4;         // float4s per staged input row run (all C channels)
+    constexpr int nq = 7 * runq;                      // per chunk
+    constexpr int QPT = (nq + kThreads - 1) / kThreads;   // per thread
+    constexpr uint32_t cinv = (65536u + C - 1) / C;    // k / C = (k * cinv) >> 16 for k < 2^11
+    const long long total = (long long)a.B * H * W * C;
 
-    const int spr = (Wo + kSeg - 1) / kSeg;   // segments per output row
-    const int nseg = a.B * Ho * spr;
-    float* dummy = lds + kBufs * L::BUF;
-    // exactly L::K DMA instructions per wave (out-of-image lanes copy zeros)
-    // Row r of the window is x[b][iy0 + r][ix0 .. ix0 + 2·kSeg + 4][0 .. C) — one
-    // contiguous run of RW floats starting at element ix0·C of the image row, so a lane's
-    // element e is in the image iff 0 <= ix0·C + e < W·C: no per-lane division.  The
-    // address math is per wave (scalar) except for that one add and compare.
-    const int WC = W * C;
-    auto issue = [&](int sg, float* buf) {
-        const int sx = sg % spr, t2 = sg / spr, oy = t2 % Ho, b = t2 / Ho;
-        const int ox0 = sx * kSeg, iy0 = 2 * oy - 3, e0 = (2 * ox0 - 3) * C;
-        const float* img = a.x + (size_t)b * H * WC;
-#pragma unroll
-        for (int k = 0; k < L::NXI; ++k) {
-            const int ins = wave + k * kWaves;
-            if (ins >= L::XI) {
-                __builtin_amdgcn_global_load_lds(a.zeros + lane, (uint32_t*)dummy, 4, 0, 0);
-                continue;
+    // a loader position (image, output row, segment) advanced one chunk at a time
+    struct Pos {
+        int seg, oh, b;
+    };
+    auto pos_of = [&](int t) {
+        Pos p;
+        const int rr = t / a.nseg;
+        p.seg = t - rr * a.nseg;
+        p.b = rr / a.Ho;
+        p.oh = rr - p.b * a.Ho;
+        return p;
+    };
+    auto advance = [&](Pos& p) {
+        if (++p.seg == a.nseg) {
+            p.seg = 0;
+            if (++p.oh == a.Ho) {
+                p.oh = 0;
+                ++p.b;
             }
-            const int r = ins / L::RI, c0 = (ins - r * L::RI) * 64;        // wave-uniform
-            const int iy = iy0 + r;
-            const bool row_ok = iy >= 0 && iy < H;
-            const int e = c0 + lane, eg = e0 + e;                          // element in the image row
-            const bool ok = row_ok && e < L::RW && (unsigned)eg < (unsigned)WC;
-            // every lane issues (the per-wave DMA count must be exactly K for the
-            // vmcnt waits): outside the image / past the row, it copies a zero
-            const float* src = ok ? img + (size_t)(row_ok ? iy : 0) * WC + eg : a.zeros + lane;
-            __builtin_amdgcn_global_load_lds(src, (uint32_t*)(buf + r * L::RWP + c0), 4, 0, 0);
-        }
-        float* dy = buf + L::XS;
-        const float* gyrow = a.gy + (size_t)(b * Ho + oy) * Wo * kCo;
-#pragma unroll
-        for (int k = 0; k < kSeg / kWaves; ++k) {
-            const int j = wave + k * kWaves, ox = ox0 + j;
-            const float* src = ox < Wo ? gyrow + (size_t)ox * kCo + lane : a.zeros + lane;
-            __builtin_amdgcn_global_load_lds(src, (uint32_t*)(dy + j * kDyS), 4, 0, 0);
         }
     };
-    int sg = blockIdx.x;
-    const int G = gridDim.x;
-    if (sg < nseg) issue(sg, lds);
-    if (sg + G < nseg) issue(sg + G, lds + L::BUF);
-    int cur = 0;
-    for (; sg < nseg; sg += G) {
-        const bool far = sg + 2 * G < nseg;
-        if (far) {
-            issue(sg + 2 * G, lds + ((cur + 2) % kBufs) * L::BUF);
-            wait_vm<2 * L::K>();                 // this segment's DMA is done
-        } else if (sg + G < nseg) {
-            wait_vm<L::K>();
-        } else {
-            wait_vm<0>();
-        }
-        block_sync();                            // every wave's DMA for this segment landed
-        const float* xb = lds + cur * L::BUF;
-        const float* dyb = xb + L::XS;
+    Pos praw = pos_of(t0), pgy = pos_of(t0);
+    // raw: float4 q = tid + kThreads j of the chunk's 7 row runs (up to 3 per thread)
+    float4 RV[QPT];
+    auto load_raw = [&]() {
+        const int ih0 = 2 * praw.oh - 3, iw0 = 2 * praw.seg * kSeg - 3;
 #pragma unroll
-        for (int i = 0; i < kSeg / 2 / kWaves; ++i) {
-            const int j = 2 * (wave + i * kWaves) + half;   // pixel within the segment
-            const float a0 = dyb[j * kDyS + col], a1 = dyb[j * kDyS + 32 + col];
-            float bv[kNTW];
+        for (int j = 0; j < QPT; ++j) {
+            const int q = tid + kThreads * j;
+            const int r = q / runq, k = 4 * (q - r * runq);
+            const int ih = ih0 + r;
+            RV[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q < nq && (unsigned)ih < (unsigned)H) {
+                const long long e0 = ((long long)(praw.b * H + ih) * W + iw0) * C + k;   // may start before the row
+                const float* p = a.x + e0;
+                if (e0 >= 0 && e0 + 4 <= total) {
+                    RV[j] = *(const float4*)p;   // 4-byte aligned dwordx4
+                } else {
+                    float v[4];
 #pragma unroll
-            for (int t = 0; t < kNTW; ++t) bv[t] = tv[t] ? xb[toff[t] + 2 * j * C] : 0.f;
-#pragma unroll
-            for (int t = 0; t < kNTW; ++t) {
-                acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bv[t], acc[0][t], 0, 0, 0);
-                acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv[t], acc[1][t], 0, 0, 0);
+                    for (int i = 0; i < 4; ++i) v[i] = (e0 + i >= 0 && e0 + i < total) ? p[i] : 0.f;
+                    RV[j] = make_float4(v[0], v[1], v[2], v[3]);
+                }
             }
         }
-        block_sync();                            // buffer `cur` is refilled two segments on
-        cur = (cur + 1) % kBufs;
-    }
-    wait_vm<0>();
-    __syncthreads();
-
-    // waves summed in wave order into LDS [co][160] (the staging buffers are free now);
-    // D layout: col = lane%32 (tap), row = (r&3) + 8(r>>2) + 4(lane/32) (channel in tile)
-    float* red = lds;
-    for (int w = 0; w < kWaves; ++w) {
-        if (wave == w) {
+    };
+    // store the group's channels de-interleaved by column parity; columns outside the
+    // image are zeros
+    auto store_raw = [&](float* dst) {
+        const int iw0 = 2 * praw.seg * kSeg - 3;
 #pragma unroll
-            for (int m = 0; m < 2; ++m)
+        for (int j = 0; j < QPT; ++j) {
+            const int q = tid + kThreads * j;
+            if (q >= nq) break;
+            const int r = q / runq, k0 = 4 * (q - r * runq);
+            const float v[4] = {RV[j].x, RV[j].y, RV[j].z, RV[j].w};
 #pragma unroll
-                for (int t = 0; t < kNTW; ++t)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int co = m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                        float* d = red + co * kNB + t * 32 + col;
-                        *d = w == 0 ? acc[m][t][r] : *d + acc[m][t][r];
-                    }
+            for (int i = 0; i < 4; ++i) {
+                const int k = k0 + i, col = (int)(((uint32_t)k * cinv) >> 16), c = k - col * C - kCG * cg;
+                const int iw = iw0 + col;
+                if (col < kRawW && (unsigned)c < (unsigned)kCG)
+                    dst[((r * kCG + c) * 2 + (col & 1)) * 36 + (col >> 1)] = (unsigned)iw < (unsigned)W ? v[i] : 0.f;
+            }
         }
-        __syncthreads();
+    };
+    // dy: threads 192 .. 319 (waves 3-4) own a 4-pixel x 4-channel micro-tile
+    const int u = tid - 192, kq = u & 7, mq = u >> 3;
+    const bool gyrole = u >= 0 && u < 128;
+    float4 GV[4];
+    auto load_gy = [&]() {
+        if (!gyrole) return;
+        const int ow0 = pgy.seg * kSeg + 4 * kq;
+        const float* row = a.gy + (size_t)(pgy.b * a.Ho + pgy.oh) * a.Wo * kCo + 4 * mq;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            GV[i] = ow0 + i < a.Wo ? *(const float4*)(row + (size_t)(ow0 + i) * kCo) : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    auto store_gy = [&]() {
+        if (!gyrole) return;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float c[3][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float x = j == 0 ? GV[i].x : (j == 1 ? GV[i].y : (j == 2 ? GV[i].z : GV[i].w));
+                const float a0 = trunc16(x), r1 = x - a0, a1 = trunc16(r1);
+                c[0][i] = a0;
+                c[1][i] = a1;
+                c[2][i] = r1 - a1;
+            }
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                u32x2 v;
+                v.x = hi16x2(c[pl][0], c[pl][1]);
+                v.y = hi16x2(c[pl][2], c[pl][3]);
+                *(u32x2*)(At + pl * kPA + xidx2(4 * mq + j, 4 * kq)) = v;
+            }
+        }
+    };
+    // B tiles from the staged rows: task id -> pixel quad g, tile row r (kx = r / 4,
+    // ci = r % 4), kernel row kh; four pixels at stride 2 of one staged row
+    // only the 21 live rows (kx < 7, ci < 3) of each tile: the dead ones are zeroed once
+    constexpr int kLive = 7 * kCG;
+    auto build = [&](const float* src) {
+#pragma unroll 2
+        for (int j = 0; j < (7 * kLive * 8 + kThreads - 1) / kThreads; ++j) {
+            const int id = tid + kThreads * j;
+            if (id >= 7 * kLive * 8) break;
+            const int g = id & 7, rl = (id >> 3) % kLive, kh = (id >> 3) / kLive;
+            const int kx = rl / kCG, ci = rl - kx * kCG, r = 4 * kx + ci;
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = src[((kh * kCG + ci) * 2 + (kx & 1)) * 36 + 4 * g + i + (kx >> 1)];
+            float c[3][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float a0 = trunc16(v[i]), r1 = v[i] - a0, a1 = trunc16(r1);
+                c[0][i] = a0;
+                c[1][i] = a1;
+                c[2][i] = r1 - a1;
+            }
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                u32x2 q;
+                q.x = hi16x2(c[pl][0], c[pl][1]);
+                q.y = hi16x2(c[pl][2], c[pl][3]);
+                *(u32x2*)(Bt + (kh * 3 + pl) * kPT + xidx2(r, 4 * g)) = q;
+            }
+        }
+    };
+
+    const int lr = lane & 31, h = lane >> 5;
+    // one accumulator per row fragment over the split: plan() caps a split at
+    // kMaxChunks chunks (2048 pixels)
+    f32x16 acc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    auto mma = [&]() {
+        const __bf16* LB = Bt + wid * 3 * kPT;
+#pragma unroll
+        for (int s = 0; s < kXBK / 16; ++s) {
+            bf16x8 fb[3];
+            const int eb = xidx2(lr, 16 * s + 8 * h);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(LB + pl * kPT + eb);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                bf16x8 fa[3];
+                const int e = xidx2(32 * i + lr, 16 * s + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(At + pl * kPA + e);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+            }
+        }
+    };
+
+    // chunk t's rows are staged (raw[t & 1]) and its dy is in registers at the top of
+    // iteration t; chunk t+1's rows are in registers
+    for (int e = tid; e < 7 * 3 * 32 * 8; e += kThreads) {   // the tiles' dead rows (kx = 7 or ci = 3)
+        const int g = e & 7, r = (e >> 3) & 31, khp = e >> 8;
+        if ((r >> 2) == 7 || (r & 3) == kCG) *(u32x2*)(Bt + khp * kPT + xidx2(r, 4 * g)) = u32x2{0u, 0u};
     }
-    float* out = a.part + ((size_t)ng * gridDim.x + blockIdx.x) * kPartStride;
-    for (int e = threadIdx.x; e < kCo * kNB; e += kThreads) out[e] = red[e];
+    if (n > 0) {
+        load_raw();
+        load_gy();
+        store_raw(raw[0]);
+        advance(praw);
+        if (n > 1) load_raw();
+    }
+    lds_sync();
+    for (int t = 0; t < n; ++t) {
+        build(raw[t & 1]);
+        store_gy();
+        if (t + 1 < n) {
+            advance(pgy);
+            load_gy();
+        }
+        lds_sync();
+        mma();
+        if (t + 1 < n) {
+            store_raw(raw[(t + 1) & 1]);
+            advance(praw);
+            if (t + 2 < n) load_raw();
+        }
+        lds_sync();
+    }
+
+    // tile row lr = 4 kx + ci of kernel row wid; output channel per accumulator element
+    const int kx = lr >> 2, ci = lr & 3;
+    if (kx < 7 && ci < kCG) {
+        float* out = a.part + (((size_t)cg * a.splits + ks) * kCo) * kOut + (wid * 7 + kx) * kCG + ci;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int co = 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+                out[(size_t)co * kOut] = acc[i][e];
+            }
+    }
 }
 
-// dW[co][n] = Σ_blocks part: a block takes 64 outputs × 4 block slices (16 loads in
-// flight per thread), slices combined in order through LDS — fixed order throughout.
-__global__ __launch_bounds__(256) void stem_wgrad_final_kernel(StemArgs a, int G) {
-    const int KC = 49 * a.C;
-    const int el = threadIdx.x & 63, sl = threadIdx.x >> 6;
-    const int e = blockIdx.x * 64 + el;
+// dW = Σ_splits partials: sixteen lanes per output, lane l summing splits l, l + 16, ...
+// in order, then the sixteen in lane order (deterministic); written in the weight's
+// memory format.  (Four lanes per output ran long serial chains over the ~500 splits.)
+constexpr int kFinOut = 16, kFinLanes = 256 / kFinOut;
+__global__ __launch_bounds__(256) void stem_wgrad_final_kernel(StemArgs a) {
+    const int NG = a.C / kCG, outs = NG * kCo * kOut;
+    const int el = threadIdx.x % kFinOut, sl = threadIdx.x / kFinOut;
+    const int e = blockIdx.x * kFinOut + el;
     float s = 0.f;
-    int co = 0, n = 0;
-    if (e < kCo * KC) {
-        co = e / KC;
-        n = e - co * KC;
-        const int ng = n / kNB, nl = n - ng * kNB;
-        const float* p = a.part + (size_t)ng * G * kPartStride + co * kNB + nl;
-        constexpr int R = 16;
-        float c[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) c[r] = 0.f;
-        for (int g0 = sl * R; g0 < G; g0 += 4 * R)
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                if (g0 + r < G) c[r] += p[(size_t)(g0 + r) * kPartStride];
-#pragma unroll
-        for (int r = 0; r < R; ++r) s += c[r];
+    if (e < outs) {
+        const int cg = e / (kCo * kOut), r = e - cg * kCo * kOut;   // r = co * 147 + tap
+        const float* p = a.part + (size_t)cg * a.splits * kCo * kOut + r;
+#pragma unroll 4
+        for (int g = sl; g < a.splits; g += kFinLanes) s += p[(size_t)g * kCo * kOut];
     }
-    __shared__ float red[4][64];
+    __shared__ float red[kFinLanes][kFinOut];
     red[sl][el] = s;
     __syncthreads();
-    if (sl != 0 || e >= kCo * KC) return;
-    s = ((red[0][el] + red[1][el]) + red[2][el]) + red[3][el];
-    if (a.w_cl) {
-        a.gw[e] = s;
-    } else {
-        const int ky = n / (7 * a.C), r = n - ky * 7 * a.C, kx = r / a.C, ci = r - kx * a.C;
-        a.gw[((co * a.C + ci) * 7 + ky) * 7 + kx] = s;
-    }
+    if (sl != 0 || e >= outs) return;
+#pragma unroll
+    for (int j = 1; j < kFinLanes; ++j) s += red[j][el];
+    const int cg = e / (kCo * kOut), r = e - cg * kCo * kOut, co = r / kOut, tap = r - co * kOut;
+    const int ky = tap / (7 * kCG), rem = tap - ky * 7 * kCG, kx = rem / kCG, ci = kCG * cg + rem - kx * kCG;
+    if (a.w_cl) a.gw[((co * 7 + ky) * 7 + kx) * a.C + ci] = s;
+    else a.gw[((co * a.C + ci) * 7 + ky) * 7 + kx] = s;
 }
 
 bool valid(const md2_stem_desc* d) {
@@ -258,21 +340,9 @@ bool valid(const md2_stem_desc* d) {
            (long long)d->batch * d->height * d->width * d->channels < (1ll << 31);
 }
 
-int groups_of(int C) { return (49 * C + kNB - 1) / kNB; }
-
-}  // namespace
-
-extern "C" {
-
-size_t md2_stem_wgrad_workspace_bytes(const md2_stem_desc* d) {
-    if (!valid(d)) return 0;
-    return sizeof(float) * ((size_t)groups_of(d->channels) * kBlocks * kPartStride + 64);
-}
-
-int md2_stem_wgrad(const md2_stem_desc* d, const float* x, const float* grad_y, float* grad_weight, void* workspace,
-                   void* stream) {
-    if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "stem_wgrad: channels 3/6/9, 32-bit element count");
-    if (!x || !grad_y || !grad_weight || !workspace) return md2_report_error(MD2_ERR_ARG, "stem_wgrad: NULL operand");
+// geometry and K split: about two blocks per CU over the channel groups, every split
+// at least one chunk
+StemArgs plan(const md2_stem_desc* d) {
     StemArgs a = {};
     a.B = d->batch;
     a.C = d->channels;
@@ -281,20 +351,43 @@ int md2_stem_wgrad(const md2_stem_desc* d, const float* x, const float* grad_y, 
     a.Ho = (d->height - 1) / 2 + 1;   // (H + 2·3 - 7) / 2 + 1
     a.Wo = (d->width - 1) / 2 + 1;
     a.w_cl = (d->flags & MD2_STEM_WEIGHT_CL) ? 1 : 0;
+    a.nseg = (a.Wo + kSeg - 1) / kSeg;
+    a.nchunks = a.B * a.Ho * a.nseg;
+    const int NG = a.C / kCG;
+    int want = 256 * kBlocksPerCU / NG;
+    want = want < 1 ? 1 : want;
+    const int need = (a.nchunks + kMaxChunks - 1) / kMaxChunks;
+    want = want > need ? want : need;
+    a.cps = (a.nchunks + want - 1) / want;
+    a.splits = (a.nchunks + a.cps - 1) / a.cps;
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t md2_stem_wgrad_workspace_bytes(const md2_stem_desc* d) {
+    if (!valid(d)) return 0;
+    const StemArgs a = plan(d);
+    return sizeof(float) * (size_t)(a.C / kCG) * a.splits * kCo * kOut;
+}
+
+int md2_stem_wgrad(const md2_stem_desc* d, const float* x, const float* grad_y, float* grad_weight, void* workspace,
+                   void* stream) {
+    if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "stem_wgrad: channels 3/6/9, 32-bit element count");
+    if (!x || !grad_y || !grad_weight || !workspace) return md2_report_error(MD2_ERR_ARG, "stem_wgrad: NULL operand");
+    StemArgs a = plan(d);
     a.x = x;
     a.gy = grad_y;
     a.part = (float*)workspace;
-    const size_t nzero = (size_t)groups_of(a.C) * kBlocks * kPartStride;
-    a.zeros = a.part + nzero;
     a.gw = grad_weight;
-    const int NG = groups_of(a.C);
-    void (*k)(StemArgs) = a.C == 3 ? stem_wgrad_kernel<3> : a.C == 6 ? stem_wgrad_kernel<6> : stem_wgrad_kernel<9>;
+    const int NG = a.C / kCG;
     const hipStream_t st = (hipStream_t)stream;
-    if (hipMemsetAsync(a.part + nzero, 0, 64 * sizeof(float), st) != hipSuccess)
-        return md2_report_error(MD2_ERR_HIP, "stem_wgrad: memset");
-    hipLaunchKernelGGL(k, dim3(kBlocks, NG), dim3(kThreads), 0, st, a);
-    const int outs = kCo * 49 * a.C;
-    hipLaunchKernelGGL(stem_wgrad_final_kernel, dim3((outs + 63) / 64), dim3(256), 0, st, a, kBlocks);
+    void (*k)(StemArgs) = a.C == 3 ? stem_x6_wgrad_kernel<3> : a.C == 6 ? stem_x6_wgrad_kernel<6> : stem_x6_wgrad_kernel<9>;
+    hipLaunchKernelGGL(k, dim3(a.splits, NG), dim3(kThreads), 0, st, a);
+    const int outs = NG * kCo * kOut;
+    hipLaunchKernelGGL(stem_wgrad_final_kernel, dim3((outs + kFinOut - 1) / kFinOut), dim3(256), 0, st, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }

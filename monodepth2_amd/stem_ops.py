@@ -1,16 +1,14 @@
 """The ResNet stem convolution (conv1: 7x7, stride 2, padding 3, C -> 64, no bias) with
-its weight gradient on f32 MFMA (csrc/stem.hip, ABI `md2_stem_*`).
+its weight gradient on split-bf16 MFMA (csrc/stem.hip, ABI `md2_stem_*`).
 
 The stem reads the normalised frames, which are data: its backward is the weight
-gradient alone, where MIOpen is at its least efficient (41 / 71 TFLOP/s for the
-depth / pose encoder).  The forward stays MIOpen's.  Same parameter (the torchvision
-`conv1.weight`), same semantics; any other case (an input that needs a gradient,
-bf16, NCHW inputs, a CPU tensor) runs the module itself.
-
-OFF by default (ENABLED): at the step's shapes it runs 131 µs (C=3) and 496 µs
-(C=6) + 19/25 µs for the partial sums, against MIOpen's 130 / 427 µs
-(tools/stem_bench.py) — the kernel is parity-tested and kept for the next round's
-work on its issue rate.
+gradient alone, MIOpen's igemm_wrw at ~125 us (C=3, depth encoder, B=12) and ~430 us
+(C=6, pose encoder, B=24) per step at 192x640.  stem_x6_wgrad_kernel (f32-class:
+three exact bf16 planes, six products) runs them in ~100 / ~413 us including its
+split reduction (rocprofv3, tools/stem_bench.py under tools/kstats.sh).  The forward
+stays MIOpen's.  Same parameter (the torchvision `conv1.weight`), same semantics; any
+other case (an input that needs a gradient, bf16, NCHW inputs, a CPU tensor) runs the
+module itself.
 """
 from __future__ import annotations
 
@@ -23,7 +21,7 @@ import torch.nn.functional as F
 from . import _lib
 
 _CL = torch.channels_last
-ENABLED = False   # MIOpen's backward-weights kernel is faster today (see the module docstring)
+ENABLED = True   # the x6 weight gradient (tests flip it to compare with MIOpen)
 
 
 class _StemConv(torch.autograd.Function):
