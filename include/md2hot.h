@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 13
+#define MD2_ABI_VERSION 14
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -492,6 +492,20 @@ size_t md2_conv_workspace_bytes(const md2_conv_desc* desc);
  * Channels must be multiples of 8. */
 int md2_conv_split_weights(const md2_conv_desc* desc, const float* weight, void* planes_fwd, void* planes_dgrad,
                            void* stream);
+/* Every conv weight of a training step split in ONE launch (the per-convolution
+ * md2_conv_split_weights launches of the forward, ~80 tiny kernels per step, become one
+ * ~10k-block grid): `table` is a DEVICE array of `n` entries; entry e covers grid blocks
+ * [block0, block0 + ceil(ci/32) * ceil(co/32) * kt) in ascending order, and
+ * `total_blocks` is the last entry's end.  Same planes as md2_conv_split_weights
+ * (planes_dgrad nullable per entry).  Graph-capturable (no host sync). */
+typedef struct md2_wsplit_entry {
+    const float* weight;        /* (co, kt, ci) channels_last conv weight        */
+    void* planes_fwd;           /* [3][co][kt][ci] bf16                           */
+    void* planes_dgrad;         /* [3][ci][kt][co] bf16, taps flipped, or NULL    */
+    int32_t co, kt, ci;         /* out channels, kernel_h * kernel_w, in channels */
+    int32_t block0;             /* first grid block of this entry                 */
+} md2_wsplit_entry;
+int md2_conv_split_weights_multi(const md2_wsplit_entry* table, int n, int total_blocks, void* stream);
 int md2_conv_fwd(const md2_conv_desc* desc, const float* x, const float* weight, float* y, void* workspace,
                  void* stream);
 /* grad_x (batch, height, width, in_channels) from grad_y (batch, Ho, Wo, out_channels):

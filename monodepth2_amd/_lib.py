@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -64,7 +64,7 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_bias_act_workspace_bytes", "md2_maxpool3s2_bwd_add", "md2_bn_bwd_multi",
            "md2_conv_fwd", "md2_conv_workspace_bytes", "md2_conv_split_weights",
            "md2_conv_dgrad", "md2_conv_wgrad", "md2_conv_direct", "md2_conv_wgrad_direct",
-           "md2_conv_wgrad_direct_workspace_bytes"]
+           "md2_conv_wgrad_direct_workspace_bytes", "md2_conv_split_weights_multi"]
 
 DTYPE_F32 = 0    # md2_desc.disp_dtype
 DTYPE_BF16 = 1
@@ -123,6 +123,12 @@ class ConvDesc(ctypes.Structure):
                 ("flags", ctypes.c_uint32)]
 
 
+class WsplitEntry(ctypes.Structure):
+    """include/md2hot.h md2_wsplit_entry (one weight of md2_conv_split_weights_multi)."""
+    _fields_ = [("weight", _vp), ("planes_fwd", _vp), ("planes_dgrad", _vp), ("co", ctypes.c_int32),
+                ("kt", ctypes.c_int32), ("ci", ctypes.c_int32), ("block0", ctypes.c_int32)]
+
+
 class PoolDesc(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int32), ("channels", ctypes.c_int32), ("height", ctypes.c_int32),
                 ("width", ctypes.c_int32), ("flags", ctypes.c_uint32), ("reserved", ctypes.c_int32)]
@@ -172,6 +178,8 @@ def _declare(L):
     L.md2_conv_wgrad_direct_workspace_bytes.restype = ctypes.c_size_t
     L.md2_conv_wgrad_direct_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc)]
     L.md2_conv_split_weights.argtypes = [ctypes.POINTER(ConvDesc)] + [_vp] * 4
+    L.md2_conv_split_weights_multi.restype = ctypes.c_int
+    L.md2_conv_split_weights_multi.argtypes = [_vp, ctypes.c_int, ctypes.c_int, _vp]
     L.md2_conv_workspace_bytes.restype = ctypes.c_size_t
     L.md2_conv_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc)]
     L.md2_stem_wgrad_workspace_bytes.restype = ctypes.c_size_t

@@ -40,6 +40,7 @@ from . import _lib
 _CL = torch.channels_last
 ENABLED = True     # tests flip this to compare with MIOpen on the same module
 AUTOTUNE = True    # False: always the MFMA kernels (tests)
+PLANE_BANK = os.environ.get("MD2_PLANE_BANK", "1") != "0"   # Trainer: one weight-split launch per step
 _ws: Dict[Tuple[int, int], torch.Tensor] = {}
 _choice: Dict[tuple, int] = {}     # (op, shape) -> index of the fastest candidate
 _times: Dict[tuple, dict] = {}     # (op, shape) -> {candidate: timed ms} (tools/conv_choices.py)
@@ -138,6 +139,114 @@ def _split_weights(x, w, stride, pad, dgrad: bool):
                                                  _lib.stream(w.device)),
                "md2_conv_split_weights")
     return pf, pd
+
+
+class PlaneBank:
+    """Persistent split-bf16 planes of every conv weight a training step multiplies on
+    the x6 path, refreshed by ONE md2_conv_split_weights_multi launch at the start of
+    the step (`Trainer._step_body`) instead of one md2_conv_split_weights launch per
+    convolution forward (~80 launches of 5-7 us per step at B=12 before).
+
+    Planes are only handed out between `begin_step()` and `end_step()` — the window
+    in which the weights do not change (the optimizer step closes it).  A weight seen
+    for the first time inside the window is split on the spot into newly allocated
+    persistent planes and joins the next refresh (never while a hipGraph is being
+    captured: then it keeps the per-call split).  Keys: the weight's storage address
+    and shape (parameters are updated in place, so both are stable)."""
+
+    def __init__(self):
+        self.entries: Dict[tuple, list] = {}   # key -> [weight, planes_fwd, planes_dgrad or None]
+        self.table = None                      # device md2_wsplit_entry array
+        self.total_blocks = 0
+        self.dirty = False
+        self.fresh = False
+        self._keep = []   # superseded tables / planes: a captured graph may still point at them
+
+    @staticmethod
+    def _blocks(w: torch.Tensor) -> int:
+        co, ci, kh, kw = w.shape
+        return ((ci + 31) // 32) * ((co + 31) // 32) * kh * kw
+
+    def _upload(self, device):
+        ents = list(self.entries.values())
+        arr = (_lib.WsplitEntry * len(ents))()
+        blk = 0
+        for e, (w, pf, pd) in zip(arr, ents):
+            co, ci, kh, kw = w.shape
+            e.weight, e.planes_fwd = w.data_ptr(), pf.data_ptr()
+            e.planes_dgrad = pd.data_ptr() if pd is not None else None
+            e.co, e.kt, e.ci, e.block0 = co, kh * kw, ci, blk
+            blk += self._blocks(w)
+        host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        if self.table is not None:
+            self._keep.append(self.table)
+        self.table = host.to(device)
+        self.total_blocks = blk
+        self.dirty = False
+
+    def begin_step(self, device: torch.device):
+        """Split every registered weight (one launch on the current stream) and open the
+        window in which `planes` hands the planes out."""
+        capturing = torch.cuda.is_current_stream_capturing()
+        if self.dirty and capturing:
+            self.fresh = False   # a new weight since the last table: per-call splits in this graph
+            return
+        if self.dirty:
+            self._upload(device)
+        if self.entries:
+            _lib.check(_lib.lib().md2_conv_split_weights_multi(self.table.data_ptr(), len(self.entries),
+                                                              self.total_blocks, _lib.stream(device)),
+                       "md2_conv_split_weights_multi")
+        self.fresh = True
+
+    def end_step(self):
+        self.fresh = False
+
+    def planes(self, x, w, stride, pad, need_dg: bool):
+        """(planes_fwd, planes_dgrad) of `w` for this step, or None outside the window."""
+        if not self.fresh:
+            return None
+        k = (w.data_ptr(), tuple(w.shape))
+        e = self.entries.get(k)
+        if e is not None and (e[2] is not None or not need_dg):
+            return e[1], e[2]
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        pf, pd = _split_weights(x, w, stride, pad, need_dg or (e is not None and e[2] is not None))
+        if e is not None:
+            self._keep.append(e)
+        self.entries[k] = [w, pf, pd]
+        self.dirty = True
+        return pf, pd
+
+
+_bank: PlaneBank | None = None
+
+
+def plane_bank() -> PlaneBank:
+    """The process's PlaneBank (created on first use; the trainer opens its window)."""
+    global _bank
+    if _bank is None:
+        _bank = PlaneBank()
+    return _bank
+
+
+def _planes_for(x, w, stride, pad, need_dg: bool):
+    """The bank's planes inside a step window, else a per-call split (one launch)."""
+    if _bank is not None:
+        got = _bank.planes(x, w, stride, pad, need_dg)
+        if got is not None:
+            return got
+    return _split_weights(x, w, stride, pad, need_dg)
+
+
+def _bank_dgrad(x, w, stride, pad):
+    """The input gradient's planes from the bank when the forward was not on x6 (the
+    dgrad then otherwise splits the weight itself, one launch per call)."""
+    if _bank is None:
+        return None
+    got = _bank.planes(x, w, stride, pad, True)
+    return got[1] if got is not None else None
 
 
 def _fwd_planes(x, w, planes, stride, pad, flags):
@@ -333,7 +442,7 @@ class _Conv(torch.autograd.Function):
         if x6 and i < len(xf):
             # the x6 forward: split the weight once for it and for the input gradient
             # (one launch), the dgrad planes kept for the backward
-            pf, planes_dg = _split_weights(x, weight, stride, pad, stride == 1 or _x6_s2_ok(x, weight, stride))
+            pf, planes_dg = _planes_for(x, weight, stride, pad, stride == 1 or _x6_s2_ok(x, weight, stride))
             y = _fwd_planes(x, weight, pf, stride, pad, xf[i])
         else:
             y = cands[i]()
@@ -359,6 +468,8 @@ class _Conv(torch.autograd.Function):
                     [lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
                 names = list(xn) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"]
                 i = _fastest("dgrad", ctx.key, cands, names)
+                if x6 and i < len(xf) and planes_dg is None:
+                    planes_dg = _bank_dgrad(x, w, s, p)
                 if x6 and i < len(xf) and planes_dg is not None:
                     gx = _dgrad_planes(gy, x, w, planes_dg, p, xf[i])
                 elif i < len(cands) - 1:
@@ -371,6 +482,8 @@ class _Conv(torch.autograd.Function):
                 cands = [(lambda f=f: _dgrad(gy, x, w, p, f, 2)) for f in sf] + \
                     [lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
                 i = _fastest("dgrad", ctx.key, cands, ["x6_s2", "x6_s2one", "miopen"])
+                if i < len(sf) and planes_dg is None:
+                    planes_dg = _bank_dgrad(x, w, s, p)
                 if i < len(sf):
                     gx = (_dgrad_planes(gy, x, w, planes_dg, p, sf[i], 2) if planes_dg is not None else cands[i]())
                 else:

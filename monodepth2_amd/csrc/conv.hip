@@ -431,10 +431,8 @@ __device__ __forceinline__ void split_store(__bf16* out, int n, int i, float v) 
     out[n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, b) >> 16));
     out[2 * n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, c) >> 16));
 }
-__global__ __launch_bounds__(256) void conv_wsplit_tile_kernel(const float* w, __bf16* fw, __bf16* dg, int Co,
-                                                               int KT, int Ci) {
-    __shared__ float tile[32][33];
-    const int tap = blockIdx.z, co0 = blockIdx.y * 32, ci0 = blockIdx.x * 32;
+__device__ __forceinline__ void wsplit_tile(const float* w, __bf16* fw, __bf16* dg, int Co, int KT, int Ci, int tap,
+                                            int co0, int ci0, float (*tile)[33]) {
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
     const int n = Co * KT * Ci;
 #pragma unroll
@@ -455,6 +453,34 @@ __global__ __launch_bounds__(256) void conv_wsplit_tile_kernel(const float* w, _
         const int ci = ci0 + r, co = co0 + tx;
         if (ci < Ci && co < Co) split_store(dg, n, (ci * KT + (KT - 1 - tap)) * Co + co, tile[tx][r]);
     }
+}
+
+// md2_conv_split_weights_multi: the tile kernel's work for every weight of the step in
+// one grid.  Block b belongs to the last entry whose block0 <= b (entries ascending;
+// a binary search over <= a few hundred entries held in the kernel's scalar path).
+__global__ __launch_bounds__(256) void conv_wsplit_multi_kernel(const md2_wsplit_entry* tab, int n) {
+    __shared__ float tile[32][33];
+    const int b = blockIdx.x;
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {   // largest e with tab[e].block0 <= b
+        const int mid = (lo + hi + 1) >> 1;
+        if (tab[mid].block0 <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    const md2_wsplit_entry e = tab[lo];
+    const int nx = (e.ci + 31) / 32, ny = (e.co + 31) / 32;
+    int t = b - e.block0;
+    const int bx = t % nx;
+    t /= nx;
+    const int by = t % ny, tap = t / ny;
+    wsplit_tile(e.weight, (__bf16*)e.planes_fwd, (__bf16*)e.planes_dgrad, e.co, e.kt, e.ci, tap, by * 32, bx * 32,
+                tile);
+}
+
+__global__ __launch_bounds__(256) void conv_wsplit_tile_kernel(const float* w, __bf16* fw, __bf16* dg, int Co,
+                                                               int KT, int Ci) {
+    __shared__ float tile[32][33];
+    wsplit_tile(w, fw, dg, Co, KT, Ci, blockIdx.z, blockIdx.y * 32, blockIdx.x * 32, tile);
 }
 
 // Tiles BMX x BN.  NT threads: 8 waves (2 x 4 / 4 x 2 / 2 x 4, wave tiles 64/128 x 32)
@@ -2010,6 +2036,13 @@ int md2_conv_split_weights(const md2_conv_desc* d, const float* weight, void* pl
     hipLaunchKernelGGL(conv_wsplit_tile_kernel, grid, dim3(256), 0, (hipStream_t)stream, weight,
                        (__bf16*)planes_fwd, (__bf16*)planes_dgrad, d->out_channels, d->kernel_h * d->kernel_w,
                        d->in_channels);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
+int md2_conv_split_weights_multi(const md2_wsplit_entry* table, int n, int total_blocks, void* stream) {
+    if (!table || n <= 0 || total_blocks <= 0) return md2_report_error(MD2_ERR_ARG, "conv_split_weights_multi: empty");
+    hipLaunchKernelGGL(conv_wsplit_multi_kernel, dim3(total_blocks), dim3(256), 0, (hipStream_t)stream, table, n);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }

@@ -31,7 +31,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.optim as optim
 
-from . import networks
+from . import conv_ops, networks
 from .distributed import FlatGradSync, wrap_ddp
 from .hotpath import HotPathConfig, generate_images, photometric_loss, predictive_mask_inputs, selection_maps
 from .bn_ops import bn_groups
@@ -448,13 +448,22 @@ class Trainer:
         return outputs, losses
 
     def _step_body(self, inputs):
-        """process_batch + backward + gradient averaging + Adam (trainer.py:205-209)."""
-        outputs, losses = self.process_batch(inputs)
-        if self.flat_sync is not None:
-            self.flat_sync.zero()
-        else:
-            self.model_optimizer.zero_grad(set_to_none=True)
-        losses["loss"].backward()
+        """process_batch + backward + gradient averaging + Adam (trainer.py:205-209).
+        The conv weights' split-bf16 planes are refreshed once for the whole step
+        (conv_ops.PlaneBank, one launch) and valid until the optimizer step."""
+        bank = conv_ops.plane_bank() if self.device.type == "cuda" and conv_ops.PLANE_BANK else None
+        if bank is not None:
+            bank.begin_step(self.device)
+        try:
+            outputs, losses = self.process_batch(inputs)
+            if self.flat_sync is not None:
+                self.flat_sync.zero()
+            else:
+                self.model_optimizer.zero_grad(set_to_none=True)
+            losses["loss"].backward()
+        finally:
+            if bank is not None:
+                bank.end_step()
         if self.flat_sync is not None:
             self.flat_sync.sync()
         self.model_optimizer.step()

@@ -225,6 +225,38 @@ def test_x6_presplit_planes_match_in_call_split():
     assert torch.equal(conv_ops._dgrad_planes(gy2, x, w, pd2, 1, conv_ops.X6, 2), conv_ops._dgrad(gy2, x, w, 1, conv_ops.X6, 2))
 
 
+def test_plane_bank_refresh_matches_per_call_split():
+    """conv_ops.PlaneBank: one md2_conv_split_weights_multi launch re-splits every
+    registered weight (3x3 / 1x1, with and without input-gradient planes, channel
+    counts that are not multiples of 32) into bitwise the planes of the per-call
+    split; outside the step window nothing is handed out."""
+    torch.manual_seed(6)
+    bank = conv_ops.PlaneBank()
+    shapes = [(64, 64, 3, 1, True), (128, 64, 1, 2, False), (40, 24, 3, 1, True), (256, 128, 3, 2, True),
+              (16, 8, 1, 1, False)]
+    ws, xs = [], []
+    for N, C, k, s, dg in shapes:
+        xs.append(torch.randn(1, C, 8, 8, device="cuda").contiguous(memory_format=CL))
+        ws.append(torch.randn(N, C, k, k, device="cuda").contiguous(memory_format=CL))
+    assert bank.planes(xs[0], ws[0], 1, 1, True) is None   # window closed
+    bank.begin_step(torch.device("cuda", 0))
+    for x, w, (N, C, k, s, dg) in zip(xs, ws, shapes):
+        pf, pd = bank.planes(x, w, s, k // 2, dg)
+        assert (pd is not None) == dg
+    bank.end_step()
+    with torch.no_grad():   # the optimizer moves the weights
+        for w in ws:
+            w.mul_(1.5).add_(0.01)
+    bank.begin_step(torch.device("cuda", 0))
+    assert not bank.dirty and bank.total_blocks > 0
+    for x, w, (N, C, k, s, dg) in zip(xs, ws, shapes):
+        pf, pd = bank.planes(x, w, s, k // 2, dg)
+        rf, rd = conv_ops._split_weights(x, w, s, k // 2, dg)
+        assert torch.equal(pf, rf)
+        assert (pd is None and rd is None) or torch.equal(pd, rd)
+    bank.end_step()
+
+
 @pytest.mark.parametrize("B,C,N,p,H,W", [(2, 16, 16, 0, 20, 34), (2, 32, 16, 0, 12, 18), (2, 16, 32, 1, 9, 13),
                                          (1, 16, 16, 1, 7, 9), (3, 32, 16, 2, 5, 6)])
 def test_direct_conv_matches_miopen(B, C, N, p, H, W):

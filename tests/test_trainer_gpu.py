@@ -150,6 +150,23 @@ def test_checkpoint_roundtrip(tmp_path):
         assert n == n2 and torch.equal(p, p2)
 
 
+def test_plane_bank_step_matches_per_call_splits(monkeypatch):
+    """Three training steps with the conv weights split once per step (conv_ops.PlaneBank,
+    one launch) update the networks bitwise like the per-convolution splits."""
+    from monodepth2_amd import conv_ops
+    monkeypatch.setattr(conv_ops, "AUTOTUNE", False)   # every eligible convolution on x6
+    results = []
+    for bank in (False, True):
+        monkeypatch.setattr(conv_ops, "PLANE_BANK", bank)
+        tr, batch = make("mono")
+        losses = [float(tr.train_step(batch)[1]["loss"]) for _ in range(3)]
+        torch.cuda.synchronize()
+        results.append((losses, [p.detach().clone() for p in tr.nets.parameters()]))
+    assert results[0][0] == results[1][0], (results[0][0], results[1][0])
+    assert all(torch.equal(a, b) for a, b in zip(results[0][1], results[1][1]))
+    assert conv_ops.plane_bank().entries, "the bank saw no x6 convolution"
+
+
 def test_hip_graph_replay_matches_eager_step():
     """A replay of the captured step (networks on two streams, fused hot path,
     backward, capturable fused Adam) computes what the same step does eagerly from
