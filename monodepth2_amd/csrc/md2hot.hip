@@ -480,6 +480,10 @@ struct PhotoArgs {
     // "every colour is exactly k/255" (null: fp32 planes only)
     const uint32_t* src8[MD2_MAX_SRC];
     const int* exact;
+    // photo_ident_kernel writes those 8-bit copies itself (it reads every source pixel
+    // anyway) when non-null: [S][B][h*w] RGBx, and clears [S][B] flags (preset to 1)
+    uint32_t* pack8;
+    int* pack_exact;
 };
 
 __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int b, WarpCtx& c) {
@@ -504,18 +508,21 @@ __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int 
 // Forward: two launches.
 //   photo_ident_kernel    identity losses of every source frame, once per step
 //                         (scale-invariant, trainer.py:432-439) -> identity planes
-//   photo_fwdall_kernel   one wave per (image, 16-row block, strip, scale): window
+//   photo_fwdall_kernel   one wave per (image, 13-row block, strip, scale): window
 //                         depths once, then one walk down the rows evaluating every
 //                         frame's warp + SSIM/L1 (trainer.py:426-430) with the target's
 //                         terms shared, each output row reduced at once to the minimum
 //                         over the identity (+ noise) and reprojection candidates
 //                         (466-482), automask code, one partial sum per wave
-// A 16-row item evaluates 18 rows (1.125x).  Round 2 wrote every reprojection loss
+// A 13-row item evaluates 15 rows (1.15x).  Round 2 wrote every reprojection loss
 // as a plane (47 MB at B=12) and re-read it in a third launch; those planes are gone,
 // and since round 3 the frames no longer walk the rows one after the other through a
 // running minimum in LDS (137 -> 124 us at B=12).
 // ----------------------------------------------------------------------------
-constexpr int kRowsP = 16;   // output rows per item of the forward passes
+#ifndef MD2_ROWS_P
+#define MD2_ROWS_P 13   // 15 window rows; 16 left a 2.06-round grid at B=12 (fwdall 124 -> 118 us)
+#endif
+constexpr int kRowsP = MD2_ROWS_P;   // output rows per item of the forward passes
 
 // one evaluated window row of the forward walk
 struct FRow {
@@ -608,6 +615,27 @@ __global__ __launch_bounds__(kBlock) void photo_ident_kernel(PhotoArgs a) {
     ctx.h = h;
     ctx.w = w;
     float* out = a.ident + ((size_t)f * a.B + it.b) * HW;
+    if (a.pack8) {
+        // the 8-bit RGBx copy of this wave's own output pixels of source frame f (the
+        // pack_src8_kernel arithmetic; these loads also warm the caches for the walk)
+        uint32_t* o8 = a.pack8 + ((size_t)f * a.B + it.b) * HW;
+        bool ok = true;
+        for (int i = 0; i < kRowsP; ++i) {
+            const int r = it.r0 + i;
+            if (!(it.colok && r < h)) continue;
+            uint32_t px = 0u;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                const float x = ldf(ctx.src, ch * HW + r * w + it.c);
+                const float k = rintf(x * 255.0f);
+                const bool in = k >= 0.f && k <= 255.f;
+                ok = ok && in && div255(k) == x;
+                px |= (uint32_t)(in ? k : 0.f) << (8 * ch);
+            }
+            o8[r * w + it.c] = px;
+        }
+        if (__ballot(!ok) != 0ull && lane == 0) a.pack_exact[f * a.B + it.b] = 0;
+    }
     loss_rows<SSIM_ON, false, false>(ctx, a.tgt + (size_t)it.b * 3 * HW, nullptr, it.r0, it.cc, lane, [&](int i, float v) {
         const int r = it.r0 + i;
         if (it.colok && r < h) out[r * w + it.c] = v;
@@ -616,7 +644,7 @@ __global__ __launch_bounds__(kBlock) void photo_ident_kernel(PhotoArgs a) {
 
 // ----------------------------------------------------------------------------
 // All-frames forward walk (photo_fwdall_kernel): one pass down the window rows per
-// (image, 16-row block, strip, scale) item evaluating every source frame at each row.
+// (image, 13-row block, strip, scale) item evaluating every source frame at each row.
 // Per row the target's colours, their horizontal sums and the camera ray are formed
 // once (not once per frame), the frames' gathers of a row are in flight together, and
 // each output row's candidates — identity (+ noise), then the frames in order — are
@@ -1947,10 +1975,18 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
             return fail(MD2_ERR_HIP, "hipMemsetAsync failed");
         const int per_img = (pk.HW + 4 * kBlock - 1) / (4 * kBlock);
         timing_slot(2, &c0, &c1);   // the whole call: pack .. finalize
-        hipExtLaunchKernelGGL(pack_src8_kernel, dim3(L.S * L.B * per_img), dim3(kBlock), 0, st, c0, nullptr, 0, pk);
         hipEvent_t e0, e1;
         timing_slot(0, &e0, &e1);
         photo_args(d, t, L, 0, L.nscales, false, ws, select_out, a);
+        if (!(d->flags & MD2_NO_AUTOMASK)) {
+            // the identity pass reads every source pixel: it writes the 8-bit copies too
+            a.pack8 = pk.out;
+            a.pack_exact = pk.exact;
+            if (c0 && hipEventRecord(c0, st) != hipSuccess) return fail(MD2_ERR_HIP, "hipEventRecord failed");
+        } else {
+            hipExtLaunchKernelGGL(pack_src8_kernel, dim3(L.S * L.B * per_img), dim3(kBlock), 0, st, c0, nullptr, 0,
+                                  pk);
+        }
         launch_photo(a, false, st, e0, e1);
     }
     if ((rc = hip_check("photo forward kernels"))) return rc;
