@@ -749,6 +749,127 @@ __device__ __forceinline__ void frowa_losses(const FRowA<NS>& A, const FRowA<NS>
     }
 }
 
+// ---- packed-channel form (MD2_PK): colour channels 0 and 1 as one 64-bit register
+// pair, so every per-channel add / mul / fma of the SSIM + L1 chain is one
+// v_pk_*_f32 (two lanes of work per issue slot, CDNA4's full f32 VALU rate) for
+// two channels, plus the scalar op for channel 2.  Same expressions as the scalar
+// form above, channel by channel.
+typedef float f2v __attribute__((ext_vector_type(2)));
+struct C3 {
+    f2v a;     // channels 0, 1
+    float b;   // channel 2
+};
+__device__ __forceinline__ C3 operator+(const C3& x, const C3& y) { return {x.a + y.a, x.b + y.b}; }
+__device__ __forceinline__ C3 operator-(const C3& x, const C3& y) { return {x.a - y.a, x.b - y.b}; }
+__device__ __forceinline__ C3 operator*(const C3& x, const C3& y) { return {x.a * y.a, x.b * y.b}; }
+__device__ __forceinline__ C3 operator*(const C3& x, float s) { return {x.a * s, x.b * s}; }
+__device__ __forceinline__ C3 operator+(const C3& x, float s) { return {x.a + s, x.b + s}; }
+__device__ __forceinline__ C3 shfl_prev3(const C3& v) {
+    return {f2v{shfl_prev(v.a.x), shfl_prev(v.a.y)}, shfl_prev(v.b)};
+}
+__device__ __forceinline__ C3 shfl_next3(const C3& v) {
+    return {f2v{shfl_next(v.a.x), shfl_next(v.a.y)}, shfl_next(v.b)};
+}
+__device__ __forceinline__ C3 ld3(const float* base, int HW, int idx) {
+    return {f2v{ldf(base, idx), ldf(base, HW + idx)}, ldf(base, 2 * HW + idx)};
+}
+__device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.f), 1.f); }
+__device__ __forceinline__ float sum3(const C3& v) { return v.a.x + v.a.y + v.b; }
+__device__ __forceinline__ C3 abs3(const C3& v) { return {f2v{fabsf(v.a.x), fabsf(v.a.y)}, fabsf(v.b)}; }
+
+template <int NS>
+struct FRowP {
+    C3 y, hy, hyy;                          // target colour, 3-tap sums of y, y^2
+    C3 x[NS], hx[NS], hxx[NS], hxy[NS];     // per frame: warped colour, sums of x, x^2, x*y
+};
+
+template <bool U8>
+__device__ __forceinline__ C3 interp3(const FastSample& s, const Corners& v) {
+    const float e = 1.f - s.tx, so = 1.f - s.ty;
+    const float wnw = so * e, wne = so * s.tx, wsw = s.ty * e, wse = s.ty * s.tx;
+    const C3 nw = {f2v{v.nw[0], v.nw[1]}, v.nw[2]}, ne = {f2v{v.ne[0], v.ne[1]}, v.ne[2]};
+    const C3 sw = {f2v{v.sw[0], v.sw[1]}, v.sw[2]}, se = {f2v{v.se[0], v.se[1]}, v.se[2]};
+    C3 o = nw * wnw + ne * wne + sw * wsw + se * wse;
+    if (U8) o = o * (1.0f / 255.0f);
+    return o;
+}
+
+template <int NS, bool SSIM_ON, bool U8>
+__device__ __forceinline__ void frowp_eval(const WarpCtx (&c)[NS], const float* tgt, float depth, int rr, int cc,
+                                           FRowP<NS>& o) {
+    const int HW = c[0].h * c[0].w;
+    const float fx = (float)cc, fy = (float)rr;
+    float pt[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        pt[i] = depth * (c[0].cm.iK[i * 3 + 0] * fx + c[0].cm.iK[i * 3 + 1] * fy + c[0].cm.iK[i * 3 + 2]);
+    o.y = ld3(tgt, HW, rr * c[0].w + cc);
+    C3 yl, yr;
+    if (SSIM_ON) {
+        yl = shfl_prev3(o.y);
+        yr = shfl_next3(o.y);
+        o.hy = yl + o.y + yr;
+        o.hyy = yl * yl + o.y * o.y + yr * yr;
+    }
+#pragma unroll
+    for (int f = 0; f < NS; ++f) {
+        FastSample s;
+        float cam[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            cam[i] = c[f].cm.P[i * 4 + 0] * pt[0] + c[f].cm.P[i * 4 + 1] * pt[1] + c[f].cm.P[i * 4 + 2] * pt[2] +
+                     c[f].cm.P[i * 4 + 3];
+        const float inv_den = rcpf(cam[2] + 1e-7f);
+        const float ix = cam[0] * inv_den * c[f].sx - 0.5f, iy = cam[1] * inv_den * c[f].sy - 0.5f;
+        const float xmax = (float)(c[f].w - 1), ymax = (float)(c[f].h - 1);
+        const float ixc = fminf(fmaxf(ix, 0.f), xmax), iyc = fminf(fmaxf(iy, 0.f), ymax);
+        const float fx0 = floorf(ixc), fy0 = floorf(iyc);
+        s.x0 = (int)fx0;
+        s.y0 = (int)fy0;
+        s.tx = ixc - fx0;
+        s.ty = iyc - fy0;
+        Corners v;
+        gather<U8>(c[f], s, v);
+        o.x[f] = interp3<U8>(s, v);
+        if (SSIM_ON) {
+            const C3 xl = shfl_prev3(o.x[f]), xr = shfl_next3(o.x[f]);
+            o.hx[f] = xl + o.x[f] + xr;
+            o.hxx[f] = xl * xl + o.x[f] * o.x[f] + xr * xr;
+            o.hxy[f] = xl * yl + o.x[f] * o.y + xr * yr;
+        }
+    }
+}
+
+template <int NS, bool SSIM_ON>
+__device__ __forceinline__ void frowp_losses(const FRowP<NS>& A, const FRowP<NS>& B, const FRowP<NS>& C,
+                                             float (&loss)[NS]) {
+    C3 my, sy;
+    if (SSIM_ON) {
+        my = (A.hy + B.hy + C.hy) * kInv9;
+        sy = (A.hyy + B.hyy + C.hyy) * kInv9 - my * my;
+    }
+#pragma unroll
+    for (int f = 0; f < NS; ++f) {
+        const float l1 = sum3(abs3(B.y - B.x[f]));
+        if (SSIM_ON) {
+            const C3 mx = (A.hx[f] + B.hx[f] + C.hx[f]) * kInv9;
+            const C3 sx = (A.hxx[f] + B.hxx[f] + C.hxx[f]) * kInv9 - mx * mx;
+            const C3 sxy = (A.hxy[f] + B.hxy[f] + C.hxy[f]) * kInv9 - mx * my;
+            const C3 n = (mx * my * 2.f + kC1) * (sxy * 2.f + kC2);
+            const C3 d = (mx * mx + my * my + kC1) * (sx + sy + kC2);
+            const float ss = clamp01((1.f - n.a.x * rcpf(d.a.x)) * 0.5f) + clamp01((1.f - n.a.y * rcpf(d.a.y)) * 0.5f) +
+                             clamp01((1.f - n.b * rcpf(d.b)) * 0.5f);
+            loss[f] = 0.85f * div3(ss) + 0.15f * div3(l1);
+        } else {
+            loss[f] = div3(l1);
+        }
+    }
+}
+
+#ifndef MD2_PK
+#define MD2_PK 1
+#endif
+
 template <int NS, bool SSIM_ON, bool MASK, bool U8>
 __device__ __forceinline__ float fwdall_walk(const PhotoArgs& a, const WarpCtx (&ctx)[NS], const FItem& it, int ls,
                                              const float (*dep)[kWave], int lane) {
@@ -763,9 +884,18 @@ __device__ __forceinline__ float fwdall_walk(const PhotoArgs& a, const WarpCtx (
     uint8_t* sel = a.sel[ls] + (size_t)it.b * HW;
     float lsum = 0.f;
     // output row i = window row k - 2 from rows (k-2, k-1, k)
-    auto out_row = [&](int i, const FRowA<NS>& A, const FRowA<NS>& B, const FRowA<NS>& Cr) {
+#if MD2_PK
+    using Row = FRowP<NS>;
+#else
+    using Row = FRowA<NS>;
+#endif
+    auto out_row = [&](int i, const Row& A, const Row& B, const Row& Cr) {
         float lf[NS];
+#if MD2_PK
+        frowp_losses<NS, SSIM_ON>(A, B, Cr, lf);
+#else
         frowa_losses<NS, SSIM_ON>(A, B, Cr, lf);
+#endif
         const int r = it.r0 + i;
         if (!(it.colok && r < h)) return;
         const int p = r * w + it.c;
@@ -830,17 +960,23 @@ __device__ __forceinline__ float fwdall_walk(const PhotoArgs& a, const WarpCtx (
         lsum += bv;
         sel[p] = (uint8_t)bc;
     };
-    FRowA<NS> R0, R1, R2;
+    Row R0, R1, R2;
+#if MD2_PK
+#define MD2_FROW_EVAL frowp_eval
+#else
+#define MD2_FROW_EVAL frowa_eval
+#endif
     static_assert((kRowsP + 2) % 3 == 0, "window rows must be a multiple of 3");
 #pragma unroll 1
     for (int k = 0; k < kRowsP + 2; k += 3) {
-        frowa_eval<NS, SSIM_ON, U8>(ctx, tgt, dep[k][lane], reflect_clamp(it.r0 - 1 + k, h), it.cc, R0);
+        MD2_FROW_EVAL<NS, SSIM_ON, U8>(ctx, tgt, dep[k][lane], reflect_clamp(it.r0 - 1 + k, h), it.cc, R0);
         if (k >= 2) out_row(k - 2, R1, R2, R0);
-        frowa_eval<NS, SSIM_ON, U8>(ctx, tgt, dep[k + 1][lane], reflect_clamp(it.r0 + k, h), it.cc, R1);
+        MD2_FROW_EVAL<NS, SSIM_ON, U8>(ctx, tgt, dep[k + 1][lane], reflect_clamp(it.r0 + k, h), it.cc, R1);
         if (k >= 1) out_row(k - 1, R2, R0, R1);
-        frowa_eval<NS, SSIM_ON, U8>(ctx, tgt, dep[k + 2][lane], reflect_clamp(it.r0 + 1 + k, h), it.cc, R2);
+        MD2_FROW_EVAL<NS, SSIM_ON, U8>(ctx, tgt, dep[k + 2][lane], reflect_clamp(it.r0 + 1 + k, h), it.cc, R2);
         out_row(k, R0, R1, R2);
     }
+#undef MD2_FROW_EVAL
     return lsum;
 }
 
@@ -1158,6 +1294,193 @@ __device__ __forceinline__ void bwd_frame_walk(const BwdFrame& F, float (*ddacc)
     }
 }
 
+// ---- packed-channel backward (MD2_PKB): the row walk above with channels (0, 1) in
+// one register pair (C3), so the SSIM sums, adjoint, 3-tap folds and the output
+// chain issue v_pk_*_f32 for two channels.  Expressions as in the scalar form.
+struct H5P {
+    C3 x, xx, xy, y, yy;
+};
+struct CarryP {
+    C3 jx, jy;
+    float px, py, inv_den;
+    float pt[3];
+    float u[3];
+    float dd;
+};
+struct RowP {
+    H5P h;
+    C3 x, y;
+    CarryP k;
+};
+struct CoefP {
+    C3 A, B, C;
+    float g;
+};
+
+__device__ __forceinline__ H5P hsum3(const C3& x, const C3& y) {
+    const C3 xl = shfl_prev3(x), xr = shfl_next3(x), yl = shfl_prev3(y), yr = shfl_next3(y);
+    return {xl + x + xr, xl * xl + x * x + xr * xr, xl * yl + x * y + xr * yr, yl + y + yr, yl * yl + y * y + yr * yr};
+}
+
+__device__ __forceinline__ float ssim1(float n, float d) { return clamp01((1.f - n * rcpf(d)) * 0.5f); }
+
+// sum over the three channels of SSIM at the middle row of (a, b, c) (ssim_from_sums)
+__device__ __forceinline__ float ssim_sum3(const H5P& a, const H5P& b, const H5P& c) {
+    const C3 mx = (a.x + b.x + c.x) * kInv9, my = (a.y + b.y + c.y) * kInv9;
+    const C3 sx = (a.xx + b.xx + c.xx) * kInv9 - mx * mx;
+    const C3 sy = (a.yy + b.yy + c.yy) * kInv9 - my * my;
+    const C3 sxy = (a.xy + b.xy + c.xy) * kInv9 - mx * my;
+    const C3 n = (mx * my * 2.f + kC1) * (sxy * 2.f + kC2);
+    const C3 d = (mx * mx + my * my + kC1) * (sx + sy + kC2);
+    return ssim1(n.a.x, d.a.x) + ssim1(n.a.y, d.a.y) + ssim1(n.b, d.b);
+}
+
+__device__ __forceinline__ float clamp_pass(float raw, float g) { return (raw >= 0.f && raw <= 1.f) ? g : 0.f; }
+
+// ssim_adjoint for the three channels
+__device__ __forceinline__ void ssim_adjoint3(const H5P& a, const H5P& b, const H5P& c, float gS, C3& dA, C3& dB,
+                                              C3& dC) {
+    const C3 mx = (a.x + b.x + c.x) * kInv9, my = (a.y + b.y + c.y) * kInv9;
+    const C3 sx = (a.xx + b.xx + c.xx) * kInv9 - mx * mx;
+    const C3 sy = (a.yy + b.yy + c.yy) * kInv9 - my * my;
+    const C3 sxy = (a.xy + b.xy + c.xy) * kInv9 - mx * my;
+    const C3 n1 = mx * my * 2.f + kC1, n2 = sxy * 2.f + kC2;
+    const C3 d1 = mx * mx + my * my + kC1, d2 = sx + sy + kC2;
+    const C3 n = n1 * n2, d = d1 * d2;
+    const C3 inv_d = {f2v{rcpf(d.a.x), rcpf(d.a.y)}, rcpf(d.b)};
+    const C3 raw = ((n * inv_d) * -1.f + 1.f) * 0.5f;
+    const C3 g = {f2v{clamp_pass(raw.a.x, gS), clamp_pass(raw.a.y, gS)}, clamp_pass(raw.b, gS)};
+    const C3 dn = g * -0.5f * inv_d;
+    const C3 dd = g * 0.5f * n * inv_d * inv_d;
+    dA = dn * (my * 2.f * (n2 - n1)) + dd * (mx * 2.f * (d2 - d1));
+    dB = dd * d1;
+    dC = dn * 2.f * n1;
+}
+
+__device__ __forceinline__ C3 sign3(const C3& v) { return {f2v{signf(v.a.x), signf(v.a.y)}, signf(v.b)}; }
+
+template <bool U8>
+__device__ __forceinline__ void make_carry3(const WarpCtx& c, const FastSample& s, const Corners& v, CarryP& k) {
+    const float e = 1.f - s.tx, so = 1.f - s.ty;
+    const float cs = U8 ? 1.0f / 255.0f : 1.0f;
+    const float mx = s.gmx * c.sx * cs, my = s.gmy * c.sy * cs;
+    const C3 nw = {f2v{v.nw[0], v.nw[1]}, v.nw[2]}, ne = {f2v{v.ne[0], v.ne[1]}, v.ne[2]};
+    const C3 sw = {f2v{v.sw[0], v.sw[1]}, v.sw[2]}, se = {f2v{v.se[0], v.se[1]}, v.se[2]};
+    k.jx = ((ne - nw) * so + (se - sw) * s.ty) * mx;
+    k.jy = ((sw - nw) * e + (se - ne) * s.tx) * my;
+    k.px = s.px;
+    k.py = s.py;
+    k.inv_den = s.inv_den;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        k.pt[i] = s.pt[i];
+        k.u[i] = c.cm.P[i * 4 + 0] * s.ray[0] + c.cm.P[i * 4 + 1] * s.ray[1] + c.cm.P[i * 4 + 2] * s.ray[2];
+    }
+    k.dd = -c.range * s.depth * s.depth;
+}
+
+template <int NS, bool SSIM_ON, bool MASK, bool U8>
+__device__ __forceinline__ void bwd_step_p(const BwdFrame& F, int k, RowP& cur, const RowP& m1, const RowP& m2,
+                                           CoefP& cnew, const CoefP& cm2, const CoefP& cm3, float (&dP)[12],
+                                           float (*ddacc)[kWave], int lane) {
+    constexpr float kThird = 1.0f / 3.0f;
+    const float l1w = SSIM_ON ? 0.15f : 1.0f;
+    const int h = F.ctx.h, w = F.ctx.w, HW = h * w;
+    const int r = F.r0 - 2 + k;
+    const int rr = reflect_clamp(r, h);
+    FastSample sm;
+    project_depth(F.ctx, rr, F.cc, F.dep[k][lane], sm);
+    Corners v;
+    gather<U8>(F.ctx, sm, v);
+    cur.x = interp3<U8>(sm, v);
+    cur.y = ld3(F.tgt, HW, rr * w + F.cc);
+    if (k >= 2 && k < kRowsB + 2) make_carry3<U8>(F.ctx, sm, v, cur.k);   // only output rows need it
+    if (SSIM_ON) cur.h = hsum3(cur.x, cur.y);
+    if (k < 2) return;
+    // coefficient row p = r - 1
+    const int p = r - 1;
+    float gp = 0.f;
+    const bool own = F.colreal && p >= 0 && p < h;
+    if (own) gp = F.gscale * frame_weight<NS>(ldb(F.sel, p * w + F.c), F.f, F.automask, F.avg);
+    if (MASK) {
+        // masked = reproj * mask (trainer.py:455): d/dreproj = g*mask, d/dmask = g*reproj
+        const size_t mi = (((size_t)F.b * NS + F.f) * h + (own ? p : 0)) * w + (own ? F.c : 0);
+        if (F.pgmask && F.colok && p >= F.r0 && p < F.r0 + kRowsB && p < h) {
+            const float ss = SSIM_ON ? ssim_sum3(m2.h, m1.h, cur.h) : 0.f;
+            const float l1 = sum3(abs3(m1.y - m1.x));
+            const float rep = SSIM_ON ? 0.85f * div3(ss) + 0.15f * div3(l1) : div3(l1);
+            F.pgmask[mi] = gp * rep;
+        }
+        gp *= own ? F.pmask[mi] : 0.f;
+    }
+    cnew.g = gp;
+    if (SSIM_ON) {
+        const float gS = gp * (0.85f / 3.f);
+        C3 dA, dB, dC;
+        ssim_adjoint3(m2.h, m1.h, cur.h, gS, dA, dB, dC);
+        if (gp == 0.f) dA = dB = dC = C3{f2v{0.f, 0.f}, 0.f};
+        cnew.A = shfl_prev3(dA) * F.wl + dA + shfl_next3(dA) * F.wr;
+        cnew.B = shfl_prev3(dB) * F.wl + dB + shfl_next3(dB) * F.wr;
+        cnew.C = shfl_prev3(dC) * F.wl + dC + shfl_next3(dC) * F.wr;
+    }
+    if (k < 4) return;
+    // output row q = r - 2 (coefficient rows q-1, q, q+1 = cm3, cm2, cnew)
+    const int q = r - 2;
+    if (!(F.colok && q < h)) return;
+    const CarryP& k2 = m2.k;
+    const float l1c = cm2.g * (l1w * kThird);
+    C3 g = sign3(m2.x - m2.y) * l1c;
+    if (SSIM_ON) {
+        const float wu = fold_lo(q), wd = fold_hi(q, h);
+        const C3 aA = cm3.A * wu + cm2.A + cnew.A * wd;
+        const C3 aB = cm3.B * wu + cm2.B + cnew.B * wd;
+        const C3 aC = cm3.C * wu + cm2.C + cnew.C * wd;
+        g = g + (aA + m2.x * 2.f * aB + m2.y * aC) * kInv9;
+    }
+    const float dpx = sum3(g * k2.jx), dpy = sum3(g * k2.jy);
+    float dc[3];
+    dc[0] = dpx * k2.inv_den;
+    dc[1] = dpy * k2.inv_den;
+    dc[2] = -(dpx * k2.px + dpy * k2.py) * k2.inv_den;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) dP[i * 4 + j] += dc[i] * k2.pt[j];
+        dP[i * 4 + 3] += dc[i];
+    }
+    const float dd = (dc[0] * k2.u[0] + dc[1] * k2.u[1] + dc[2] * k2.u[2]) * k2.dd;
+    if (F.f == 0) ddacc[q - F.r0][lane] = dd;
+    else ddacc[q - F.r0][lane] += dd;
+}
+
+template <int NS, bool SSIM_ON, bool MASK, bool U8>
+__device__ __forceinline__ void bwd_frame_walk_p(const BwdFrame& F, float (*ddacc)[kWave], float* dst, int lane) {
+    float dP[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) dP[j] = 0.f;
+    RowP S0, S1, S2;
+    CoefP C0, C1, C2;
+    constexpr int kSteps = kRowsB + 4;
+    int k = 0;
+#pragma unroll 1
+    for (; k + 3 <= kSteps; k += 3) {
+        bwd_step_p<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
+        bwd_step_p<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
+        bwd_step_p<NS, SSIM_ON, MASK, U8>(F, k + 2, S2, S1, S0, C1, C0, C2, dP, ddacc, lane);
+    }
+    if (kSteps % 3 >= 1) bwd_step_p<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
+    if (kSteps % 3 >= 2) bwd_step_p<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        const float t = wave_sum(dP[j]);
+        if (lane == 0) dst[j] = t;
+    }
+}
+
+#ifndef MD2_PKB
+#define MD2_PKB 1
+#endif
+
 // One work item of the backward: (image b, local scale ls, strip st, row block rb),
 // all source frames.  Writes dL/d(upsampled disp) for its 60 x kRowsB pixels and one
 // 12-float dL/dP partial per frame.
@@ -1194,10 +1517,17 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
         F.f = f;
         make_ctx(a, ls, f, b, F.ctx);
         float* dst = a.dP_part[ls] + ((size_t)f * a.B * a.wpi + item_in_scale) * 12;
+#if MD2_PKB
+        if (F.ctx.src8)
+            bwd_frame_walk_p<NS, SSIM_ON, MASK, true>(F, ddacc, dst, lane);
+        else
+            bwd_frame_walk_p<NS, SSIM_ON, MASK, false>(F, ddacc, dst, lane);
+#else
         if (F.ctx.src8)
             bwd_frame_walk<NS, SSIM_ON, MASK, true>(F, ddacc, dst, lane);
         else
             bwd_frame_walk<NS, SSIM_ON, MASK, false>(F, ddacc, dst, lane);
+#endif
     }
     const int upsh = a.upsh[ls];
 #ifdef MD2_NO_FOLD   // timing experiments only: results are wrong
