@@ -384,64 +384,95 @@ __device__ __forceinline__ void interp(const SampleT& s, const Corners& v, float
     }
 }
 
-template <bool U8>
-__device__ __forceinline__ void warp_value(const WarpCtx& c, int y, int x, float depth, float out[3]) {
-    FastSample s;
-    project_depth(c, y, x, depth, s);
-    Corners v;
-    gather<U8>(c, s, v);
-    interp<U8>(s, v, out);
-}
-
 // ----------------------------------------------------------------------------
-// SSIM pieces
+// Colour channels as C3: channels 0 and 1 in one 64-bit register pair, channel 2 alone,
+// so every per-channel add / mul / fma of the SSIM + L1 chains (and their adjoint) is
+// one v_pk_*_f32 for two channels (two lanes of work per issue slot, the f32 VALU peak
+// of CDNA4) plus the scalar op for the third.  Round 3 moved the kernels from per-channel
+// scalars to C3 (static VALU -12 %: fwdall 117 -> 113 us, photo_bwd 271 -> 257 us at B=12).
 // ----------------------------------------------------------------------------
-struct H5 {  // horizontal 3-tap sums of x, x^2, x*y, y, y^2 for one channel
-    float x, xx, xy, y, yy;
+typedef float f2v __attribute__((ext_vector_type(2)));
+struct C3 {
+    f2v a;     // channels 0, 1
+    float b;   // channel 2
 };
+__device__ __forceinline__ C3 operator+(const C3& x, const C3& y) { return {x.a + y.a, x.b + y.b}; }
+__device__ __forceinline__ C3 operator-(const C3& x, const C3& y) { return {x.a - y.a, x.b - y.b}; }
+__device__ __forceinline__ C3 operator*(const C3& x, const C3& y) { return {x.a * y.a, x.b * y.b}; }
+__device__ __forceinline__ C3 operator*(const C3& x, float s) { return {x.a * s, x.b * s}; }
+__device__ __forceinline__ C3 operator+(const C3& x, float s) { return {x.a + s, x.b + s}; }
+__device__ __forceinline__ C3 shfl_prev3(const C3& v) {
+    return {f2v{shfl_prev(v.a.x), shfl_prev(v.a.y)}, shfl_prev(v.b)};
+}
+__device__ __forceinline__ C3 shfl_next3(const C3& v) {
+    return {f2v{shfl_next(v.a.x), shfl_next(v.a.y)}, shfl_next(v.b)};
+}
+__device__ __forceinline__ C3 ld3(const float* base, int HW, int idx) {
+    return {f2v{ldf(base, idx), ldf(base, HW + idx)}, ldf(base, 2 * HW + idx)};
+}
+__device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.f), 1.f); }
+__device__ __forceinline__ float sum3(const C3& v) { return v.a.x + v.a.y + v.b; }
+__device__ __forceinline__ C3 abs3(const C3& v) { return {f2v{fabsf(v.a.x), fabsf(v.a.y)}, fabsf(v.b)}; }
 
-__device__ __forceinline__ H5 hsum(float x, float y) {
-    const float xl = shfl_prev(x), xr = shfl_next(x);
-    const float yl = shfl_prev(y), yr = shfl_next(y);
-    H5 o;
-    o.x = xl + x + xr;
-    o.xx = xl * xl + x * x + xr * xr;
-    o.xy = xl * yl + x * y + xr * yr;
-    o.y = yl + y + yr;
-    o.yy = yl * yl + y * y + yr * yr;
+template <bool U8>
+__device__ __forceinline__ C3 interp3(const FastSample& s, const Corners& v) {
+    const float e = 1.f - s.tx, so = 1.f - s.ty;
+    const float wnw = so * e, wne = so * s.tx, wsw = s.ty * e, wse = s.ty * s.tx;
+    const C3 nw = {f2v{v.nw[0], v.nw[1]}, v.nw[2]}, ne = {f2v{v.ne[0], v.ne[1]}, v.ne[2]};
+    const C3 sw = {f2v{v.sw[0], v.sw[1]}, v.sw[2]}, se = {f2v{v.se[0], v.se[1]}, v.se[2]};
+    C3 o = nw * wnw + ne * wne + sw * wsw + se * wse;
+    if (U8) o = o * (1.0f / 255.0f);
     return o;
 }
 
-__device__ __forceinline__ float ssim_from_sums(const H5& a, const H5& b, const H5& c) {
-    const float mx = (a.x + b.x + c.x) * kInv9, my = (a.y + b.y + c.y) * kInv9;
-    const float sx = (a.xx + b.xx + c.xx) * kInv9 - mx * mx;
-    const float sy = (a.yy + b.yy + c.yy) * kInv9 - my * my;
-    const float sxy = (a.xy + b.xy + c.xy) * kInv9 - mx * my;
-    const float n = (2.f * mx * my + kC1) * (2.f * sxy + kC2);
-    const float d = (mx * mx + my * my + kC1) * (sx + sy + kC2);
-    return fminf(fmaxf((1.f - n * rcpf(d)) * 0.5f, 0.f), 1.f);
+// ----------------------------------------------------------------------------
+// SSIM pieces (layers.py:218-248), three channels at once
+// ----------------------------------------------------------------------------
+struct H5P {  // horizontal 3-tap sums of x, x^2, x*y, y, y^2
+    C3 x, xx, xy, y, yy;
+};
+
+__device__ __forceinline__ H5P hsum3(const C3& x, const C3& y) {
+    const C3 xl = shfl_prev3(x), xr = shfl_next3(x), yl = shfl_prev3(y), yr = shfl_next3(y);
+    return {xl + x + xr, xl * xl + x * x + xr * xr, xl * yl + x * y + xr * yr, yl + y + yr, yl * yl + y * y + yr * yr};
 }
 
-// dL/d(box mean of x), dL/d(box mean of x^2), dL/d(box mean of x*y) at one pixel,
-// given dL/dSSIM (layers.py:238-248 differentiated by hand)
-__device__ __forceinline__ void ssim_adjoint(const H5& a, const H5& b, const H5& c, float gS, float& dA,
-                                             float& dB, float& dC) {
-    const float mx = (a.x + b.x + c.x) * kInv9, my = (a.y + b.y + c.y) * kInv9;
-    const float sx = (a.xx + b.xx + c.xx) * kInv9 - mx * mx;
-    const float sy = (a.yy + b.yy + c.yy) * kInv9 - my * my;
-    const float sxy = (a.xy + b.xy + c.xy) * kInv9 - mx * my;
-    const float n1 = 2.f * mx * my + kC1, n2 = 2.f * sxy + kC2;
-    const float d1 = mx * mx + my * my + kC1, d2 = sx + sy + kC2;
-    const float n = n1 * n2, d = d1 * d2;
-    const float inv_d = rcpf(d);
-    const float raw = (1.f - n * inv_d) * 0.5f;
-    const float g = (raw >= 0.f && raw <= 1.f) ? gS : 0.f;  // clamp passes [0,1] inclusive
-    const float dn = -0.5f * g * inv_d;
-    const float dd = 0.5f * g * n * inv_d * inv_d;
-    dA = dn * (2.f * my * (n2 - n1)) + dd * (2.f * mx * (d2 - d1));
+__device__ __forceinline__ float ssim1(float n, float d) { return clamp01((1.f - n * rcpf(d)) * 0.5f); }
+
+// sum over the three channels of SSIM at the middle row of (a, b, c) (ssim_from_sums)
+__device__ __forceinline__ float ssim_sum3(const H5P& a, const H5P& b, const H5P& c) {
+    const C3 mx = (a.x + b.x + c.x) * kInv9, my = (a.y + b.y + c.y) * kInv9;
+    const C3 sx = (a.xx + b.xx + c.xx) * kInv9 - mx * mx;
+    const C3 sy = (a.yy + b.yy + c.yy) * kInv9 - my * my;
+    const C3 sxy = (a.xy + b.xy + c.xy) * kInv9 - mx * my;
+    const C3 n = (mx * my * 2.f + kC1) * (sxy * 2.f + kC2);
+    const C3 d = (mx * mx + my * my + kC1) * (sx + sy + kC2);
+    return ssim1(n.a.x, d.a.x) + ssim1(n.a.y, d.a.y) + ssim1(n.b, d.b);
+}
+
+__device__ __forceinline__ float clamp_pass(float raw, float g) { return (raw >= 0.f && raw <= 1.f) ? g : 0.f; }
+
+// ssim_adjoint for the three channels
+__device__ __forceinline__ void ssim_adjoint3(const H5P& a, const H5P& b, const H5P& c, float gS, C3& dA, C3& dB,
+                                              C3& dC) {
+    const C3 mx = (a.x + b.x + c.x) * kInv9, my = (a.y + b.y + c.y) * kInv9;
+    const C3 sx = (a.xx + b.xx + c.xx) * kInv9 - mx * mx;
+    const C3 sy = (a.yy + b.yy + c.yy) * kInv9 - my * my;
+    const C3 sxy = (a.xy + b.xy + c.xy) * kInv9 - mx * my;
+    const C3 n1 = mx * my * 2.f + kC1, n2 = sxy * 2.f + kC2;
+    const C3 d1 = mx * mx + my * my + kC1, d2 = sx + sy + kC2;
+    const C3 n = n1 * n2, d = d1 * d2;
+    const C3 inv_d = {f2v{rcpf(d.a.x), rcpf(d.a.y)}, rcpf(d.b)};
+    const C3 raw = ((n * inv_d) * -1.f + 1.f) * 0.5f;
+    const C3 g = {f2v{clamp_pass(raw.a.x, gS), clamp_pass(raw.a.y, gS)}, clamp_pass(raw.b, gS)};
+    const C3 dn = g * -0.5f * inv_d;
+    const C3 dd = g * 0.5f * n * inv_d * inv_d;
+    dA = dn * (my * 2.f * (n2 - n1)) + dd * (mx * 2.f * (d2 - d1));
     dB = dd * d1;
     dC = dn * 2.f * n1;
 }
+
+__device__ __forceinline__ C3 sign3(const C3& v) { return {f2v{signf(v.a.x), signf(v.a.y)}, signf(v.b)}; }
 
 // ----------------------------------------------------------------------------
 // kernel arguments
@@ -524,61 +555,24 @@ __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int 
 #endif
 constexpr int kRowsP = MD2_ROWS_P;   // output rows per item of the forward passes
 
-// one evaluated window row of the forward walk
-struct FRow {
-    H5 h[3];
-    float x[3], y[3];
+// one evaluated window row of the identity walk (target and unwarped source)
+struct IRow {
+    H5P h;
+    C3 x, y;
 };
 
-template <bool SSIM_ON, bool WARPED, bool U8>
-__device__ __forceinline__ void frow_eval(const WarpCtx& c, const float* tgt, const float (*dep)[kWave], int k,
-                                          int rr, int cc, int lane, FRow& o) {
-    const int HW = c.h * c.w;
-    if (WARPED) {
-        warp_value<U8>(c, rr, cc, dep[k][lane], o.x);
-    } else {
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) o.x[ch] = ldf(c.src, ch * HW + rr * c.w + cc);
-    }
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) o.y[ch] = ldf(tgt, ch * HW + rr * c.w + cc);
-    if (SSIM_ON) {
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) o.h[ch] = hsum(o.x[ch], o.y[ch]);
-    }
+template <bool SSIM_ON>
+__device__ __forceinline__ void irow_eval(const float* src, const float* tgt, int HW, int idx, IRow& o) {
+    o.x = ld3(src, HW, idx);
+    o.y = ld3(tgt, HW, idx);
+    if (SSIM_ON) o.h = hsum3(o.x, o.y);
 }
 
 // loss of the middle row of (a, b, c) at this lane (trainer.py:393-405)
 template <bool SSIM_ON>
-__device__ __forceinline__ float frow_loss(const FRow& a, const FRow& b, const FRow& c) {
-    float ss = 0.f, l1 = 0.f;
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-        if (SSIM_ON) ss += ssim_from_sums(a.h[ch], b.h[ch], c.h[ch]);
-        l1 += fabsf(b.y[ch] - b.x[ch]);
-    }
-    return SSIM_ON ? 0.85f * div3(ss) + 0.15f * div3(l1) : div3(l1);
-}
-
-// Losses of output rows r0 .. r0+kRowsP-1 at this lane's column; emit(i, v) per row.
-// The 3-row window rotates through three statically named slots (unrolled by 3).
-template <bool SSIM_ON, bool WARPED, bool U8, class Emit>
-__device__ __forceinline__ void loss_rows(const WarpCtx& c, const float* tgt, const float (*dep)[kWave], int r0,
-                                          int cc, int lane, Emit emit) {
-    const int h = c.h;
-    FRow R0, R1, R2;
-    // window row k = 0 .. kRowsP+1 is image row r0 - 1 + k; output row i = k - 2 + ... :
-    // after evaluating row k (k >= 2) the rows k-2, k-1, k give output row k-2
-    static_assert((kRowsP + 2) % 3 == 0, "window rows must be a multiple of 3");
-#pragma unroll 1
-    for (int k = 0; k < kRowsP + 2; k += 3) {
-        frow_eval<SSIM_ON, WARPED, U8>(c, tgt, dep, k, reflect_clamp(r0 - 1 + k, h), cc, lane, R0);
-        if (k >= 2) emit(k - 2, frow_loss<SSIM_ON>(R1, R2, R0));
-        frow_eval<SSIM_ON, WARPED, U8>(c, tgt, dep, k + 1, reflect_clamp(r0 + k, h), cc, lane, R1);
-        if (k >= 1) emit(k - 1, frow_loss<SSIM_ON>(R2, R0, R1));
-        frow_eval<SSIM_ON, WARPED, U8>(c, tgt, dep, k + 2, reflect_clamp(r0 + 1 + k, h), cc, lane, R2);
-        emit(k, frow_loss<SSIM_ON>(R0, R1, R2));
-    }
+__device__ __forceinline__ float irow_loss(const IRow& a, const IRow& b, const IRow& c) {
+    const float l1 = sum3(abs3(b.y - b.x));
+    return SSIM_ON ? 0.85f * div3(ssim_sum3(a.h, b.h, c.h)) + 0.15f * div3(l1) : div3(l1);
 }
 
 // item geometry of the split forward: 62-column strips with one halo lane per side
@@ -636,10 +630,24 @@ __global__ __launch_bounds__(kBlock) void photo_ident_kernel(PhotoArgs a) {
         }
         if (__ballot(!ok) != 0ull && lane == 0) a.pack_exact[f * a.B + it.b] = 0;
     }
-    loss_rows<SSIM_ON, false, false>(ctx, a.tgt + (size_t)it.b * 3 * HW, nullptr, it.r0, it.cc, lane, [&](int i, float v) {
+    // window row k = 0 .. kRowsP+1 is image row r0 - 1 + k; rows (k-2, k-1, k) give output
+    // row k - 2; the window rotates through three statically named slots (unrolled by 3)
+    const float* tgt = a.tgt + (size_t)it.b * 3 * HW;
+    auto emit = [&](int i, float v) {
         const int r = it.r0 + i;
         if (it.colok && r < h) out[r * w + it.c] = v;
-    });
+    };
+    IRow R0, R1, R2;
+    static_assert((kRowsP + 2) % 3 == 0, "window rows must be a multiple of 3");
+#pragma unroll 1
+    for (int k = 0; k < kRowsP + 2; k += 3) {
+        irow_eval<SSIM_ON>(ctx.src, tgt, HW, reflect_clamp(it.r0 - 1 + k, h) * w + it.cc, R0);
+        if (k >= 2) emit(k - 2, irow_loss<SSIM_ON>(R1, R2, R0));
+        irow_eval<SSIM_ON>(ctx.src, tgt, HW, reflect_clamp(it.r0 + k, h) * w + it.cc, R1);
+        if (k >= 1) emit(k - 1, irow_loss<SSIM_ON>(R2, R0, R1));
+        irow_eval<SSIM_ON>(ctx.src, tgt, HW, reflect_clamp(it.r0 + 1 + k, h) * w + it.cc, R2);
+        emit(k, irow_loss<SSIM_ON>(R0, R1, R2));
+    }
 }
 
 // ----------------------------------------------------------------------------
@@ -649,150 +657,13 @@ __global__ __launch_bounds__(kBlock) void photo_ident_kernel(PhotoArgs a) {
 // once (not once per frame), the frames' gathers of a row are in flight together, and
 // each output row's candidates — identity (+ noise), then the frames in order — are
 // reduced to the minimum at once, so no running minimum goes through LDS.
-// Arithmetic per frame as frow_eval / ssim_from_sums (the same expressions).
+// Arithmetic per frame as the identity walk (irow_eval / irow_loss).
 // ----------------------------------------------------------------------------
-template <int NS>
-struct FRowA {
-    float y[3], hy[3], hyy[3];                          // target colour, 3-tap sums of y, y^2
-    float x[NS][3], hx[NS][3], hxx[NS][3], hxy[NS][3];  // per frame: warped colour, sums of x, x^2, x*y
-};
-
-template <int NS, bool SSIM_ON, bool U8>
-__device__ __forceinline__ void frowa_eval(const WarpCtx (&c)[NS], const float* tgt, float depth, int rr, int cc,
-                                           FRowA<NS>& o) {
-    const int HW = c[0].h * c[0].w;
-    const float fx = (float)cc, fy = (float)rr;
-    float ray[3], pt[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        ray[i] = c[0].cm.iK[i * 3 + 0] * fx + c[0].cm.iK[i * 3 + 1] * fy + c[0].cm.iK[i * 3 + 2];
-        pt[i] = depth * ray[i];
-    }
-    float yl[3], yr[3];
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-        o.y[ch] = ldf(tgt, ch * HW + rr * c[0].w + cc);
-        if (SSIM_ON) {
-            yl[ch] = shfl_prev(o.y[ch]);
-            yr[ch] = shfl_next(o.y[ch]);
-            o.hy[ch] = yl[ch] + o.y[ch] + yr[ch];
-            o.hyy[ch] = yl[ch] * yl[ch] + o.y[ch] * o.y[ch] + yr[ch] * yr[ch];
-        }
-    }
-#pragma unroll
-    for (int f = 0; f < NS; ++f) {
-        FastSample s;
-        s.depth = depth;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            s.ray[i] = ray[i];
-            s.pt[i] = pt[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-            s.cam[i] = c[f].cm.P[i * 4 + 0] * s.pt[0] + c[f].cm.P[i * 4 + 1] * s.pt[1] +
-                       c[f].cm.P[i * 4 + 2] * s.pt[2] + c[f].cm.P[i * 4 + 3];
-        s.inv_den = rcpf(s.cam[2] + 1e-7f);
-        s.px = s.cam[0] * s.inv_den;
-        s.py = s.cam[1] * s.inv_den;
-        const float ix = s.px * c[f].sx - 0.5f, iy = s.py * c[f].sy - 0.5f;
-        const float xmax = (float)(c[f].w - 1), ymax = (float)(c[f].h - 1);
-        const float ixc = fminf(fmaxf(ix, 0.f), xmax), iyc = fminf(fmaxf(iy, 0.f), ymax);
-        const float fx0 = floorf(ixc), fy0 = floorf(iyc);
-        s.x0 = (int)fx0;
-        s.y0 = (int)fy0;
-        s.tx = ixc - fx0;
-        s.ty = iyc - fy0;
-        Corners v;
-        gather<U8>(c[f], s, v);
-        interp<U8>(s, v, o.x[f]);
-        if (SSIM_ON) {
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-                const float x = o.x[f][ch], xl = shfl_prev(x), xr = shfl_next(x);
-                o.hx[f][ch] = xl + x + xr;
-                o.hxx[f][ch] = xl * xl + x * x + xr * xr;
-                o.hxy[f][ch] = xl * yl[ch] + x * o.y[ch] + xr * yr[ch];
-            }
-        }
-    }
-}
-
-// reprojection loss of frame f at the middle row of (A, B, C) (as frow_loss)
-template <int NS, bool SSIM_ON>
-__device__ __forceinline__ void frowa_losses(const FRowA<NS>& A, const FRowA<NS>& B, const FRowA<NS>& C,
-                                             float (&loss)[NS]) {
-    float my[3], sy[3];
-    if (SSIM_ON) {
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) {
-            my[ch] = (A.hy[ch] + B.hy[ch] + C.hy[ch]) * kInv9;
-            sy[ch] = (A.hyy[ch] + B.hyy[ch] + C.hyy[ch]) * kInv9 - my[ch] * my[ch];
-        }
-    }
-#pragma unroll
-    for (int f = 0; f < NS; ++f) {
-        float ss = 0.f, l1 = 0.f;
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) {
-            if (SSIM_ON) {
-                const float mx = (A.hx[f][ch] + B.hx[f][ch] + C.hx[f][ch]) * kInv9;
-                const float sx = (A.hxx[f][ch] + B.hxx[f][ch] + C.hxx[f][ch]) * kInv9 - mx * mx;
-                const float sxy = (A.hxy[f][ch] + B.hxy[f][ch] + C.hxy[f][ch]) * kInv9 - mx * my[ch];
-                const float n = (2.f * mx * my[ch] + kC1) * (2.f * sxy + kC2);
-                const float d = (mx * mx + my[ch] * my[ch] + kC1) * (sx + sy[ch] + kC2);
-                ss += fminf(fmaxf((1.f - n * rcpf(d)) * 0.5f, 0.f), 1.f);
-            }
-            l1 += fabsf(B.y[ch] - B.x[f][ch]);
-        }
-        loss[f] = SSIM_ON ? 0.85f * div3(ss) + 0.15f * div3(l1) : div3(l1);
-    }
-}
-
-// ---- packed-channel form (MD2_PK): colour channels 0 and 1 as one 64-bit register
-// pair, so every per-channel add / mul / fma of the SSIM + L1 chain is one
-// v_pk_*_f32 (two lanes of work per issue slot, CDNA4's full f32 VALU rate) for
-// two channels, plus the scalar op for channel 2.  Same expressions as the scalar
-// form above, channel by channel.
-typedef float f2v __attribute__((ext_vector_type(2)));
-struct C3 {
-    f2v a;     // channels 0, 1
-    float b;   // channel 2
-};
-__device__ __forceinline__ C3 operator+(const C3& x, const C3& y) { return {x.a + y.a, x.b + y.b}; }
-__device__ __forceinline__ C3 operator-(const C3& x, const C3& y) { return {x.a - y.a, x.b - y.b}; }
-__device__ __forceinline__ C3 operator*(const C3& x, const C3& y) { return {x.a * y.a, x.b * y.b}; }
-__device__ __forceinline__ C3 operator*(const C3& x, float s) { return {x.a * s, x.b * s}; }
-__device__ __forceinline__ C3 operator+(const C3& x, float s) { return {x.a + s, x.b + s}; }
-__device__ __forceinline__ C3 shfl_prev3(const C3& v) {
-    return {f2v{shfl_prev(v.a.x), shfl_prev(v.a.y)}, shfl_prev(v.b)};
-}
-__device__ __forceinline__ C3 shfl_next3(const C3& v) {
-    return {f2v{shfl_next(v.a.x), shfl_next(v.a.y)}, shfl_next(v.b)};
-}
-__device__ __forceinline__ C3 ld3(const float* base, int HW, int idx) {
-    return {f2v{ldf(base, idx), ldf(base, HW + idx)}, ldf(base, 2 * HW + idx)};
-}
-__device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.f), 1.f); }
-__device__ __forceinline__ float sum3(const C3& v) { return v.a.x + v.a.y + v.b; }
-__device__ __forceinline__ C3 abs3(const C3& v) { return {f2v{fabsf(v.a.x), fabsf(v.a.y)}, fabsf(v.b)}; }
-
 template <int NS>
 struct FRowP {
     C3 y, hy, hyy;                          // target colour, 3-tap sums of y, y^2
     C3 x[NS], hx[NS], hxx[NS], hxy[NS];     // per frame: warped colour, sums of x, x^2, x*y
 };
-
-template <bool U8>
-__device__ __forceinline__ C3 interp3(const FastSample& s, const Corners& v) {
-    const float e = 1.f - s.tx, so = 1.f - s.ty;
-    const float wnw = so * e, wne = so * s.tx, wsw = s.ty * e, wse = s.ty * s.tx;
-    const C3 nw = {f2v{v.nw[0], v.nw[1]}, v.nw[2]}, ne = {f2v{v.ne[0], v.ne[1]}, v.ne[2]};
-    const C3 sw = {f2v{v.sw[0], v.sw[1]}, v.sw[2]}, se = {f2v{v.se[0], v.se[1]}, v.se[2]};
-    C3 o = nw * wnw + ne * wne + sw * wsw + se * wse;
-    if (U8) o = o * (1.0f / 255.0f);
-    return o;
-}
 
 template <int NS, bool SSIM_ON, bool U8>
 __device__ __forceinline__ void frowp_eval(const WarpCtx (&c)[NS], const float* tgt, float depth, int rr, int cc,
@@ -866,10 +737,6 @@ __device__ __forceinline__ void frowp_losses(const FRowP<NS>& A, const FRowP<NS>
     }
 }
 
-#ifndef MD2_PK
-#define MD2_PK 1
-#endif
-
 template <int NS, bool SSIM_ON, bool MASK, bool U8>
 __device__ __forceinline__ float fwdall_walk(const PhotoArgs& a, const WarpCtx (&ctx)[NS], const FItem& it, int ls,
                                              const float (*dep)[kWave], int lane) {
@@ -884,18 +751,10 @@ __device__ __forceinline__ float fwdall_walk(const PhotoArgs& a, const WarpCtx (
     uint8_t* sel = a.sel[ls] + (size_t)it.b * HW;
     float lsum = 0.f;
     // output row i = window row k - 2 from rows (k-2, k-1, k)
-#if MD2_PK
     using Row = FRowP<NS>;
-#else
-    using Row = FRowA<NS>;
-#endif
     auto out_row = [&](int i, const Row& A, const Row& B, const Row& Cr) {
         float lf[NS];
-#if MD2_PK
         frowp_losses<NS, SSIM_ON>(A, B, Cr, lf);
-#else
-        frowa_losses<NS, SSIM_ON>(A, B, Cr, lf);
-#endif
         const int r = it.r0 + i;
         if (!(it.colok && r < h)) return;
         const int p = r * w + it.c;
@@ -961,22 +820,16 @@ __device__ __forceinline__ float fwdall_walk(const PhotoArgs& a, const WarpCtx (
         sel[p] = (uint8_t)bc;
     };
     Row R0, R1, R2;
-#if MD2_PK
-#define MD2_FROW_EVAL frowp_eval
-#else
-#define MD2_FROW_EVAL frowa_eval
-#endif
     static_assert((kRowsP + 2) % 3 == 0, "window rows must be a multiple of 3");
 #pragma unroll 1
     for (int k = 0; k < kRowsP + 2; k += 3) {
-        MD2_FROW_EVAL<NS, SSIM_ON, U8>(ctx, tgt, dep[k][lane], reflect_clamp(it.r0 - 1 + k, h), it.cc, R0);
+        frowp_eval<NS, SSIM_ON, U8>(ctx, tgt, dep[k][lane], reflect_clamp(it.r0 - 1 + k, h), it.cc, R0);
         if (k >= 2) out_row(k - 2, R1, R2, R0);
-        MD2_FROW_EVAL<NS, SSIM_ON, U8>(ctx, tgt, dep[k + 1][lane], reflect_clamp(it.r0 + k, h), it.cc, R1);
+        frowp_eval<NS, SSIM_ON, U8>(ctx, tgt, dep[k + 1][lane], reflect_clamp(it.r0 + k, h), it.cc, R1);
         if (k >= 1) out_row(k - 1, R2, R0, R1);
-        MD2_FROW_EVAL<NS, SSIM_ON, U8>(ctx, tgt, dep[k + 2][lane], reflect_clamp(it.r0 + 1 + k, h), it.cc, R2);
+        frowp_eval<NS, SSIM_ON, U8>(ctx, tgt, dep[k + 2][lane], reflect_clamp(it.r0 + 1 + k, h), it.cc, R2);
         out_row(k, R0, R1, R2);
     }
-#undef MD2_FROW_EVAL
     return lsum;
 }
 
@@ -1086,11 +939,6 @@ __device__ __forceinline__ int up_src0(int x, int n_in, float sc) {
     return min((int)sx, n_in - 1);
 }
 
-struct Coef {  // horizontally folded SSIM adjoint of one row, 3 channels
-    float A[3], B[3], C[3];
-    float g;     // per-pixel loss weight at this row (centre lane)
-};
-
 // weight of the reflection-padded 3-tap adjoint: how often neighbour (i-1) / (i+1)
 // contributes to position i (reflection pad folds index -1 onto 1 and n onto n-2)
 __device__ __forceinline__ float fold_lo(int i) { return i == 0 ? 0.f : (i == 1 ? 2.f : 1.f); }
@@ -1110,44 +958,6 @@ __device__ __forceinline__ float frame_weight(int code, int f, bool automask, bo
     return code == (automask ? NS : 0) + f ? 1.f : 0.f;
 }
 
-// What the output row of the backward needs from its own forward sample, carried
-// two rows down the sliding window instead of re-projecting and re-gathering.
-struct Carry {
-    float jx[3], jy[3];  // d warp_c / d px, d warp_c / d py (bilinear slope x clip mask x W/(W-1))
-    float px, py, inv_den;
-    float pt[3];         // camera point = depth * ray
-    float u[3];          // P[:3,:3] @ ray  (d cam / d depth)
-    float dd;            // d depth / d disp = -range * depth^2
-};
-
-template <bool U8>
-__device__ __forceinline__ void make_carry(const WarpCtx& c, const FastSample& s, const Corners& v, Carry& k) {
-    const float e = 1.f - s.tx, so = 1.f - s.ty;
-    const float cs = U8 ? 1.0f / 255.0f : 1.0f;
-    const float mx = s.gmx * c.sx * cs, my = s.gmy * c.sy * cs;
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-        k.jx[ch] = ((v.ne[ch] - v.nw[ch]) * so + (v.se[ch] - v.sw[ch]) * s.ty) * mx;
-        k.jy[ch] = ((v.sw[ch] - v.nw[ch]) * e + (v.se[ch] - v.ne[ch]) * s.tx) * my;
-    }
-    k.px = s.px;
-    k.py = s.py;
-    k.inv_den = s.inv_den;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        k.pt[i] = s.pt[i];
-        k.u[i] = c.cm.P[i * 4 + 0] * s.ray[0] + c.cm.P[i * 4 + 1] * s.ray[1] + c.cm.P[i * 4 + 2] * s.ray[2];
-    }
-    k.dd = -c.range * s.depth * s.depth;
-}
-
-// One evaluated row of the backward window (row r = r0 - 2 + k of the item).
-struct RowS {
-    H5 h[3];           // horizontal 3-tap sums (SSIM)
-    float x[3], y[3];  // warped source / target colour at this lane
-    Carry k;           // what the output step needs from this row's sample
-};
-
 // Per-(item, frame) constants of the backward.
 struct BwdFrame {
     WarpCtx ctx;
@@ -1161,145 +971,8 @@ struct BwdFrame {
     float wl, wr, gscale;
 };
 
-// One step of the backward row walk at window index k (row r = r0 - 2 + k):
-//   evaluate row r (warp, target, horizontal sums, carry) into `cur`;
-//   k >= 2: SSIM adjoint coefficients of row p = r - 1 into `cnew` (from the sums of
-//           rows r-2, r-1, r = m2, m1, cur);
-//   k >= 4: output row q = r - 2: dL/dwarp from coefficient rows q-1, q, q+1
-//           (cm3, cm2, cnew) + the L1 term, through the carried bilinear slopes and
-//           projection into dL/dP and dL/d(upsampled disp).
-// The window state lives in three statically named ring slots (rows and coefficient
-// rows mod 3) that the caller rotates by unrolling three steps, so moving the window
-// down costs no register copies; every slot is updated unconditionally.
-template <int NS, bool SSIM_ON, bool MASK, bool U8>
-__device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, RowS& cur, const RowS& m1, const RowS& m2,
-                                         Coef& cnew, const Coef& cm2, const Coef& cm3, float (&dP)[12],
-                                         float (*ddacc)[kWave], int lane) {
-    constexpr float kThird = 1.0f / 3.0f;
-    const float l1w = SSIM_ON ? 0.15f : 1.0f;
-    const int h = F.ctx.h, w = F.ctx.w, HW = h * w;
-    const int r = F.r0 - 2 + k;
-    const int rr = reflect_clamp(r, h);
-    FastSample sm;
-    project_depth(F.ctx, rr, F.cc, F.dep[k][lane], sm);
-    Corners v;
-    gather<U8>(F.ctx, sm, v);
-    interp<U8>(sm, v, cur.x);
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) cur.y[ch] = ldf(F.tgt, ch * HW + rr * w + F.cc);
-    if (k >= 2 && k < kRowsB + 2) make_carry<U8>(F.ctx, sm, v, cur.k);  // only output rows need it
-    if (SSIM_ON) {
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) cur.h[ch] = hsum(cur.x[ch], cur.y[ch]);
-    }
-    if (k < 2) return;
-    // coefficient row p = r - 1
-    const int p = r - 1;
-    float gp = 0.f;
-    const bool own = F.colreal && p >= 0 && p < h;
-    if (own) gp = F.gscale * frame_weight<NS>(ldb(F.sel, p * w + F.c), F.f, F.automask, F.avg);
-    if (MASK) {
-        // masked = reproj * mask (trainer.py:455): d/dreproj = g*mask, d/dmask = g*reproj
-        const size_t mi = (((size_t)F.b * NS + F.f) * h + (own ? p : 0)) * w + (own ? F.c : 0);
-        if (F.pgmask && F.colok && p >= F.r0 && p < F.r0 + kRowsB && p < h) {
-            float ss = 0.f, l1 = 0.f;
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-                if (SSIM_ON) ss += ssim_from_sums(m2.h[ch], m1.h[ch], cur.h[ch]);
-                l1 += fabsf(m1.y[ch] - m1.x[ch]);
-            }
-            const float rep = SSIM_ON ? 0.85f * div3(ss) + 0.15f * div3(l1) : div3(l1);
-            F.pgmask[mi] = gp * rep;
-        }
-        gp *= own ? F.pmask[mi] : 0.f;
-    }
-    cnew.g = gp;
-    if (SSIM_ON) {
-        const float gS = gp * (0.85f / 3.f);
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) {
-            float dA, dB, dC;
-            ssim_adjoint(m2.h[ch], m1.h[ch], cur.h[ch], gS, dA, dB, dC);
-            if (gp == 0.f) dA = dB = dC = 0.f;
-            cnew.A[ch] = pick(F.wl, shfl_prev(dA)) + dA + pick(F.wr, shfl_next(dA));
-            cnew.B[ch] = pick(F.wl, shfl_prev(dB)) + dB + pick(F.wr, shfl_next(dB));
-            cnew.C[ch] = pick(F.wl, shfl_prev(dC)) + dC + pick(F.wr, shfl_next(dC));
-        }
-    }
-    if (k < 4) return;
-    // output row q = r - 2 (coefficient rows q-1, q, q+1 = cm3, cm2, cnew)
-    const int q = r - 2;
-    if (!(F.colok && q < h)) return;
-    const Carry& k2 = m2.k;
-    const float l1c = cm2.g * (l1w * kThird);
-    float dpx = 0.f, dpy = 0.f;
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-        float g = l1c * signf(m2.x[ch] - m2.y[ch]);
-        if (SSIM_ON) {
-            const float wu = fold_lo(q), wd = fold_hi(q, h);
-            const float aA = pick(wu, cm3.A[ch]) + cm2.A[ch] + pick(wd, cnew.A[ch]);
-            const float aB = pick(wu, cm3.B[ch]) + cm2.B[ch] + pick(wd, cnew.B[ch]);
-            const float aC = pick(wu, cm3.C[ch]) + cm2.C[ch] + pick(wd, cnew.C[ch]);
-            g += (aA + 2.f * m2.x[ch] * aB + m2.y[ch] * aC) * kInv9;
-        }
-        dpx += g * k2.jx[ch];
-        dpy += g * k2.jy[ch];
-    }
-    float dc[3];
-    dc[0] = dpx * k2.inv_den;
-    dc[1] = dpy * k2.inv_den;
-    dc[2] = -(dpx * k2.px + dpy * k2.py) * k2.inv_den;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) dP[i * 4 + j] += dc[i] * k2.pt[j];
-        dP[i * 4 + 3] += dc[i];
-    }
-    const float dd = (dc[0] * k2.u[0] + dc[1] * k2.u[1] + dc[2] * k2.u[2]) * k2.dd;
-    // frames accumulate in LDS; the item's result leaves once (bwd_item)
-    if (F.f == 0) ddacc[q - F.r0][lane] = dd;
-    else ddacc[q - F.r0][lane] += dd;
-}
-
-// One work item of the backward: (image b, local scale ls, strip st, row block rb),
-// all source frames.  Writes dL/d(upsampled disp) for its 60 x kRowsB pixels and one
-// 12-float dL/dP partial per frame.
-// One source frame of a backward item: the row walk and its dL/dP partial.  U8:
-// this (frame, image)'s gathers read the 8-bit copy (wave-uniform choice).
-template <int NS, bool SSIM_ON, bool MASK, bool U8>
-__device__ __forceinline__ void bwd_frame_walk(const BwdFrame& F, float (*ddacc)[kWave], float* dst, int lane) {
-    float dP[12];
-#pragma unroll
-    for (int j = 0; j < 12; ++j) dP[j] = 0.f;
-    RowS S0, S1, S2;
-    Coef C0, C1, C2;
-    // window indices k = 0 .. kRowsB+3; slots: row k -> S[k%3], coefficient row
-    // k-1 -> C[(k-1)%3]
-    constexpr int kSteps = kRowsB + 4;
-    int k = 0;
-#pragma unroll 1
-    for (; k + 3 <= kSteps; k += 3) {
-        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
-        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
-        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 2, S2, S1, S0, C1, C0, C2, dP, ddacc, lane);
-    }
-    if (kSteps % 3 >= 1) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
-    if (kSteps % 3 >= 2) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
-    // one 12-float partial of dL/dP per (item, frame)
-#pragma unroll
-    for (int j = 0; j < 12; ++j) {
-        const float t = wave_sum(dP[j]);
-        if (lane == 0) dst[j] = t;
-    }
-}
-
-// ---- packed-channel backward (MD2_PKB): the row walk above with channels (0, 1) in
-// one register pair (C3), so the SSIM sums, adjoint, 3-tap folds and the output
-// chain issue v_pk_*_f32 for two channels.  Expressions as in the scalar form.
-struct H5P {
-    C3 x, xx, xy, y, yy;
-};
+// Carried two rows down the sliding window from an output row's own forward sample
+// (instead of re-projecting and re-gathering it).
 struct CarryP {
     C3 jx, jy;
     float px, py, inv_den;
@@ -1316,48 +989,6 @@ struct CoefP {
     C3 A, B, C;
     float g;
 };
-
-__device__ __forceinline__ H5P hsum3(const C3& x, const C3& y) {
-    const C3 xl = shfl_prev3(x), xr = shfl_next3(x), yl = shfl_prev3(y), yr = shfl_next3(y);
-    return {xl + x + xr, xl * xl + x * x + xr * xr, xl * yl + x * y + xr * yr, yl + y + yr, yl * yl + y * y + yr * yr};
-}
-
-__device__ __forceinline__ float ssim1(float n, float d) { return clamp01((1.f - n * rcpf(d)) * 0.5f); }
-
-// sum over the three channels of SSIM at the middle row of (a, b, c) (ssim_from_sums)
-__device__ __forceinline__ float ssim_sum3(const H5P& a, const H5P& b, const H5P& c) {
-    const C3 mx = (a.x + b.x + c.x) * kInv9, my = (a.y + b.y + c.y) * kInv9;
-    const C3 sx = (a.xx + b.xx + c.xx) * kInv9 - mx * mx;
-    const C3 sy = (a.yy + b.yy + c.yy) * kInv9 - my * my;
-    const C3 sxy = (a.xy + b.xy + c.xy) * kInv9 - mx * my;
-    const C3 n = (mx * my * 2.f + kC1) * (sxy * 2.f + kC2);
-    const C3 d = (mx * mx + my * my + kC1) * (sx + sy + kC2);
-    return ssim1(n.a.x, d.a.x) + ssim1(n.a.y, d.a.y) + ssim1(n.b, d.b);
-}
-
-__device__ __forceinline__ float clamp_pass(float raw, float g) { return (raw >= 0.f && raw <= 1.f) ? g : 0.f; }
-
-// ssim_adjoint for the three channels
-__device__ __forceinline__ void ssim_adjoint3(const H5P& a, const H5P& b, const H5P& c, float gS, C3& dA, C3& dB,
-                                              C3& dC) {
-    const C3 mx = (a.x + b.x + c.x) * kInv9, my = (a.y + b.y + c.y) * kInv9;
-    const C3 sx = (a.xx + b.xx + c.xx) * kInv9 - mx * mx;
-    const C3 sy = (a.yy + b.yy + c.yy) * kInv9 - my * my;
-    const C3 sxy = (a.xy + b.xy + c.xy) * kInv9 - mx * my;
-    const C3 n1 = mx * my * 2.f + kC1, n2 = sxy * 2.f + kC2;
-    const C3 d1 = mx * mx + my * my + kC1, d2 = sx + sy + kC2;
-    const C3 n = n1 * n2, d = d1 * d2;
-    const C3 inv_d = {f2v{rcpf(d.a.x), rcpf(d.a.y)}, rcpf(d.b)};
-    const C3 raw = ((n * inv_d) * -1.f + 1.f) * 0.5f;
-    const C3 g = {f2v{clamp_pass(raw.a.x, gS), clamp_pass(raw.a.y, gS)}, clamp_pass(raw.b, gS)};
-    const C3 dn = g * -0.5f * inv_d;
-    const C3 dd = g * 0.5f * n * inv_d * inv_d;
-    dA = dn * (my * 2.f * (n2 - n1)) + dd * (mx * 2.f * (d2 - d1));
-    dB = dd * d1;
-    dC = dn * 2.f * n1;
-}
-
-__device__ __forceinline__ C3 sign3(const C3& v) { return {f2v{signf(v.a.x), signf(v.a.y)}, signf(v.b)}; }
 
 template <bool U8>
 __device__ __forceinline__ void make_carry3(const WarpCtx& c, const FastSample& s, const Corners& v, CarryP& k) {
@@ -1379,8 +1010,18 @@ __device__ __forceinline__ void make_carry3(const WarpCtx& c, const FastSample& 
     k.dd = -c.range * s.depth * s.depth;
 }
 
+// One step of the backward row walk at window index k (row r = r0 - 2 + k):
+//   evaluate row r (warp, target, horizontal sums, carry) into `cur`;
+//   k >= 2: SSIM adjoint coefficients of row p = r - 1 into `cnew` (from the sums of
+//           rows r-2, r-1, r = m2, m1, cur);
+//   k >= 4: output row q = r - 2: dL/dwarp from coefficient rows q-1, q, q+1
+//           (cm3, cm2, cnew) + the L1 term, through the carried bilinear slopes and
+//           projection into dL/dP and dL/d(upsampled disp).
+// The window state lives in three statically named ring slots (rows and coefficient
+// rows mod 3) that the caller rotates by unrolling three steps, so moving the window
+// down costs no register copies; every slot is updated unconditionally.
 template <int NS, bool SSIM_ON, bool MASK, bool U8>
-__device__ __forceinline__ void bwd_step_p(const BwdFrame& F, int k, RowP& cur, const RowP& m1, const RowP& m2,
+__device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, RowP& cur, const RowP& m1, const RowP& m2,
                                            CoefP& cnew, const CoefP& cm2, const CoefP& cm3, float (&dP)[12],
                                            float (*ddacc)[kWave], int lane) {
     constexpr float kThird = 1.0f / 3.0f;
@@ -1454,7 +1095,7 @@ __device__ __forceinline__ void bwd_step_p(const BwdFrame& F, int k, RowP& cur, 
 }
 
 template <int NS, bool SSIM_ON, bool MASK, bool U8>
-__device__ __forceinline__ void bwd_frame_walk_p(const BwdFrame& F, float (*ddacc)[kWave], float* dst, int lane) {
+__device__ __forceinline__ void bwd_frame_walk(const BwdFrame& F, float (*ddacc)[kWave], float* dst, int lane) {
     float dP[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) dP[j] = 0.f;
@@ -1464,22 +1105,18 @@ __device__ __forceinline__ void bwd_frame_walk_p(const BwdFrame& F, float (*ddac
     int k = 0;
 #pragma unroll 1
     for (; k + 3 <= kSteps; k += 3) {
-        bwd_step_p<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
-        bwd_step_p<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
-        bwd_step_p<NS, SSIM_ON, MASK, U8>(F, k + 2, S2, S1, S0, C1, C0, C2, dP, ddacc, lane);
+        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
+        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
+        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 2, S2, S1, S0, C1, C0, C2, dP, ddacc, lane);
     }
-    if (kSteps % 3 >= 1) bwd_step_p<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
-    if (kSteps % 3 >= 2) bwd_step_p<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
+    if (kSteps % 3 >= 1) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
+    if (kSteps % 3 >= 2) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
         const float t = wave_sum(dP[j]);
         if (lane == 0) dst[j] = t;
     }
 }
-
-#ifndef MD2_PKB
-#define MD2_PKB 1
-#endif
 
 // One work item of the backward: (image b, local scale ls, strip st, row block rb),
 // all source frames.  Writes dL/d(upsampled disp) for its 60 x kRowsB pixels and one
@@ -1517,17 +1154,10 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
         F.f = f;
         make_ctx(a, ls, f, b, F.ctx);
         float* dst = a.dP_part[ls] + ((size_t)f * a.B * a.wpi + item_in_scale) * 12;
-#if MD2_PKB
-        if (F.ctx.src8)
-            bwd_frame_walk_p<NS, SSIM_ON, MASK, true>(F, ddacc, dst, lane);
-        else
-            bwd_frame_walk_p<NS, SSIM_ON, MASK, false>(F, ddacc, dst, lane);
-#else
         if (F.ctx.src8)
             bwd_frame_walk<NS, SSIM_ON, MASK, true>(F, ddacc, dst, lane);
         else
             bwd_frame_walk<NS, SSIM_ON, MASK, false>(F, ddacc, dst, lane);
-#endif
     }
     const int upsh = a.upsh[ls];
 #ifdef MD2_NO_FOLD   // timing experiments only: results are wrong
