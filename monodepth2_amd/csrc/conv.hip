@@ -398,6 +398,20 @@ __device__ __forceinline__ void split3(float4 v, bf16x4& p0, bf16x4& p1, bf16x4&
 
 // element index of (row r, k) in a [rows][32] bf16 plane, 16-byte quads swizzled
 __device__ __forceinline__ int xidx(int r, int k) { return r * XBK + ((((k >> 3) ^ (r >> 2)) & 3) << 3) + (k & 7); }
+// xidx with rows r and r ^ 1 swapped in every odd row quad: the same ds_read_b128
+// banks as xidx (a fragment group's rows map onto the same row set), and an 8-byte
+// store of row 4 q + j by the 16 lanes of two quads (q, q + 1) then lands on both
+// 16-bank halves (row parity differs) instead of two-way on one
+__device__ __forceinline__ int xidx2(int r, int k) { return xidx(r ^ ((r >> 2) & 1), k); }
+// The 16x16x32 MFMA path's operand layout: k-octet slot kq ^ (row >> 2 & 2).  Its
+// ds_read_b128 lane groups ({0-3, 12-15, 20-27}, ...) read rows c, 12 + c at one octet
+// and 4 + c, 8 + c at the next, which xidx's kq ^ (row >> 2) puts on the same 16-byte
+// bank slot (two-way on every fragment read); this slot function keeps all four apart.
+template <int MT>
+__device__ __forceinline__ int xsw(int r, int k) {
+    if constexpr (MT == 32) return xidx(r, k);
+    return r * XBK + ((((k >> 3) ^ ((r >> 2) & 2)) & 3) << 3) + (k & 7);
+}
 
 // Weights split once per call into three bf16 planes [3][R][KT][Ck] in row-k order:
 // forward R = Co, Ck = Ci (w as is); input gradient R = Ci, Ck = Co with the taps
@@ -588,8 +602,8 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
     }
     // B staging by LDS-DMA: BQ pieces per wave and chunk, each 1 KiB = 16 rows of one
     // plane (64 B per row).  Lane l fills row 16 rb + l/4, quad slot l&3 — the slot
-    // that xidx() gives k-quad (slot ^ (row >> 2)) & 3 — so the DMA's linear lane
-    // order writes the swizzled layout.
+    // that xsw() gives k-quad (slot ^ (row >> 2)) & 3, or (slot ^ (row >> 2 & 2)) & 3 on
+    // the 16x16 path — so the DMA's linear lane order writes the swizzled layout.
     constexpr int RB16 = BN / 16;
     int bsrc[BQ], bk8[BQ], bdst[BQ];
     const __amdgpu_buffer_rsrc_t br =
@@ -597,7 +611,7 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
 #pragma unroll
     for (int j = 0; j < BQ; ++j) {
         const int piece = wid + NW * j, pl = piece / RB16, rb = piece - pl * RB16;
-        const int r = rb * 16 + (lane >> 2), q = ((lane & 3) ^ (r >> 2)) & 3;
+        const int r = rb * 16 + (lane >> 2), q = ((lane & 3) ^ (G::MT == 16 ? (r >> 2) & 2 : r >> 2)) & 3;
         const int n = n0 + r;
         bk8[j] = 8 * q;
         bsrc[j] = n < a.N ? ((pl * a.N + n) * KT) * a.C + 8 * q : -1;
@@ -676,7 +690,7 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
         __bf16* L = lds[buf];
 #pragma unroll
         for (int j = 0; j < AQ; ++j) {
-            const int e = xidx(ra + (NT / 8) * j, 4 * qa);
+            const int e = xsw<G::MT>(ra + (NT / 8) * j, 4 * qa);
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) *(bf16x4*)(L + pl * PA + e) = sa[j][pl];
         }
@@ -688,13 +702,13 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
             // 16x16x32: lane l holds row / column l & 15, k = 8 (l >> 4) .. + 7
             const int l16 = lane & 15, kq = lane >> 4;
             bf16x8 fb[3];
-            const int eb = xidx(wn * 16 + l16, 8 * kq);
+            const int eb = xsw<16>(wn * 16 + l16, 8 * kq);
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 bf16x8 fa[3];
-                const int e = xidx(wm * (TM * 16) + 16 * i + l16, 8 * kq);
+                const int e = xsw<16>(wm * (TM * 16) + 16 * i + l16, 8 * kq);
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(L + pl * PA + e);
                 acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
@@ -1033,11 +1047,11 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
 #pragma unroll
         for (int e = 0; e < 16; ++e) tot[i][e] = 0.f;
 
-    float4 v0[4], v1[4];
-    auto load = [&](int t, float4 (&V)[4]) {
+    auto load = [&](auto side_c, int t, float4 (&V)[4]) {
+        constexpr int SIDE = decltype(side_c)::value;
         const int p0 = (t0 + t) * XBK + 4 * kq;
         const bool live = t < nchunks && rok;
-        if (side == 0) {
+        if constexpr (SIDE == 0) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int p = p0 + i;
@@ -1084,10 +1098,10 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
                 pk[pl][j][1] = hi16x2(c[pl][2][j], c[pl][3][j]);
             }
     };
-    auto store = [&](int buf) {
-        if (!stager) return;
-        __bf16* L = lds[buf] + (side ? 3 * PA : 0);
-        const int P = side ? PB : PA;
+    auto store = [&](auto side_c, int buf) {
+        constexpr int SIDE = decltype(side_c)::value;
+        __bf16* L = lds[buf] + (SIDE ? 3 * PA : 0);
+        constexpr int P = SIDE ? PB : PA;
         typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
@@ -1096,7 +1110,7 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
                 u32x2 q;
                 q.x = pk[pl][j][0];
                 q.y = pk[pl][j][1];
-                *(u32x2*)(L + pl * P + xidx(row + j, 4 * kq)) = q;
+                *(u32x2*)(L + pl * P + xidx2(row + j, 4 * kq)) = q;
             }
     };
     const int lr = lane & 31, h = lane >> 5;
@@ -1111,11 +1125,11 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
             bf16x8 fa[TM][3], fb[3];
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                const int e = xidx(wm * (TM * 32) + 32 * i + lr, 16 * s + 8 * h);
+                const int e = xidx2(wm * (TM * 32) + 32 * i + lr, 16 * s + 8 * h);
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl) fa[i][pl] = *(const bf16x8*)(L + pl * PA + e);
             }
-            const int eb = xidx(wn * 32 + lr, 16 * s + 8 * h);
+            const int eb = xidx2(wn * 32 + lr, 16 * s + 8 * h);
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
 #pragma unroll
@@ -1133,6 +1147,33 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
     };
 
     if (wid >= 4) __builtin_amdgcn_s_setprio(1);   // as in conv_x6_kernel
+    // one loop per staging side (wave-uniform, compile-time inside): the step — fetch
+    // chunk t+2, split chunk t+1, multiply chunk t, store chunk t+1 — is one basic block
+    // the scheduler can interleave (the MFMA shadows hide the split VALU), as in
+    // conv_x6pw_kernel's per-role loops
+    auto run = [&](auto side_c) {
+        float4 v0[4], v1[4];
+        load(side_c, 0, v0);
+        load(side_c, 1, v1);
+        split(v0);
+        store(side_c, 0);
+        __syncthreads();
+        for (int t = 0; t < nchunks; t += 2) {
+            load(side_c, t + 2, v0);
+            split(v1);
+            mma(0);
+            asm volatile("" ::: "memory");
+            store(side_c, 1);
+            __syncthreads();
+            if (t + 1 >= nchunks) break;
+            load(side_c, t + 3, v1);
+            split(v0);
+            mma(1);
+            asm volatile("" ::: "memory");
+            store(side_c, 0);
+            __syncthreads();
+        }
+    };
     if (!stager) {
         // waves 2-3 at BMW = 64: multiply only
         __syncthreads();
@@ -1143,27 +1184,10 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
             mma(1);
             __syncthreads();
         }
+    } else if (side == 0) {
+        run(std::integral_constant<int, 0>());
     } else {
-    load(0, v0);
-    load(1, v1);
-    split(v0);
-    store(0);
-    __syncthreads();
-    for (int t = 0; t < nchunks; t += 2) {
-        load(t + 2, v0);
-        split(v1);
-        mma(0);
-        asm volatile("" ::: "memory");
-        store(1);
-        __syncthreads();
-        if (t + 1 >= nchunks) break;
-        load(t + 3, v1);
-        split(v0);
-        mma(1);
-        asm volatile("" ::: "memory");
-        store(0);
-        __syncthreads();
-    }
+        run(std::integral_constant<int, 1>());
     }
 
     float* out = a.y + (size_t)ks * a.M * a.N;
@@ -1179,11 +1203,6 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
     }
 }
 
-// xidx with rows r and r ^ 1 swapped in every odd row quad: the same ds_read_b128
-// banks as xidx (a fragment group's rows map onto the same row set), and an 8-byte
-// store of row 4 q + j by the 16 lanes of two quads (q, q + 1) then lands on both
-// 16-bank halves (row parity differs) instead of two-way on one
-__device__ __forceinline__ int xidx2(int r, int k) { return xidx(r ^ ((r >> 2) & 1), k); }
 
 // Patch-staged split-bf16 weight gradient (MD2_CONV_X6 | MD2_CONV_PATCH; 3x3, stride 1).
 // conv_x6_wgrad_kernel stages x once per (tap, ci) column, so every activation is

@@ -172,7 +172,10 @@ XFLAGS = (conv_ops.X6, conv_ops.X6 | conv_ops.BM256, conv_ops.X6 | conv_ops.PATC
           conv_ops.X6 | conv_ops.S2_ONE | conv_ops.BM256)
 
 
-@pytest.mark.parametrize("B,C,N,k,s,p,H,W", [sh for sh in SHAPES if sh[1] % 8 == 0 and sh[2] % 8 == 0])
+# + the decoder's narrow layers: 16 output channels take the 16x16x32 MFMA tile (its own
+# LDS slot swizzle), 32 the 128 x 32 one
+@pytest.mark.parametrize("B,C,N,k,s,p,H,W", [sh for sh in SHAPES if sh[1] % 8 == 0 and sh[2] % 8 == 0] +
+                         [(2, 16, 16, 3, 1, 0, 20, 34), (2, 32, 16, 3, 1, 0, 12, 18), (2, 96, 32, 3, 1, 0, 10, 12)])
 def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
     """The split-bf16 path (MD2_CONV_X6: exact three-plane split, six bf16 MFMA
     products, f32 accumulation) against an fp64 reference: its error is of the order

@@ -9,7 +9,10 @@ cd "$(dirname "$0")/.."
 SRC=${SRC:-monodepth2_amd/csrc/md2hot.hip}
 mkdir -p variants/$name
 obj=variants/$name/$(basename ${SRC%.hip}).o
-/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -Iinclude -fno-slp-vectorize "$@" -c $SRC -o $obj
+# the in-tree build flags (monodepth2_amd/build.py): -fno-slp-vectorize for md2hot.hip only
+slp=""
+[ "$(basename $SRC)" = "md2hot.hip" ] && slp="-fno-slp-vectorize"
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -Iinclude $slp "$@" -c $SRC -o $obj
 others=$(ls monodepth2_amd/csrc/obj/*.o | grep -v "/$(basename ${SRC%.hip}).o$")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared -o variants/$name/libmd2hot.so $obj $others
 rm -f $obj
