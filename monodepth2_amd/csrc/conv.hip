@@ -815,6 +815,19 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
     }
 }
 
+// Patch layout of the 16-column tiles (TC = 16): patch pixel pix = (pr, pc) at LDS row
+// pix, k-octet slot kq ^ (pr & 1) ^ (pc >> 2 & 1) << 1.  A 32-lane fragment there spans
+// two output rows (16 + 16 pixels, patch pitch 18), so a ds_read_b128 lane group reads
+// columns x .. x+3, x+12 .. x+15 of one patch row and x+4 .. x+11 of the next, which
+// xidx's kq ^ (pix >> 2) maps two-way onto the same bank slots; with this slot function
+// the 16 lanes of every group hit 16 distinct slots at every tap offset (an exhaustive
+// check over the row parities and tap columns chose it).  The 8-byte patch stores (two
+// consecutive pixels per 16 lanes) stay conflict-free under any per-pixel permutation.
+__device__ __forceinline__ int pidx16(int pix, int pr, int pc, int k) {
+    const int sw = (pr & 1) ^ (((pc >> 2) & 1) << 1);
+    return pix * XBK + ((((k >> 3) ^ sw) & 3) << 3) + (k & 7);
+}
+
 // Patch-staged split-bf16 3x3 stride-1 convolution (forward, and the stride-1 input
 // gradient as the "full" convolution of gy with the flipped planes).  conv_x6_kernel
 // stages its A tile per (tap, 32 channels) chunk: every activation is fetched, split and
@@ -897,7 +910,13 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
             if (PP * 8 % NT && f >= PP * 8) break;
             bf16x4 p0, p1, p2;
             split3(RA[j], p0, p1, p2);
-            const int e = xidx(f >> 3, 4 * (f & 7));
+            int e;
+            if constexpr (TC == 16) {
+                const int pix = f >> 3, pr = pix / PW;
+                e = pidx16(pix, pr, pix - pr * PW, 4 * (f & 7));
+            } else {
+                e = xidx(f >> 3, 4 * (f & 7));
+            }
             *(bf16x4*)(lds + e) = p0;
             *(bf16x4*)(lds + PA + e) = p1;
             *(bf16x4*)(lds + 2 * PA + e) = p2;
@@ -914,15 +933,17 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
         }
     };
     const int lr = lane & 31, h = lane >> 5;
-    int abase[TM];   // this lane's patch pixel at tap (0, 0), per row fragment
+    int abase[TM], arow[TM], acol[TM];   // this lane's patch pixel at tap (0, 0), per row fragment
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         const int ml = wm * (TM * 32) + 32 * i + lr, r = ml / TC, c = ml - r * TC;
         abase[i] = r * PW + c;
+        arow[i] = r;
+        acol[i] = c;
     }
     auto mma = [&](int buf, int tap) {
         const __bf16* LB = lds + 3 * PA + buf * 3 * PB;
-        const int th = tap / 3, toff = th * PW + (tap - 3 * th);
+        const int th = tap / 3, tw = tap - 3 * th, toff = th * PW + tw;
 #pragma unroll
         for (int s = 0; s < XBK / 16; ++s) {
             bf16x8 fb[3];
@@ -932,7 +953,8 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 bf16x8 fa[3];
-                const int e = xidx(abase[i] + toff, 16 * s + 8 * h);
+                const int e = TC == 16 ? pidx16(abase[i] + toff, arow[i] + th, acol[i] + tw, 16 * s + 8 * h)
+                                       : xidx(abase[i] + toff, 16 * s + 8 * h);
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(lds + pl * PA + e);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[i], 0, 0, 0);

@@ -48,7 +48,12 @@ constexpr int kThreads = 64 * kWaves;
 constexpr int kSeg = 32;                // output pixels per chunk (one output row segment)
 constexpr int kRawW = 2 * kSeg + 5;     // input columns under a segment
 constexpr int kCG = 3;                  // channels per group (one frame)
-constexpr int kRaw = 7 * kCG * 2 * 36;   // floats per staged chunk ([kh][ci][parity][36])
+// pitch of one staged (kernel row, channel, column parity) run: 35 columns used; 39
+// (= 3 mod 4) spreads the build's 32-lane read groups —
+// four tile rows x 8 pixel quads — over distinct banks (36: four-way on every read;
+// 39: 2.6x fewer conflict cycles in an exhaustive model of the build and the store)
+constexpr int kRP = 39;
+constexpr int kRaw = 7 * kCG * 2 * kRP;  // floats per staged chunk ([kh][ci][parity][kRP])
 constexpr int kXBK = 32;
 constexpr int kPA = kCo * kXBK;         // bf16 per dy plane (64 co x 32 pixels)
 constexpr int kPT = 32 * kXBK;          // bf16 per B tile plane (32 rows x 32 pixels)
@@ -85,7 +90,7 @@ __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\
 // two 7-wave blocks per CU put four waves on two of the SIMDs: <= 128 VGPRs
 template <int C>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void stem_x6_wgrad_kernel(StemArgs a) {
-    __shared__ float raw[2][kRaw];   // [kh][ci][column parity][36]: x[2oh-3+kh][iw0 + 2m + parity][3cg+ci]
+    __shared__ float raw[2][kRaw];   // [kh][ci][column parity][kRP]: x[2oh-3+kh][iw0 + 2m + parity][3cg+ci]
     __shared__ __bf16 At[3 * kPA];
     __shared__ __bf16 Bt[7 * 3 * kPT];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -160,7 +165,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
                 const int k = k0 + i, col = (int)(((uint32_t)k * cinv) >> 16), c = k - col * C - kCG * cg;
                 const int iw = iw0 + col;
                 if (col < kRawW && (unsigned)c < (unsigned)kCG)
-                    dst[((r * kCG + c) * 2 + (col & 1)) * 36 + (col >> 1)] = (unsigned)iw < (unsigned)W ? v[i] : 0.f;
+                    dst[((r * kCG + c) * 2 + (col & 1)) * kRP + (col >> 1)] = (unsigned)iw < (unsigned)W ? v[i] : 0.f;
             }
         }
     };
@@ -211,7 +216,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             const int kx = rl / kCG, ci = rl - kx * kCG, r = 4 * kx + ci;
             float v[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = src[((kh * kCG + ci) * 2 + (kx & 1)) * 36 + 4 * g + i + (kx >> 1)];
+            for (int i = 0; i < 4; ++i) v[i] = src[((kh * kCG + ci) * 2 + (kx & 1)) * kRP + 4 * g + i + (kx >> 1)];
             float c[3][4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {

@@ -35,6 +35,14 @@ def main():
             row["wgrad_x6_tf"] = round(gf / timeit(lambda: wgrad(gy, x, w, s, p, X6)), 1)
             print(json.dumps(row), flush=True)
             continue
+        if "s3" in modes:   # x6 forward / patch forward / per-tap weight gradient (layout A/B)
+            gy = torch.randn_like(F.conv2d(x, w, None, s, p)).contiguous(memory_format=CL)
+            row["fwd_x6_tf"] = round(gf / timeit(lambda: fwd(x, w, s, p, X6)), 1)
+            if k == 3 and s == 1:
+                row["fwd_x6p_tf"] = round(gf / timeit(lambda: fwd(x, w, s, p, X6 | _lib.CONV_PATCH)), 1)
+            row["wgrad_x6_tf"] = round(gf / timeit(lambda: wgrad(gy, x, w, s, p, X6)), 1)
+            print(json.dumps(row), flush=True)
+            continue
         if "quick" in modes:   # x6 timings only (A/B of variant builds)
             row["fwd_x6_tf"] = round(gf / timeit(lambda: fwd(x, w, s, p, X6)), 1)
             row["fwd_x6_256_tf"] = round(gf / timeit(lambda: fwd(x, w, s, p, X6 | _lib.CONV_BM256)), 1)
