@@ -1,6 +1,6 @@
 """Per-step GPU time by kernel (and by launch shape for chosen families) from a
 rocprofv3 --kernel-trace csv of an eager bench run: the last `steps` steps, split at
-the photometric forward's first kernel (pack_src8).
+the photometric forward's first kernel (photo_ident; pack_src8 before round 3).
     python tools/trace_breakdown.py <kernel_trace.csv> [steps] [family ...]"""
 import collections
 import csv
@@ -14,7 +14,8 @@ def main():
     fams = sys.argv[3:]
     rows = list(csv.DictReader(open(path)))
     names = [r["Kernel_Name"] for r in rows]
-    marks = [i for i, n in enumerate(names) if "pack_src8" in n]
+    marks = [i for i, n in enumerate(names) if "photo_ident" in n] or \
+        [i for i, n in enumerate(names) if "pack_src8" in n]
     sel = rows[marks[-steps]:]
     t0, t1 = int(sel[0]["Start_Timestamp"]), int(sel[-1]["End_Timestamp"])
     agg = collections.defaultdict(lambda: [0, 0])
