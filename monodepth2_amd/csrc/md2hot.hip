@@ -834,7 +834,13 @@ __device__ __forceinline__ float fwdall_walk(const PhotoArgs& a, const WarpCtx (
 }
 
 template <int NS, bool SSIM_ON, bool MASK>
+// MD2_FWD_MINB: waves per SIMD the forward walk is compiled for (default: the
+// compiler's choice, 157 VGPRs = 3 waves; 4 spills 88 B/lane) — an A/B knob
+#ifdef MD2_FWD_MINB
+__global__ __launch_bounds__(kBlock, MD2_FWD_MINB) void photo_fwdall_kernel(PhotoArgs a) {
+#else
 __global__ __launch_bounds__(kBlock) void photo_fwdall_kernel(PhotoArgs a) {
+#endif
     __shared__ float dep_s[kWavesPerBlock][kRowsP + 2][kWave];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
     float (*dep)[kWave] = dep_s[wid];

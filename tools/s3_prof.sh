@@ -1,9 +1,13 @@
 #!/bin/bash
-# Session-3 profiling call: the round's rocprofv3 trace + PMC passes (tools/profile_round.sh)
-# at the session's final tree, then the default bench line.
+# Session-3 profiling call at the session's tree: per-step kernel breakdown of the eager
+# step, the round's rocprofv3 trace + PMC passes (tools/profile_round.sh), default bench.
 set -o pipefail
 export TMPDIR=/tmp
-ROUND=r03s3 bash tools/profile_round.sh || exit 1
 mkdir -p gpurun_out/s3
+bash tools/ab_hot.sh hbase hf4 > gpurun_out/s3/ab_hot.log 2>&1 || exit 1
+echo abhot ok
+bash tools/step_trace.sh s3trace2 > gpurun_out/s3/step_trace.log 2>&1 || exit 1
+echo steptrace ok
+ROUND=r03s3 bash tools/profile_round.sh || exit 1
 timeout -k 10 300 python bench.py > gpurun_out/s3/bench_final.log 2>&1 || exit 1
 echo bench ok
