@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 14
+#define MD2_ABI_VERSION 15
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -425,6 +425,18 @@ int md2_bn_bwd_multi(const md2_bn_desc* desc, const void* x, const void* y, cons
                      const void* grad_y2, const void* grad_y3, const float* gamma, const float* save_mean,
                      const float* save_invstd, void* grad_x, void* grad_residual, float* grad_gamma,
                      float* grad_beta, void* workspace, void* stream);
+/* ABI 15: the ReLU mask instead of y.  md2_bn_fwd_mask = md2_bn_fwd that also writes
+ * relu_mask (MD2_BN_RELU only; NULL = none): one byte per element quad of y, bit i set
+ * when element 4q + i of y (as stored: bf16 after rounding) is > 0 — pixels*channels/4
+ * bytes.  md2_bn_bwd_mask = md2_bn_bwd_multi gated by that mask instead of reading y
+ * (1/16 of y's bytes in fp32): same results, bit for bit. */
+int md2_bn_fwd_mask(const md2_bn_desc* desc, const void* x, const float* gamma, const float* beta,
+                    const void* residual, float* running_mean, float* running_var, void* y, uint8_t* relu_mask,
+                    float* save_mean, float* save_invstd, void* workspace, void* stream);
+int md2_bn_bwd_mask(const md2_bn_desc* desc, const void* x, const uint8_t* relu_mask, const void* grad_y,
+                    const void* grad_y2, const void* grad_y3, const float* gamma, const float* save_mean,
+                    const float* save_invstd, void* grad_x, void* grad_residual, float* grad_gamma,
+                    float* grad_beta, void* workspace, void* stream);
 
 /*
  * The ResNet stem's MaxPool2d(3, stride 2, padding 1) on channels_last activations

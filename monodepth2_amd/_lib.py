@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -64,7 +64,8 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_bias_act_workspace_bytes", "md2_maxpool3s2_bwd_add", "md2_bn_bwd_multi",
            "md2_conv_fwd", "md2_conv_workspace_bytes", "md2_conv_split_weights",
            "md2_conv_dgrad", "md2_conv_wgrad", "md2_conv_direct", "md2_conv_wgrad_direct",
-           "md2_conv_wgrad_direct_workspace_bytes", "md2_conv_split_weights_multi"]
+           "md2_conv_wgrad_direct_workspace_bytes", "md2_conv_split_weights_multi", "md2_bn_fwd_mask",
+           "md2_bn_bwd_mask"]
 
 DTYPE_F32 = 0    # md2_desc.disp_dtype
 DTYPE_BF16 = 1
@@ -247,6 +248,10 @@ def _declare(L):
     L.md2_maxpool3s2_bwd.argtypes = [ctypes.POINTER(PoolDesc), _vp, _vp, _vp, _vp]
     L.md2_bn_bwd_multi.restype = ctypes.c_int
     L.md2_bn_bwd_multi.argtypes = [ctypes.POINTER(BnDesc)] + [_vp] * 14
+    L.md2_bn_fwd_mask.restype = ctypes.c_int
+    L.md2_bn_fwd_mask.argtypes = [ctypes.POINTER(BnDesc)] + [_vp] * 12
+    L.md2_bn_bwd_mask.restype = ctypes.c_int
+    L.md2_bn_bwd_mask.argtypes = [ctypes.POINTER(BnDesc)] + [_vp] * 14
     L.md2_maxpool3s2_bwd_add.restype = ctypes.c_int
     L.md2_maxpool3s2_bwd_add.argtypes = [ctypes.POINTER(PoolDesc)] + [_vp] * 5
     L.md2_timing_begin.restype = ctypes.c_int

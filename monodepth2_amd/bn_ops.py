@@ -90,14 +90,17 @@ class _BNAct(torch.autograd.Function):
         y = torch.empty_like(x, memory_format=_CL)
         stats = torch.empty(2, groups, C, device=x.device)   # saved mean, invstd
         mean, invstd = stats[0], stats[1]
+        # with ReLU the backward needs only y > 0: one mask byte per element quad (ABI 15)
+        mask = torch.empty(x.numel() // 4, dtype=torch.uint8, device=x.device) if relu else None
         stream = _lib.stream(x.device)
-        rc = L.md2_bn_fwd(ctypes.byref(d), x.data_ptr(), weight.data_ptr(), bias.data_ptr(),
-                          residual.data_ptr() if residual is not None else None,
-                          running_mean.data_ptr() if running_mean is not None else None,
-                          running_var.data_ptr() if running_var is not None else None,
-                          y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ws.data_ptr(), stream)
-        _lib.check(rc, "md2_bn_fwd")
-        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        rc = L.md2_bn_fwd_mask(ctypes.byref(d), x.data_ptr(), weight.data_ptr(), bias.data_ptr(),
+                               residual.data_ptr() if residual is not None else None,
+                               running_mean.data_ptr() if running_mean is not None else None,
+                               running_var.data_ptr() if running_var is not None else None,
+                               y.data_ptr(), mask.data_ptr() if mask is not None else None,
+                               mean.data_ptr(), invstd.data_ptr(), ws.data_ptr(), stream)
+        _lib.check(rc, "md2_bn_fwd_mask")
+        ctx.save_for_backward(x, mask, weight, mean, invstd)
         ctx.desc = key
         ctx.has_res = residual is not None
         if aliases:
@@ -109,7 +112,7 @@ class _BNAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
-        x, y, weight, mean, invstd = ctx.saved_tensors
+        x, mask, weight, mean, invstd = ctx.saved_tensors
         gs = [g.to(x.dtype).contiguous(memory_format=_CL) for g in grads if g is not None]
         if not gs:
             return (None,) * 11
@@ -121,13 +124,15 @@ class _BNAct(torch.autograd.Function):
         gr = torch.empty_like(x, memory_format=_CL) if ctx.has_res else None
         gw = torch.empty_like(weight)
         gb = torch.empty_like(weight)
-        rc = L.md2_bn_bwd_multi(ctypes.byref(d), x.data_ptr(), y.data_ptr() if y is not None else None,
-                                gy.data_ptr(), gs[1].data_ptr() if len(gs) > 1 else None,
-                                gs[2].data_ptr() if len(gs) > 2 else None,
-                                weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gx.data_ptr(),
-                                gr.data_ptr() if gr is not None else None, gw.data_ptr(), gb.data_ptr(), ws.data_ptr(),
-                                _lib.stream(x.device))
-        _lib.check(rc, "md2_bn_bwd_multi")
+        bwd, name = (L.md2_bn_bwd_mask, "md2_bn_bwd_mask") if mask is not None else \
+            (L.md2_bn_bwd_multi, "md2_bn_bwd_multi")
+        rc = bwd(ctypes.byref(d), x.data_ptr(), mask.data_ptr() if mask is not None else None,
+                 gy.data_ptr(), gs[1].data_ptr() if len(gs) > 1 else None,
+                 gs[2].data_ptr() if len(gs) > 2 else None,
+                 weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gx.data_ptr(),
+                 gr.data_ptr() if gr is not None else None, gw.data_ptr(), gb.data_ptr(), ws.data_ptr(),
+                 _lib.stream(x.device))
+        _lib.check(rc, name)
         return gx, gw, gb, None, None, gr, None, None, None, None, None
 
 

@@ -191,13 +191,22 @@ __global__ void __launch_bounds__(kThreads) bn_stats_final_kernel(long long P, i
 // Elementwise passes: blockIdx.y = BatchNorm group, 32-bit quad index inside the group
 // (valid() bounds it), channel quad = index & (Q - 1) (Q a power of two) — no 64-bit
 // division or modulo per element.
-template <typename T, bool RELU, bool RES>
+// y > 0 as stored (a bf16 y is compared after rounding, as the backward would read it)
+template <typename T>
+__device__ __forceinline__ bool stored_pos(float o) {
+    if constexpr (sizeof(T) == 4) return o > 0.f;
+    else return md2::bf2f(md2::f2bf(o)) > 0.f;
+}
+
+// ReLU mask (MOUT): one byte per element quad, bit i = (y[4 i' + i] > 0) — what the
+// backward needs of y, at 1/16 (fp32) or 1/8 (bf16) of its bytes
+template <typename T, bool RELU, bool RES, bool MOUT = false>
 __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ r,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta,
                                                             const float* __restrict__ smean,
                                                             const float* __restrict__ sinvstd, void* __restrict__ y,
-                                                            int n4g, int Q) {
+                                                            int n4g, int Q, uint8_t* __restrict__ mask = nullptr) {
     const size_t base = (size_t)blockIdx.y * n4g;   // this group's first quad
     const float* mug = smean + (size_t)blockIdx.y * 4 * Q;
     const float* isg = sinvstd + (size_t)blockIdx.y * 4 * Q;
@@ -219,7 +228,24 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const void* __restri
             o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
         }
         stT<T>(y, 4 * i, o);
+        if (MOUT)
+            mask[i] = (uint8_t)((stored_pos<T>(o.x) ? 1 : 0) | (stored_pos<T>(o.y) ? 2 : 0) |
+                                (stored_pos<T>(o.z) ? 4 : 0) | (stored_pos<T>(o.w) ? 8 : 0));
     }
+}
+
+// the ReLU gate of the backward from y (fp32 / bf16) or from the forward's mask byte
+template <typename T, bool MIN>
+__device__ __forceinline__ float4 relu_gate(const void* y, size_t off, float4 g) {
+    if constexpr (MIN) {
+        const uint32_t m = ((const uint8_t*)y)[off >> 2];
+        g.x = (m & 1) ? g.x : 0.f; g.y = (m & 2) ? g.y : 0.f; g.z = (m & 4) ? g.z : 0.f; g.w = (m & 8) ? g.w : 0.f;
+    } else {
+        const float4 yv = ldT<T>(y, off);
+        g.x = yv.x > 0.f ? g.x : 0.f; g.y = yv.y > 0.f ? g.y : 0.f;
+        g.z = yv.z > 0.f ? g.z : 0.f; g.w = yv.w > 0.f ? g.w : 0.f;
+    }
+    return g;
 }
 
 // the output gradient: g (+ g2 + g3, the gradients of the output's aliases — its
@@ -238,7 +264,7 @@ __device__ __forceinline__ float4 ld_grad(const void* g, const void* g2, const v
     return v;
 }
 
-template <typename T, bool RELU>
+template <typename T, bool RELU, bool MIN = false>
 __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const void* __restrict__ x,
                                                                  const void* __restrict__ y,
                                                                  const void* __restrict__ g,
@@ -254,29 +280,29 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const void* __r
         const int q = (threadIdx.x % m.Q) + qq * kThreads, pl = threadIdx.x / m.Q;
         const float4 mu = ld4(smean + grp * C + 4 * q);
         float4 s = {0.f, 0.f, 0.f, 0.f}, sx = {0.f, 0.f, 0.f, 0.f};
-        auto acc = [&](float4 gv, const float4 yv, const float4 v) {
-            if (RELU) {
-                gv.x = yv.x > 0.f ? gv.x : 0.f; gv.y = yv.y > 0.f ? gv.y : 0.f;
-                gv.z = yv.z > 0.f ? gv.z : 0.f; gv.w = yv.w > 0.f ? gv.w : 0.f;
-            }
+        auto acc = [&](float4 gv, const float4 v) {   // gv already ReLU-gated
             s.x += gv.x; s.y += gv.y; s.z += gv.z; s.w += gv.w;
             sx.x += gv.x * (v.x - mu.x); sx.y += gv.y * (v.y - mu.y);
             sx.z += gv.z * (v.z - mu.z); sx.w += gv.w * (v.w - mu.w);
         };
         const long long stride = (long long)G * m.PPB;
-        const float4 zero = {0.f, 0.f, 0.f, 0.f};
         long long p = (long long)blockIdx.x * m.PPB + pl;
         for (; p + stride < P; p += 2 * stride) {   // two pixels (up to six loads) in flight per lane
             const size_t o0 = base + p * C + 4 * q, o1 = base + (p + stride) * C + 4 * q;
-            const float4 g0 = ld_grad<T>(g, g2, g3, o0), g1 = ld_grad<T>(g, g2, g3, o1);
-            const float4 y0 = RELU ? ldT<T>(y, o0) : zero, y1 = RELU ? ldT<T>(y, o1) : zero;
+            float4 g0 = ld_grad<T>(g, g2, g3, o0), g1 = ld_grad<T>(g, g2, g3, o1);
+            if (RELU) {
+                g0 = relu_gate<T, MIN>(y, o0, g0);
+                g1 = relu_gate<T, MIN>(y, o1, g1);
+            }
             const float4 v0 = ldT<T>(x, o0), v1 = ldT<T>(x, o1);
-            acc(g0, y0, v0);
-            acc(g1, y1, v1);
+            acc(g0, v0);
+            acc(g1, v1);
         }
         for (; p < P; p += stride) {
             const size_t o = base + p * C + 4 * q;
-            acc(ld_grad<T>(g, g2, g3, o), RELU ? ldT<T>(y, o) : zero, ldT<T>(x, o));
+            float4 gv = ld_grad<T>(g, g2, g3, o);
+            if (RELU) gv = relu_gate<T, MIN>(y, o, gv);
+            acc(gv, ldT<T>(x, o));
         }
         block_partials(s, sx, q, pl, m, C, NG * G, grp * G + blockIdx.x, w, lds);
     }
@@ -309,7 +335,7 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_final_kernel(long long P, int
     }
 }
 
-template <typename T, bool RELU, bool RES>
+template <typename T, bool RELU, bool RES, bool MIN = false>
 __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const void* __restrict__ x,
                                                                 const void* __restrict__ y,
                                                                 const void* __restrict__ g,
@@ -324,11 +350,7 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const void* __re
         const size_t i = base + j;
         const size_t c = gc + 4 * (j & (Q - 1));
         float4 gv = ld_grad<T>(g, g2, g3, 4 * i);
-        if (RELU) {
-            const float4 yv = ldT<T>(y, 4 * i);
-            gv.x = yv.x > 0.f ? gv.x : 0.f; gv.y = yv.y > 0.f ? gv.y : 0.f;
-            gv.z = yv.z > 0.f ? gv.z : 0.f; gv.w = yv.w > 0.f ? gv.w : 0.f;
-        }
+        if (RELU) gv = relu_gate<T, MIN>(y, 4 * i, gv);
         const float4 v = ldT<T>(x, 4 * i), mu = ld4(smean + c), k1 = ld4(coef + c),
                      k2 = ld4(coef + (size_t)NG * C + c), k3 = ld4(coef + 2 * (size_t)NG * C + c);
         float4 o;
@@ -368,7 +390,7 @@ bool valid(const md2_bn_desc* d) {
 template <typename T>
 void launch_fwd(const md2_bn_desc* d, const void* x, const float* gamma, const float* beta, const void* residual,
                 float* running_mean, float* running_var, void* y, float* save_mean, float* save_invstd,
-                void* workspace, hipStream_t st) {
+                void* workspace, hipStream_t st, uint8_t* mask = nullptr) {
     const int NG = groups_of(d);
     const long long P = d->pixels / NG;   // per group
     const int C = d->channels, G = blocks_for_stats(P, C);
@@ -377,29 +399,33 @@ void launch_fwd(const md2_bn_desc* d, const void* x, const float* gamma, const f
                        running_mean, running_var, save_mean, save_invstd, workspace);
     const int n4g = (int)(P * C / 4);
     const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
-    auto k = relu ? (res ? bn_apply_kernel<T, true, true> : bn_apply_kernel<T, true, false>)
+    auto k = relu ? (mask ? (res ? bn_apply_kernel<T, true, true, true> : bn_apply_kernel<T, true, false, true>)
+                          : (res ? bn_apply_kernel<T, true, true> : bn_apply_kernel<T, true, false>))
                   : (res ? bn_apply_kernel<T, false, true> : bn_apply_kernel<T, false, false>);
     hipLaunchKernelGGL(k, dim3(grid_elem(n4g, NG), NG), dim3(kThreads), 0, st, x, residual, gamma, beta, save_mean,
-                       save_invstd, y, n4g, C / 4);
+                       save_invstd, y, n4g, C / 4, mask);
 }
 
 template <typename T>
 void launch_bwd(const md2_bn_desc* d, const void* x, const void* y, const void* grad_y, const void* grad_y2,
                 const void* grad_y3, const float* gamma,
                 const float* save_mean, const float* save_invstd, void* grad_x, void* grad_residual,
-                float* grad_gamma, float* grad_beta, void* workspace, hipStream_t st) {
+                float* grad_gamma, float* grad_beta, void* workspace, hipStream_t st, bool mask_in = false) {
     const int NG = groups_of(d);
     const long long P = d->pixels / NG;
     const int C = d->channels, G = blocks_for_stats(P, C);
     const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
-    auto red = relu ? bn_bwd_reduce_kernel<T, true> : bn_bwd_reduce_kernel<T, false>;
+    // mask_in: y is the forward's ReLU mask (one byte per element quad), not y itself
+    auto red = relu ? (mask_in ? bn_bwd_reduce_kernel<T, true, true> : bn_bwd_reduce_kernel<T, true>)
+                    : bn_bwd_reduce_kernel<T, false>;
     hipLaunchKernelGGL(red, dim3(G, NG), dim3(kThreads), 0, st, x, y, grad_y, grad_y2, grad_y3, P, C, G, save_mean,
                        workspace);
     hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, NG, gamma, save_invstd,
                        grad_gamma, grad_beta, workspace);
     const int n4g = (int)(P * C / 4);
     const float* coef = work(workspace, G, C, NG).coef;
-    auto k = relu ? (res ? bn_bwd_apply_kernel<T, true, true> : bn_bwd_apply_kernel<T, true, false>)
+    auto k = relu ? (mask_in ? (res ? bn_bwd_apply_kernel<T, true, true, true> : bn_bwd_apply_kernel<T, true, false, true>)
+                             : (res ? bn_bwd_apply_kernel<T, true, true> : bn_bwd_apply_kernel<T, true, false>))
                   : (res ? bn_bwd_apply_kernel<T, false, true> : bn_bwd_apply_kernel<T, false, false>);
     hipLaunchKernelGGL(k, dim3(grid_elem(n4g, NG), NG), dim3(kThreads), 0, st, x, y, grad_y, grad_y2, grad_y3,
                        save_mean, coef, grad_x, grad_residual, n4g, C / 4, C, NG);
@@ -416,20 +442,47 @@ size_t md2_bn_workspace_bytes(const md2_bn_desc* d) {
     return (2 * (size_t)NG * G * d->channels + 3 * (size_t)NG * d->channels) * sizeof(float);
 }
 
-int md2_bn_fwd(const md2_bn_desc* d, const void* x, const float* gamma, const float* beta, const void* residual,
-               float* running_mean, float* running_var, void* y, float* save_mean, float* save_invstd,
-               void* workspace, void* stream) {
+int md2_bn_fwd_mask(const md2_bn_desc* d, const void* x, const float* gamma, const float* beta, const void* residual,
+                    float* running_mean, float* running_var, void* y, uint8_t* relu_mask, float* save_mean,
+                    float* save_invstd, void* workspace, void* stream) {
     if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "bn: need pixels >= 2 and channels a multiple of 4 "
                                                         "with channels/4 dividing (or a multiple of) 256");
     if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !workspace ||
         ((d->flags & MD2_BN_RESIDUAL) && !residual) || (!running_mean != !running_var))
         return md2_report_error(MD2_ERR_ARG, "bn_fwd: NULL operand");
+    if (relu_mask && !(d->flags & MD2_BN_RELU)) return md2_report_error(MD2_ERR_ARG, "bn_fwd: relu_mask without MD2_BN_RELU");
     if (d->flags & MD2_BN_BF16)
         launch_fwd<uint16_t>(d, x, gamma, beta, residual, running_mean, running_var, y, save_mean, save_invstd,
-                             workspace, (hipStream_t)stream);
+                             workspace, (hipStream_t)stream, relu_mask);
     else
         launch_fwd<float>(d, x, gamma, beta, residual, running_mean, running_var, y, save_mean, save_invstd,
-                          workspace, (hipStream_t)stream);
+                          workspace, (hipStream_t)stream, relu_mask);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
+int md2_bn_fwd(const md2_bn_desc* d, const void* x, const float* gamma, const float* beta, const void* residual,
+               float* running_mean, float* running_var, void* y, float* save_mean, float* save_invstd,
+               void* workspace, void* stream) {
+    return md2_bn_fwd_mask(d, x, gamma, beta, residual, running_mean, running_var, y, nullptr, save_mean, save_invstd,
+                           workspace, stream);
+}
+
+static int bn_bwd_impl(const md2_bn_desc* d, const void* x, const void* y, bool mask_in, const void* grad_y,
+                       const void* grad_y2, const void* grad_y3, const float* gamma, const float* save_mean,
+                       const float* save_invstd, void* grad_x, void* grad_residual, float* grad_gamma,
+                       float* grad_beta, void* workspace, void* stream) {
+    if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "bn: unsupported shape");
+    const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
+    if (!x || !grad_y || !gamma || !save_mean || !save_invstd || !grad_x || !grad_gamma || !grad_beta ||
+        !workspace || (relu && !y) || (res && !grad_residual) || (grad_y3 && !grad_y2))
+        return md2_report_error(MD2_ERR_ARG, "bn_bwd: NULL operand");
+    if (d->flags & MD2_BN_BF16)
+        launch_bwd<uint16_t>(d, x, y, grad_y, grad_y2, grad_y3, gamma, save_mean, save_invstd, grad_x,
+                             grad_residual, grad_gamma, grad_beta, workspace, (hipStream_t)stream, mask_in);
+    else
+        launch_bwd<float>(d, x, y, grad_y, grad_y2, grad_y3, gamma, save_mean, save_invstd, grad_x, grad_residual,
+                          grad_gamma, grad_beta, workspace, (hipStream_t)stream, mask_in);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }
@@ -438,19 +491,17 @@ int md2_bn_bwd_multi(const md2_bn_desc* d, const void* x, const void* y, const v
                      const void* grad_y3, const float* gamma, const float* save_mean, const float* save_invstd,
                      void* grad_x, void* grad_residual, float* grad_gamma, float* grad_beta, void* workspace,
                      void* stream) {
-    if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "bn: unsupported shape");
-    const bool relu = d->flags & MD2_BN_RELU, res = d->flags & MD2_BN_RESIDUAL;
-    if (!x || !grad_y || !gamma || !save_mean || !save_invstd || !grad_x || !grad_gamma || !grad_beta ||
-        !workspace || (relu && !y) || (res && !grad_residual) || (grad_y3 && !grad_y2))
-        return md2_report_error(MD2_ERR_ARG, "bn_bwd: NULL operand");
-    if (d->flags & MD2_BN_BF16)
-        launch_bwd<uint16_t>(d, x, y, grad_y, grad_y2, grad_y3, gamma, save_mean, save_invstd, grad_x,
-                             grad_residual, grad_gamma, grad_beta, workspace, (hipStream_t)stream);
-    else
-        launch_bwd<float>(d, x, y, grad_y, grad_y2, grad_y3, gamma, save_mean, save_invstd, grad_x, grad_residual,
-                          grad_gamma, grad_beta, workspace, (hipStream_t)stream);
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+    return bn_bwd_impl(d, x, y, false, grad_y, grad_y2, grad_y3, gamma, save_mean, save_invstd, grad_x, grad_residual,
+                       grad_gamma, grad_beta, workspace, stream);
+}
+
+int md2_bn_bwd_mask(const md2_bn_desc* d, const void* x, const uint8_t* relu_mask, const void* grad_y,
+                    const void* grad_y2, const void* grad_y3, const float* gamma, const float* save_mean,
+                    const float* save_invstd, void* grad_x, void* grad_residual, float* grad_gamma, float* grad_beta,
+                    void* workspace, void* stream) {
+    if (!(d && (d->flags & MD2_BN_RELU))) return md2_report_error(MD2_ERR_ARG, "bn_bwd_mask: needs MD2_BN_RELU");
+    return bn_bwd_impl(d, x, relu_mask, true, grad_y, grad_y2, grad_y3, gamma, save_mean, save_invstd, grad_x,
+                       grad_residual, grad_gamma, grad_beta, workspace, stream);
 }
 
 int md2_bn_bwd(const md2_bn_desc* d, const void* x, const void* y, const void* grad_y, const float* gamma,

@@ -256,3 +256,55 @@ def test_bn_bwd_multi_sums_alias_gradients(bf16, groups, used):
     tol = 1e-2 if bf16 else 1e-4
     for a, b, name in zip(got, ref, ["x", "residual", "weight", "bias"]):
         assert float((a.float() - b).norm() / b.norm()) < tol, name
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("res,groups", [(False, 1), (True, 1), (False, 2)])
+def test_relu_mask_path_is_bit_equal_to_y_path(dtype, res, groups):
+    """ABI 15: md2_bn_fwd_mask writes y (bit-equal to md2_bn_fwd) plus one mask byte per
+    element quad with bit i = (y[4q+i] > 0); md2_bn_bwd_mask gated by it gives the same
+    bits as md2_bn_bwd_multi reading y.  x is offset so some bf16 outputs sit near 0."""
+    import ctypes
+    from monodepth2_amd import _lib
+    torch.manual_seed(7)
+    B, C, H, W = 4, 64, 12, 20
+    x = (torch.randn(B, C, H, W, device="cuda") * 0.5).to(dtype).contiguous(memory_format=CL)
+    r = torch.randn(B, C, H, W, device="cuda").to(dtype).contiguous(memory_format=CL) if res else None
+    gamma = torch.rand(C, device="cuda") + 0.5
+    beta = torch.rand(C, device="cuda") - 0.5
+    flags = _lib.BN_RELU | (_lib.BN_RESIDUAL if res else 0) | (_lib.BN_BF16 if dtype == torch.bfloat16 else 0)
+    d = _lib.BnDesc(B * H * W, C, flags, 1e-5, 0.1, groups, 0)
+    L = _lib.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    ws = torch.empty(L.md2_bn_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device="cuda")
+    rp = r.data_ptr() if res else None
+    outs = []
+    for use_mask in (False, True):
+        y = torch.empty_like(x)
+        mean = torch.empty(groups, C, device="cuda")
+        inv = torch.empty(groups, C, device="cuda")
+        mask = torch.empty(x.numel() // 4, dtype=torch.uint8, device="cuda")
+        if use_mask:
+            _lib.check(L.md2_bn_fwd_mask(ctypes.byref(d), x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), rp, None,
+                                         None, y.data_ptr(), mask.data_ptr(), mean.data_ptr(), inv.data_ptr(),
+                                         ws.data_ptr(), st), "fwd_mask")
+        else:
+            _lib.check(L.md2_bn_fwd(ctypes.byref(d), x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), rp, None, None,
+                                    y.data_ptr(), mean.data_ptr(), inv.data_ptr(), ws.data_ptr(), st), "fwd")
+        g = torch.randn(B, C, H, W, device="cuda", generator=torch.Generator("cuda").manual_seed(3)).to(dtype)
+        g = g.contiguous(memory_format=CL)
+        gx, gr = torch.empty_like(x), (torch.empty_like(x) if res else None)
+        gw, gb = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+        args = (g.data_ptr(), None, None, gamma.data_ptr(), mean.data_ptr(), inv.data_ptr(), gx.data_ptr(),
+                gr.data_ptr() if res else None, gw.data_ptr(), gb.data_ptr(), ws.data_ptr(), st)
+        if use_mask:
+            _lib.check(L.md2_bn_bwd_mask(ctypes.byref(d), x.data_ptr(), mask.data_ptr(), *args), "bwd_mask")
+            # NHWC element e = 4 q + i: bit i of byte q
+            bits = (mask.view(-1, 1).to(torch.int32) >> torch.arange(4, device="cuda")) & 1
+            pos = (y.permute(0, 2, 3, 1).reshape(-1, 4).float() > 0).to(torch.int32)
+            assert torch.equal(bits, pos)
+        else:
+            _lib.check(L.md2_bn_bwd_multi(ctypes.byref(d), x.data_ptr(), y.data_ptr(), *args), "bwd")
+        outs.append([t for t in (y, mean, inv, gx, gr, gw, gb) if t is not None])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
