@@ -4,9 +4,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/s3
-bash tools/ab_hot.sh hbase hf4 > gpurun_out/s3/ab_hot.log 2>&1 || exit 1
-echo abhot ok
-bash tools/step_trace.sh s3trace2 > gpurun_out/s3/step_trace.log 2>&1 || exit 1
+bash tools/step_trace.sh s3trace3 > gpurun_out/s3/step_trace.log 2>&1 || exit 1
 echo steptrace ok
 ROUND=r03s3 bash tools/profile_round.sh || exit 1
 timeout -k 10 300 python bench.py > gpurun_out/s3/bench_final.log 2>&1 || exit 1
