@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 15
+#define MD2_ABI_VERSION 16
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -103,6 +103,10 @@ typedef struct md2_tensors {
 
 int md2_abi_version(void);
 const char* md2_last_error(void);
+/* Hash of the sources the library was built from (monodepth2_amd/build.py
+ * source_hash(): every .hip source, the headers, the flags and the target), so the
+ * Python binding can refuse a prebuilt library that is stale for the tree. */
+const char* md2_build_id(void);
 
 /* Scratch needed by one forward + backward pair (bytes, 256-B aligned). */
 size_t md2_workspace_bytes(const md2_desc* desc);

@@ -13,13 +13,15 @@ import threading
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 from .build import LIB_PATH as _BUILT_LIB
+from .build import source_hash
 
-# MD2_LIB overrides the library path (A/B runs of alternative builds)
+# MD2_LIB overrides the library path (A/B runs of alternative builds: their build id
+# is not checked against the tree)
 LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -65,7 +67,7 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_conv_fwd", "md2_conv_workspace_bytes", "md2_conv_split_weights",
            "md2_conv_dgrad", "md2_conv_wgrad", "md2_conv_direct", "md2_conv_wgrad_direct",
            "md2_conv_wgrad_direct_workspace_bytes", "md2_conv_split_weights_multi", "md2_bn_fwd_mask",
-           "md2_bn_bwd_mask"]
+           "md2_bn_bwd_mask", "md2_build_id"]
 
 DTYPE_F32 = 0    # md2_desc.disp_dtype
 DTYPE_BF16 = 1
@@ -195,6 +197,8 @@ def _declare(L):
     L.md2_disp_head_bwd.argtypes = [ctypes.POINTER(HeadDesc)] + [_vp] * 9
     L.md2_abi_version.restype = ctypes.c_int
     L.md2_abi_version.argtypes = []
+    L.md2_build_id.restype = ctypes.c_char_p
+    L.md2_build_id.argtypes = []
     L.md2_last_error.restype = ctypes.c_char_p
     L.md2_last_error.argtypes = []
     L.md2_workspace_bytes.restype = ctypes.c_size_t
@@ -280,6 +284,12 @@ def lib():
             v = L.md2_abi_version()
             if v != ABI_VERSION:
                 raise RuntimeError(f"libmd2hot ABI {v} != expected {ABI_VERSION}")
+            if LIB_PATH == _BUILT_LIB:
+                got, want = L.md2_build_id().decode(), source_hash()
+                if got != want:
+                    raise RuntimeError(
+                        f"{LIB_PATH} was built from other sources (build id {got}, tree {want}): "
+                        "rebuild it with `python -m monodepth2_amd.build`")
             _lib = L
     return _lib
 

@@ -6,6 +6,7 @@ repository snapshot; it is git-ignored.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -43,6 +44,21 @@ def needs_build() -> bool:
 FLAGS = {"md2hot.hip": ["-fno-slp-vectorize"]}
 
 
+def source_hash() -> str:
+    """Hash of everything the library is built from (sources, headers, per-source
+    flags, target architecture): baked into the library as md2_build_id() and checked
+    against the tree by _lib.lib(), so a stale prebuilt .so cannot load silently."""
+    h = hashlib.sha256()
+    for path in [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(INCLUDE, "md2hot.h"),
+                                                          os.path.join(CSRC, "md2_bf16.h")]:
+        h.update(os.path.basename(path).encode())
+        with open(path, "rb") as f:
+            h.update(f.read())
+    h.update(repr(sorted(FLAGS.items())).encode())
+    h.update(ARCH.encode())
+    return h.hexdigest()[:16]
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB_PATH
@@ -50,10 +66,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objdir = os.path.join(CSRC, "obj")
     os.makedirs(objdir, exist_ok=True)
     base = [hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-I" + INCLUDE]
+    bid = ['-DMD2_BUILD_ID="%s"' % source_hash()]
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
-        cmd = base + FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = base + FLAGS.get(src, []) + (bid if src == "glue.hip" else []) + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)

@@ -368,7 +368,22 @@ def _fastest(op: str, key: tuple, cands, names=None) -> int:
     _times[k] = dict(zip(names, times))
     best = min(range(len(cands) - 1), key=lambda i: times[i]) if len(cands) > 1 else 0
     _choice[k] = best if times[best] < 0.97 * times[-1] else len(cands) - 1
+    _choice[k] = _rank0_choice(_choice[k])
     return _choice[k]
+
+
+def _rank0_choice(mine: int) -> int:
+    """Under data parallelism every rank runs rank 0's choice: the ranks' timings can
+    disagree, and different kernels round differently, so the replicas would drift
+    apart.  Every rank meets the same shapes in the same order (same networks and
+    batch shape), so one small broadcast per newly timed shape lines them up; a table
+    loaded with load_choices (the same file on every rank) needs none."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return mine
+    box = [mine]
+    dist.broadcast_object_list(box, src=0)
+    return int(box[0])
 
 
 _DIRECT = ((16, 16), (32, 16), (16, 32))   # (in, out) channels of md2_conv_direct

@@ -80,7 +80,14 @@ __global__ __launch_bounds__(kThreads) void encoder_input_v4_kernel(InputArgs a)
 
 }  // namespace
 
+#ifndef MD2_BUILD_ID
+#define MD2_BUILD_ID "unset"
+#endif
+
 extern "C" {
+
+// the source hash monodepth2_amd/build.py bakes in (see md2hot.h)
+const char* md2_build_id(void) { return MD2_BUILD_ID; }
 
 int md2_encoder_input(int groups, int batch, int slots, int height, int width, const float* const* src, float mean,
                       float std_, float* out, void* stream) {

@@ -73,10 +73,10 @@ __device__ __forceinline__ int reflect_clamp(int i, int n) {
 // lane i-1, wave_shl:1 of lane i+1 (checked on MI355X); lanes 0 / 63 receive 0,
 // they are halo lanes whose results are never used.
 __device__ __forceinline__ float shfl_prev(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float shfl_next(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, true));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -171,6 +171,10 @@ __device__ __forceinline__ float2 noise_pair(uint32_t key, uint32_t q, int j) {
 // ----------------------------------------------------------------------------
 // per-(image, frame) camera: P = (K @ T)[:3] and inv_K[:3,:3]   layers.py:164,183
 // ----------------------------------------------------------------------------
+__device__ __forceinline__ float uniformf(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
 struct Cam {
     float iK[9];
     float P[12];
@@ -187,6 +191,11 @@ __device__ __forceinline__ void load_cam(Cam& cm, const float* K, const float* i
     for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) cm.iK[i * 3 + j] = iK[i * 4 + j];
+    // wave-uniform: keep them in SGPRs (VALU operands), not in 21 VGPRs
+#pragma unroll
+    for (int i = 0; i < 12; ++i) cm.P[i] = uniformf(cm.P[i]);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) cm.iK[i] = uniformf(cm.iK[i]);
 }
 
 // everything a warp of one (image, frame, scale) needs
@@ -292,13 +301,19 @@ __device__ __forceinline__ float depth_at(const WarpCtx& c, int y, int x) {
     return rcpf(c.min_disp + c.range * disp_at(c, y, x));
 }
 
+// component i of the ray inv_K[:3,:3] @ [x, y, 1] (layers.py:164): one expression
+// for the projection and the backward's output step, so both round identically
+__device__ __forceinline__ float ray_at(const Cam& cm, int i, float fx, float fy) {
+    return cm.iK[i * 3 + 0] * fx + cm.iK[i * 3 + 1] * fy + cm.iK[i * 3 + 2];
+}
+
 // projection of pixel (y, x) at a given depth
 __device__ __forceinline__ void project_depth(const WarpCtx& c, int y, int x, float depth, FastSample& s) {
     s.depth = depth;
     const float fx = (float)x, fy = (float)y;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        s.ray[i] = c.cm.iK[i * 3 + 0] * fx + c.cm.iK[i * 3 + 1] * fy + c.cm.iK[i * 3 + 2];
+        s.ray[i] = ray_at(c.cm, i, fx, fy);
         s.pt[i] = s.depth * s.ray[i];
     }
 #pragma unroll
@@ -414,8 +429,8 @@ __device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.f), 
 __device__ __forceinline__ float sum3(const C3& v) { return v.a.x + v.a.y + v.b; }
 __device__ __forceinline__ C3 abs3(const C3& v) { return {f2v{fabsf(v.a.x), fabsf(v.a.y)}, fabsf(v.b)}; }
 
-template <bool U8>
-__device__ __forceinline__ C3 interp3(const FastSample& s, const Corners& v) {
+template <bool U8, class SampleT>
+__device__ __forceinline__ C3 interp3(const SampleT& s, const Corners& v) {
     const float e = 1.f - s.tx, so = 1.f - s.ty;
     const float wnw = so * e, wne = so * s.tx, wsw = s.ty * e, wse = s.ty * s.tx;
     const C3 nw = {f2v{v.nw[0], v.nw[1]}, v.nw[2]}, ne = {f2v{v.ne[0], v.ne[1]}, v.ne[2]};
@@ -978,13 +993,14 @@ struct BwdFrame {
 };
 
 // Carried two rows down the sliding window from an output row's own forward sample
-// (instead of re-projecting and re-gathering it).
+// (instead of re-projecting and re-gathering it): the bilinear slopes and the
+// perspective terms.  The rest of the projection chain (ray, camera point, dcam/ddepth)
+// is recomputed at the output step from the row's depth in LDS with the same
+// expressions (ray_at, the same products), so it rounds exactly as the carried values
+// did, while the three ring slots carry 9 floats each instead of 16.
 struct CarryP {
     C3 jx, jy;
     float px, py, inv_den;
-    float pt[3];
-    float u[3];
-    float dd;
 };
 struct RowP {
     H5P h;
@@ -996,8 +1012,95 @@ struct CoefP {
     float g;
 };
 
+// A window row whose projection is done and whose loads are in flight.  The walk is
+// software-pipelined by one row: row k+1's corner gathers, target colours and the
+// argmin code its step needs are issued right after row k's loads are consumed, so
+// row k's SSIM adjoint and output step (most of a step's VALU work) cover their
+// latency instead of every step waiting on its own gathers.
 template <bool U8>
-__device__ __forceinline__ void make_carry3(const WarpCtx& c, const FastSample& s, const Corners& v, CarryP& k) {
+struct PendRaw;
+template <>
+struct PendRaw<true> {
+    uint2_a4 t, u;            // RGBx corner pairs of the top / bottom row
+};
+template <>
+struct PendRaw<false> {
+    float2_a4 t[3], u[3];     // per channel
+};
+template <bool U8>
+struct PendRow {
+    float tx, ty, px, py, inv_den, gmx, gmy;
+    bool vx1, vy1;
+    PendRaw<U8> raw;
+    C3 y;
+    int code;                 // argmin code of the coefficient row of the step (trainer.py:478)
+};
+
+// project window row k (depth from LDS) and issue its loads
+template <bool U8>
+__device__ __forceinline__ void bwd_issue(const BwdFrame& F, int k, PendRow<U8>& pd, int lane) {
+    const int h = F.ctx.h, w = F.ctx.w, HW = h * w;
+    const int r = F.r0 - 2 + k;
+    const int rr = reflect_clamp(r, h);
+    FastSample sm;
+    project_depth(F.ctx, rr, F.cc, F.dep[k][lane], sm);
+    pd.tx = sm.tx;
+    pd.ty = sm.ty;
+    pd.px = sm.px;
+    pd.py = sm.py;
+    pd.inv_den = sm.inv_den;
+    pd.gmx = sm.gmx;
+    pd.gmy = sm.gmy;
+    pd.vx1 = sm.x0 + 1 < w;
+    pd.vy1 = sm.y0 + 1 < h;
+    const int y1 = pd.vy1 ? sm.y0 + 1 : sm.y0;
+    const int xa = pd.vx1 ? sm.x0 : sm.x0 - 1;
+    const int ot = sm.y0 * w + xa, ob = y1 * w + xa;
+    if constexpr (U8) {
+        pd.raw.t = *(const uint2_a4*)((const char*)F.ctx.src8 + ((uint32_t)ot << 2));
+        pd.raw.u = *(const uint2_a4*)((const char*)F.ctx.src8 + ((uint32_t)ob << 2));
+    } else {
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            pd.raw.t[ch] = ldf2(F.ctx.src, ch * HW + ot);
+            pd.raw.u[ch] = ldf2(F.ctx.src, ch * HW + ob);
+        }
+    }
+    pd.y = ld3(F.tgt, HW, rr * w + F.cc);
+    // coefficient row p = r - 1, read at a clamped address (used only where it is real)
+    const int p = min(max(r - 1, 0), h - 1);
+    pd.code = ldb(F.sel, p * w + F.cc);
+}
+
+// the four masked corners of a pending row (gather()'s selects)
+template <bool U8>
+__device__ __forceinline__ void bwd_corners(const PendRow<U8>& pd, Corners& v) {
+    const bool vx1 = pd.vx1, vy1 = pd.vy1;
+    if constexpr (U8) {
+        const uint2_a4 t = pd.raw.t, u = pd.raw.u;
+        const uint32_t pnw = vx1 ? t.x : t.y, pne = vx1 ? t.y : 0u;
+        const uint32_t psw = vy1 ? (vx1 ? u.x : u.y) : 0u, pse = (vx1 && vy1) ? u.y : 0u;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            v.nw[ch] = (float)((pnw >> (8 * ch)) & 255u);
+            v.ne[ch] = (float)((pne >> (8 * ch)) & 255u);
+            v.sw[ch] = (float)((psw >> (8 * ch)) & 255u);
+            v.se[ch] = (float)((pse >> (8 * ch)) & 255u);
+        }
+    } else {
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            const float2_a4 t = pd.raw.t[ch], u = pd.raw.u[ch];
+            v.nw[ch] = vx1 ? t.x : t.y;
+            v.ne[ch] = vx1 ? t.y : 0.f;
+            v.sw[ch] = vy1 ? (vx1 ? u.x : u.y) : 0.f;
+            v.se[ch] = (vx1 && vy1) ? u.y : 0.f;
+        }
+    }
+}
+
+template <bool U8, class SampleT>
+__device__ __forceinline__ void make_carry3(const WarpCtx& c, const SampleT& s, const Corners& v, CarryP& k) {
     const float e = 1.f - s.tx, so = 1.f - s.ty;
     const float cs = U8 ? 1.0f / 255.0f : 1.0f;
     const float mx = s.gmx * c.sx * cs, my = s.gmy * c.sy * cs;
@@ -1008,16 +1111,11 @@ __device__ __forceinline__ void make_carry3(const WarpCtx& c, const FastSample& 
     k.px = s.px;
     k.py = s.py;
     k.inv_den = s.inv_den;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        k.pt[i] = s.pt[i];
-        k.u[i] = c.cm.P[i * 4 + 0] * s.ray[0] + c.cm.P[i * 4 + 1] * s.ray[1] + c.cm.P[i * 4 + 2] * s.ray[2];
-    }
-    k.dd = -c.range * s.depth * s.depth;
 }
 
 // One step of the backward row walk at window index k (row r = r0 - 2 + k):
-//   evaluate row r (warp, target, horizontal sums, carry) into `cur`;
+//   row r from the pending loads (warp, target, horizontal sums, carry) into `cur`,
+//   then row k+1's loads are issued into `pd`;
 //   k >= 2: SSIM adjoint coefficients of row p = r - 1 into `cnew` (from the sums of
 //           rows r-2, r-1, r = m2, m1, cur);
 //   k >= 4: output row q = r - 2: dL/dwarp from coefficient rows q-1, q, q+1
@@ -1027,28 +1125,34 @@ __device__ __forceinline__ void make_carry3(const WarpCtx& c, const FastSample& 
 // rows mod 3) that the caller rotates by unrolling three steps, so moving the window
 // down costs no register copies; every slot is updated unconditionally.
 template <int NS, bool SSIM_ON, bool MASK, bool U8>
-__device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, RowP& cur, const RowP& m1, const RowP& m2,
-                                           CoefP& cnew, const CoefP& cm2, const CoefP& cm3, float (&dP)[12],
-                                           float (*ddacc)[kWave], int lane) {
+__device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, PendRow<U8>& pd, RowP& cur, const RowP& m1,
+                                         const RowP& m2, CoefP& cnew, const CoefP& cm2, const CoefP& cm3,
+                                         float (&dP)[12], float (*ddacc)[kWave], int lane) {
     constexpr float kThird = 1.0f / 3.0f;
+    constexpr int kSteps = kRowsB + 4;
     const float l1w = SSIM_ON ? 0.15f : 1.0f;
-    const int h = F.ctx.h, w = F.ctx.w, HW = h * w;
+    const int h = F.ctx.h, w = F.ctx.w;
     const int r = F.r0 - 2 + k;
-    const int rr = reflect_clamp(r, h);
-    FastSample sm;
-    project_depth(F.ctx, rr, F.cc, F.dep[k][lane], sm);
-    Corners v;
-    gather<U8>(F.ctx, sm, v);
-    cur.x = interp3<U8>(sm, v);
-    cur.y = ld3(F.tgt, HW, rr * w + F.cc);
-    if (k >= 2 && k < kRowsB + 2) make_carry3<U8>(F.ctx, sm, v, cur.k);   // only output rows need it
+    // the fp32-plane path (12 corner floats per row in flight) issues its own row here:
+    // pipelined it would not fit the register file
+    if constexpr (!U8) bwd_issue<U8>(F, k, pd, lane);
+    {
+        Corners v;
+        bwd_corners<U8>(pd, v);
+        cur.x = interp3<U8>(pd, v);
+        cur.y = pd.y;
+        if (k >= 2 && k < kRowsB + 2) make_carry3<U8>(F.ctx, pd, v, cur.k);   // only output rows need it
+    }
     if (SSIM_ON) cur.h = hsum3(cur.x, cur.y);
+    const int code = pd.code;
+    // the next row's loads (the last step re-issues its own row: same addresses, unused)
+    if constexpr (U8) bwd_issue<U8>(F, min(k + 1, kSteps - 1), pd, lane);
     if (k < 2) return;
     // coefficient row p = r - 1
     const int p = r - 1;
     float gp = 0.f;
     const bool own = F.colreal && p >= 0 && p < h;
-    if (own) gp = F.gscale * frame_weight<NS>(ldb(F.sel, p * w + F.c), F.f, F.automask, F.avg);
+    if (own) gp = F.gscale * frame_weight<NS>(code, F.f, F.automask, F.avg);
     if (MASK) {
         // masked = reproj * mask (trainer.py:455): d/dreproj = g*mask, d/dmask = g*reproj
         const size_t mi = (((size_t)F.b * NS + F.f) * h + (own ? p : 0)) * w + (own ? F.c : 0);
@@ -1089,13 +1193,28 @@ __device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, RowP& cur, co
     dc[0] = dpx * k2.inv_den;
     dc[1] = dpy * k2.inv_den;
     dc[2] = -(dpx * k2.px + dpy * k2.py) * k2.inv_den;
+    // the sample's ray / camera point / dcam-ddepth, recomputed (output rows are inside
+    // the image, so the sample row was q itself, unreflected)
+    const float depth = F.dep[k - 2][lane];
+    const float fx = (float)F.cc, fy = (float)q;
+    float ray[3], pt[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        ray[i] = ray_at(F.ctx.cm, i, fx, fy);
+        pt[i] = depth * ray[i];
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
 #pragma unroll
-        for (int j = 0; j < 3; ++j) dP[i * 4 + j] += dc[i] * k2.pt[j];
+        for (int j = 0; j < 3; ++j) dP[i * 4 + j] += dc[i] * pt[j];
         dP[i * 4 + 3] += dc[i];
     }
-    const float dd = (dc[0] * k2.u[0] + dc[1] * k2.u[1] + dc[2] * k2.u[2]) * k2.dd;
+    float u[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        u[i] = F.ctx.cm.P[i * 4 + 0] * ray[0] + F.ctx.cm.P[i * 4 + 1] * ray[1] + F.ctx.cm.P[i * 4 + 2] * ray[2];
+    const float ddd = -F.ctx.range * depth * depth;
+    const float dd = (dc[0] * u[0] + dc[1] * u[1] + dc[2] * u[2]) * ddd;
     if (F.f == 0) ddacc[q - F.r0][lane] = dd;
     else ddacc[q - F.r0][lane] += dd;
 }
@@ -1107,16 +1226,18 @@ __device__ __forceinline__ void bwd_frame_walk(const BwdFrame& F, float (*ddacc)
     for (int j = 0; j < 12; ++j) dP[j] = 0.f;
     RowP S0, S1, S2;
     CoefP C0, C1, C2;
+    PendRow<U8> pd;
     constexpr int kSteps = kRowsB + 4;
+    if constexpr (U8) bwd_issue<U8>(F, 0, pd, lane);
     int k = 0;
 #pragma unroll 1
     for (; k + 3 <= kSteps; k += 3) {
-        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
-        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
-        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 2, S2, S1, S0, C1, C0, C2, dP, ddacc, lane);
+        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, pd, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
+        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, pd, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
+        bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 2, pd, S2, S1, S0, C1, C0, C2, dP, ddacc, lane);
     }
-    if (kSteps % 3 >= 1) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
-    if (kSteps % 3 >= 2) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
+    if (kSteps % 3 >= 1) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 0, pd, S0, S2, S1, C2, C1, C0, dP, ddacc, lane);
+    if (kSteps % 3 >= 2) bwd_step<NS, SSIM_ON, MASK, U8>(F, k + 1, pd, S1, S0, S2, C0, C2, C1, dP, ddacc, lane);
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
         const float t = wave_sum(dP[j]);
@@ -1166,9 +1287,6 @@ __device__ __forceinline__ void bwd_item(const PhotoArgs& a, int b, int ls, int 
             bwd_frame_walk<NS, SSIM_ON, MASK, false>(F, ddacc, dst, lane);
     }
     const int upsh = a.upsh[ls];
-#ifdef MD2_NO_FOLD   // timing experiments only: results are wrong
-    if (upsh != 0) return;
-#endif
     if (upsh == 0) {   // no upsample: dL/d(disp) at this resolution, written once
         float* dfull = a.dfull[ls] + (size_t)b * HW;
         if (F.colok)

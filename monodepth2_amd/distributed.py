@@ -53,15 +53,23 @@ def ignored_parameters(module: nn.Module):
             or n.endswith("encoder.fc.bias")]
 
 
-class GradReadyEvents:
-    """Per-parameter "gradient final" events for a backward that runs on several HIP
-    streams (the trainer's pose network has its own).  A post-accumulate-grad hook
-    records an event on the stream that produced the gradient (the current stream
-    inside the hook is the autograd node's), so a consumer can wait for exactly the
-    gradients it reads instead of for everything queued on every stream."""
+class GradStreams:
+    """Which HIP stream produced each parameter's gradient this step (the trainer's
+    pose network runs its backward on its own stream).  A post-accumulate-grad hook
+    notes the current stream inside the hook — the autograd node's — per parameter.
+
+    DDP's comm hook uses it: DDP copies a gradient that autograd handed over as a fresh
+    tensor (zero_grad(set_to_none=True)) into its bucket in its own hook, on the
+    producing stream, AFTER this hook ran — so an event recorded here would not cover
+    that copy.  But a bucket's comm hook only fires once every copy of the bucket has
+    been queued; waiting there for the whole queue of each other producing stream
+    covers them (the bucket's last gradient is on the current stream, which the
+    collective's stream follows anyway).  Buckets whose gradients all came from the
+    current stream wait for nothing, so the depth network's buckets still go out while
+    the pose stream is busy."""
 
     def __init__(self, params):
-        self.events = {}
+        self.stream_of = {}
         self.handles = []
         for p in params:
             if p.requires_grad:
@@ -69,24 +77,19 @@ class GradReadyEvents:
 
     def _ready(self, p):
         if p.is_cuda:
-            ev = self.events.get(p)
-            if ev is None:
-                ev = self.events[p] = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(p.device))
+            self.stream_of[p] = torch.cuda.current_stream(p.device)
 
     def wait(self, params, stream):
-        for p in params:
-            ev = self.events.get(p)
-            if ev is not None:
-                stream.wait_event(ev)
+        for s in {self.stream_of[p] for p in params if p in self.stream_of}:
+            if s != stream:
+                stream.wait_stream(s)
 
 
-def _event_synced_allreduce(state, bucket):
-    """DDP comm hook: the bucket's all-reduce waits for the ready events of ITS
-    parameters' gradients (GradReadyEvents), not for whole streams, so the depth
-    network's buckets go out while the pose stream is still busy."""
+def _stream_synced_allreduce(state, bucket):
+    """DDP comm hook: the bucket's all-reduce follows every stream that produced one of
+    its gradients (GradStreams), then the default all-reduce (average)."""
     from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
-    state["events"].wait(bucket.parameters(), torch.cuda.current_stream())
+    state["streams"].wait(bucket.parameters(), torch.cuda.current_stream())
     return default_hooks.allreduce_hook(state["group"], bucket)
 
 
@@ -95,18 +98,18 @@ def wrap_ddp(module: nn.Module, device: torch.device, streams=None):
     gradients on (more than one -> the per-bucket event comm hook above)."""
     from torch.nn.parallel import DistributedDataParallel as DDP
     DDP._set_params_and_buffers_to_ignore_for_model(module, ignored_parameters(module))
-    events = None
+    gs = None
     if streams and len(streams) > 1:
-        # registered BEFORE DDP's own autograd hooks, so a parameter's event is recorded
-        # before DDP can find its bucket ready and call the comm hook
-        events = GradReadyEvents(module.parameters())
+        # registered before DDP's own autograd hooks: a parameter's producing stream is
+        # noted before DDP can find its bucket ready and call the comm hook
+        gs = GradStreams(module.parameters())
     kw = dict(broadcast_buffers=False, bucket_cap_mb=BUCKET_CAP_MB, gradient_as_bucket_view=True)
     if device.type == "cuda":
         kw.update(device_ids=[device.index], output_device=device.index)
     ddp = DDP(module, **kw)
-    if events is not None:
-        ddp.register_comm_hook({"group": None, "events": events}, _event_synced_allreduce)
-        ddp._md2_grad_events = events
+    if gs is not None:
+        ddp.register_comm_hook({"group": None, "streams": gs}, _stream_synced_allreduce)
+        ddp._md2_grad_streams = gs
     return ddp
 
 
@@ -130,8 +133,9 @@ class FlatGradSync:
     finishes them, as DDP).  `zero()` drops the gradients (autograd then hands each
     producer's output over instead of adding it into a zeroed buffer); a post-
     accumulate-grad hook per parameter notes the gradient and the stream it was
-    produced on, and when a bucket's last gradient is final the bucket goes out at
-    once: the communication stream waits for the producing streams, copies the
+    produced on, and when a bucket's last gradient is final the bucket goes out (as
+    soon as every bucket before it has: the collectives keep one order on every rank):
+    the communication stream waits for the producing streams, copies the
     gradients into the flat buffer (one multi-tensor copy), and all-reduces it
     (ReduceOp.AVG on RCCL) — while the backward of the earlier layers continues.
     `sync()` sends any bucket still pending (parameters that got no gradient this step
@@ -182,6 +186,7 @@ class FlatGradSync:
         self.comm = torch.cuda.Stream(self.flat[0].device) if cuda else None
         self.pending = [dict() for _ in self.buckets]   # bucket -> {param: (grad, stream)}
         self.sent = [False] * len(self.buckets)
+        self.next_send = 0   # buckets go out strictly in index order (see _ready)
         self.handles = [p.register_post_accumulate_grad_hook(self._ready) for plist in self.buckets for p in plist]
         self.works = []
 
@@ -195,6 +200,7 @@ class FlatGradSync:
                 p.grad = None
         self.pending = [dict() for _ in self.buckets]
         self.sent = [False] * len(self.buckets)
+        self.next_send = 0
         self.works = []
 
     def _ready(self, p):
@@ -203,8 +209,14 @@ class FlatGradSync:
             return
         stream = torch.cuda.current_stream(p.device) if p.is_cuda else None
         self.pending[bi][p] = (p.grad, stream)
-        if len(self.pending[bi]) == len(self.buckets[bi]):
-            self._send(bi)
+        # RCCL needs the same collective order on every rank, and autograd's hook order
+        # need not be the same everywhere (a parameter without a gradient, another
+        # stream finishing first): a complete bucket waits until every bucket before it
+        # has gone out, as DDP's reducer launches its buckets in index order
+        while (self.next_send < len(self.buckets)
+               and len(self.pending[self.next_send]) == len(self.buckets[self.next_send])):
+            self._send(self.next_send)
+            self.next_send += 1
 
     def _send(self, bi):
         self.sent[bi] = True
@@ -241,9 +253,9 @@ class FlatGradSync:
             for buf in self.flat:
                 dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.group)
             return
-        for bi in range(len(self.buckets)):
-            if not self.sent[bi]:
-                self._send(bi)
+        for bi in range(self.next_send, len(self.buckets)):   # in index order
+            self._send(bi)
+        self.next_send = len(self.buckets)
         if self.comm is not None:
             torch.cuda.current_stream(self.flat[0].device).wait_stream(self.comm)
         for w in self.works:   # CPU (gloo): the asynchronous all-reduces

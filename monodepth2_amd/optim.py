@@ -55,7 +55,11 @@ class FusedAdam(torch.optim.Adam):
             sd["state"] = {k: ({**v, "step": v["step"].detach().clone().cpu()} if "step" in v else v)
                            for k, v in sd["state"].items()}
         if self.capturable:
-            sd["param_groups"] = [{**g, "lr": float(g["lr"]), "capturable": False, "fused": None}
+            # every tensor hyper-parameter as a float: lr, and StepLR's initial_lr (a
+            # cloned device fp64 tensor in torch 2.10) — adam.pth then holds no CUDA
+            # tensor and loads on a CPU-only machine like the reference's
+            sd["param_groups"] = [{**{k: (float(v) if torch.is_tensor(v) else v) for k, v in g.items()},
+                                   "capturable": False, "fused": None}
                                   for g in sd["param_groups"]]
         return sd
 

@@ -159,9 +159,13 @@ class Trainer:
         # one GPU needs no buckets: under capture the gradients are allocated (and
         # freed) in the graph's private pool like every other tensor, at the same
         # addresses on every replay, and autograd hands each producer's output over
-        # instead of adding it into a pre-zeroed bucket (~150 add launches per step)
+        # instead of adding it into a pre-zeroed bucket (~150 add launches per step).
+        # An explicit --grad_sync flat builds them anyway (buckets, communication
+        # stream, stream waits and copies, no collective at world size 1): the
+        # multi-GPU graph path exercised on one GPU.
+        explicit_flat = getattr(self.opt, "grad_sync", "auto") == "flat"
         self.flat_sync = FlatGradSync(self.nets.named_parameters(), world_size) \
-            if (world_size > 1 and (sync == "flat" or self.use_graph)) else None
+            if ((world_size > 1 and (sync == "flat" or self.use_graph)) or explicit_flat) else None
         self.graph = None
         self.seed_tensor = None
 

@@ -35,6 +35,13 @@ def test_abi_version(L):
     assert L.md2_abi_version() == _lib.ABI_VERSION
 
 
+def test_build_id_matches_tree(L):
+    """the in-tree library is the build of these sources (a stale prebuilt .so of the
+    same ABI would be refused by _lib.lib())"""
+    from monodepth2_amd.build import source_hash
+    assert L.md2_build_id().decode() == source_hash()
+
+
 def test_struct_sizes():
     assert ctypes.sizeof(_lib.Desc) == 48
     assert ctypes.sizeof(_lib.Tensors) == 8 * (4 + 16 + 4 + 4 + 4)

@@ -164,3 +164,26 @@ def test_overlapped_buckets_equal_post_backward_sync(tmp_path):
                 assert (a[n] is None or float(a[n].abs().sum()) == 0) and (b[n] is None or float(b[n].abs().sum()) == 0)
                 continue
             assert torch.equal(a[n], b[n]), n
+
+
+def test_flat_sync_sends_buckets_in_index_order():
+    """FlatGradSync hands buckets to the collective strictly in index order, whatever
+    order the gradients finish in (RCCL needs one collective order on every rank;
+    DDP's reducer launches its buckets in index order too).  Host logic only: the
+    gradient hooks are fired by hand in a scrambled order."""
+    params = [torch.nn.Parameter(torch.randn(4, 4)) for _ in range(6)]
+    sync = FlatGradSync([(f"p{i}", p) for i, p in enumerate(params)], world=1, bucket_cap_mb=0)
+    assert len(sync.buckets) == 6   # a zero cap: one parameter per bucket
+    sent = []
+    real_send = sync._send
+    sync._send = lambda bi: (sent.append(bi), real_send(bi))
+    sync.zero()
+    order = [sync.buckets[i][0] for i in (3, 0, 5, 1, 2)]   # bucket 4 never gets a gradient
+    for p in order:
+        p.grad = torch.ones_like(p)
+        sync._ready(p)
+    assert sent == [0, 1, 2, 3]          # 3 waited for 1 and 2; 5 waits for 4
+    sync.sync()
+    assert sent == [0, 1, 2, 3, 4, 5]    # the rest, in order (4 counts as zero)
+    b4 = sync.buckets[4][0]
+    assert torch.equal(b4.grad, torch.zeros_like(b4)) and torch.equal(sync.buckets[5][0].grad, torch.ones(4, 4))

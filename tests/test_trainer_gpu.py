@@ -208,6 +208,27 @@ def test_hip_graph_replay_matches_eager_step():
     assert worst < 1e-6, worst
 
 
+def test_hip_graph_flat_sync_step_replays_eager_bitwise():
+    """The multi-GPU graph path on one GPU: --grad_sync flat at world size 1 builds
+    FlatGradSync's buckets (the collective itself is skipped at world size 1), so the
+    captured step holds the per-parameter stream bookkeeping, the communication
+    stream's waits on the producing streams (pose network on its own stream), the
+    bucket copies and the join back.  A replay must equal the same step run eagerly
+    from the same state, bit for bit, and every gradient must be its bucket view."""
+    tr, batch = make("mono", hip_graph=True, grad_sync="flat")
+    fs = tr.flat_sync
+    assert fs is not None and fs.overlap and fs.comm is not None and len(fs.buckets) >= 1
+    assert tr._pose_stream is not None
+    tr.train_step(batch)                       # capture (+ warm-up steps) and one replay
+    tr.train_step(batch)
+    for plist, views in zip(fs.buckets, fs.views):
+        for p, v in zip(plist, views):
+            assert p.grad is not None and p.grad.data_ptr() == v.data_ptr()
+    loss_g, loss_e, worst, delta = _replay_vs_eager(tr, batch)
+    assert delta > 0
+    assert loss_g == loss_e and worst == 0.0, (loss_g, loss_e, worst)
+
+
 def _graph_state(tr):
     return ([p.detach().clone() for p in tr.nets.parameters()],
             [b.detach().clone() for b in tr.nets.buffers()])
@@ -373,6 +394,9 @@ def test_hip_graph_resume_keeps_device_lr(tmp_path):
     folder = tr.save_model()
     sd = torch.load(os.path.join(folder, "adam.pth"), weights_only=True)
     assert all(isinstance(g["lr"], float) and not g["capturable"] for g in sd["param_groups"])
+    # no tensor hyper-parameter (StepLR's initial_lr included): loadable without a GPU
+    assert not any(torch.is_tensor(v) for g in sd["param_groups"] for v in g.values())
+    torch.load(os.path.join(folder, "adam.pth"), weights_only=True, map_location="cpu")
     assert all(v["step"].device.type == "cpu" and float(v["step"]) == 2.0 for v in sd["state"].values())
     tr2, batch2 = make("mono", log_dir=str(tmp_path), hip_graph=True, load_weights_folder=folder)
     g = tr2.model_optimizer.param_groups[0]
