@@ -110,7 +110,14 @@ def pmc_traffic(args, S, timeout=150):
         per[counter] = {k: sum(v) / len(v) for k, v in vals.items()}
         shutil.rmtree(d, ignore_errors=True)
     kernels = sorted(set(per["FETCH_SIZE"]) | set(per["WRITE_SIZE"]))
-    by_kernel = {k: int(1024 * (2 * per["FETCH_SIZE"].get(k, 0.0) + per["WRITE_SIZE"].get(k, 0.0)))
+    # raw = FETCH + WRITE; corrected = 2 FETCH + WRITE.  tools/fetch_calib.py measured on
+    # MI355X (profiles/r04/fetch_calib.json): FETCH_SIZE counts half the bytes of 4-, 8-
+    # and 16-B-per-lane reads alike (coalesced or one line per lane), WRITE_SIZE every
+    # width exactly; 1- and 2-B-per-lane reads are not counted at all (the argmin-code
+    # bytes the backward reads are missing from both figures)
+    by_kernel = {k: {"raw": int(1024 * (per["FETCH_SIZE"].get(k, 0.0) + per["WRITE_SIZE"].get(k, 0.0))),
+                     "corrected": int(1024 * (2 * per["FETCH_SIZE"].get(k, 0.0) + per["WRITE_SIZE"].get(k, 0.0))),
+                     "write": int(1024 * per["WRITE_SIZE"].get(k, 0.0))}
                  for k in kernels}
     return by_kernel, None
 
@@ -389,8 +396,10 @@ def main():
         dt = float(t)
     final_loss = float(losses["loss"])
 
+    timed_standalone = False
     if rank == 0 and kt.n_bwd == 0:
         kt = time_hot_kernels(trainer, batch)
+        timed_standalone = True
         log("hot-path kernels timed stand-alone (graph mode)")
     if rank == 0:
         S = len(frame_ids) - 1
@@ -410,10 +419,12 @@ def main():
         if args.pmc and world == 1:
             pmc_kernels, err = pmc_traffic(args, S)
             if pmc_kernels is not None:
-                traffic = sum(pmc_kernels.values())
+                traffic = sum(v["corrected"] for v in pmc_kernels.values())
                 pmc_note = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in this run over a 3-step run of this "
-                            "training step (bench.py --steps 3); 2*FETCH+WRITE (KB->B) per dispatch, summed over "
-                            "the hot path's kernels")
+                            "training step (bench.py --steps 3); per dispatch, summed over the hot path's kernels: "
+                            "2*FETCH+WRITE (KB->B), the x2 calibrated for the 4/8/16-B-per-lane reads these kernels "
+                            "issue (tools/fetch_calib.py, profiles/r04/fetch_calib.json); raw = FETCH+WRITE per "
+                            "kernel beside it")
             else:
                 pmc_note = err
             log(f"pmc traffic: {traffic} B/step ({pmc_note[:80]})")
@@ -428,6 +439,10 @@ def main():
                 "hbm": {"achieved_gbs": round(gbs, 2), "peak": HBM_PEAK_GBS, "frac": round(hbm_frac, 5)},
                 "valu": {"achieved_tflops": round(tfs, 3), "peak": F32_VALU_PEAK_TFLOPS, "frac": round(valu_frac, 5)},
                 "avg_ms_per_step": round(hot_ms, 5), "fwd_call_ms": round(fcall, 5), "bwd_call_ms": round(bcall, 5),
+                "timing": ("stand-alone: HIP events on the step's own tensors right after the timed replays "
+                           "(a captured step's kernels are not individually instrumented)" if timed_standalone
+                           else "in the timed steps: HIP events the library stamps on each call's first and last "
+                                "kernel, on the launch stream"),
                 "calls": kt.n_bwd_call, "traffic_source": pmc_note, "traffic_by_kernel": pmc_kernels,
                 "photo_bwd": {"avg_launch_ms": round(bwd_ms, 5), "launches": kt.n_bwd,
                               "share_of_hot_path": round(bwd_ms / hot_ms, 3) if hot_ms else None},

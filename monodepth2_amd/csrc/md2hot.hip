@@ -1036,14 +1036,14 @@ struct PendRow {
     int code;                 // argmin code of the coefficient row of the step (trainer.py:478)
 };
 
-// project window row k (depth from LDS) and issue its loads
+// project window row k at its depth (from LDS, read by the caller) and issue its loads
 template <bool U8>
-__device__ __forceinline__ void bwd_issue(const BwdFrame& F, int k, PendRow<U8>& pd, int lane) {
+__device__ __forceinline__ void bwd_issue(const BwdFrame& F, int k, float depth, PendRow<U8>& pd) {
     const int h = F.ctx.h, w = F.ctx.w, HW = h * w;
     const int r = F.r0 - 2 + k;
     const int rr = reflect_clamp(r, h);
     FastSample sm;
-    project_depth(F.ctx, rr, F.cc, F.dep[k][lane], sm);
+    project_depth(F.ctx, rr, F.cc, depth, sm);
     pd.tx = sm.tx;
     pd.ty = sm.ty;
     pd.px = sm.px;
@@ -1133,9 +1133,18 @@ __device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, PendRow<U8>& 
     const float l1w = SSIM_ON ? 0.15f : 1.0f;
     const int h = F.ctx.h, w = F.ctx.w;
     const int r = F.r0 - 2 + k;
+    const int q = r - 2;
+    // this step's LDS operands, read up front so their latency hides behind the row's
+    // interpolation and sums: the next row's depth (its projection), the output row's
+    // depth (its recomputed projection chain) and the frames' running dL/ddepth
+    const int kn = U8 ? min(k + 1, kSteps - 1) : k;
+    const float dep_next = F.dep[kn][lane];
+    const bool outrow = k >= 4 && F.colok && q < h;
+    const float dep_out = k >= 4 ? F.dep[k - 2][lane] : 0.f;
+    const float dd_old = (outrow && F.f != 0) ? ddacc[q - F.r0][lane] : 0.f;
     // the fp32-plane path (12 corner floats per row in flight) issues its own row here:
     // pipelined it would not fit the register file
-    if constexpr (!U8) bwd_issue<U8>(F, k, pd, lane);
+    if constexpr (!U8) bwd_issue<U8>(F, k, dep_next, pd);
     {
         Corners v;
         bwd_corners<U8>(pd, v);
@@ -1146,7 +1155,7 @@ __device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, PendRow<U8>& 
     if (SSIM_ON) cur.h = hsum3(cur.x, cur.y);
     const int code = pd.code;
     // the next row's loads (the last step re-issues its own row: same addresses, unused)
-    if constexpr (U8) bwd_issue<U8>(F, min(k + 1, kSteps - 1), pd, lane);
+    if constexpr (U8) bwd_issue<U8>(F, kn, dep_next, pd);
     if (k < 2) return;
     // coefficient row p = r - 1
     const int p = r - 1;
@@ -1166,18 +1175,18 @@ __device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, PendRow<U8>& 
     }
     cnew.g = gp;
     if (SSIM_ON) {
+        // gp == 0 (a pixel this frame does not win) zeroes dA, dB, dC through the clamp
+        // pass already (every factor is finite: d >= C1 C2 > 0)
         const float gS = gp * (0.85f / 3.f);
         C3 dA, dB, dC;
         ssim_adjoint3(m2.h, m1.h, cur.h, gS, dA, dB, dC);
-        if (gp == 0.f) dA = dB = dC = C3{f2v{0.f, 0.f}, 0.f};
         cnew.A = shfl_prev3(dA) * F.wl + dA + shfl_next3(dA) * F.wr;
         cnew.B = shfl_prev3(dB) * F.wl + dB + shfl_next3(dB) * F.wr;
         cnew.C = shfl_prev3(dC) * F.wl + dC + shfl_next3(dC) * F.wr;
     }
     if (k < 4) return;
     // output row q = r - 2 (coefficient rows q-1, q, q+1 = cm3, cm2, cnew)
-    const int q = r - 2;
-    if (!(F.colok && q < h)) return;
+    if (!outrow) return;
     const CarryP& k2 = m2.k;
     const float l1c = cm2.g * (l1w * kThird);
     C3 g = sign3(m2.x - m2.y) * l1c;
@@ -1195,7 +1204,7 @@ __device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, PendRow<U8>& 
     dc[2] = -(dpx * k2.px + dpy * k2.py) * k2.inv_den;
     // the sample's ray / camera point / dcam-ddepth, recomputed (output rows are inside
     // the image, so the sample row was q itself, unreflected)
-    const float depth = F.dep[k - 2][lane];
+    const float depth = dep_out;
     const float fx = (float)F.cc, fy = (float)q;
     float ray[3], pt[3];
 #pragma unroll
@@ -1215,8 +1224,7 @@ __device__ __forceinline__ void bwd_step(const BwdFrame& F, int k, PendRow<U8>& 
         u[i] = F.ctx.cm.P[i * 4 + 0] * ray[0] + F.ctx.cm.P[i * 4 + 1] * ray[1] + F.ctx.cm.P[i * 4 + 2] * ray[2];
     const float ddd = -F.ctx.range * depth * depth;
     const float dd = (dc[0] * u[0] + dc[1] * u[1] + dc[2] * u[2]) * ddd;
-    if (F.f == 0) ddacc[q - F.r0][lane] = dd;
-    else ddacc[q - F.r0][lane] += dd;
+    ddacc[q - F.r0][lane] = F.f == 0 ? dd : dd_old + dd;
 }
 
 template <int NS, bool SSIM_ON, bool MASK, bool U8>
@@ -1228,7 +1236,7 @@ __device__ __forceinline__ void bwd_frame_walk(const BwdFrame& F, float (*ddacc)
     CoefP C0, C1, C2;
     PendRow<U8> pd;
     constexpr int kSteps = kRowsB + 4;
-    if constexpr (U8) bwd_issue<U8>(F, 0, pd, lane);
+    if constexpr (U8) bwd_issue<U8>(F, 0, F.dep[0][lane], pd);
     int k = 0;
 #pragma unroll 1
     for (; k + 3 <= kSteps; k += 3) {
@@ -1379,6 +1387,7 @@ struct SmoothArgs {
     const float* disp[MD2_MAX_SCALES];
     const float* img[MD2_MAX_SCALES];   // target colour at the native scale
     float* part[MD2_MAX_SCALES];        // [B][chunks][3]
+    float* sgrad[MD2_MAX_SCALES];       // (B, hs, ws): the smoothness term's per-unit gradient
     int disp_bf16;
 };
 
@@ -1408,9 +1417,11 @@ __device__ __forceinline__ void block_sum3(float& a, float& b, float& c) {
 }
 
 __global__ __launch_bounds__(kBlock) void smooth_fwd_kernel(SmoothArgs a) {
+    // consecutive chunks share their boundary rows (p + ws): keep them on one XCD's L2
+    const int bid = xcd_contiguous_block(blockIdx.x, gridDim.x);
     int s = 0;
-    while (s + 1 < a.num_scales && (int)blockIdx.x >= a.block_base[s + 1]) ++s;
-    const int local = blockIdx.x - a.block_base[s];
+    while (s + 1 < a.num_scales && bid >= a.block_base[s + 1]) ++s;
+    const int local = bid - a.block_base[s];
     const int b = local / a.chunks[s], chunk = local - b * a.chunks[s];
     const int hs = a.hs[s], ws = a.ws[s], HW = hs * ws;
     const bool bf = a.disp_bf16 != 0;
@@ -1418,12 +1429,30 @@ __global__ __launch_bounds__(kBlock) void smooth_fwd_kernel(SmoothArgs a) {
     const float* img = a.img[s] + (size_t)b * 3 * HW;
     float sd = 0.f, sx = 0.f, sy = 0.f;
     const int p0 = chunk * kSmoothChunk;
+    // per-unit gradient of the smoothness sums (layers.py:202-215): the sign stencil of
+    // |d_p - d_q| e_pq over the pixel's four edges, with the x / y means' normalisers
+    // folded in.  The backward scales it by dL/dloss_s, the weight and 1/mean
+    // (disp_grad_kernel), so it never re-reads the target pyramid or the neighbours
+    float* sg = a.sgrad[s] + (size_t)b * HW;
+    const float cx = 1.0f / ((float)hs * (float)(ws - 1)), cy = 1.0f / ((float)(hs - 1) * (float)ws);
     for (int p = p0 + threadIdx.x; p < min(p0 + kSmoothChunk, HW); p += kBlock) {
         const int i = p / ws, j = p - i * ws;
         const float v = ldd(d, p, bf);
         sd += v;
-        if (j + 1 < ws) sx += fabsf(v - ldd(d, p + 1, bf)) * edge_weight(img, HW, p, p + 1);
-        if (i + 1 < hs) sy += fabsf(v - ldd(d, p + ws, bf)) * edge_weight(img, HW, p, p + ws);
+        float gx = 0.f, gy = 0.f;
+        if (j + 1 < ws) {
+            const float dv = v - ldd(d, p + 1, bf), e = edge_weight(img, HW, p, p + 1);
+            sx += fabsf(dv) * e;
+            gx += signf(dv) * e;
+        }
+        if (j > 0) gx -= signf(ldd(d, p - 1, bf) - v) * edge_weight(img, HW, p - 1, p);
+        if (i + 1 < hs) {
+            const float dv = v - ldd(d, p + ws, bf), e = edge_weight(img, HW, p, p + ws);
+            sy += fabsf(dv) * e;
+            gy += signf(dv) * e;
+        }
+        if (i > 0) gy -= signf(ldd(d, p - ws, bf) - v) * edge_weight(img, HW, p - ws, p);
+        sg[p] = gx * cx + gy * cy;
     }
     block_sum3(sd, sx, sy);
     if (threadIdx.x == 0) {
@@ -1551,8 +1580,7 @@ struct DispGradArgs {
     int bpr[MD2_MAX_SCALES];                      // blocks per native row
     const float* dfull[MD2_MAX_SCALES];           // upsh == 0: (B, lh, lw) dL/d(disp)
     const float* upart[MD2_MAX_SCALES];           // upsh > 0: per-item partial grids (bwd_item)
-    const float* disp[MD2_MAX_SCALES];            // (B, 1, hs, ws)
-    const float* img[MD2_MAX_SCALES];             // (B, 3, hs, ws) target colour at this scale
+    const float* sgrad[MD2_MAX_SCALES];           // (B, hs, ws) per-unit smoothness gradient (smooth_fwd)
     const float* stats;                           // [scale][B][4]
     const float* grad_loss;
     float smoothness;
@@ -1565,11 +1593,15 @@ struct DispGradArgs {
 // Upsampled scales: the sum of the <= 2 x 2 backward items' partials that reach this
 // pixel (row blocks, then strips, ascending: fixed order); plus the smoothness gradient.
 __global__ __launch_bounds__(kBlock) void disp_grad_kernel(DispGradArgs a) {
+    // a block reads the rows above and below its own (smoothness stencil, edge
+    // weights): consecutive rows on one XCD, so its L2 serves those re-reads (blocks are
+    // dealt round-robin over the 8 XCDs otherwise — every row fetched three times)
+    const int bid = xcd_contiguous_block(blockIdx.x, gridDim.x);
     int s = 0;
-    while (s + 1 < a.num_scales && (int)blockIdx.x >= a.block_base[s + 1]) ++s;
+    while (s + 1 < a.num_scales && bid >= a.block_base[s + 1]) ++s;
     const int sh = a.upsh[s];
     const int hs = a.hs[s], ws = a.ws[s], lh = a.lh[s], lw = a.lw[s], HWs = hs * ws;
-    const int rb = (int)blockIdx.x - a.block_base[s], bpr = a.bpr[s];
+    const int rb = bid - a.block_base[s], bpr = a.bpr[s];
     const int row = rb / bpr, chunk = rb - row * bpr;
     const int b = row / hs, i = row - b * hs;
     const int j = chunk * kBlock + threadIdx.x;
@@ -1600,7 +1632,9 @@ __global__ __launch_bounds__(kBlock) void disp_grad_kernel(DispGradArgs a) {
             }
         }
     }
-    // smoothness gradient on disp / (mean + 1e-7)
+    // smoothness gradient on disp / (mean + 1e-7): the forward's per-unit stencil
+    // gradient scaled by dL/dloss_s, the weight / 2^s, 1/B and 1/mean, plus the term
+    // through the mean (trainer.py:486-490)
     const float gl = a.grad_loss[s] + a.grad_loss[a.num_scales] / (float)a.num_scales;
     const float* st = a.stats + ((size_t)s * a.B + b) * 4;
     const float m = st[0];
@@ -1608,14 +1642,7 @@ __global__ __launch_bounds__(kBlock) void disp_grad_kernel(DispGradArgs a) {
     const float ax = wsm / ((float)a.B * hs * (ws - 1)) / m;
     const float ay = wsm / ((float)a.B * (hs - 1) * ws) / m;
     const bool bf = a.disp_bf16 != 0;
-    const float* d = disp_off(a.disp[s], (size_t)b * HWs, bf);
-    const float* img = a.img[s] + (size_t)b * 3 * HWs;
-    const float v = ldd(d, p, bf);
-    float sg = 0.f;
-    if (j + 1 < ws) sg += ax * signf(v - ldd(d, p + 1, bf)) * edge_weight(img, HWs, p, p + 1);
-    if (j > 0) sg -= ax * signf(ldd(d, p - 1, bf) - v) * edge_weight(img, HWs, p - 1, p);
-    if (i + 1 < hs) sg += ay * signf(v - ldd(d, p + ws, bf)) * edge_weight(img, HWs, p, p + ws);
-    if (i > 0) sg -= ay * signf(ldd(d, p - ws, bf) - v) * edge_weight(img, HWs, p - ws, p);
+    float sg = wsm / ((float)a.B * m) * a.sgrad[s][(size_t)b * HWs + p];
     sg -= (ax * st[1] + ay * st[2]) / (m * (float)HWs);
     // the gradient in the disparity's own dtype (bf16: round to nearest even, as the
     // cast-up's autograd backward would)
@@ -1786,6 +1813,7 @@ struct Layout {
     int chunks[MD2_MAX_SCALES];
     size_t ident_off, src8_off, exact_off;
     size_t photo_off[MD2_MAX_SCALES], dP_off[MD2_MAX_SCALES], smooth_off[MD2_MAX_SCALES];
+    size_t sgrad_off[MD2_MAX_SCALES];
     size_t dfull_off[MD2_MAX_SCALES], stats_off, total;
     size_t sel_off[MD2_MAX_SCALES], sel_total;
     size_t noise_off[MD2_MAX_SCALES];
@@ -1835,6 +1863,8 @@ int make_layout(const md2_desc* d, Layout& L) {
         off = align256(off + sizeof(float) * (size_t)L.S * L.B * L.bwpi[s] * 12);
         L.smooth_off[s] = off;
         off = align256(off + sizeof(float) * (size_t)L.B * L.chunks[s] * 3);
+        L.sgrad_off[s] = off;   // the smoothness gradient plane, forward -> backward
+        off = align256(off + sizeof(float) * (size_t)L.B * L.hs[s] * L.ws[s]);
         L.dfull_off[s] = off;   // upsampled scales: the backward items' partial grids instead
         const int upsh = L.v1 ? 0 : s;
         off = align256(off + sizeof(float) * (upsh == 0 ? (size_t)L.B * L.lh[s] * L.lw[s]
@@ -2089,6 +2119,7 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
         sa.disp[s] = t->disp[s];
         sa.img[s] = t->color[s][0];
         sa.part[s] = (float*)(ws + L.smooth_off[s]);
+        sa.sgrad[s] = (float*)(ws + L.sgrad_off[s]);
     }
     sa.block_base[L.nscales] = blocks;
     sa.disp_bf16 = d->disp_dtype == MD2_DTYPE_BF16;
@@ -2171,8 +2202,7 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
         g.upart[s] = (const float*)(ws + L.dfull_off[s]);
         g.strips[s] = L.bstrips[s];
         g.rowblocks[s] = L.brows[s];
-        g.disp[s] = t->disp[s];
-        g.img[s] = t->color[s][0];
+        g.sgrad[s] = (const float*)(ws + L.sgrad_off[s]);
         g.out[s] = grad_disp[s];
         g.block_base[s] = gblocks;
         g.bpr[s] = (L.ws[s] + kBlock - 1) / kBlock;

@@ -64,14 +64,14 @@ def depth_from_disp(disp, min_depth, max_depth):
 def cam_points(depth, inv_K):
     """layers.py:163-168: (B,1,h,w) depth -> (B,4,h*w) homogeneous points."""
     B, _, h, w = depth.shape
-    dev = depth.device
-    ys, xs = torch.meshgrid(torch.arange(h, dtype=torch.float32, device=dev),
-                            torch.arange(w, dtype=torch.float32, device=dev), indexing="ij")
-    pix = torch.stack([xs.reshape(-1), ys.reshape(-1), torch.ones(h * w, device=dev)], 0)
+    dev, dt = depth.device, depth.dtype   # fp32 as the reference; fp64 for the parity floor
+    ys, xs = torch.meshgrid(torch.arange(h, dtype=dt, device=dev),
+                            torch.arange(w, dtype=dt, device=dev), indexing="ij")
+    pix = torch.stack([xs.reshape(-1), ys.reshape(-1), torch.ones(h * w, dtype=dt, device=dev)], 0)
     pix = pix.unsqueeze(0).expand(B, 3, h * w)
     rays = torch.matmul(inv_K[:, :3, :3], pix)
     pts = depth.view(B, 1, -1) * rays
-    return torch.cat([pts, torch.ones(B, 1, h * w, device=dev)], 1)
+    return torch.cat([pts, torch.ones(B, 1, h * w, dtype=dt, device=dev)], 1)
 
 
 def project(points, K, T, h, w, eps=1e-7):

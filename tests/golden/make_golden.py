@@ -93,17 +93,22 @@ def import_reference(ref):
     return ref_trainer, ref_layers
 
 
-def run_case(ref_trainer, ref_layers, name, spec, seed=0):
+def run_case(ref_trainer, ref_layers, name, spec, seed=0, dtype=torch.float32, pin=None):
+    """dtype=torch.float64 runs the reference's methods in double precision on the same
+    (fp32-valued) inputs and noise; pin = [argmin (B,h,w) per scale] then replaces the
+    argmin of trainer.py:478 by the given one (the fp32 run's), so the fp64 gradients
+    follow the fp32 reference's routing: the exact-arithmetic anchor (--fp64)."""
     B, H, W, frame_ids, flags, pose_scale, keep_full = spec[:7]
     checksums_only = len(spec) > 7 and spec[7]
     scales = [0, 1, 2, 3]
     S = len(frame_ids) - 1
     inputs = synthetic_batch(B, H, W, frame_ids, 4, seed=seed, eight_bit=flags.get("eight_bit", False))
+    inputs = {k: (v.to(dtype) if torch.is_tensor(v) and v.is_floating_point() else v) for k, v in inputs.items()}
     hp = synthetic_hotpath(B, H, W, num_src=S, seed=seed, pose_scale=pose_scale)
-    disps = {s: hp["disps"][s].clone().requires_grad_(True) for s in scales}
+    disps = {s: hp["disps"][s].to(dtype).clone().requires_grad_(True) for s in scales}
     temporal = [f for f in frame_ids[1:] if f != "s"]
-    axis = hp["axisangle"][:len(temporal)].clone().requires_grad_(True)
-    trans = hp["translation"][:len(temporal)].clone().requires_grad_(True)
+    axis = hp["axisangle"][:len(temporal)].to(dtype).clone().requires_grad_(True)
+    trans = hp["translation"][:len(temporal)].to(dtype).clone().requires_grad_(True)
 
     opt = types.SimpleNamespace(
         scales=scales, frame_ids=list(frame_ids), height=H, width=W,
@@ -112,12 +117,12 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
         no_ssim=flags.get("no_ssim", False), avg_reprojection=flags.get("avg_reprojection", False),
         predictive_mask=flags.get("predictive_mask", False), disparity_smoothness=1e-3, batch_size=B)
     self = types.SimpleNamespace(opt=opt, device=torch.device("cpu"), num_scales=len(scales))
-    self.ssim = ref_layers.SSIM()
+    self.ssim = ref_layers.SSIM().to(dtype)
     self.backproject_depth, self.project_3d = {}, {}
     for s in scales:
         h, w = H // 2 ** s, W // 2 ** s
-        self.backproject_depth[s] = ref_layers.BackprojectDepth(B, h, w)
-        self.project_3d[s] = ref_layers.Project3D(B, h, w)
+        self.backproject_depth[s] = ref_layers.BackprojectDepth(B, h, w).to(dtype)
+        self.project_3d[s] = ref_layers.Project3D(B, h, w).to(dtype)
     self.compute_reprojection_loss = types.MethodType(
         ref_trainer.Trainer.compute_reprojection_loss, self)
 
@@ -130,6 +135,11 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
             h, w = H // 2 ** s, W // 2 ** s
             masks[s] = torch.sigmoid(torch.randn(B, S, h, w, generator=mgen)).requires_grad_(True)
         outputs["predictive_mask"] = {("disp", s): masks[s] for s in scales}
+    # the reference builds its pose matrices from torch.zeros() (layers.py:53, 93), i.e.
+    # in the default dtype: an fp64 run makes that the default from here on (the inputs
+    # above and the noise draws below are fp32 values either way)
+    real_default = torch.get_default_dtype()
+    torch.set_default_dtype(dtype)
     camT = {}
     for i, f in enumerate(temporal):
         T = ref_layers.transformation_from_parameters(axis[i], trans[i], invert=(f < 0))
@@ -143,9 +153,9 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
     real_randn = torch.randn
 
     def fake_randn(shape, device=None, **kw):
-        n = real_randn(*shape, generator=gen)
+        n = real_randn(*shape, generator=gen, dtype=torch.float32)
         drawn.append(n.clone())
-        return n
+        return n.to(dtype)
 
     # the per-pixel argmin of trainer.py:478 (torch.min(combined, dim=1)), recorded as the
     # reference computes it: the tests compare gradients away from pixels whose argmin
@@ -154,9 +164,14 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
     real_min = torch.min
 
     def recording_min(*a, **k):
-        r = real_min(*a, **k)
-        if k.get("dim") == 1 or (len(a) > 1 and a[1] == 1):
-            argmins.append(r[1].clone())
+        if not (k.get("dim") == 1 or (len(a) > 1 and a[1] == 1)):
+            return real_min(*a, **k)
+        if pin is not None:   # the given argmin; min's gradient routing through gather
+            idx = torch.from_numpy(pin[len(argmins)].astype(np.int64))
+            r = (a[0].gather(1, idx.unsqueeze(1)).squeeze(1), idx)
+        else:
+            r = real_min(*a, **k)
+        argmins.append(r[1].clone())
         return r
 
     ref_trainer.torch.randn = fake_randn
@@ -170,7 +185,10 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
         ref_trainer.torch.randn = real_randn
         ref_trainer.torch.min = real_min
         torch.Tensor.cuda = real_cuda
-    losses["loss"].backward()
+    try:
+        losses["loss"].backward()
+    finally:
+        torch.set_default_dtype(real_default)
 
     rec = {"B": B, "H": H, "W": W, "S": S, "seed": seed, "pose_scale": pose_scale,
            "frame_ids": np.array([str(f) for f in frame_ids]),
@@ -227,13 +245,43 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0):
     return rec
 
 
+# the full-size cases whose gradient parity is anchored on the fp64 floor
+FP64_CASES = ["full_mono_b2_192x640", "full_mono_b2_320x1024", "full_stereo_b2_192x640", "c2_mono_b12_192x640"]
+F64_KEYS = ("loss", "loss_", "grad_disp_sum_", "grad_disp_abs_", "grad_disp_sq_", "grad_disp_abs_img_",
+            "grad_axisangle", "grad_translation")
+
+
+def add_fp64(ref_trainer, ref_layers, name):
+    """Augment an existing fixture with the reference's own fp64 run (argmin pinned to
+    the fixture's fp32 argmin): scalars and gradient checksums under "f64_*" keys.
+    tests/test_oracle_golden.py pins the oracle's fp64 mode to them; the GPU floor test
+    then measures the HIP path and the fp32 oracle against that fp64 oracle."""
+    path = os.path.join(HERE, name + ".npz")
+    z = dict(np.load(path, allow_pickle=False))
+    spec = CASES[name]
+    spec64 = spec[:6] + (False, True)   # checksums only
+    pin = [z[f"argmin_{s}"] for s in range(4)]
+    rec = run_case(ref_trainer, ref_layers, name, spec64, seed=int(z["seed"]), dtype=torch.float64, pin=pin)
+    for k, v in rec.items():
+        if k.startswith(F64_KEYS) and not k.startswith("loss_shape"):
+            z["f64_" + k] = v
+    np.savez_compressed(path, **z)
+    print(f"{name}: fp64 loss={float(rec['loss']):.10f} (fp32 {float(z['loss']):.7f}) -> {os.path.relpath(path, REPO)}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--only", default=None)
+    ap.add_argument("--fp64", action="store_true", help="add the fp64 anchors to the full-size fixtures")
     args = ap.parse_args()
     torch.set_num_threads(8)
     ref_trainer, ref_layers = import_reference(args.ref)
+    if args.fp64:
+        for name in FP64_CASES:
+            if not args.only or name == args.only:
+                add_fp64(ref_trainer, ref_layers, name)
+        return
     for name, spec in CASES.items():
         if args.only and name != args.only:
             continue

@@ -70,12 +70,15 @@ def run_hip(case: Case, device="cuda"):
     return cfg, out
 
 
-def run_oracle(case: Case, selection=None, device="cpu"):
+def run_oracle(case: Case, selection=None, device="cpu", dtype=torch.float32):
     """The CPU oracle on the case's inputs; selection optionally pins the argmin.
 
     device="cuda" runs the same ATen formulation on PyTorch-ROCm (the reference's own
     ops on the GPU): a yardstick for how far two fp32 platforms of the reference
-    itself drift apart at bilinear cell boundaries, never a product path."""
+    itself drift apart at bilinear cell boundaries, never a product path.
+    dtype=torch.float64: the same formulation in double precision on the same fp32
+    input values — the exact-arithmetic anchor the fp32 implementations are measured
+    against (pinned to the reference's own fp64 run by make_golden.py --fp64)."""
     from oracle.md2_oracle import HotPathOptions, hot_path
     opt = HotPathOptions(height=case.H, width=case.W, frame_ids=case.frame_ids,
                          v1_multiscale="v1_multiscale" in case.flags, no_ssim="no_ssim" in case.flags,
@@ -83,12 +86,13 @@ def run_oracle(case: Case, selection=None, device="cpu"):
                          disable_automasking="disable_automasking" in case.flags,
                          predictive_mask="predictive_mask" in case.flags)
     dev = torch.device(device)
-    masks = ({s: m.to(dev).clone().requires_grad_(True) for s, m in case.masks.items()}
+    masks = ({s: m.to(dev, dtype).clone().requires_grad_(True) for s, m in case.masks.items()}
              if case.masks else None)
-    disps = {s: d.to(dev).clone().requires_grad_(True) for s, d in case.disps.items()}
-    axis = case.axisangle.to(dev).clone().requires_grad_(True)
-    trans = case.translation.to(dev).clone().requires_grad_(True)
-    inputs = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in case.inputs.items()}
+    disps = {s: d.to(dev, dtype).clone().requires_grad_(True) for s, d in case.disps.items()}
+    axis = case.axisangle.to(dev, dtype).clone().requires_grad_(True)
+    trans = case.translation.to(dev, dtype).clone().requires_grad_(True)
+    inputs = {k: (v.to(dev, dtype) if torch.is_tensor(v) and v.is_floating_point() else v)
+              for k, v in case.inputs.items()}
     camT = {}
     for i, f in enumerate(case.temporal):
         camT[f] = transformation_from_parameters(axis[i], trans[i], invert=(f < 0))
@@ -97,7 +101,7 @@ def run_oracle(case: Case, selection=None, device="cpu"):
     sel = None
     if selection is not None:
         sel = {s: torch.from_numpy(v).long().to(dev) for s, v in selection.items()}
-    noise = {s: n.to(dev) for s, n in case.noise.items()} if case.noise else None
+    noise = {s: n.to(dev, dtype) for s, n in case.noise.items()} if case.noise else None
     losses, outputs = hot_path(opt, disps, inputs, camT, noise=noise, selection=sel, masks=masks)
     losses["loss"].backward()
     res = {"loss": [float(losses[f"loss/{s}"]) for s in range(4)] + [float(losses["loss"])],

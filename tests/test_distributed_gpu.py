@@ -26,6 +26,10 @@ def _free_port():
 
 def _init(rank, world, port, backend):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # the local and the synced gradients come from two separate backward passes: the
+    # convolutions MIOpen keeps must not use atomics (run-to-run rounding differences
+    # would read as averaging errors); our own kernels are deterministic anyway
+    torch.backends.cudnn.deterministic = True
     if backend == "nccl":
         torch.cuda.set_device(rank)
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))

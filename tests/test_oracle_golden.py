@@ -92,3 +92,33 @@ def test_known_answers():
     assert float(ssim_map(x, x).max()) == 0.0
     d = torch.full((2, 1, 8, 6), 0.3)
     assert float(smooth_loss(d, x)) == 0.0
+
+
+def _fp64_cases():
+    return [n for n in case_names() if "f64_loss" in Case(n).z.files]
+
+
+@pytest.mark.parametrize("name", _fp64_cases())
+def test_oracle_fp64_matches_reference_fp64(name):
+    """The parity floor's anchor: the oracle in double precision (same fp32 input
+    values, argmin pinned to the reference's own fp32 argmin) reproduces the
+    reference's fp64 run of the same methods (make_golden.py --fp64) — losses,
+    gradient checksums per scale and per image, pose gradients — to ~1e-10.  The GPU
+    floor test (tests/test_parity_floor_gpu.py) measures the HIP path and the fp32
+    oracle against this anchor."""
+    from hotpath_case import run_oracle as run_pinned
+    torch.set_num_threads(8)
+    case = Case(name)
+    pin = {s: case.expected(f"argmin_{s}") for s in range(4)}
+    ref = run_pinned(case, selection=pin, dtype=torch.float64)
+    for s in range(4):
+        assert abs(ref["loss"][s] - float(case.expected(f"f64_loss_{s}"))) <= 1e-12, s
+    assert abs(ref["loss"][4] - float(case.expected("f64_loss"))) <= 1e-12
+    for s in range(4):
+        g = ref["grad_disp"][s].astype(np.float64)
+        for key, v in (("sum", g.sum()), ("abs", np.abs(g).sum()), ("sq", np.square(g).sum())):
+            want = float(case.expected(f"f64_grad_disp_{key}_{s}"))
+            assert abs(v - want) <= 1e-9 * max(abs(want), np.abs(g).sum() * 1e-3), (s, key, v, want)
+        np.testing.assert_allclose(np.abs(g).sum((1, 2, 3)), case.expected(f"f64_grad_disp_abs_img_{s}"), rtol=1e-9)
+    np.testing.assert_allclose(ref["grad_axis"], case.expected("f64_grad_axisangle"), rtol=1e-8, atol=1e-14)
+    np.testing.assert_allclose(ref["grad_trans"], case.expected("f64_grad_translation"), rtol=1e-8, atol=1e-14)

@@ -1,0 +1,90 @@
+"""Full-size gradient parity anchored on the fp32 floor.
+
+At 640x192 and 1024x320 the per-pixel gradient of the reference's own fp32
+formulation is ill-conditioned: a few sample coordinates per image land within fp32
+rounding of a bilinear cell boundary, where dL/dgrid jumps, and every coarse pixel
+aggregating one inherits the jump.  How large that is for the REFERENCE itself is
+measured here, not assumed: the oracle (the reference's ATen formulation, pinned to
+the reference by tests/test_oracle_golden.py) runs once in fp32 and once in fp64 on
+the same fp32 input values, both with the argmin pinned to the reference's own
+recorded fp32 argmin (trainer.py:478), and the fp64 run is the anchor — itself pinned
+to the reference's own fp64 run (make_golden.py --fp64,
+test_oracle_fp64_matches_reference_fp64).
+
+The bar: per scale, the HIP path's distance to the fp64 anchor is at most
+K_FLOOR = 3 times the fp32 floor, untrimmed and with the largest 0.1 % of differences
+left out (pixels whose HIP argmin differs from the reference's — fp32 near-ties — are
+excluded from every side, with their SSIM / upsample footprint).  The fp32 floor is
+the reference formulation's own distance to the anchor on the two fp32 platforms at
+hand, the host CPU and PyTorch-ROCm on this GPU (the larger of the two: at a coarse
+scale a single cell flip dominates the untrimmed norm, and which platform hits one is
+chance — full_stereo scale 3 measured 1.4e-3 on the CPU, 6.1e-3 with ATen on the GPU).
+Nothing in the bar is calibrated on the HIP path.  tools/parity_floor.py writes the
+same numbers to profiles/r04/parity_floor.json.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import Case, case_names
+from hotpath_case import run_hip, run_oracle
+from test_hotpath_gpu import FLIP_FRAC, flip_footprint, rel_l2, trimmed_rel_l2
+
+pytestmark = pytest.mark.gpu
+
+K_FLOOR = 3.0
+
+
+def fp64_cases():
+    return [n for n in case_names() if "f64_loss" in Case(n).z.files]
+
+
+def in_tol(g, r):
+    return float((np.abs(g - r) <= 1e-4 * np.abs(r).max() + 1e-3 * np.abs(r)).mean())
+
+
+def floor_metrics(case, hip_out, runs, r64):
+    """per scale, outside the HIP-vs-reference argmin flips' footprint: the distance to
+    the fp64 anchor (rel_l2, trimmed_rel_l2, fraction within 1e-4 max + 1e-3 |ref|) of
+    the HIP path and of every fp32 run of the reference formulation in `runs`"""
+    rows = []
+    for s in range(4):
+        flips = hip_out["select"][s] != case.expected(f"argmin_{s}")
+        keep = ~flip_footprint(flips, s)
+        r = r64["grad_disp"][s][keep]
+        row = {"scale": s, "flips": int(flips.sum()), "kept_px": int(keep.sum())}
+        for k, g in [("hip", hip_out["grad_disp"][s])] + [(k, v["grad_disp"][s]) for k, v in runs.items()]:
+            row[f"{k}_f64"] = rel_l2(g[keep], r)
+            row[f"{k}_f64_trim"] = trimmed_rel_l2(g[keep], r)
+            row[f"{k}_f64_in_tol"] = in_tol(g[keep], r)
+        row["floor"] = max(row[f"{k}_f64"] for k in runs)
+        row["floor_trim"] = max(row[f"{k}_f64_trim"] for k in runs)
+        rows.append(row)
+    return rows
+
+
+def floor_runs(case):
+    """the fp64 anchor and the reference formulation's fp32 runs (host CPU, ATen on the
+    GPU), all with the argmin pinned to the reference's own"""
+    pin = {s: case.expected(f"argmin_{s}") for s in range(4)}
+    r64 = run_oracle(case, selection=pin, dtype=torch.float64)
+    runs = {"cpu32": run_oracle(case, selection=pin), "aten": run_oracle(case, selection=pin, device="cuda")}
+    return r64, runs
+
+
+@pytest.mark.parametrize("name", fp64_cases())
+def test_hip_gradients_within_fp32_floor(name):
+    torch.set_num_threads(16)
+    case = Case(name)
+    _, out = run_hip(case)
+    r64, runs = floor_runs(case)
+    for s in range(5):   # fp32 losses against the exact ones (north_star: < 1e-4)
+        assert abs(out["loss"][s] - r64["loss"][s]) <= 2e-6, (s, out["loss"][s], r64["loss"][s])
+    for s, m in enumerate(floor_metrics(case, out, runs, r64)):
+        assert m["flips"] <= max(3, FLIP_FRAC * out["select"][s].size), (s, m)
+        assert m["hip_f64"] <= K_FLOOR * m["floor"], (s, m)
+        assert m["hip_f64_trim"] <= K_FLOOR * m["floor_trim"], (s, m)
+    for key in ("grad_axis", "grad_trans"):
+        e_hip = rel_l2(out[key], r64[key])
+        floor = max(rel_l2(v[key], r64[key]) for v in runs.values())
+        assert e_hip <= K_FLOOR * floor, (key, e_hip, floor)
