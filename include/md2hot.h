@@ -494,6 +494,8 @@ int md2_maxpool3s2_bwd_add(const md2_pool_desc* desc, const uint32_t* idx, const
                                         once for the nine taps (conv_x6pw_kernel)           */
 #define MD2_CONV_S2_ONE    (1u << 9) /* x6 stride-2 input gradient: the four parity classes
                                         in one launch, no K split                           */
+#define MD2_CONV_WS        (1u << 10) /* x6 forward / stride-1 input gradient, 128-wide tiles: the
+                                         warp-specialised kernel (4 MFMA + 4 staging waves) */
 
 typedef struct md2_conv_desc {
     int32_t batch, height, width, in_channels; /* input */

@@ -117,6 +117,7 @@ CONV_BM256 = 1 << 6
 CONV_PRESPLIT = 1 << 7
 CONV_PATCH = 1 << 8
 CONV_S2_ONE = 1 << 9
+CONV_WS = 1 << 10
 
 
 class ConvDesc(ctypes.Structure):

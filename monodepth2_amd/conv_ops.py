@@ -50,21 +50,30 @@ PRESPLIT = _lib.CONV_PRESPLIT
 PATCH = _lib.CONV_PATCH
 S2_ONE = _lib.CONV_S2_ONE
 NO_SPLIT = _lib.CONV_NO_SPLIT
+WS = _lib.CONV_WS
 # the x6 candidates, in candidate order: 128 / 256-row tiles, each with the planner's K
 # split and without one (the split's partials round trip is timed, not modelled)
 _FLAGS = (X6, X6 | BM256, X6 | NO_SPLIT, X6 | BM256 | NO_SPLIT)
 _PFLAGS = (X6 | PATCH, X6 | PATCH | BM256, X6 | PATCH | NO_SPLIT, X6 | PATCH | BM256 | NO_SPLIT)
 _NAMES_X6 = ("x6", "x6_256", "x6_ns", "x6_256_ns")
 _NAMES_X6P = ("x6p", "x6p_256", "x6p_ns", "x6p_256_ns")
+# the warp-specialised per-tap kernel (4 MFMA + 4 staging waves, 128-wide tiles)
+_WFLAGS = (X6 | WS, X6 | WS | BM256)
+_NAMES_WS = ("x6ws", "x6ws_256")
 
 
 def _x6_flags(gemm_c: int, k: int, stride: int, n_out: int):
     """The x6 flag variants for a forward / stride-1 input gradient whose GEMM reads
     gemm_c channels, and their candidate names: the patch kernel needs 3x3, stride 1,
-    gemm_c % 32 == 0 and more than 16 GEMM columns (csrc/conv.hip use_x6p)."""
+    gemm_c % 32 == 0 and more than 16 GEMM columns (csrc/conv.hip use_x6p); the
+    warp-specialised one a 128-wide tile (more than 64 columns) and whole 32-channel
+    chunks (csrc/conv.hip launch_x6)."""
+    flags, names = _FLAGS, _NAMES_X6
+    if n_out > 64 and gemm_c >= 32:
+        flags, names = flags + _WFLAGS, names + _NAMES_WS
     if k == 3 and stride == 1 and gemm_c % 32 == 0 and n_out > 16:
-        return _FLAGS + _PFLAGS, _NAMES_X6 + _NAMES_X6P
-    return _FLAGS, _NAMES_X6
+        return flags + _PFLAGS, names + _NAMES_X6P
+    return flags, names
 
 
 def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:

@@ -815,6 +815,192 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
     }
 }
 
+// Warp-specialised split-bf16 GEMM for the forward / stride-1 input gradient with a
+// 128-wide tile (MD2_CONV_WS): the 8-wave block is 4 MFMA waves and 4 staging waves,
+// one of each per SIMD (waves are dealt to the SIMDs round-robin: wave w and w + 4 share
+// SIMD w).  conv_x6_kernel's 8 waves all stage and all multiply, in lockstep between
+// two barriers per chunk pair, so a SIMD's split VALU, LDS stores and address math sit
+// between its own MFMAs (its MFMA pipe measured 0.19-0.21 busy on the 12x40 / 6x20
+// layers).  Here the MFMA wave of a SIMD only reads fragments and multiplies while the
+// staging wave beside it fetches chunk t+2, splits and stores chunk t+1 and DMAs its
+// weights — on the VALU, LDS and memory pipes, beside the matrix pipe.  One barrier per
+// chunk hands the double-buffered LDS over.  MFMA wave tile (BMX/2) x 64: per 16 k,
+// BMX/64 + 2 fragment triples for 6 (BMX/32) MFMAs (0.375 reads per MFMA at BMX = 256
+// instead of 0.625).  Same operands, same products in the same order per output as
+// conv_x6_kernel: bitwise equal results (tests/test_conv_gpu.py).
+template <int BMX>
+__global__ __launch_bounds__(512, 1) void conv_x6ws_kernel(ConvArgs a) {
+    constexpr int BN = 128, NP = 256;              // tile width, staging threads
+    constexpr int TMc = BMX / 64, TNc = 2;         // MFMA row / column blocks per MFMA wave
+    constexpr int AQ = BMX * XBK / 4 / NP;         // f32 quads of A per staging thread
+    constexpr int PIECES = 3 * BN / 16, BQ = PIECES / 4;   // B: 1 KiB DMA pieces per chunk / per staging wave
+    constexpr int PA = BMX * XBK, PB = BN * XBK;
+    static_assert(AQ * NP * 4 == BMX * XBK && BQ * 4 == PIECES, "staging must tile the chunk");
+    __shared__ __bf16 lds[2][3 * (PA + PB)];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool mfma_wave = wid < 4;   // wave-uniform: scalar branches between the roles
+    int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int nb = blk % a.nblocks;
+    blk /= a.nblocks;
+    const int mb = blk % a.mblocks, ks = blk / a.mblocks;
+    const int m0 = mb * BMX, n0 = nb * BN;
+    const int t0 = ks * a.chunks_per_split;
+    const int nchunks = min(a.chunks_per_split, a.nchunks - t0);
+    const int KT = a.KH * a.KW;
+    const int cchunks = (a.C + XBK - 1) / XBK;
+
+    // ---- staging waves: A rows ra + 32 j, f32 quad qa; B pieces sw + 4 j ----
+    const int st = tid - 256, sw = wid - 4;
+    const int qa = st & 7, ra = st >> 3;
+    int aih[AQ], aiw[AQ], apb[AQ];
+    int bsrc[BQ], bk8[BQ], bdst[BQ];
+    const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * 2, 0x00020000);
+    if (!mfma_wave) {
+#pragma unroll
+        for (int j = 0; j < AQ; ++j) {
+            const int m = m0 + ra + (NP / 8) * j;
+            if (m < a.M) {
+                const int b = m / (a.Ho * a.Wo), rem = m - b * a.Ho * a.Wo;
+                const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+                aih[j] = oh * a.stride - a.pad;
+                aiw[j] = ow * a.stride - a.pad;
+                apb[j] = ((b * a.H + aih[j]) * a.W + aiw[j]) * a.C + 4 * qa;
+            } else {
+                aih[j] = -(1 << 20);
+                aiw[j] = 0;
+                apb[j] = 0;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < BQ; ++j) {
+            const int piece = sw + 4 * j, pl = piece / (BN / 16), rb = piece - pl * (BN / 16);
+            const int r = rb * 16 + (lane >> 2), q = ((lane & 3) ^ (r >> 2)) & 3;
+            const int n = n0 + r;
+            bk8[j] = 8 * q;
+            bsrc[j] = n < a.N ? ((pl * a.N + n) * KT) * a.C + 8 * q : -1;
+            bdst[j] = (3 * PA + pl * PB + rb * 16 * XBK) * 2;
+        }
+    }
+    float4 RA[AQ];
+    auto load = [&](int t) {
+        const int tt = t0 + t;
+        const int tap = tt / cchunks, c0 = (tt - tap * cchunks) * XBK;
+        const int kh = tap / a.KW, kw = tap - kh * a.KW;
+        const int off = (kh * a.W + kw) * a.C + c0;
+        const bool cok = t < nchunks && c0 + 4 * qa < a.C;
+#pragma unroll
+        for (int j = 0; j < AQ; ++j) {
+            const bool ok = cok && (unsigned)(aih[j] + kh) < (unsigned)a.H && (unsigned)(aiw[j] + kw) < (unsigned)a.W;
+            RA[j] = bload(ar, ok ? (apb[j] + off) * 4 : kBad);
+        }
+    };
+    auto dma = [&](int t, int buf) {   // every staging wave issues BQ pieces (zeros past the last chunk)
+        const int tt = t0 + t;
+        const int tap = tt / cchunks, c0 = (tt - tap * cchunks) * XBK;
+        const int kofs = tap * a.C + c0, klim = tap * a.C + a.C;
+        char* base = (char*)lds[buf];
+#pragma unroll
+        for (int j = 0; j < BQ; ++j) {
+            const bool ok = t < nchunks && bsrc[j] >= 0 && kofs + bk8[j] < klim;
+            dma16(br, base + bdst[j], ok ? (bsrc[j] + kofs) * 2 : kBad);
+        }
+    };
+    auto split_store = [&](int buf) {
+        __bf16* L = lds[buf];
+#pragma unroll
+        for (int j = 0; j < AQ; ++j) {
+            bf16x4 p0, p1, p2;
+            split3(RA[j], p0, p1, p2);
+            const int e = xidx(ra + (NP / 8) * j, 4 * qa);
+            *(bf16x4*)(L + e) = p0;
+            *(bf16x4*)(L + PA + e) = p1;
+            *(bf16x4*)(L + 2 * PA + e) = p2;
+        }
+    };
+
+    // ---- MFMA waves: 2 x 2, wave tile (BMX/2) x 64 ----
+    const int wm = wid >> 1, wn = wid & 1;
+    const int lr = lane & 31, h = lane >> 5;
+    f32x16 acc[TMc][TNc];
+#pragma unroll
+    for (int i = 0; i < TMc; ++i)
+#pragma unroll
+        for (int jn = 0; jn < TNc; ++jn)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
+    auto mma = [&](int buf) {
+        const __bf16* L = lds[buf];
+#pragma unroll
+        for (int s2 = 0; s2 < XBK / 16; ++s2) {
+            bf16x8 fb[TNc][3];
+#pragma unroll
+            for (int jn = 0; jn < TNc; ++jn) {
+                const int eb = xidx(wn * 64 + 32 * jn + lr, 16 * s2 + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fb[jn][pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
+            }
+#pragma unroll
+            for (int i = 0; i < TMc; ++i) {
+                bf16x8 fa[3];
+                const int e = xidx(wm * (BMX / 2) + 32 * i + lr, 16 * s2 + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(L + pl * PA + e);
+#pragma unroll
+                for (int jn = 0; jn < TNc; ++jn) {
+                    // small terms first: x2y0, x1y1, x0y2, x1y0, x0y1, x0y0 (conv_x6_kernel's order)
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[jn][0], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[jn][1], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[jn][2], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[jn][0], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[jn][1], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[jn][0], acc[i][jn], 0, 0, 0);
+                }
+            }
+        }
+    };
+
+    // prologue: chunk 0 staged, chunk 1's A in registers
+    if (!mfma_wave) {
+        load(0);
+        dma(0, 0);
+        wait_vm<BQ>();   // A(0) landed (the DMA pieces were issued after it)
+        split_store(0);
+        load(1);
+        wait_vm<AQ>();   // DMA(0) landed
+    }
+    lds_sync();
+    for (int t = 0; t < nchunks; ++t) {
+        if (mfma_wave) {
+            mma(t & 1);
+        } else if (t + 1 < nchunks) {
+            // the other buffer was released by the last barrier: chunk t+1 into it
+            dma(t + 1, (t + 1) & 1);
+            wait_vm<BQ>();   // A(t+1), loaded during the previous chunk
+            split_store((t + 1) & 1);
+            load(t + 2);
+            wait_vm<AQ>();   // DMA(t+1)
+        }
+        lds_sync();
+    }
+    if (!mfma_wave) return;
+
+    float* out = a.y + (size_t)ks * a.M * a.N;
+#pragma unroll
+    for (int jn = 0; jn < TNc; ++jn) {
+        const int n = n0 + wn * 64 + 32 * jn + lr;
+        if (n >= a.N) continue;
+#pragma unroll
+        for (int i = 0; i < TMc; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int m = m0 + wm * (BMX / 2) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (m < a.M) out[(size_t)m * a.N + n] = acc[i][jn][e];
+            }
+    }
+}
+
 // Patch layout of the 16-column tiles (TC = 16): patch pixel pix = (pr, pc) at LDS row
 // pix, k-octet slot kq ^ (pr & 1) ^ (pc >> 2 & 1) << 1.  A 32-lane fragment there spans
 // two output rows (16 + 16 pixels, patch pitch 18), so a ds_read_b128 lane group reads
@@ -1729,8 +1915,13 @@ void flat_k(ConvArgs& a, int mode) {
     }
 }
 
-void launch_x6(const ConvArgs& a, hipStream_t st) {
+void launch_x6(const ConvArgs& a, hipStream_t st, bool ws = false) {
     const dim3 grid(a.mblocks * a.nblocks * a.splits);
+    if (ws && a.bn == 128 && !a.flatk && !a.par) {   // warp-specialised (MD2_CONV_WS)
+        if (a.bm == 256) hipLaunchKernelGGL((conv_x6ws_kernel<256>), grid, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv_x6ws_kernel<128>), grid, dim3(512), 0, st, a);
+        return;
+    }
     if (a.bm == 256) hipLaunchKernelGGL((conv_x6_kernel<128, 256>), grid, dim3(X6Geo<128, 256>::NT), 0, st, a);
     else if (a.bn == 128) hipLaunchKernelGGL((conv_x6_kernel<128, 128>), grid, dim3(X6Geo<128, 128>::NT), 0, st, a);
     else if (a.bn == 64) hipLaunchKernelGGL((conv_x6_kernel<64, 128>), grid, dim3(X6Geo<64, 128>::NT), 0, st, a);
@@ -2014,7 +2205,7 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
             hipLaunchKernelGGL(conv_wsplit_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, B, planes,
                                d->out_channels, d->kernel_h * d->kernel_w, d->in_channels, mode == MODE_DGRAD ? 1 : 0);
         if (patch) launch_x6p(a, st);
-        else launch_x6(a, st);
+        else launch_x6(a, st, (d->flags & MD2_CONV_WS) != 0);
     } else if (mode == MODE_FWD) launch<MODE_FWD>(a, BN, st);
     else if (mode == MODE_DGRAD) launch<MODE_DGRAD>(a, BN, st);
     else launch<MODE_WGRAD>(a, BN, st);

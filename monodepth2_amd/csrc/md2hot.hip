@@ -530,6 +530,9 @@ struct PhotoArgs {
     // anyway) when non-null: [S][B][h*w] RGBx, and clears [S][B] flags (preset to 1)
     uint32_t* pack8;
     int* pack_exact;
+    // the identity losses are computed inside photo_fwdall_kernel, by the four scale
+    // waves of a block (one item) together, into LDS: no photo_ident_kernel, no planes
+    int ident_fused;
 };
 
 __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int b, WarpCtx& c) {
@@ -752,9 +755,30 @@ __device__ __forceinline__ void frowp_losses(const FRowP<NS>& A, const FRowP<NS>
     }
 }
 
-template <int NS, bool SSIM_ON, bool MASK, bool U8>
+// identity losses (trainer.py:432-439) of source frame f for the item's output rows
+// [i0, i1) into LDS rows dst[i] (the photo_ident_kernel walk, rows rotated by copies)
+template <bool SSIM_ON>
+__device__ __forceinline__ void ident_rows_lds(const PhotoArgs& a, int f, const FItem& it, int i0, int i1,
+                                               float (*dst)[kWave], int lane) {
+    const int h = a.h, w = a.w, HW = h * w;
+    const float* src = a.src[f] + (size_t)it.b * 3 * HW;
+    const float* tgt = a.tgt + (size_t)it.b * 3 * HW;
+    IRow A, Bq, C;
+    irow_eval<SSIM_ON>(src, tgt, HW, reflect_clamp(it.r0 + i0 - 1, h) * w + it.cc, A);
+    irow_eval<SSIM_ON>(src, tgt, HW, reflect_clamp(it.r0 + i0, h) * w + it.cc, Bq);
+#pragma unroll 1
+    for (int i = i0; i < i1; ++i) {
+        irow_eval<SSIM_ON>(src, tgt, HW, reflect_clamp(it.r0 + i + 1, h) * w + it.cc, C);
+        dst[i][lane] = irow_loss<SSIM_ON>(A, Bq, C);
+        A = Bq;
+        Bq = C;
+    }
+}
+
+template <int NS, bool SSIM_ON, bool MASK, bool U8, bool IDL>
 __device__ __forceinline__ float fwdall_walk(const PhotoArgs& a, const WarpCtx (&ctx)[NS], const FItem& it, int ls,
-                                             const float (*dep)[kWave], int lane) {
+                                             const float (*dep)[kWave], const float (*idl)[kRowsP][kWave],
+                                             int lane) {
     const int h = a.h, w = a.w, HW = h * w;
     const bool automask = !(a.flags & MD2_NO_AUTOMASK);
     const bool avg = (a.flags & MD2_AVG_REPROJECTION) != 0;
@@ -790,7 +814,8 @@ __device__ __forceinline__ float fwdall_walk(const PhotoArgs& a, const WarpCtx (
             }
             float id[NS];
 #pragma unroll
-            for (int f = 0; f < NS; ++f) id[f] = a.ident[((size_t)f * a.B + it.b) * HW + p];
+            for (int f = 0; f < NS; ++f)
+                id[f] = IDL ? idl[f][i][lane] : a.ident[((size_t)f * a.B + it.b) * HW + p];
             for (int ch = 0; ch < C; ++ch) {
                 float v;
                 if (avg) {
@@ -848,20 +873,22 @@ __device__ __forceinline__ float fwdall_walk(const PhotoArgs& a, const WarpCtx (
     return lsum;
 }
 
-template <int NS, bool SSIM_ON, bool MASK>
-// MD2_FWD_MINB: waves per SIMD the forward walk is compiled for (default: the
-// compiler's choice, 157 VGPRs = 3 waves; 4 spills 88 B/lane) — an A/B knob
-#ifdef MD2_FWD_MINB
-__global__ __launch_bounds__(kBlock, MD2_FWD_MINB) void photo_fwdall_kernel(PhotoArgs a) {
-#else
-__global__ __launch_bounds__(kBlock) void photo_fwdall_kernel(PhotoArgs a) {
+// MD2_FWD_MINB: blocks per CU (= waves per SIMD) the forward walk is compiled for.
+// Round 4: 4 — with the identity losses read from LDS the compiler's own choice is 152
+// VGPRs (3 waves); at 4 it keeps 128 and spills ~21 dwords outside the row loop's hot
+// path: fused forward 0.1245 vs 0.128 ms (profiles/r04/ab_fused_forward.log)
+#ifndef MD2_FWD_MINB
+#define MD2_FWD_MINB 4
 #endif
+template <int NS, bool SSIM_ON, bool MASK>
+__global__ __launch_bounds__(kBlock, MD2_FWD_MINB) void photo_fwdall_kernel(PhotoArgs a) {
     __shared__ float dep_s[kWavesPerBlock][kRowsP + 2][kWave];
+    __shared__ float idl_s[NS][kRowsP][kWave];   // ident_fused: the item's identity losses
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
     float (*dep)[kWave] = dep_s[wid];
     const int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
     const int wv = __builtin_amdgcn_readfirstlane(blk * kWavesPerBlock + wid);
-    if (wv >= a.B * a.wpi * a.nsc) return;
+    if (wv >= a.B * a.wpi * a.nsc) return;   // never with ident_fused (exact grid: no barrier skipped)
     const int ls = wv % a.nsc;   // scale fastest: the waves sharing a strip's rows run together
     const int item = wv / a.nsc;
     const FItem it = fitem(a, item, lane);
@@ -874,9 +901,28 @@ __global__ __launch_bounds__(kBlock) void photo_fwdall_kernel(PhotoArgs a) {
     }
 #pragma unroll
     for (int k = 0; k < kRowsP + 2; ++k) dep[k][lane] = depth_at(ctx[0], reflect_clamp(it.r0 - 1 + k, a.h), it.cc);
+    const float (*idl)[kRowsP][kWave] = nullptr;
+    if (a.ident_fused) {
+        // the four waves of the block are the four scales of ONE item (nsc == 4): the
+        // identity losses, scale-invariant, are computed once for all of them — the
+        // tasks (frame, upper / lower half of the item's rows) spread over the waves
+        constexpr int kMid = (kRowsP + 1) / 2;
+        const int rows = min(kRowsP, a.h - it.r0);
+        for (int task = wid; task < 2 * NS; task += kWavesPerBlock) {
+            const int f = task >> 1, i0 = (task & 1) ? kMid : 0, i1 = (task & 1) ? rows : min(kMid, rows);
+            if (i0 < i1) ident_rows_lds<SSIM_ON>(a, f, it, i0, i1, idl_s[f], lane);
+        }
+        __syncthreads();
+        idl = idl_s;
+    }
     // every frame's sources 8-bit exact (wave-uniform), else all frames on the fp32 planes
-    const float lsum = u8 ? fwdall_walk<NS, SSIM_ON, MASK, true>(a, ctx, it, ls, dep, lane)
-                          : fwdall_walk<NS, SSIM_ON, MASK, false>(a, ctx, it, ls, dep, lane);
+    float lsum;
+    if (idl)
+        lsum = u8 ? fwdall_walk<NS, SSIM_ON, MASK, true, true>(a, ctx, it, ls, dep, idl, lane)
+                  : fwdall_walk<NS, SSIM_ON, MASK, false, true>(a, ctx, it, ls, dep, idl, lane);
+    else
+        lsum = u8 ? fwdall_walk<NS, SSIM_ON, MASK, true, false>(a, ctx, it, ls, dep, idl, lane)
+                  : fwdall_walk<NS, SSIM_ON, MASK, false, false>(a, ctx, it, ls, dep, idl, lane);
     const float t = wave_sum(lsum);
     if (lane == 0) a.photo_part[ls][item] = t;
 }
@@ -1968,14 +2014,14 @@ void photo_args(const md2_desc* d, const md2_tensors* t, const Layout& L, int s_
 template <int NS, bool SSIM, bool MASK>
 void launch_fwd_t(const PhotoArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
     // the timing events bracket the three launches (start on the first, stop on the last)
-    const bool automask = !(a.flags & MD2_NO_AUTOMASK);
-    if (automask) {
+    const bool ident_kernel = !(a.flags & MD2_NO_AUTOMASK) && !a.ident_fused;
+    if (ident_kernel) {
         const int blocks = (a.B * a.wpi * NS + kWavesPerBlock - 1) / kWavesPerBlock;
         hipExtLaunchKernelGGL((photo_ident_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, e0, nullptr, 0, a);
     }
     const int rblocks = (a.B * a.wpi * a.nsc + kWavesPerBlock - 1) / kWavesPerBlock;
     hipExtLaunchKernelGGL((photo_fwdall_kernel<NS, SSIM, MASK>), dim3(rblocks), dim3(kBlock), 0, st,
-                          automask ? nullptr : e0, e1, 0, a);
+                          ident_kernel ? nullptr : e0, e1, 0, a);
 }
 // number of workgroups that can be resident at once for a kernel (cached per
 // kernel and device); the persistent-loop kernels launch exactly that many
@@ -2092,8 +2138,12 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
         hipEvent_t e0, e1;
         timing_slot(0, &e0, &e1);
         photo_args(d, t, L, 0, L.nscales, false, ws, select_out, a);
-        if (!(d->flags & MD2_NO_AUTOMASK)) {
-            // the identity pass reads every source pixel: it writes the 8-bit copies too
+        // four scales: the forward walk's blocks are (item, 4 scales) and compute the
+        // identity losses themselves (no identity planes: round 4, -24 MB of traffic
+        // and one launch per step); otherwise the identity pass writes them, and the
+        // 8-bit copies too (it reads every source pixel anyway)
+        a.ident_fused = (L.nscales == kWavesPerBlock && !(d->flags & MD2_NO_AUTOMASK)) ? 1 : 0;
+        if (!(d->flags & MD2_NO_AUTOMASK) && !a.ident_fused) {
             a.pack8 = pk.out;
             a.pack_exact = pk.exact;
             if (c0 && hipEventRecord(c0, st) != hipSuccess) return fail(MD2_ERR_HIP, "hipEventRecord failed");

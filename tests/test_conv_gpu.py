@@ -169,7 +169,8 @@ def test_conv_abi_dgrad_wgrad(B, C, N, k, s, p, H, W):
 # the one-launch stride-2 input gradient (inert at stride 1)
 XFLAGS = (conv_ops.X6, conv_ops.X6 | conv_ops.BM256, conv_ops.X6 | conv_ops.PATCH,
           conv_ops.X6 | conv_ops.PATCH | conv_ops.BM256, conv_ops.X6 | conv_ops.S2_ONE,
-          conv_ops.X6 | conv_ops.S2_ONE | conv_ops.BM256)
+          conv_ops.X6 | conv_ops.S2_ONE | conv_ops.BM256, conv_ops.X6 | conv_ops.WS,
+          conv_ops.X6 | conv_ops.WS | conv_ops.BM256)
 
 
 # + the decoder's narrow layers: 16 output channels take the 16x16x32 MFMA tile (its own
@@ -208,6 +209,25 @@ def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
                                                (False, True, False))[1].double().cpu()
     e_x6, e_mi = _rel(w_x6, wref), _rel(w_mi, wref)
     assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, ("wgrad", e_x6, e_mi)
+
+
+@pytest.mark.parametrize("B,C,N,k,s,p,H,W", [(2, 64, 128, 3, 1, 1, 24, 40), (3, 128, 128, 3, 1, 1, 12, 20),
+                                             (2, 256, 256, 3, 1, 1, 6, 10), (2, 512, 512, 3, 1, 1, 3, 5),
+                                             (2, 64, 128, 3, 2, 1, 23, 39), (2, 64, 128, 1, 2, 0, 24, 40),
+                                             (1, 96, 136, 3, 1, 1, 7, 9), (2, 512, 256, 3, 1, 1, 6, 20)])
+def test_x6_warp_specialised_is_bitwise_the_per_tap_kernel(B, C, N, k, s, p, H, W):
+    """MD2_CONV_WS (4 MFMA waves + 4 staging waves per block) computes the same products
+    in the same order per output as conv_x6_kernel with the same tile height: forward and
+    stride-1 input gradient bitwise equal, K splits, M / N tails, stride 2 included."""
+    torch.manual_seed(3 + C + N + H)
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    w = (torch.randn(N, C, k, k, device="cuda") / (C * k * k) ** 0.5).contiguous(memory_format=CL)
+    for extra in (0, conv_ops.BM256, conv_ops.NO_SPLIT, conv_ops.BM256 | conv_ops.NO_SPLIT):
+        base = conv_ops.X6 | extra
+        assert torch.equal(conv_ops._fwd(x, w, s, p, base | conv_ops.WS), conv_ops._fwd(x, w, s, p, base)), extra
+        if s == 1:
+            gy = torch.randn(conv_ops._fwd(x, w, s, p, base).shape, device="cuda").contiguous(memory_format=CL)
+            assert torch.equal(conv_ops._dgrad(gy, x, w, p, base | conv_ops.WS), conv_ops._dgrad(gy, x, w, p, base)), extra
 
 
 def test_x6_presplit_planes_match_in_call_split():
