@@ -877,11 +877,12 @@ __device__ __forceinline__ float fwdall_walk(const PhotoArgs& a, const WarpCtx (
 // Round 4: 4 — with the identity losses read from LDS the compiler's own choice is 152
 // VGPRs (3 waves); at 4 it keeps 128 and spills ~21 dwords outside the row loop's hot
 // path: fused forward 0.1245 vs 0.128 ms (profiles/r04/ab_fused_forward.log)
+// Three source frames (mono + stereo) carry half as much state again: 2 (~194 VGPRs).
 #ifndef MD2_FWD_MINB
 #define MD2_FWD_MINB 4
 #endif
 template <int NS, bool SSIM_ON, bool MASK>
-__global__ __launch_bounds__(kBlock, MD2_FWD_MINB) void photo_fwdall_kernel(PhotoArgs a) {
+__global__ __launch_bounds__(kBlock, NS <= 2 ? MD2_FWD_MINB : 2) void photo_fwdall_kernel(PhotoArgs a) {
     __shared__ float dep_s[kWavesPerBlock][kRowsP + 2][kWave];
     __shared__ float idl_s[NS][kRowsP][kWave];   // ident_fused: the item's identity losses
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
