@@ -13,7 +13,7 @@
 // it is producer waves that build chunk t+1 while the multiplying waves run chunk t.
 //
 // Here the channels go in groups of three (one frame; the pose encoder's pair is two
-// groups, blockIdx.y) padded to four, and K in chunks of one 32-pixel segment of one
+// groups) padded to four, and K in chunks of one 32-pixel segment of one
 // output row.  Per chunk a block stages the 7 input rows x 69 columns x 3 channels
 // under the segment ONCE (fp32, coalesced row runs, one LDS buffer per chunk), and
 // builds from them the seven B tiles — kernel row kh: rows (kx, ci) = 4 kx + ci, 32
@@ -94,7 +94,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     __shared__ __bf16 At[3 * kPA];
     __shared__ __bf16 Bt[7 * 3 * kPT];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int ks = blockIdx.x, cg = blockIdx.y;
+    // the channel groups of one K split (same input rows, same dy) on one XCD, dispatched
+    // close together, so the second group's fetches hit the first one's L2 lines: blocks
+    // are dealt round-robin over the 8 XCDs (bid & 7); group cg of split ks gets
+    // bid = 8 (NG (ks / 8) + cg) + ks % 8.  The grid is padded to whole octets of splits.
+    const int NG = a.C / kCG;
+    const int j8 = blockIdx.x >> 3;
+    const int cg = j8 % NG, ks = (j8 / NG) * 8 + (blockIdx.x & 7);
+    if (ks >= a.splits) return;
     const int t0 = ks * a.cps;
     const int n = min(a.cps, a.nchunks - t0);
     const int H = a.H, W = a.W;
@@ -390,7 +397,7 @@ int md2_stem_wgrad(const md2_stem_desc* d, const float* x, const float* grad_y, 
     const int NG = a.C / kCG;
     const hipStream_t st = (hipStream_t)stream;
     void (*k)(StemArgs) = a.C == 3 ? stem_x6_wgrad_kernel<3> : a.C == 6 ? stem_x6_wgrad_kernel<6> : stem_x6_wgrad_kernel<9>;
-    hipLaunchKernelGGL(k, dim3(a.splits, NG), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(k, dim3(NG * ((a.splits + 7) / 8) * 8), dim3(kThreads), 0, st, a);
     const int outs = NG * kCo * kOut;
     hipLaunchKernelGGL(stem_wgrad_final_kernel, dim3((outs + kFinOut - 1) / kFinOut), dim3(256), 0, st, a);
     const hipError_t e = hipGetLastError();
