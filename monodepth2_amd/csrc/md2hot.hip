@@ -755,20 +755,37 @@ __device__ __forceinline__ void frowp_losses(const FRowP<NS>& A, const FRowP<NS>
     }
 }
 
-// identity losses (trainer.py:432-439) of source frame f for the item's output rows
-// [i0, i1) into LDS rows dst[i] (the photo_ident_kernel walk, rows rotated by copies)
+// one identity-walk row with the source from its 8-bit copy: k / 255 decoded correctly
+// rounded (div255) is the fp32 colour itself for an exact image, so the losses are
+// bit-identical to irow_eval's, from 4 bytes per pixel instead of 12
 template <bool SSIM_ON>
-__device__ __forceinline__ void ident_rows_lds(const PhotoArgs& a, int f, const FItem& it, int i0, int i1,
-                                               float (*dst)[kWave], int lane) {
+__device__ __forceinline__ void irow_eval8(const uint32_t* src8, const float* tgt, int HW, int idx, IRow& o) {
+    const uint32_t px = src8[(uint32_t)idx];
+    o.x = {f2v{div255((float)(px & 255u)), div255((float)((px >> 8) & 255u))}, div255((float)((px >> 16) & 255u))};
+    o.y = ld3(tgt, HW, idx);
+    if (SSIM_ON) o.h = hsum3(o.x, o.y);
+}
+
+// identity losses (trainer.py:432-439) of source frame f for the item's output rows
+// [i0, i1) into LDS rows dst[i] (the photo_ident_kernel walk, rows rotated by copies);
+// src8: the frame's exact 8-bit copy for this image, or null (fp32 planes)
+template <bool SSIM_ON>
+__device__ __forceinline__ void ident_rows_lds(const PhotoArgs& a, int f, const uint32_t* src8, const FItem& it,
+                                               int i0, int i1, float (*dst)[kWave], int lane) {
     const int h = a.h, w = a.w, HW = h * w;
     const float* src = a.src[f] + (size_t)it.b * 3 * HW;
     const float* tgt = a.tgt + (size_t)it.b * 3 * HW;
+    auto row = [&](int r, IRow& o) {
+        const int idx = reflect_clamp(r, h) * w + it.cc;
+        if (src8) irow_eval8<SSIM_ON>(src8, tgt, HW, idx, o);
+        else irow_eval<SSIM_ON>(src, tgt, HW, idx, o);
+    };
     IRow A, Bq, C;
-    irow_eval<SSIM_ON>(src, tgt, HW, reflect_clamp(it.r0 + i0 - 1, h) * w + it.cc, A);
-    irow_eval<SSIM_ON>(src, tgt, HW, reflect_clamp(it.r0 + i0, h) * w + it.cc, Bq);
+    row(it.r0 + i0 - 1, A);
+    row(it.r0 + i0, Bq);
 #pragma unroll 1
     for (int i = i0; i < i1; ++i) {
-        irow_eval<SSIM_ON>(src, tgt, HW, reflect_clamp(it.r0 + i + 1, h) * w + it.cc, C);
+        row(it.r0 + i + 1, C);
         dst[i][lane] = irow_loss<SSIM_ON>(A, Bq, C);
         A = Bq;
         Bq = C;
@@ -911,7 +928,7 @@ __global__ __launch_bounds__(kBlock, NS <= 2 ? MD2_FWD_MINB : 2) void photo_fwda
         const int rows = min(kRowsP, a.h - it.r0);
         for (int task = wid; task < 2 * NS; task += kWavesPerBlock) {
             const int f = task >> 1, i0 = (task & 1) ? kMid : 0, i1 = (task & 1) ? rows : min(kMid, rows);
-            if (i0 < i1) ident_rows_lds<SSIM_ON>(a, f, it, i0, i1, idl_s[f], lane);
+            if (i0 < i1) ident_rows_lds<SSIM_ON>(a, f, ctx[f].src8, it, i0, i1, idl_s[f], lane);
         }
         __syncthreads();
         idl = idl_s;
