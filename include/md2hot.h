@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 16
+#define MD2_ABI_VERSION 17
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -254,6 +254,15 @@ typedef struct md2_stem_desc {
 size_t md2_stem_wgrad_workspace_bytes(const md2_stem_desc* desc);
 int md2_stem_wgrad(const md2_stem_desc* desc, const float* x, const float* grad_y, float* grad_weight,
                    void* workspace, void* stream);
+
+/*
+ * Forward of the same convolution: y (batch, Ho, Wo, 64) NHWC fp32 = conv(x, weight),
+ * stride 2, padding 3, on split-bf16 MFMA (f32-class), channels 3 / 6.  weight
+ * (64, channels, 7, 7) in the memory format MD2_STEM_WEIGHT_CL names.  No workspace.
+ * Replaces MIOpen's forward convolution for this layer (torchvision conv1 forward,
+ * networks/resnet_encoder.py:93).
+ */
+int md2_stem_fwd(const md2_stem_desc* desc, const float* x, const float* weight, float* y, void* stream);
 
 /*
  * Conv bias (+ ReLU) epilogue on NHWC fp32 activations (networks/pose_decoder.py:43-54:

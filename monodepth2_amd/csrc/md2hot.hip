@@ -928,7 +928,12 @@ __global__ __launch_bounds__(kBlock, NS <= 2 ? MD2_FWD_MINB : 2) void photo_fwda
         const int rows = min(kRowsP, a.h - it.r0);
         for (int task = wid; task < 2 * NS; task += kWavesPerBlock) {
             const int f = task >> 1, i0 = (task & 1) ? kMid : 0, i1 = (task & 1) ? rows : min(kMid, rows);
-            if (i0 < i1) ident_rows_lds<SSIM_ON>(a, f, ctx[f].src8, it, i0, i1, idl_s[f], lane);
+            // ctx[f] by selects: indexing the array with a runtime f would put all of
+            // ctx in scratch memory (320 B per lane, written out by every wave)
+            const uint32_t* src8 = ctx[0].src8;
+#pragma unroll
+            for (int g = 1; g < NS; ++g) src8 = f == g ? ctx[g].src8 : src8;
+            if (i0 < i1) ident_rows_lds<SSIM_ON>(a, f, src8, it, i0, i1, idl_s[f], lane);
         }
         __syncthreads();
         idl = idl_s;

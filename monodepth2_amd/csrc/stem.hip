@@ -32,6 +32,8 @@
 
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "md2hot.h"
 
 int md2_report_error(int code, const char* msg);
@@ -41,6 +43,7 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kCo = 64;
 constexpr int kWaves = 7;               // one per kernel row
@@ -346,6 +349,171 @@ __global__ __launch_bounds__(256) void stem_wgrad_final_kernel(StemArgs a) {
     else a.gw[((co * a.C + ci) * 7 + ky) * 7 + kx] = s;
 }
 
+// ---------------------------------------------------------------------------------
+// Forward: y[p][co] = Σ_kh Σ_k X_kh[p][k] · W[kh][k][co], a GEMM with M = output pixels,
+// N = 64, K = 7 kernel rows x KP.  Within one kernel row the 7 x C window taps of an
+// output pixel are C·7 CONSECUTIVE floats of the NHWC input row — x[ih][2 ow - 3 + kx][ci]
+// sits at flat offset (2 ow - 3)·C + k with k = kx·C + ci — so an MFMA A fragment (eight
+// consecutive k of one pixel) is two float4 loads straight from the input, no im2col:
+// lanes of one pixel group read overlapping windows, the overlap served by L1.  K is
+// padded to KP = 16·⌈7C/16⌉ with zero weights (C = 3: 21 -> 32, C = 6: 42 -> 48).
+// The fragments are split into bf16 planes in registers (exact truncation split, six
+// products: f32-class, conv.hip's x6 scheme); the weights, split once per block into
+// their fragment image in LDS (84 KB at C = 3, 126 KB at C = 6), are read conflict-free
+// as 1-KB runs.  A wave owns 64 pixels of one output row x all 64 channels (2 x 2
+// 32x32 accumulators) and walks its tiles persistently; the next step's fragments are
+// loaded behind the current step's 24 MFMAs.  MIOpen's igemm_fwd ran these at 89 /
+// 334 us (B = 12, C = 3 / B = 24, C = 6; 192x640).
+constexpr int kFwdWaves = 8;
+constexpr int kFwdSeg = 64;   // output pixels per wave tile
+
+struct StemFwdArgs {
+    int B, C, H, W, Ho, Wo;
+    int w_cl;
+    int nseg, tiles;
+    const float* x;
+    const float* w;
+    float* y;
+};
+
+// One wave tile (64 pixels of output row oh x 64 channels).  EDGE: window rows outside
+// the image or fragments crossing a row end (zeros), pixels past the row (not stored).
+// The (kernel row, k step) loop is unrolled with its fragment loads kPD steps ahead.
+constexpr int kPD = 3;
+template <int C, bool EDGE>
+__device__ __forceinline__ void stem_fwd_tile(const StemFwdArgs& a, const u32x4* __restrict__ wf, int b, int oh,
+                                              int ow0, int lane) {
+    constexpr int KP = (7 * C + 15) / 16 * 16, S = KP / 16, NQ = 7 * S;
+    const int lr = lane & 31, h = lane >> 5;
+    const int H = a.H, rowlen = a.W * C;
+    const float* img = a.x + (size_t)b * H * rowlen;
+    int base[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) base[p] = (2 * (ow0 + 32 * p + lr) - 3) * C + 8 * h;
+    // step q = (kh, s): the two pixel groups' eight k values, from input row 2 oh - 3 + kh
+    auto load = [&](int q, float (&r)[2][8]) {
+        const int kh = q / S, s = q - kh * S, ih = 2 * oh - 3 + kh;
+        const bool rowok = !EDGE || (unsigned)ih < (unsigned)H;
+        const float* rowp = img + (size_t)(rowok ? ih : 0) * rowlen;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int o = base[p] + 16 * s;
+            if (!EDGE || (rowok && o >= 0 && o + 8 <= rowlen)) {
+                const float4 u = *(const float4*)(rowp + o), v = *(const float4*)(rowp + o + 4);
+                r[p][0] = u.x; r[p][1] = u.y; r[p][2] = u.z; r[p][3] = u.w;
+                r[p][4] = v.x; r[p][5] = v.y; r[p][6] = v.z; r[p][7] = v.w;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int f = o + i;
+                    r[p][i] = (rowok && f >= 0 && f < rowlen) ? rowp[f] : 0.f;
+                }
+            }
+        }
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[p][j][e] = 0.f;
+    float raw[kPD + 1][2][8];
+#pragma unroll
+    for (int q = 0; q < kPD && q < NQ; ++q) load(q, raw[q]);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        if (q + kPD < NQ) load(q + kPD, raw[(q + kPD) % (kPD + 1)]);
+        const float (&cur)[2][8] = raw[q % (kPD + 1)];
+        bf16x8 fa[2][3];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            uint32_t pk[3][4];
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) {
+                const float x0 = cur[p][i], x1 = cur[p][i + 1];
+                const float a0 = trunc16(x0), r0 = x0 - a0, m0 = trunc16(r0);
+                const float a1 = trunc16(x1), r1 = x1 - a1, m1 = trunc16(r1);
+                pk[0][i / 2] = hi16x2(a0, a1);
+                pk[1][i / 2] = hi16x2(m0, m1);
+                pk[2][i / 2] = hi16x2(r0 - m0, r1 - m1);
+            }
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                fa[p][pl] = __builtin_bit_cast(bf16x8, u32x4{pk[pl][0], pk[pl][1], pk[pl][2], pk[pl][3]});
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            bf16x8 fb[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) fb[pl] = __builtin_bit_cast(bf16x8, wf[((q * 2 + j) * 3 + pl) * 64 + lane]);
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                acc[p][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[p][2], fb[0], acc[p][j], 0, 0, 0);
+                acc[p][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[p][1], fb[1], acc[p][j], 0, 0, 0);
+                acc[p][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[p][0], fb[2], acc[p][j], 0, 0, 0);
+                acc[p][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[p][1], fb[0], acc[p][j], 0, 0, 0);
+                acc[p][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[p][0], fb[1], acc[p][j], 0, 0, 0);
+                acc[p][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[p][0], fb[0], acc[p][j], 0, 0, 0);
+            }
+        }
+    }
+    // D row (pixel) = 32 p + (e & 3) + 8 (e >> 2) + 4 h, column (channel) = 32 j + lr
+    float* yrow = a.y + (size_t)(b * a.Ho + oh) * a.Wo * kCo;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int ow = ow0 + 32 * p + (e & 3) + 8 * (e >> 2) + 4 * h;
+            if (!EDGE || ow < a.Wo) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) yrow[(size_t)ow * kCo + 32 * j + lr] = acc[p][j][e];
+            }
+        }
+}
+
+template <int C>
+__global__ __launch_bounds__(64 * kFwdWaves, 1) void stem_x6_fwd_kernel(StemFwdArgs a) {
+    constexpr int KP = (7 * C + 15) / 16 * 16, S = KP / 16;
+    constexpr int NQ = 7 * S;                       // (kernel row, k step) pairs
+    __shared__ u32x4 wf[NQ * 2 * 3 * 64];           // [kh][s][co half][plane][lane] x 8 bf16
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // the weight fragment image: lane l of fragment (kh, s, j) holds W[kh][16 s + 8 h + i][32 j + l % 32]
+#pragma unroll
+    for (int id = tid; id < NQ * 2 * 64; id += 64 * kFwdWaves) {   // unrolled: the rounds' loads in flight together
+        const int l = id & 63, j = (id >> 6) & 1, q = id >> 7;
+        const int kh = q / S, s = q - kh * S;
+        const int co = 32 * j + (l & 31), k0 = 16 * s + 8 * (l >> 5);
+        float c[3][8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int k = k0 + i, kw = k / C, ci = k - kw * C;
+            float v = 0.f;
+            if (k < 7 * C)
+                v = a.w_cl ? a.w[((co * 7 + kh) * 7 + kw) * C + ci] : a.w[((co * C + ci) * 7 + kh) * 7 + kw];
+            const float a0 = trunc16(v), r1 = v - a0, a1 = trunc16(r1);
+            c[0][i] = a0;
+            c[1][i] = a1;
+            c[2][i] = r1 - a1;
+        }
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+            wf[((q * 2 + j) * 3 + pl) * 64 + l] = u32x4{hi16x2(c[pl][0], c[pl][1]), hi16x2(c[pl][2], c[pl][3]),
+                                                        hi16x2(c[pl][4], c[pl][5]), hi16x2(c[pl][6], c[pl][7])};
+    }
+    __syncthreads();
+
+    for (int t = blockIdx.x * kFwdWaves + wid; t < a.tiles; t += gridDim.x * kFwdWaves) {
+        const int rr = t / a.nseg, seg = t - rr * a.nseg, b = rr / a.Ho, oh = rr - b * a.Ho;
+        const int ow0 = seg * kFwdSeg;
+        // interior tile: every window row in the image and every fragment inside its row
+        const bool inner = 2 * oh - 3 >= 0 && 2 * oh + 3 < a.H && ow0 >= 2 &&
+                           (2 * (ow0 + kFwdSeg - 1) - 3) * C + KP <= a.W * C && ow0 + kFwdSeg <= a.Wo;
+        if (inner) stem_fwd_tile<C, false>(a, wf, b, oh, ow0, lane);
+        else stem_fwd_tile<C, true>(a, wf, b, oh, ow0, lane);
+    }
+}
+
 bool valid(const md2_stem_desc* d) {
     return d && d->batch >= 1 && d->height >= 1 && d->width >= 1 &&
            (d->channels == 3 || d->channels == 6 || d->channels == 9) &&
@@ -400,6 +568,31 @@ int md2_stem_wgrad(const md2_stem_desc* d, const float* x, const float* grad_y, 
     hipLaunchKernelGGL(k, dim3(NG * ((a.splits + 7) / 8) * 8), dim3(kThreads), 0, st, a);
     const int outs = NG * kCo * kOut;
     hipLaunchKernelGGL(stem_wgrad_final_kernel, dim3((outs + kFinOut - 1) / kFinOut), dim3(256), 0, st, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
+int md2_stem_fwd(const md2_stem_desc* d, const float* x, const float* weight, float* y, void* stream) {
+    if (!valid(d) || (d->channels != 3 && d->channels != 6))
+        return md2_report_error(MD2_ERR_ARG, "stem_fwd: channels 3/6, 32-bit element count");
+    if (!x || !weight || !y) return md2_report_error(MD2_ERR_ARG, "stem_fwd: NULL operand");
+    StemFwdArgs a = {};
+    a.B = d->batch;
+    a.C = d->channels;
+    a.H = d->height;
+    a.W = d->width;
+    a.Ho = (d->height - 1) / 2 + 1;
+    a.Wo = (d->width - 1) / 2 + 1;
+    a.w_cl = (d->flags & MD2_STEM_WEIGHT_CL) ? 1 : 0;
+    a.nseg = (a.Wo + kFwdSeg - 1) / kFwdSeg;
+    a.tiles = a.B * a.Ho * a.nseg;
+    a.x = x;
+    a.w = weight;
+    a.y = y;
+    // one block per CU (the weight image fills most of the LDS), tiles walked persistently
+    const int blocks = std::min(256, (a.tiles + kFwdWaves - 1) / kFwdWaves);
+    void (*k)(StemFwdArgs) = a.C == 3 ? stem_x6_fwd_kernel<3> : stem_x6_fwd_kernel<6>;
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * kFwdWaves), 0, (hipStream_t)stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }

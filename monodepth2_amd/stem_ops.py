@@ -1,14 +1,15 @@
-"""The ResNet stem convolution (conv1: 7x7, stride 2, padding 3, C -> 64, no bias) with
-its weight gradient on split-bf16 MFMA (csrc/stem.hip, ABI `md2_stem_*`).
+"""The ResNet stem convolution (conv1: 7x7, stride 2, padding 3, C -> 64, no bias) on
+split-bf16 MFMA (csrc/stem.hip, ABI `md2_stem_*`): forward and weight gradient.
 
 The stem reads the normalised frames, which are data: its backward is the weight
 gradient alone, MIOpen's igemm_wrw at ~125 us (C=3, depth encoder, B=12) and ~430 us
 (C=6, pose encoder, B=24) per step at 192x640.  stem_x6_wgrad_kernel (f32-class:
-three exact bf16 planes, six products) runs them in ~100 / ~413 us including its
+three exact bf16 planes, six products) runs them in ~80 / ~380 us including its
 split reduction (rocprofv3, tools/stem_bench.py under tools/kstats.sh).  The forward
-stays MIOpen's.  Same parameter (the torchvision `conv1.weight`), same semantics; any
-other case (an input that needs a gradient, bf16, NCHW inputs, a CPU tensor) runs the
-module itself.
+(MIOpen's igemm_fwd: 89 / 334 us) runs on stem_x6_fwd_kernel for C = 3 / 6 (the input
+windows read straight from the NHWC rows as MFMA fragments, FWD_ENABLED).  Same
+parameter (the torchvision `conv1.weight`), same semantics; any other case (an input
+that needs a gradient, bf16, NCHW inputs, a CPU tensor) runs the module itself.
 """
 from __future__ import annotations
 
@@ -21,7 +22,24 @@ import torch.nn.functional as F
 from . import _lib
 
 _CL = torch.channels_last
-ENABLED = True   # the x6 weight gradient (tests flip it to compare with MIOpen)
+ENABLED = True       # the x6 weight gradient (tests flip it to compare with MIOpen)
+FWD_ENABLED = True   # the x6 forward (C = 3 / 6)
+
+
+def _fwd(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """conv2d(x, weight, stride 2, padding 3) on md2_stem_fwd, or MIOpen's forward."""
+    B, C, H, W = x.shape
+    if not (FWD_ENABLED and C in (3, 6)):
+        return F.conv2d(x, weight, None, 2, 3)
+    w_cl = weight.is_contiguous(memory_format=_CL)
+    if not (w_cl or weight.is_contiguous()):
+        weight = weight.contiguous()
+    d = _lib.StemDesc(B, C, H, W, _lib.STEM_WEIGHT_CL if w_cl else 0)
+    y = torch.empty((B, 64, (H - 1) // 2 + 1, (W - 1) // 2 + 1), device=x.device, dtype=torch.float32,
+                    memory_format=_CL)
+    rc = _lib.lib().md2_stem_fwd(ctypes.byref(d), x.data_ptr(), weight.data_ptr(), y.data_ptr(), _lib.stream(x.device))
+    _lib.check(rc, "md2_stem_fwd")
+    return y
 
 
 class _StemConv(torch.autograd.Function):
@@ -31,7 +49,7 @@ class _StemConv(torch.autograd.Function):
         ctx.save_for_backward(x)
         ctx.w_cl = weight.is_contiguous(memory_format=_CL)
         ctx.w_shape = weight.shape
-        return F.conv2d(x, weight, None, 2, 3)
+        return _fwd(x, weight)
 
     @staticmethod
     def backward(ctx, gy):
@@ -61,6 +79,8 @@ def supports_stem(conv: nn.Conv2d, x: torch.Tensor) -> bool:
 def stem_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     """conv(x) for the encoder's stem; the weight gradient runs on md2_stem_wgrad when
     supports_stem(conv, x), else the module runs as is."""
-    if ENABLED and supports_stem(conv, x) and torch.is_grad_enabled() and conv.weight.requires_grad:
-        return _StemConv.apply(x, conv.weight)
+    if ENABLED and supports_stem(conv, x):
+        if torch.is_grad_enabled() and conv.weight.requires_grad:
+            return _StemConv.apply(x, conv.weight)
+        return _fwd(x, conv.weight.detach())
     return conv(x)

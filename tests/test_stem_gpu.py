@@ -1,6 +1,7 @@
-"""Stem convolution weight gradient (stem_ops / md2_stem_wgrad, f32 MFMA) vs MIOpen's
-conv2d backward on the same inputs, against an fp64 reference (fixed-order fp32 sums
-over up to 92k pixels: ours must be no worse than 2x MIOpen's drift)."""
+"""Stem convolution forward and weight gradient (stem_ops / md2_stem_fwd, md2_stem_wgrad,
+split-bf16 MFMA) vs MIOpen's conv2d forward / backward on the same inputs, against an
+fp64 reference (fixed-order fp32 sums over 147-294 taps / up to 92k pixels: ours must be
+no worse than 2x MIOpen's drift)."""
 import pytest
 import torch
 
@@ -13,6 +14,13 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(autouse=True)
 def _enabled(monkeypatch):
     monkeypatch.setattr(stem_ops, "ENABLED", True)
+    monkeypatch.setattr(stem_ops, "FWD_ENABLED", True)
+
+
+def _no_worse(ours, ref, exact, rel=1e-6):
+    e_ours = (ours.double() - exact).abs().max().item()
+    e_ref = (ref.double() - exact).abs().max().item()
+    assert e_ours <= 2 * e_ref + rel * exact.abs().max().item() + 1e-6, (e_ours, e_ref)
 
 
 @pytest.mark.parametrize("B,C,H,W", [(2, 3, 64, 128), (3, 6, 30, 50), (1, 9, 17, 23), (2, 3, 192, 640),
@@ -28,7 +36,12 @@ def test_stem_wgrad_matches_conv_backward(B, C, H, W, w_cl):
     assert supports_stem(conv, x)
     y = stem_conv(conv, x)
     ref = torch.nn.functional.conv2d(x, conv.weight, None, 2, 3)
-    assert torch.equal(y, ref)                      # the forward is MIOpen's
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=CL)
+    y64 = torch.nn.functional.conv2d(x.double(), conv.weight.double(), None, 2, 3)
+    if C == 9:
+        assert torch.equal(y, ref)                  # the forward is MIOpen's for three frames
+    else:
+        _no_worse(y.detach(), ref.detach(), y64.detach())
     g = torch.randn_like(ref).contiguous(memory_format=CL)
     assert y.grad_fn is not None and "StemConv" in type(y.grad_fn).__name__
     gw, = torch.autograd.grad(y, conv.weight, g)
@@ -36,9 +49,23 @@ def test_stem_wgrad_matches_conv_backward(B, C, H, W, w_cl):
     assert gw.shape == gwr.shape and gw.is_contiguous(memory_format=CL) == w_cl
     gw64, = torch.autograd.grad(torch.nn.functional.conv2d(x.double(), conv.weight.double(), None, 2, 3),
                                 conv.weight, g.double())
-    e_ours = (gw.double() - gw64).abs().max().item()
-    e_ref = (gwr.double() - gw64).abs().max().item()
-    assert e_ours <= 2 * e_ref + 1e-6 * gw64.abs().max().item() + 1e-6, (e_ours, e_ref)
+    _no_worse(gw, gwr, gw64)
+
+
+@pytest.mark.parametrize("B,C,H,W", [(2, 6, 192, 640), (1, 3, 1, 1), (2, 3, 5, 130), (1, 6, 64, 200)])
+def test_stem_fwd_without_grad(B, C, H, W):
+    """The eval / no-grad forward runs md2_stem_fwd too: ragged widths (a partial last
+    64-pixel tile), single-pixel images, rows where most of the 7x7 window is padding."""
+    torch.manual_seed(3)
+    CL = torch.channels_last
+    conv = torch.nn.Conv2d(C, 64, 7, 2, 3, bias=False).cuda()
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    with torch.no_grad():
+        y = stem_conv(conv, x)
+        ref = torch.nn.functional.conv2d(x, conv.weight, None, 2, 3)
+        y64 = torch.nn.functional.conv2d(x.double(), conv.weight.double(), None, 2, 3)
+    assert y.shape == ref.shape
+    _no_worse(y, ref, y64)
 
 
 def test_stem_falls_back_when_the_input_needs_a_gradient():
