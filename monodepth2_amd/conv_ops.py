@@ -333,6 +333,9 @@ def clear_choices():
 
 
 _names: Dict[tuple, list] = {}    # (op, shape) -> candidate names, in candidate order
+# A/B knob: MD2_CONV_EXCLUDE=name,name... never picks those candidates (MIOpen, the last
+# candidate, always stays), e.g. to time a training step without one kernel family
+_EXCLUDE = frozenset(n for n in os.environ.get("MD2_CONV_EXCLUDE", "").split(",") if n)
 
 
 def _cached(op: str, key: tuple):
@@ -363,7 +366,10 @@ def _fastest(op: str, key: tuple, cands, names=None) -> int:
     if torch.cuda.is_current_stream_capturing():
         return len(cands) - 1
     times = []
-    for fn in cands:
+    for name, fn in zip(names, cands):
+        if name in _EXCLUDE and name != names[-1]:
+            times.append(float("inf"))
+            continue
         fn()
         ts = []
         for _ in range(3):
@@ -405,14 +411,15 @@ def _direct_ok(cin: int, cout: int, k: int, stride: int) -> bool:
     return k == 3 and stride == 1 and (cin, cout) in _DIRECT
 
 
-def _direct(a: torch.Tensor, wk: torch.Tensor, pad: int, cout: int) -> torch.Tensor:
-    """a (B, C, H, W) channels_last correlated with wk [3][3][C][cout], zero padding `pad`."""
+def _direct(a: torch.Tensor, wk: torch.Tensor, pad: int, cout: int, flags: int = 0) -> torch.Tensor:
+    """a (B, C, H, W) channels_last correlated with wk [3][3][C][cout], zero padding `pad`
+    (flags X6: the split-bf16 MFMA form, else the f32 VALU form)."""
     B, C, H, W = a.shape
     y = torch.empty(B, cout, H + 2 * pad - 2, W + 2 * pad - 2, device=a.device, memory_format=_CL)
-    k = (tuple(a.shape), cout, pad)
+    k = (tuple(a.shape), cout, pad, flags)
     d = _ddescs.get(k)
     if d is None:
-        d = _ddescs[k] = _lib.ConvDesc(B, H, W, C, cout, 3, 3, 1, pad, 0)
+        d = _ddescs[k] = _lib.ConvDesc(B, H, W, C, cout, 3, 3, 1, pad, flags)
     _lib.check(_lib.lib().md2_conv_direct(ctypes.byref(d), a.data_ptr(), wk.data_ptr(), y.data_ptr(),
                                           _lib.stream(a.device)), "md2_conv_direct")
     return y
@@ -430,13 +437,13 @@ def _direct_wgrad(gy, x, w, pad):
     return gw
 
 
-def _direct_fwd(x, w, pad):
-    return _direct(x, w.permute(2, 3, 1, 0).contiguous(), pad, w.shape[0])
+def _direct_fwd(x, w, pad, flags=0):
+    return _direct(x, w.permute(2, 3, 1, 0).contiguous(), pad, w.shape[0], flags)
 
 
-def _direct_dgrad(gy, w, pad):
+def _direct_dgrad(gy, w, pad, flags=0):
     # gx = gy correlated with the flipped weight, channel roles swapped, pad 2 - pad
-    return _direct(gy, w.flip(2, 3).permute(2, 3, 0, 1).contiguous(), 2 - pad, w.shape[1])
+    return _direct(gy, w.flip(2, 3).permute(2, 3, 0, 1).contiguous(), 2 - pad, w.shape[1], flags)
 
 
 def _fits(cin: int, cout: int) -> bool:
@@ -457,9 +464,9 @@ class _Conv(torch.autograd.Function):
             direct = _direct_ok(weight.shape[1], weight.shape[0], weight.shape[2], stride)
             cands = [(lambda f=f: _fwd(x, weight, stride, pad, f)) for f in xf] + \
                 [lambda: _fwd(x, weight, stride, pad)] + \
-                ([lambda: _direct_fwd(x, weight, pad)] if direct else []) + \
+                ([lambda: _direct_fwd(x, weight, pad), lambda: _direct_fwd(x, weight, pad, X6)] if direct else []) + \
                 [lambda: F.conv2d(x, weight, None, stride, pad)]
-            names = list(xn) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"]
+            names = list(xn) + ["f32mfma"] + (["direct", "direct_x6"] if direct else []) + ["miopen"]
             if i is None:
                 i = _fastest("fwd", ctx.key, cands, names)
         planes_dg = None
@@ -488,9 +495,10 @@ class _Conv(torch.autograd.Function):
                 xf, xn = _x6_flags(w.shape[0], w.shape[2], 1, w.shape[1]) if x6 else ((), ())
                 direct = _direct_ok(w.shape[0], w.shape[1], w.shape[2], s)
                 cands = [(lambda f=f: _dgrad(gy, x, w, p, f)) for f in xf] + \
-                    [lambda: _dgrad(gy, x, w, p)] + ([lambda: _direct_dgrad(gy, w, p)] if direct else []) + \
+                    [lambda: _dgrad(gy, x, w, p)] + \
+                    ([lambda: _direct_dgrad(gy, w, p), lambda: _direct_dgrad(gy, w, p, X6)] if direct else []) + \
                     [lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
-                names = list(xn) + ["f32mfma"] + (["direct"] if direct else []) + ["miopen"]
+                names = list(xn) + ["f32mfma"] + (["direct", "direct_x6"] if direct else []) + ["miopen"]
                 i = _fastest("dgrad", ctx.key, cands, names)
                 if x6 and i < len(xf) and planes_dg is None:
                     planes_dg = _bank_dgrad(x, w, s, p)

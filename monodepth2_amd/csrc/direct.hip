@@ -128,6 +128,136 @@ __global__ __launch_bounds__(kThreads) void conv3_direct_lds_kernel(const float*
     for (int o = 0; o < COUT / 4; ++o) yp[o] = float4{acc[4 * o], acc[4 * o + 1], acc[4 * o + 2], acc[4 * o + 3]};
 }
 
+// Split-bf16 MFMA form (MD2_CONV_X6 in the descriptor's flags): the same correlation as
+// a GEMM with M = output pixels, N = COUT, K = 9 taps x CIN (k = tap·CIN + ci, padded to
+// whole 32-k steps with zero weights), on v_mfma_f32_16x16x32_bf16 with six products of
+// three exact bf16 planes per operand (f32-class, conv.hip's x6 scheme).  The GEMM is 16
+// or 32 columns wide, so the weights — KS steps x NB column blocks x 3 planes of one
+// fragment per lane, 60-120 VGPRs — live in registers for the block's whole life; a
+// block walks output tiles (4 rows x 64 columns) persistently: it stages the tile's
+// (4+2) x (64+2) x CIN input patch ONCE, split into three bf16 planes in LDS ([row]
+// [col][ci], zeros outside the image), and wave w multiplies output row w: per
+// 16-pixel group and k step one 16-byte fragment read per plane (eight consecutive
+// channels of one tap at the pixel's window position) and 6 x NB MFMAs.  Every input
+// element is split once per tile instead of once per tap.
+constexpr int kXR = 4, kXC = 64;
+
+__device__ __forceinline__ float x6_trunc16(float x) {
+    return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, x) & 0xFFFF0000u);
+}
+__device__ __forceinline__ uint32_t x6_hi16x2(float lo, float hi) {
+    return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo), 0x07060302u);
+}
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int CIN, int COUT>
+__global__ __launch_bounds__(kThreads, 2) void conv3_x6_kernel(const float* __restrict__ x,
+                                                               const float* __restrict__ wk, float* __restrict__ y,
+                                                               int B, int H, int W, int Ho, int Wo, int pad,
+                                                               int tiles_r, int tiles_c) {
+    constexpr int PR = kXR + 2, PC = kXC + 2, PE = PR * PC * CIN;   // patch elements per plane
+    constexpr int KS = (9 * CIN + 31) / 32, NB = COUT / 16;
+    constexpr int NQ = PE / 4;                                      // float4s per patch
+    static_assert(kThreads == 64 * kXR, "one wave per output row of the tile");
+    __shared__ u32x2 patch[3][NQ];                                  // 4 bf16 per entry
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int col = lane & 15, g = lane >> 4;
+    // the weight fragments: B[k = 32 s + 8 g + j][n = 16 nb + col] = wk[k][n] (k < 9 CIN)
+    bf16x8 wf[KS][NB][3];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+            float c[3][8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = 32 * s + 8 * g + j;
+                const float v = k < 9 * CIN ? wk[k * COUT + 16 * nb + col] : 0.f;
+                const float a0 = x6_trunc16(v), r1 = v - a0, a1 = x6_trunc16(r1);
+                c[0][j] = a0;
+                c[1][j] = a1;
+                c[2][j] = r1 - a1;
+            }
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                wf[s][nb][pl] = __builtin_bit_cast(
+                    bf16x8, u32x4{x6_hi16x2(c[pl][0], c[pl][1]), x6_hi16x2(c[pl][2], c[pl][3]),
+                                  x6_hi16x2(c[pl][4], c[pl][5]), x6_hi16x2(c[pl][6], c[pl][7])});
+        }
+    const int ntiles = B * tiles_r * tiles_c;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int tcb = t % tiles_c, rest = t / tiles_c, trb = rest % tiles_r, b = rest / tiles_r;
+        const int oh0 = trb * kXR, ow0 = tcb * kXC;
+        // stage the patch: float4 i = (pixel, channel quad), split into three planes
+        for (int i = tid; i < NQ; i += kThreads) {
+            const int pix = i / (CIN / 4), q = i - pix * (CIN / 4), pr = pix / PC, pc = pix - pr * PC;
+            const int ih = oh0 - pad + pr, iw = ow0 - pad + pc;
+            float4 v = {0.f, 0.f, 0.f, 0.f};
+            if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+                v = ((const float4*)x)[((size_t)(b * H + ih) * W + iw) * (CIN / 4) + q];
+            const float e[4] = {v.x, v.y, v.z, v.w};
+            float c[3][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float a0 = x6_trunc16(e[j]), r1 = e[j] - a0, a1 = x6_trunc16(r1);
+                c[0][j] = a0;
+                c[1][j] = a1;
+                c[2][j] = r1 - a1;
+            }
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) patch[pl][i] = u32x2{x6_hi16x2(c[pl][0], c[pl][1]), x6_hi16x2(c[pl][2], c[pl][3])};
+        }
+        __syncthreads();
+        const int oh = oh0 + wid;
+        const __bf16* P0 = (const __bf16*)patch[0];
+        const __bf16* P1 = (const __bf16*)patch[1];
+        const __bf16* P2 = (const __bf16*)patch[2];
+#pragma unroll
+        for (int m = 0; m < kXC / 16; ++m) {
+            f32x4 acc[NB];
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                // A[m-pixel col][k = 32 s + 8 g + j]: tap, eight channels from ci0 (tap 9 of
+                // the padding step reads tap 8's place: finite, zero weights)
+                const int k0 = 32 * s + 8 * g, tap = min(k0 / CIN, 8), ci0 = k0 - (k0 / CIN) * CIN;
+                const int kh = tap / 3, kw = tap - kh * 3;
+                const int e = ((wid + kh) * PC + 16 * m + col + kw) * CIN + ci0;
+                bf16x8 fa[3];
+                fa[0] = *(const bf16x8*)(P0 + e);
+                fa[1] = *(const bf16x8*)(P1 + e);
+                fa[2] = *(const bf16x8*)(P2 + e);
+#pragma unroll
+                for (int nb = 0; nb < NB; ++nb) {
+                    acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], wf[s][nb][0], acc[nb], 0, 0, 0);
+                    acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wf[s][nb][1], acc[nb], 0, 0, 0);
+                    acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wf[s][nb][2], acc[nb], 0, 0, 0);
+                    acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wf[s][nb][0], acc[nb], 0, 0, 0);
+                    acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wf[s][nb][1], acc[nb], 0, 0, 0);
+                    acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wf[s][nb][0], acc[nb], 0, 0, 0);
+                }
+            }
+            // D[row = 4 g + i][col]: pixel ow0 + 16 m + 4 g + i, channel 16 nb + col
+            if (oh < Ho) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int ow = ow0 + 16 * m + 4 * g + i;
+                    if (ow < Wo) {
+                        float* yp = y + ((size_t)(b * Ho + oh) * Wo + ow) * COUT + col;
+#pragma unroll
+                        for (int nb = 0; nb < NB; ++nb) yp[16 * nb] = acc[nb][i];
+                    }
+                }
+            }
+        }
+        __syncthreads();   // the patch is restaged for the next tile
+    }
+}
+
 bool direct_lds() {   // A/B knob: MD2_DIRECT_LDS=0 selects the global-load form
     static const bool on = [] {
         const char* e = getenv("MD2_DIRECT_LDS");
@@ -284,6 +414,26 @@ int md2_conv_direct(const md2_conv_desc* d, const float* x, const float* wk, flo
     const dim3 grid((unsigned)((M + kThreads - 1) / kThreads));
     const hipStream_t st = (hipStream_t)stream;
     const int ci = d->in_channels, co = d->out_channels;
+    if (d->flags & MD2_CONV_X6) {
+        const int tr = (Ho + kXR - 1) / kXR, tc = (Wo + kXC - 1) / kXC;
+        const long long nt = (long long)d->batch * tr * tc;
+        // persistent: as many blocks as fit on a CU (LDS / VGPRs: 4 for 16 -> 16, else 2)
+        const long long cap = 256ll * ((ci == 16 && co == 16) ? 4 : 2);
+        const dim3 g2((unsigned)(nt < cap ? nt : cap));
+        if (ci == 16 && co == 16)
+            hipLaunchKernelGGL((conv3_x6_kernel<16, 16>), g2, dim3(kThreads), 0, st, x, wk, y, d->batch, d->height,
+                               d->width, Ho, Wo, d->pad, tr, tc);
+        else if (ci == 32 && co == 16)
+            hipLaunchKernelGGL((conv3_x6_kernel<32, 16>), g2, dim3(kThreads), 0, st, x, wk, y, d->batch, d->height,
+                               d->width, Ho, Wo, d->pad, tr, tc);
+        else if (ci == 16 && co == 32)
+            hipLaunchKernelGGL((conv3_x6_kernel<16, 32>), g2, dim3(kThreads), 0, st, x, wk, y, d->batch, d->height,
+                               d->width, Ho, Wo, d->pad, tr, tc);
+        else
+            return md2_report_error(MD2_ERR_ARG, "conv_direct: (in, out) channels (16,16), (32,16) or (16,32)");
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+    }
     // the LDS-tiled form where it measured faster: 16 output channels (16->16 forward /
     // input gradient 95 / 100 vs 104 / 104 us, 32->16 forward 72 vs 83 us); with 32
     // output channels (the 32->16 layer's input gradient) the global form (56 vs 76 us)

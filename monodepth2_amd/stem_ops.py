@@ -14,6 +14,7 @@ that needs a gradient, bf16, NCHW inputs, a CPU tensor) runs the module itself.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -23,7 +24,7 @@ from . import _lib
 
 _CL = torch.channels_last
 ENABLED = True       # the x6 weight gradient (tests flip it to compare with MIOpen)
-FWD_ENABLED = True   # the x6 forward (C = 3 / 6)
+FWD_ENABLED = os.environ.get("MD2_STEM_FWD", "1") != "0"   # the x6 forward (C = 3 / 6); 0: MIOpen's (A/B)
 
 
 def _fwd(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:

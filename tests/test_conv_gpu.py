@@ -281,20 +281,23 @@ def test_plane_bank_refresh_matches_per_call_split():
 
 
 @pytest.mark.parametrize("B,C,N,p,H,W", [(2, 16, 16, 0, 20, 34), (2, 32, 16, 0, 12, 18), (2, 16, 32, 1, 9, 13),
-                                         (1, 16, 16, 1, 7, 9), (3, 32, 16, 2, 5, 6)])
-def test_direct_conv_matches_miopen(B, C, N, p, H, W):
-    """md2_conv_direct (f32 VALU, one thread per output pixel) for the DepthDecoder's
-    16-output-channel layers: forward and input gradient vs MIOpen fp32 (the two are
-    f32 FMA chains in different orders)."""
+                                         (1, 16, 16, 1, 7, 9), (3, 32, 16, 2, 5, 6), (2, 16, 16, 0, 70, 131),
+                                         (1, 32, 16, 1, 9, 200)])
+@pytest.mark.parametrize("flags", [0, conv_ops.X6], ids=["valu", "x6"])
+def test_direct_conv_matches_miopen(B, C, N, p, H, W, flags):
+    """md2_conv_direct for the DepthDecoder's 16-output-channel layers — f32 VALU (one
+    thread per output pixel) or split-bf16 MFMA (X6, weights in registers, patch planes
+    in LDS; partial 4 x 64 tiles at the ragged sizes): forward and input gradient vs
+    MIOpen fp32 (f32-class sums in different orders)."""
     torch.manual_seed(B * 10 + C + N + p)
     x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
     w = (torch.randn(N, C, 3, 3, device="cuda") / (9 * C) ** 0.5).contiguous(memory_format=CL)
-    y = conv_ops._direct_fwd(x, w, p)
+    y = conv_ops._direct_fwd(x, w, p, flags)
     yr = F.conv2d(x, w, padding=p)
     assert y.shape == yr.shape and y.is_contiguous(memory_format=CL)
     assert _rel(y, yr) < 2e-5
     gy = torch.randn_like(yr).contiguous(memory_format=CL)
-    gx = conv_ops._direct_dgrad(gy, w, p)
+    gx = conv_ops._direct_dgrad(gy, w, p, flags)
     gxr = torch.ops.aten.convolution_backward(gy, x, w, None, (1, 1), (p, p), (1, 1), False, (0, 0), 1,
                                               (True, False, False))[0]
     assert gx.shape == x.shape
