@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 17
+#define MD2_ABI_VERSION 18
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -541,6 +541,13 @@ int md2_conv_fwd(const md2_conv_desc* desc, const float* x, const float* weight,
  * over its taps, scattered into grad_x) */
 int md2_conv_dgrad(const md2_conv_desc* desc, const float* grad_y, const float* weight, float* grad_x,
                    void* workspace, void* stream);
+/* The gather half of a strided input gradient computed as one GEMM: cols (batch, Ho, Wo,
+ * kernel_h, kernel_w, in_channels) — grad_y times the weight as [out][(kh, kw, ci)], a 1x1
+ * md2_conv_fwd with kernel_h*kernel_w*in_channels outputs — summed into grad_x (batch,
+ * height, width, in_channels): each pixel gathers its taps in (kh, kw) order, written
+ * (not accumulated).  in_channels % 4; replaces the parity-class launches of a stride-2
+ * md2_conv_dgrad (MIOpen's backward-data convolution, networks/resnet_encoder.py). */
+int md2_conv_col2im(const md2_conv_desc* desc, const float* cols, float* grad_x, void* stream);
 /* grad_weight (out_channels, kernel_h, kernel_w, in_channels) = channels_last layout */
 int md2_conv_wgrad(const md2_conv_desc* desc, const float* x, const float* grad_y, float* grad_weight,
                    void* workspace, void* stream);

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -62,7 +62,7 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_pose_fwd", "md2_pose_bwd", "md2_aug_plan_create", "md2_aug_plan_destroy", "md2_aug_run",
            "md2_bn_workspace_bytes", "md2_bn_fwd", "md2_bn_bwd", "md2_maxpool3s2_fwd", "md2_maxpool3s2_bwd",
            "md2_disp_head_workspace_bytes", "md2_disp_head_fwd", "md2_disp_head_bwd",
-           "md2_stem_wgrad_workspace_bytes", "md2_stem_wgrad", "md2_stem_fwd", "md2_bias_act_fwd", "md2_bias_act_bwd",
+           "md2_stem_wgrad_workspace_bytes", "md2_stem_wgrad", "md2_stem_fwd", "md2_conv_col2im", "md2_bias_act_fwd", "md2_bias_act_bwd",
            "md2_bias_act_workspace_bytes", "md2_maxpool3s2_bwd_add", "md2_bn_bwd_multi",
            "md2_conv_fwd", "md2_conv_workspace_bytes", "md2_conv_split_weights",
            "md2_conv_dgrad", "md2_conv_wgrad", "md2_conv_direct", "md2_conv_wgrad_direct",
@@ -191,6 +191,8 @@ def _declare(L):
     L.md2_stem_wgrad.restype = ctypes.c_int
     L.md2_stem_wgrad.argtypes = [ctypes.POINTER(StemDesc)] + [_vp] * 5
     L.md2_stem_fwd.restype = ctypes.c_int
+    L.md2_conv_col2im.restype = ctypes.c_int
+    L.md2_conv_col2im.argtypes = [ctypes.POINTER(ConvDesc)] + [_vp] * 3
     L.md2_stem_fwd.argtypes = [ctypes.POINTER(StemDesc)] + [_vp] * 4
     L.md2_disp_head_workspace_bytes.restype = ctypes.c_size_t
     L.md2_disp_head_workspace_bytes.argtypes = [ctypes.POINTER(HeadDesc)]

@@ -128,6 +128,22 @@ def _dgrad(gy, x, w, pad, flags=0, stride=1):
     return gx
 
 
+def _dgrad_col(gy, x, w, stride, pad, flags):
+    """A strided input gradient as ONE GEMM and a gather: cols = gy x W' with W'[(kh, kw,
+    c)][n] = w[n][c][kh][kw] (a 1x1 x6 forward, KH*KW*C outputs), then md2_conv_col2im
+    sums each grad_x pixel's taps.  Every GEMM tile has the same K (the parity-class form
+    runs 1-, 2- and 4-tap GEMMs, the heaviest setting the time)."""
+    N, C, KH, KW = w.shape
+    B, _, H, W = x.shape
+    wcol = w.permute(2, 3, 1, 0).reshape(KH * KW * C, N, 1, 1).contiguous()
+    cols = _fwd(gy, wcol, 1, 0, flags)
+    gx = torch.empty_like(x, memory_format=_CL)
+    d = _lib.ConvDesc(B, H, W, C, N, KH, KW, stride, pad, 0)
+    _lib.check(_lib.lib().md2_conv_col2im(ctypes.byref(d), cols.data_ptr(), gx.data_ptr(), _lib.stream(x.device)),
+               "md2_conv_col2im")
+    return gx
+
+
 def _x6_ok(x, w) -> bool:
     return x.shape[1] % 8 == 0 and w.shape[0] % 8 == 0
 
@@ -510,14 +526,18 @@ class _Conv(torch.autograd.Function):
                     mi_x = True
             elif _x6_s2_ok(x, w, s):
                 # per-class launches (K split) / the four classes in one launch
+                # or one GEMM over every tap + a gather (x6_col)
                 sf = (X6, X6 | S2_ONE)
                 cands = [(lambda f=f: _dgrad(gy, x, w, p, f, 2)) for f in sf] + \
+                    [lambda: _dgrad_col(gy, x, w, s, p, X6), lambda: _dgrad_col(gy, x, w, s, p, X6 | BM256)] + \
                     [lambda: _miopen_bwd(gy, x, w, s, p, (True, False, False))[0]]
-                i = _fastest("dgrad", ctx.key, cands, ["x6_s2", "x6_s2one", "miopen"])
+                i = _fastest("dgrad", ctx.key, cands, ["x6_s2", "x6_s2one", "x6_col", "x6_col_256", "miopen"])
                 if i < len(sf) and planes_dg is None:
                     planes_dg = _bank_dgrad(x, w, s, p)
                 if i < len(sf):
                     gx = (_dgrad_planes(gy, x, w, planes_dg, p, sf[i], 2) if planes_dg is not None else cands[i]())
+                elif i < len(cands) - 1:
+                    gx = cands[i]()
                 else:
                     mi_x = True
             else:

@@ -138,11 +138,23 @@ __global__ void __launch_bounds__(kThreads) bn_stats_kernel(const void* __restri
 // sums in thread 0.
 __device__ bool channel_sums(Work w, int rows, int r0, int G, int C, int c, double& a, double& b) {
     __shared__ double red[2][kThreads / 64];
+    // G <= kMaxBlocks = 4 x 256: all of a thread's (up to four) partial pairs are loaded
+    // at once, then added in row order — one L2 round trip instead of a dependent chain
+    // of them (5.0-6.2 us per launch with the rolled loop)
+    static_assert(kMaxBlocks <= 4 * kThreads, "four partial rows per thread at most");
+    float pa[4], pb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int g = threadIdx.x + u * kThreads;
+        pa[u] = g < G ? w.part[(size_t)(r0 + g) * C + c] : 0.f;
+        pb[u] = g < G ? w.part[((size_t)rows + r0 + g) * C + c] : 0.f;
+    }
     a = 0.0;
     b = 0.0;
-    for (int g = threadIdx.x; g < G; g += kThreads) {
-        a += w.part[(size_t)(r0 + g) * C + c];
-        b += w.part[((size_t)rows + r0 + g) * C + c];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        a += pa[u];
+        b += pb[u];
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {

@@ -2169,6 +2169,46 @@ int run_dgrad_s2(const md2_conv_desc* d, const float* gy, const float* w, float*
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }
 
+// Input gradient of a strided convolution as ONE dense GEMM plus a gather: cols
+// (B, Ho, Wo, KH, KW, C) = grad_y (B, Ho, Wo, N) x W'[N][(kh, kw, c)] (a 1x1 forward
+// convolution with KH·KW·C output channels, run by the caller), then
+//   gx[b][y][x][c] = Σ_{kh, kw: y = s i - p + kh, x = s j - p + kw} cols[b][i][j][kh][kw][c]
+// — each grad_x pixel gathers its 1, 2 or 4 (stride 2, 3x3) tap contributions in (kh, kw)
+// order: deterministic, no atomics.  The GEMM's tiles are all the same K (N), where the
+// parity-class form runs four GEMMs of 1, 2, 2 and 4 taps whose heaviest sets the time.
+// One thread per grad_x pixel and channel quad.
+__global__ __launch_bounds__(256) void conv_col2im_kernel(const float4* __restrict__ cols, float4* __restrict__ gx,
+                                                          int B, int H, int W, int Q, int Ho, int Wo, int KH, int KW,
+                                                          int stride, int pad) {
+    const long long n = (long long)B * H * W * Q;
+    for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < n; t += (long long)gridDim.x * 256) {
+        const int q = (int)(t % Q);
+        long long r = t / Q;
+        const int x = (int)(r % W);
+        r /= W;
+        const int y = (int)(r % H), b = (int)(r / H);
+        float4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int kh = 0; kh < KH; ++kh) {
+            const int ty = y + pad - kh;
+            if (ty < 0 || ty % stride) continue;
+            const int i = ty / stride;
+            if (i >= Ho) continue;
+            for (int kw = 0; kw < KW; ++kw) {
+                const int tx = x + pad - kw;
+                if (tx < 0 || tx % stride) continue;
+                const int j = tx / stride;
+                if (j >= Wo) continue;
+                const float4 v = cols[(((size_t)(b * Ho + i) * Wo + j) * (KH * KW) + kh * KW + kw) * Q + q];
+                acc.x += v.x;
+                acc.y += v.y;
+                acc.z += v.z;
+                acc.w += v.w;
+            }
+        }
+        gx[t] = acc;
+    }
+}
+
 int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float* out, void* ws, void* stream,
         const char* name) {
     ConvArgs a = (mode == MODE_WGRAD && use_x6(d, mode)) ? args_x6_wgrad(d) : args_of(d, mode);
@@ -2301,6 +2341,24 @@ int md2_conv_wgrad(const md2_conv_desc* d, const float* x, const float* grad_y, 
     if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "conv_wgrad: channels % 4, pad < kernel, sizes < 2^29");
     if (!x || !grad_y || !grad_weight) return md2_report_error(MD2_ERR_ARG, "conv_wgrad: NULL operand");
     return run(d, MODE_WGRAD, x, grad_y, grad_weight, workspace, stream, "conv_wgrad: workspace required (K split)");
+}
+
+int md2_conv_col2im(const md2_conv_desc* d, const float* cols, float* grad_x, void* stream) {
+    if (!d || !cols || !grad_x) return md2_report_error(MD2_ERR_ARG, "conv_col2im: NULL operand");
+    if (d->in_channels % 4 || d->stride < 1 || d->pad < 0 || d->kernel_h < 1 || d->kernel_w < 1 || d->batch < 1 ||
+        d->height < 1 || d->width < 1)
+        return md2_report_error(MD2_ERR_ARG, "conv_col2im: channels % 4, stride >= 1, pad >= 0");
+    const int Ho = (d->height + 2 * d->pad - d->kernel_h) / d->stride + 1;
+    const int Wo = (d->width + 2 * d->pad - d->kernel_w) / d->stride + 1;
+    if (Ho < 1 || Wo < 1) return md2_report_error(MD2_ERR_ARG, "conv_col2im: empty output");
+    const int Q = d->in_channels / 4;
+    const long long n = (long long)d->batch * d->height * d->width * Q;
+    const long long blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(conv_col2im_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0,
+                       (hipStream_t)stream, (const float4*)cols, (float4*)grad_x, d->batch, d->height, d->width, Q,
+                       Ho, Wo, d->kernel_h, d->kernel_w, d->stride, d->pad);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }
 
 }  // extern "C"

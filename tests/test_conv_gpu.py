@@ -201,6 +201,10 @@ def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
         for fl in XFLAGS:
             e_x6 = _rel(conv_ops._dgrad(gy, x, w, p, fl, s).double().cpu(), gref)
             assert e_x6 < max(3 * e_mi, 1e-7) and e_x6 < 2e-6, (fl, s, e_x6, e_mi)
+        if s == 2:   # one GEMM over every tap + md2_conv_col2im's gather
+            for fl in (conv_ops.X6, conv_ops.X6 | conv_ops.BM256):
+                e_col = _rel(conv_ops._dgrad_col(gy, x, w, s, p, fl).double().cpu(), gref)
+                assert e_col < max(3 * e_mi, 1e-7) and e_col < 2e-6, (fl, e_col, e_mi)
     gy = torch.randn(ref.shape, device="cuda").contiguous(memory_format=CL)
     wref = torch.ops.aten.convolution_backward(gy.double().cpu(), x.double().cpu(), w.double().cpu(), None, (s, s),
                                                (p, p), (1, 1), False, (0, 0), 1, (False, True, False))[1]

@@ -1,5 +1,5 @@
 """Stride-2 input gradients of the step: per-class x6 launches vs the one-launch form
-(MD2_CONV_S2_ONE) vs MIOpen, ms per call.
+(MD2_CONV_S2_ONE) vs one GEMM + gather (conv_ops._dgrad_col) vs MIOpen, ms per call.
     python tools/s2_bench.py"""
 import json
 import os
@@ -12,7 +12,7 @@ import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 from conv_bench import CL, dgrad, timeit, rel  # noqa: E402
-from monodepth2_amd import _lib  # noqa: E402
+from monodepth2_amd import _lib, conv_ops  # noqa: E402
 
 X6, ONE, B256 = _lib.CONV_X6, _lib.CONV_S2_ONE, _lib.CONV_BM256
 SHAPES = [(12, 64, 128, 3, 1, 48, 160), (12, 128, 256, 3, 1, 24, 80), (12, 256, 512, 3, 1, 12, 40),
@@ -32,6 +32,9 @@ def main():
         for tag, fl in (("x6_s2", X6), ("one", X6 | ONE), ("one_256", X6 | ONE | B256)):
             row[tag] = round(timeit(lambda: dgrad(gy, x, w, 2, p, fl)), 4)
             row["err_" + tag] = float(rel(dgrad(gy, x, w, 2, p, fl), ref))
+        for tag, fl in (("col", X6), ("col_256", X6 | B256)):
+            row[tag] = round(timeit(lambda: conv_ops._dgrad_col(gy, x, w, 2, p, fl)), 4)
+            row["err_" + tag] = float(rel(conv_ops._dgrad_col(gy, x, w, 2, p, fl), ref))
         row["miopen"] = round(timeit(mi), 4)
         print(json.dumps(row), flush=True)
 
