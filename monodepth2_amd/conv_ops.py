@@ -441,11 +441,12 @@ def _direct(a: torch.Tensor, wk: torch.Tensor, pad: int, cout: int, flags: int =
     return y
 
 
-def _direct_wgrad(gy, x, w, pad):
-    """md2_conv_wgrad_direct: the weight gradient of a (16|32) -> 16 3x3 convolution."""
+def _direct_wgrad(gy, x, w, pad, flags=0):
+    """md2_conv_wgrad_direct: the weight gradient of a (16|32) -> 16 3x3 convolution (flags
+    X6: the split-bf16 MFMA form, else the f32 VALU form)."""
     N, C = w.shape[0], w.shape[1]
     gw = torch.empty_like(w, memory_format=_CL)
-    d = _desc(x, w, 1, pad)
+    d = _desc(x, w, 1, pad, flags)
     nbytes = _lib.lib().md2_conv_wgrad_direct_workspace_bytes(ctypes.byref(d))
     ws = _workspace(x.device, nbytes)
     _lib.check(_lib.lib().md2_conv_wgrad_direct(ctypes.byref(d), x.data_ptr(), gy.data_ptr(), gw.data_ptr(),
@@ -549,11 +550,11 @@ class _Conv(torch.autograd.Function):
             pw = x6 and w.shape[2] == 3 and w.shape[3] == 3 and s == 1
             cands = ([lambda: _wgrad(gy, x, w, s, p, X6)] if x6 else []) + \
                 ([lambda: _wgrad(gy, x, w, s, p, X6 | PATCH)] if pw else []) + [lambda: _wgrad(gy, x, w, s, p)] + \
-                ([lambda: _direct_wgrad(gy, x, w, p)] if direct else []) + \
+                ([lambda: _direct_wgrad(gy, x, w, p), lambda: _direct_wgrad(gy, x, w, p, X6)] if direct else []) + \
                 [lambda: _miopen_bwd(gy, x, w, s, p, (False, True, False))[1]]
             i = _fastest("wgrad", ctx.key, cands,
                          (["x6"] if x6 else []) + (["x6pw"] if pw else []) + ["f32mfma"] +
-                         (["direct"] if direct else []) + ["miopen"])
+                         (["direct", "direct_x6"] if direct else []) + ["miopen"])
             if i < len(cands) - 1:
                 gw = cands[i]()
             else:

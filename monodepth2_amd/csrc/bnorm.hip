@@ -53,7 +53,9 @@ __host__ __device__ inline Map make_map(int C) {
     return m;
 }
 
-// workspace layout (floats): partial[2][NG*G][C] (row = group*G + block) | coef[3][NG][C]
+// workspace layout (floats): partial[2][C][NG*G] (channel-major: a channel's partials,
+// row = group*G + block, contiguous for the finalising block's coalesced reads) |
+// coef[3][NG][C]
 struct Work {
     float* part;
     float* coef;
@@ -94,8 +96,10 @@ __device__ void block_partials(float4 a, float4 b, int q, int pl, const Map& m, 
         __syncthreads();
     }
     if (pl == 0) {
-        st4(w.part + (size_t)row * C + 4 * q, a);
-        st4(w.part + ((size_t)rows + row) * C + 4 * q, b);
+        float* pa = w.part + (size_t)(4 * q) * rows + row;
+        float* pb = w.part + ((size_t)C + 4 * q) * rows + row;
+        pa[0] = a.x; pa[rows] = a.y; pa[2 * (size_t)rows] = a.z; pa[3 * (size_t)rows] = a.w;
+        pb[0] = b.x; pb[rows] = b.y; pb[2 * (size_t)rows] = b.z; pb[3 * (size_t)rows] = b.w;
     }
     __syncthreads();
 }
@@ -139,15 +143,16 @@ __global__ void __launch_bounds__(kThreads) bn_stats_kernel(const void* __restri
 __device__ bool channel_sums(Work w, int rows, int r0, int G, int C, int c, double& a, double& b) {
     __shared__ double red[2][kThreads / 64];
     // G <= kMaxBlocks = 4 x 256: all of a thread's (up to four) partial pairs are loaded
-    // at once, then added in row order — one L2 round trip instead of a dependent chain
-    // of them (5.0-6.2 us per launch with the rolled loop)
+    // at once, coalesced (the channel's partials are contiguous), then added in row order
     static_assert(kMaxBlocks <= 4 * kThreads, "four partial rows per thread at most");
+    const float* ca = w.part + (size_t)c * rows + r0;
+    const float* cb = w.part + ((size_t)C + c) * rows + r0;
     float pa[4], pb[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int g = threadIdx.x + u * kThreads;
-        pa[u] = g < G ? w.part[(size_t)(r0 + g) * C + c] : 0.f;
-        pb[u] = g < G ? w.part[((size_t)rows + r0 + g) * C + c] : 0.f;
+        pa[u] = g < G ? ca[g] : 0.f;
+        pb[u] = g < G ? cb[g] : 0.f;
     }
     a = 0.0;
     b = 0.0;

@@ -1411,7 +1411,6 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
     }
 }
 
-
 // Patch-staged split-bf16 weight gradient (MD2_CONV_X6 | MD2_CONV_PATCH; 3x3, stride 1).
 // conv_x6_wgrad_kernel stages x once per (tap, ci) column, so every activation is
 // fetched and split nine times.  Here a K chunk is one 32-pixel segment of one output

@@ -258,6 +258,150 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_kernel(const float* __re
     }
 }
 
+// Weight gradient on split-bf16 MFMA (MD2_CONV_X6): per tap a 16 x CIN GEMM over the
+// output pixels, D_tap[co][ci] += Σ_p gy[p][co] · x[p + tap][ci] — K runs over pixels, so
+// both operands need eight consecutive pixels of ONE channel per lane, the transpose of
+// the NHWC layout.  The block stages its tile's gy (4 x 64 pixels x 16) and input patch
+// ((4+2) x (64+2) x CIN) as three bf16 planes each, pixel-major as in memory, and reads
+// the fragments with ds_read_b64_tr_b16, the hardware transpose read: lane 4q+p of a
+// 16-lane group points at pixel q's channels 4p..4p+3, lane i receives channel i of
+// the four pixels.  Two reads give a lane its eight pixels; a tap's window shift is a
+// different pixel per lane, so the nine taps read the one patch (no shifted copies).
+// Pixels are stored XOR-swizzled so the two 16-lane groups of a 32-lane half (pixels
+// 8 apart) land on disjoint banks.  A wave owns output row w of the tile and the 9 x
+// CIN/16 accumulators of all taps for the block's whole walk; the waves' sums meet in
+// LDS in wave order and each block writes one partial row [16][9][CIN], summed in block
+// order by conv3_wgrad_reduce_kernel (deterministic, no atomics).
+template <int C>
+__device__ __forceinline__ int wg_off(int pix, int q4) {   // bf16 offset of channel quad q4 of pixel pix
+    if constexpr (C == 16) return ((pix ^ (((pix >> 3) & 1) << 2)) * 16) + 4 * q4;
+    else return pix * 32 + 4 * (q4 ^ (((pix >> 3) & 1) << 2));
+}
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ s16x4 tr_read(const __bf16* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+}
+
+template <int CIN, int TR>
+__global__ __launch_bounds__(kThreads, 2) void conv3_x6_wgrad_kernel(const float* __restrict__ x,
+                                                                     const float* __restrict__ gy,
+                                                                     float* __restrict__ part, int B, int H, int W,
+                                                                     int Ho, int Wo, int pad, int tiles_r,
+                                                                     int tiles_c) {
+    // TR tile rows: 4 (wave w: row w, both 32-pixel steps) or 2 (CIN 32, whose patch
+    // planes would otherwise leave room for one block per CU: wave w: row w/2, step w%2)
+    constexpr int COUT = 16, PR = TR + 2, PC = kXC + 2, CB = CIN / 16, KSW = TR == 4 ? 2 : 1;
+    static_assert(TR == 4 || TR == 2, "tile rows");
+    // bf16 per plane; the pixel swizzle permutes within aligned groups of 16 pixels, so the
+    // patch plane is padded to whole groups (396 -> 400 pixels)
+    constexpr int XE = (PR * PC + 15) / 16 * 16 * CIN, GE = TR * kXC * COUT;
+    __shared__ __attribute__((aligned(16))) __bf16 xs[3][XE];
+    __shared__ __attribute__((aligned(16))) __bf16 gs[3][GE];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int g16 = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+    f32x4 acc[9][CB];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) acc[t][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto put = [&](__bf16* base, int stride, int off, float4 v) {
+        const float e[4] = {v.x, v.y, v.z, v.w};
+        float c[3][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float a0 = x6_trunc16(e[j]), r1 = e[j] - a0, a1 = x6_trunc16(r1);
+            c[0][j] = a0;
+            c[1][j] = a1;
+            c[2][j] = r1 - a1;
+        }
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+            *(u32x2*)(base + pl * stride + off) = u32x2{x6_hi16x2(c[pl][0], c[pl][1]), x6_hi16x2(c[pl][2], c[pl][3])};
+    };
+    const int ntiles = B * tiles_r * tiles_c;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int tcb = t % tiles_c, rest = t / tiles_c, trb = rest % tiles_r, b = rest / tiles_r;
+        const int oh0 = trb * TR, ow0 = tcb * kXC;
+        for (int i = tid; i < PR * PC * CIN / 4; i += kThreads) {   // input patch, zeros outside the image
+            const int pix = i / (CIN / 4), q4 = i - pix * (CIN / 4), pr = pix / PC, pc = pix - pr * PC;
+            const int ih = oh0 - pad + pr, iw = ow0 - pad + pc;
+            float4 v = {0.f, 0.f, 0.f, 0.f};
+            if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+                v = ((const float4*)x)[((size_t)(b * H + ih) * W + iw) * (CIN / 4) + q4];
+            put(&xs[0][0], XE, wg_off<CIN>(pix, q4), v);
+        }
+        for (int i = tid; i < GE / 4; i += kThreads) {   // output gradient, zeros past the output
+            const int pix = i >> 2, q4 = i & 3, pr = pix / kXC, pc = pix - pr * kXC;
+            const int oh = oh0 + pr, ow = ow0 + pc;
+            float4 v = {0.f, 0.f, 0.f, 0.f};
+            if (oh < Ho && ow < Wo) v = ((const float4*)gy)[((size_t)(b * Ho + oh) * Wo + ow) * 4 + q4];
+            put(&gs[0][0], GE, wg_off<16>(pix, q4), v);
+        }
+        __syncthreads();
+        const int wrow = TR == 4 ? wid : wid >> 1, ks0 = TR == 4 ? 0 : wid & 1;
+#pragma unroll
+        for (int kk = 0; kk < KSW; ++kk) {
+            const int ks = ks0 + kk;
+            // A = gy^T: row co = lane & 15, k = pixel 8 g16 + j of this 32-pixel step
+            bf16x8 fa[3];
+            const int gp = wrow * kXC + 32 * ks + 8 * g16 + q;
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                const s16x4 lo = tr_read(&gs[pl][wg_off<16>(gp, p4)]), hi = tr_read(&gs[pl][wg_off<16>(gp + 4, p4)]);
+                fa[pl] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int kh = tap / 3, kw = tap - kh * 3;
+                const int xp = (wrow + kh) * PC + 32 * ks + 8 * g16 + q + kw;
+#pragma unroll
+                for (int cb = 0; cb < CB; ++cb) {
+                    bf16x8 fb[3];
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl) {
+                        const s16x4 lo = tr_read(&xs[pl][wg_off<CIN>(xp, 4 * cb + p4)]),
+                                    hi = tr_read(&xs[pl][wg_off<CIN>(xp + 4, 4 * cb + p4)]);
+                        fb[pl] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                    }
+                    f32x4 c = acc[tap][cb];
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fb[0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[2], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[1], c, 0, 0, 0);
+                    acc[tap][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[0], c, 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();   // the planes are restaged for the next tile
+    }
+    // the four waves' sums in wave order through LDS (the x planes, free now):
+    // ((w0 + w1) + w2) + w3, then this block's partial row [co][tap][ci]:
+    // D[row = co = 4 g16 + e][col = ci = 16 cb + lane & 15]
+    float* red = (float*)&xs[0][0];
+    static_assert(9 * CB * 256 * 4 <= 3 * XE * 2, "reduction buffer fits in the patch planes");
+    for (int w = 0; w < 4; ++w) {
+        if (wid == w) {
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+                for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float* r = &red[(tap * CB + cb) * 256 + e * 64 + lane];
+                        *r = w == 0 ? acc[tap][cb][e] : *r + acc[tap][cb][e];
+                    }
+        }
+        __syncthreads();
+    }
+    float* out = part + (size_t)blockIdx.x * COUT * 9 * CIN;
+    for (int i = tid; i < 9 * CB * 256; i += kThreads) {
+        const int tc = i >> 8, r = i & 255, e = r >> 6, l = r & 63, tap = tc / CB, cb = tc - tap * CB;
+        const int co = 4 * (l >> 4) + e, ci = 16 * cb + (l & 15);
+        out[(co * 9 + tap) * CIN + ci] = red[i];
+    }
+}
+
 bool direct_lds() {   // A/B knob: MD2_DIRECT_LDS=0 selects the global-load form
     static const bool on = [] {
         const char* e = getenv("MD2_DIRECT_LDS");
@@ -484,6 +628,34 @@ int md2_conv_wgrad_direct(const md2_conv_desc* d, const float* x, const float* g
     const long long P = (long long)d->batch * Ho * Wo;
     if (P * 32 >= (1ll << 31) || (long long)d->batch * d->height * d->width * 32 >= (1ll << 31))
         return md2_report_error(MD2_ERR_ARG, "conv_wgrad_direct: tensors of < 2^26 pixels");
+    const hipStream_t st0 = (hipStream_t)stream;
+    if (d->flags & MD2_CONV_X6) {
+        if (d->out_channels != 16 || (d->in_channels != 16 && d->in_channels != 32))
+            return md2_report_error(MD2_ERR_ARG, "conv_wgrad_direct: (in, out) channels (16,16) or (32,16)");
+        static const int tr16 = [] {   // A/B knob: MD2_WGRAD_TR16=2 runs the 16-channel form on 2-row tiles
+            const char* e = getenv("MD2_WGRAD_TR16");
+            return e && e[0] == '2' ? 2 : 4;
+        }();
+        const int TRW = d->in_channels == 16 ? tr16 : 2;
+        const int tr = (Ho + TRW - 1) / TRW, tc = (Wo + kXC - 1) / kXC;
+        const long long nt = (long long)d->batch * tr * tc;
+        const int nb = (int)(nt < kWBlocks ? nt : kWBlocks);
+        float* part = (float*)workspace;
+        if (d->in_channels == 16 && TRW == 4)
+            hipLaunchKernelGGL((conv3_x6_wgrad_kernel<16, 4>), dim3(nb), dim3(kThreads), 0, st0, x, grad_y, part,
+                               d->batch, d->height, d->width, Ho, Wo, d->pad, tr, tc);
+        else if (d->in_channels == 16)
+            hipLaunchKernelGGL((conv3_x6_wgrad_kernel<16, 2>), dim3(nb), dim3(kThreads), 0, st0, x, grad_y, part,
+                               d->batch, d->height, d->width, Ho, Wo, d->pad, tr, tc);
+        else
+            hipLaunchKernelGGL((conv3_x6_wgrad_kernel<32, 2>), dim3(nb), dim3(kThreads), 0, st0, x, grad_y, part,
+                               d->batch, d->height, d->width, Ho, Wo, d->pad, tr, tc);
+        const int n = 16 * 9 * d->in_channels;
+        hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3((n + kRedO - 1) / kRedO), dim3(kThreads), 0, st0, part,
+                           grad_weight, n, nb);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+    }
     const int chunks = (int)((P + kWChunk - 1) / kWChunk);
     const int per = (chunks + kWBlocks - 1) / kWBlocks;
     const int nblk = (chunks + per - 1) / per;

@@ -497,7 +497,13 @@ class Trainer:
         dot = os.environ.get("MD2_GRAPH_DOT")
         if dot:
             self.graph.enable_debug_mode()
-        with torch.cuda.graph(self.graph):
+        # capture on the warm-up's stream: a parameter's AccumulateGrad node is created
+        # once and keeps the stream of its first backward, so capturing on torch's own
+        # capture stream after warming up on `side` made autograd accumulate those
+        # gradients across streams (its "AccumulateGrad node's stream does not match"
+        # warning at the capture; variants of this step traced 60 of 88 main-network
+        # parameters on the warm-up stream during the capture)
+        with torch.cuda.graph(self.graph, stream=side):
             self.static_outputs, self.static_losses = self._step_body(self.static_inputs)
         if dot:
             self.graph.debug_dump(dot)

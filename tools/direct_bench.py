@@ -38,5 +38,11 @@ for C, N, H, W in ((16, 16, 194, 642), (32, 16, 98, 322)):
          "x6": timed(lambda: conv_ops._direct_dgrad(gy, w, 0, conv_ops.X6)),
          "miopen": timed(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, (1, 1), (0, 0), (1, 1), False,
                                                                      (0, 0), 1, (True, False, False)))}
+    wg = {"valu": timed(lambda: conv_ops._direct_wgrad(gy, x, w, 0)),
+          "x6": timed(lambda: conv_ops._direct_wgrad(gy, x, w, 0, conv_ops.X6)),
+          "x6pw": timed(lambda: conv_ops._wgrad(gy, x, w, 1, 0, conv_ops.X6 | conv_ops.PATCH)),
+          "miopen": timed(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, (1, 1), (0, 0), (1, 1), False,
+                                                                      (0, 0), 1, (False, True, False)))}
     print(f"{C}->{N} {H}x{W}: fwd " + ", ".join(f"{k} {v:.4f}" for k, v in f.items()) +
-          " ms; dgrad " + ", ".join(f"{k} {v:.4f}" for k, v in d.items()) + " ms", flush=True)
+          " ms; dgrad " + ", ".join(f"{k} {v:.4f}" for k, v in d.items()) +
+          " ms; wgrad " + ", ".join(f"{k} {v:.4f}" for k, v in wg.items()) + " ms", flush=True)

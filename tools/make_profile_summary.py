@@ -39,7 +39,7 @@ def main():
     res = {}
     for r in rows:
         k = short(r["Name"])
-        if k.startswith(HOT) or any(t in k for t in ("conv_x6", "conv_wsplit", "stem_x6")):
+        if k.startswith(HOT) or any(t in k for t in ("conv_x6", "conv3_x6", "conv_wsplit", "stem_x6", "col2im", "bn_")):
             res.setdefault(k, {}).update(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
                                          share_of_gpu_time=float(r["TotalDurationNs"]) / total)
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
