@@ -33,6 +33,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <stdlib.h>
 
 #include "md2hot.h"
 
@@ -327,6 +328,141 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Weight gradient without the im2col build (round 4): per kernel row kh the GEMM
+// D_kh[co][n] += Σ_p dy[p][co] · X_kh[p][n], n = kw·CP + ci (CP = C padded to 4 / 8),
+// K = output pixels.  Both operands need eight consecutive PIXELS of one column per lane
+// — the transpose of the staged layouts — and gfx950's ds_read_b64_tr_b16 reads exactly
+// that: lane 4q+p of a 16-lane group addresses pixel q's four consecutive elements, lane
+// i receives element i of the four pixels.  dy is staged pixel-major ([px][64 co]) and
+// the seven input rows under the chunk column-major ([kh][col][CP]); the window of
+// output pixel px at tap (kh, kw) starts at column 2 px + kw, so the taps are just
+// per-lane addresses into the one staged copy — the old kernel built 7 x 21 x 32 tile
+// elements per 32 pixels (the build, not the MFMAs, set its time).  Wave kh (7 waves)
+// multiplies its kernel row for all 64 channels x 8·CP n; a chunk is 64 pixels of one
+// output row; all channel groups in one block (their dy fragments shared).  Same
+// partials as the old kernel ([group][split][64][147]), same final sum.
+constexpr int kTSeg = 64, kTWaves = 7, kTThreads = 64 * kTWaves;
+constexpr int kTCols = 144;   // staged input columns (2·63 + 7 + 1 = 134 used), padded for the column swizzle
+template <int CP>
+__device__ __forceinline__ int tr_xcol(int c) {   // C = 6: columns 16 apart on disjoint banks
+    return CP == 8 ? (c ^ (((c >> 4) & 1) << 3)) : c;
+}
+__device__ __forceinline__ int tr_goff(int px, int co4) {   // dy: 4 pixels of one parity on distinct banks
+    const int sw = ((px >> 1) & 1) | (((px >> 3) & 1) << 1);
+    return px * kCo + 4 * (co4 ^ (sw << 2));
+}
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bf16x8 tr_pair(const __bf16* lo, const __bf16* hi) {
+    const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)lo);
+    const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)hi);
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int C>
+__global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs a) {
+    constexpr int CP = C == 3 ? 4 : 8, NB = CP / 2;   // n blocks of 16 per kernel row
+    constexpr int XE = 7 * kTCols * CP, GE = kTSeg * kCo;
+    __shared__ __attribute__((aligned(16))) __bf16 xs[3][XE];
+    __shared__ __attribute__((aligned(16))) __bf16 gs[3][GE];
+    const int tid = threadIdx.x, lane = tid & 63, kh = tid >> 6;
+    const int ks = blockIdx.x;
+    const int t0 = ks * a.cps, n = min(a.cps, a.nchunks - t0);
+    const int g16 = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+    // the padding channels ci = C .. CP-1 are never staged: zero them once
+    for (int e = tid; e < 7 * kTCols * (CP - C); e += kTThreads) {
+        const int cell = e / (CP - C), ci = C + e % (CP - C);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) xs[pl][cell * CP + ci] = __bf16(0.f);
+    }
+    f32x4 acc[4][NB];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NB; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int H = a.H, W = a.W;
+    for (int t = 0; t < n; ++t) {
+        const int tt = t0 + t, rr = tt / a.nseg, seg = tt - rr * a.nseg, b = rr / a.Ho, oh = rr - b * a.Ho;
+        const int ow0 = seg * kTSeg, iw0 = 2 * ow0 - 3;
+        // dy: 64 pixels x 16 channel quads
+        for (int i = tid; i < kTSeg * 16; i += kTThreads) {
+            const int px = i >> 4, co4 = i & 15, ow = ow0 + px;
+            float4 v = {0.f, 0.f, 0.f, 0.f};
+            if (ow < a.Wo) v = *(const float4*)(a.gy + ((size_t)(b * a.Ho + oh) * a.Wo + ow) * kCo + 4 * co4);
+            const float e[4] = {v.x, v.y, v.z, v.w};
+            float c[3][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float a0 = trunc16(e[j]), r1 = e[j] - a0, a1 = trunc16(r1);
+                c[0][j] = a0;
+                c[1][j] = a1;
+                c[2][j] = r1 - a1;
+            }
+            const int o = tr_goff(px, co4);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) *(u32x2*)&gs[pl][o] = u32x2{hi16x2(c[pl][0], c[pl][1]), hi16x2(c[pl][2], c[pl][3])};
+        }
+        // the seven input rows: contiguous runs of 134 columns x C channels (zeros outside)
+        constexpr int RUN = (2 * kTSeg + 6) * C;
+        for (int e = tid; e < 7 * RUN; e += kTThreads) {
+            const int r = e / RUN, rem = e - r * RUN, col = rem / C, ci = rem - col * C;
+            const int ih = 2 * oh - 3 + r, iw = iw0 + col;
+            float v = 0.f;
+            if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) v = a.x[((size_t)(b * H + ih) * W + iw) * C + ci];
+            const float a0 = trunc16(v), r1 = v - a0, a1 = trunc16(r1);
+            const int o = (r * kTCols + tr_xcol<CP>(col)) * CP + ci;
+            xs[0][o] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, a0) >> 16));
+            xs[1][o] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, a1) >> 16));
+            xs[2][o] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, r1 - a1) >> 16));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < kTSeg / 32; ++kk) {
+            const int px = 32 * kk + 8 * g16 + q;   // this lane's pixel of the tr reads (and + 4)
+            bf16x8 fb[NB][3];
+#pragma unroll
+            for (int ni = 0; ni < NB; ++ni) {
+                const int n0 = 16 * ni + 4 * p4, kw = n0 / CP, ci0 = n0 - kw * CP;
+                const int olo = (kh * kTCols + tr_xcol<CP>(2 * px + kw)) * CP + ci0;
+                const int ohi = (kh * kTCols + tr_xcol<CP>(2 * (px + 4) + kw)) * CP + ci0;
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fb[ni][pl] = tr_pair(&xs[pl][olo], &xs[pl][ohi]);
+            }
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                bf16x8 fa[3];
+                const int glo = tr_goff(px, 4 * mi + p4), ghi = tr_goff(px + 4, 4 * mi + p4);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fa[pl] = tr_pair(&gs[pl][glo], &gs[pl][ghi]);
+#pragma unroll
+                for (int ni = 0; ni < NB; ++ni) {
+                    f32x4 c = acc[mi][ni];
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fb[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[ni][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[ni][2], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[ni][1], c, 0, 0, 0);
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[ni][0], c, 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();   // restaged next chunk
+    }
+    // D[row = co = 16 mi + 4 g16 + e][col = n = 16 ni + lane & 15], n = kw·CP + ci
+#pragma unroll
+    for (int ni = 0; ni < NB; ++ni) {
+        const int nn = 16 * ni + (lane & 15), kw = nn / CP, ci = nn - kw * CP;
+        if (kw >= 7 || ci >= C) continue;
+        const int cg = ci / kCG, cl = ci - cg * kCG;
+        float* out = a.part + ((size_t)cg * a.splits + ks) * kCo * kOut + (kh * 7 + kw) * kCG + cl;
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) out[(size_t)(16 * mi + 4 * g16 + e) * kOut] = acc[mi][ni][e];
+    }
+}
+
 // dW = Σ_splits partials: sixteen lanes per output, lane l summing splits l, l + 16, ...
 // in order, then the sixteen in lane order (deterministic); written in the weight's
 // memory format.  (Four lanes per output ran long serial chains over the ~500 splits.)
@@ -552,13 +688,35 @@ StemArgs plan(const md2_stem_desc* d) {
     return a;
 }
 
+// the transposed-read kernel (C = 3 / 6): 64-pixel chunks, all channel groups per block,
+// about two blocks per CU, at most 32 chunks (2048 pixels) per K split
+bool use_tr(const md2_stem_desc* d) {
+    static const bool tr = [] {   // MD2_STEM_WGRAD_TR=1: the transposed-read kernel (unverified: off)
+        const char* e = getenv("MD2_STEM_WGRAD_TR");
+        return e && e[0] == '1';
+    }();
+    return tr && (d->channels == 3 || d->channels == 6);
+}
+
+StemArgs plan_tr(const md2_stem_desc* d) {
+    StemArgs a = plan(d);
+    a.nseg = (a.Wo + kTSeg - 1) / kTSeg;
+    a.nchunks = a.B * a.Ho * a.nseg;
+    int want = 256 * 2;
+    const int need = (a.nchunks + 31) / 32;
+    want = want > need ? want : need;
+    a.cps = (a.nchunks + want - 1) / want;
+    a.splits = (a.nchunks + a.cps - 1) / a.cps;
+    return a;
+}
+
 }  // namespace
 
 extern "C" {
 
 size_t md2_stem_wgrad_workspace_bytes(const md2_stem_desc* d) {
     if (!valid(d)) return 0;
-    const StemArgs a = plan(d);
+    const StemArgs a = use_tr(d) ? plan_tr(d) : plan(d);
     return sizeof(float) * (size_t)(a.C / kCG) * a.splits * kCo * kOut;
 }
 
@@ -566,15 +724,22 @@ int md2_stem_wgrad(const md2_stem_desc* d, const float* x, const float* grad_y, 
                    void* stream) {
     if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "stem_wgrad: channels 3/6/9, 32-bit element count");
     if (!x || !grad_y || !grad_weight || !workspace) return md2_report_error(MD2_ERR_ARG, "stem_wgrad: NULL operand");
-    StemArgs a = plan(d);
+    const bool tr = use_tr(d);
+    StemArgs a = tr ? plan_tr(d) : plan(d);
     a.x = x;
     a.gy = grad_y;
     a.part = (float*)workspace;
     a.gw = grad_weight;
     const int NG = a.C / kCG;
     const hipStream_t st = (hipStream_t)stream;
-    void (*k)(StemArgs) = a.C == 3 ? stem_x6_wgrad_kernel<3> : a.C == 6 ? stem_x6_wgrad_kernel<6> : stem_x6_wgrad_kernel<9>;
-    hipLaunchKernelGGL(k, dim3(NG * ((a.splits + 7) / 8) * 8), dim3(kThreads), 0, st, a);
+    if (tr) {
+        void (*k)(StemArgs) = a.C == 3 ? stem_x6_wgrad_tr_kernel<3> : stem_x6_wgrad_tr_kernel<6>;
+        hipLaunchKernelGGL(k, dim3(a.splits), dim3(kTThreads), 0, st, a);
+    } else {
+        void (*k)(StemArgs) =
+            a.C == 3 ? stem_x6_wgrad_kernel<3> : a.C == 6 ? stem_x6_wgrad_kernel<6> : stem_x6_wgrad_kernel<9>;
+        hipLaunchKernelGGL(k, dim3(NG * ((a.splits + 7) / 8) * 8), dim3(kThreads), 0, st, a);
+    }
     const int outs = NG * kCo * kOut;
     hipLaunchKernelGGL(stem_wgrad_final_kernel, dim3((outs + kFinOut - 1) / kFinOut), dim3(256), 0, st, a);
     const hipError_t e = hipGetLastError();
