@@ -32,6 +32,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -2048,21 +2049,22 @@ void launch_fwd_t(const PhotoArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t 
 }
 // number of workgroups that can be resident at once for a kernel (cached per
 // kernel and device); the persistent-loop kernels launch exactly that many
+// (keyed by the kernel's address: every instantiation has the same function type, so a
+// per-template static would hand one instantiation's occupancy to all of them)
 template <class K>
 int resident_blocks(K kernel) {
     static std::mutex mu;
-    static int cache_dev = -1, cache_val = 0;
+    static std::map<std::pair<const void*, int>, int> cache;
     int dev = 0;
     (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> lk(mu);
-    if (dev != cache_dev) {
-        int cus = 0, per_cu = 0;
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0);
-        cache_val = max(1, cus) * max(1, per_cu);
-        cache_dev = dev;
-    }
-    return cache_val;
+    const auto key = std::make_pair((const void*)kernel, dev);
+    const auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int cus = 0, per_cu = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0);
+    return cache[key] = max(1, cus) * max(1, per_cu);
 }
 
 template <int NS, bool SSIM, bool MASK>

@@ -8,9 +8,10 @@
 // over every output pixel p — a GEMM with M = 64 output channels, N = 49·C window taps
 // and K = B·Ho·Wo output pixels (368k at B=12, 192x640).  MIOpen's backward-weights
 // kernel (igemm_wrw) runs it in ~125 / ~430 us at the step's shapes (C = 3, B = 12 /
-// C = 6, B = 24; 192x640); this one in ~100 / ~413 us with its split reduction.  Its
-// phases (fetch, build, multiply) do not overlap within a block — the next step for
-// it is producer waves that build chunk t+1 while the multiplying waves run chunk t.
+// C = 6, B = 24; 192x640); the im2col-build kernel below in ~100 / ~405 us with its split
+// reduction, and the transposed-read kernel (stem_x6_wgrad_tr_kernel, the default for
+// C = 3 / 6; MD2_STEM_WGRAD_BUILD=1 selects the build kernel) in ~0.082 / ~0.21 ms: the
+// build, not the multiply, set the old kernel's time.
 //
 // Here the channels go in groups of three (one frame; the pose encoder's pair is two
 // groups) padded to four, and K in chunks of one 32-pixel segment of one
@@ -343,11 +344,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // output row; all channel groups in one block (their dy fragments shared).  Same
 // partials as the old kernel ([group][split][64][147]), same final sum.
 constexpr int kTSeg = 64, kTWaves = 7, kTThreads = 64 * kTWaves;
-constexpr int kTCols = 144;   // staged input columns (2·63 + 7 + 1 = 134 used), padded for the column swizzle
-template <int CP>
-__device__ __forceinline__ int tr_xcol(int c) {   // C = 6: columns 16 apart on disjoint banks
-    return CP == 8 ? (c ^ (((c >> 4) & 1) << 3)) : c;
-}
+constexpr int kTCols = 136;   // staged input columns (2·63 + 7 + 1 = 134 used)
 __device__ __forceinline__ int tr_goff(int px, int co4) {   // dy: 4 pixels of one parity on distinct banks
     const int sw = ((px >> 1) & 1) | (((px >> 3) & 1) << 1);
     return px * kCo + 4 * (co4 ^ (sw << 2));
@@ -362,7 +359,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int C>
 __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs a) {
-    constexpr int CP = C == 3 ? 4 : 8, NB = CP / 2;   // n blocks of 16 per kernel row
+    // CP: channels per staged column — 3 padded to 4 (a column pair is then 8-byte
+    // aligned for the tr read); 6 unpadded (24-byte column pairs are 8-byte aligned, a
+    // 4-element read may run into the next column, which is the next window tap anyway):
+    // 48 instead of 64 n per kernel row for 42 real
+    constexpr int CP = C == 3 ? 4 : 6, NB = (7 * CP + 15) / 16;   // n blocks of 16 per kernel row
     constexpr int XE = 7 * kTCols * CP, GE = kTSeg * kCo;
     __shared__ __attribute__((aligned(16))) __bf16 xs[3][XE];
     __shared__ __attribute__((aligned(16))) __bf16 gs[3][GE];
@@ -370,12 +371,6 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
     const int ks = blockIdx.x;
     const int t0 = ks * a.cps, n = min(a.cps, a.nchunks - t0);
     const int g16 = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
-    // the padding channels ci = C .. CP-1 are never staged: zero them once
-    for (int e = tid; e < 7 * kTCols * (CP - C); e += kTThreads) {
-        const int cell = e / (CP - C), ci = C + e % (CP - C);
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) xs[pl][cell * CP + ci] = __bf16(0.f);
-    }
     f32x4 acc[4][NB];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
@@ -403,18 +398,64 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) *(u32x2*)&gs[pl][o] = u32x2{hi16x2(c[pl][0], c[pl][1]), hi16x2(c[pl][2], c[pl][3])};
         }
-        // the seven input rows: contiguous runs of 134 columns x C channels (zeros outside)
-        constexpr int RUN = (2 * kTSeg + 6) * C;
-        for (int e = tid; e < 7 * RUN; e += kTThreads) {
-            const int r = e / RUN, rem = e - r * RUN, col = rem / C, ci = rem - col * C;
-            const int ih = 2 * oh - 3 + r, iw = iw0 + col;
-            float v = 0.f;
-            if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) v = a.x[((size_t)(b * H + ih) * W + iw) * C + ci];
-            const float a0 = trunc16(v), r1 = v - a0, a1 = trunc16(r1);
-            const int o = (r * kTCols + tr_xcol<CP>(col)) * CP + ci;
-            xs[0][o] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, a0) >> 16));
-            xs[1][o] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, a1) >> 16));
-            xs[2][o] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, r1 - a1) >> 16));
+        if constexpr (CP == 4) {
+            // the seven input rows, one column (3 channels + a zero) per task: three
+            // loads, one 8-byte store per plane
+            for (int e = tid; e < 7 * (2 * kTSeg + 6); e += kTThreads) {
+                const int r = e / (2 * kTSeg + 6), col = e - r * (2 * kTSeg + 6);
+                const int ih = 2 * oh - 3 + r, iw = iw0 + col;
+                float v[4] = {0.f, 0.f, 0.f, 0.f};
+                if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
+                    const float* px = a.x + ((size_t)(b * H + ih) * W + iw) * C;
+#pragma unroll
+                    for (int ci = 0; ci < C; ++ci) v[ci] = px[ci];
+                }
+                const int o = (r * kTCols + col) * CP;
+                u32x2 pk[3];
+#pragma unroll
+                for (int j = 0; j < 4; j += 2) {
+                    const float a0 = trunc16(v[j]), r0 = v[j] - a0, m0 = trunc16(r0);
+                    const float a1 = trunc16(v[j + 1]), r1 = v[j + 1] - a1, m1 = trunc16(r1);
+                    pk[0][j / 2] = hi16x2(a0, a1);
+                    pk[1][j / 2] = hi16x2(m0, m1);
+                    pk[2][j / 2] = hi16x2(r0 - m0, r1 - m1);
+                }
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) *(u32x2*)&xs[pl][o] = pk[pl];
+            }
+        } else {
+            // C = 6: each row's 134 columns x 6 channels are one contiguous run of the
+            // NHWC input, staged as is: four floats per task, one 8-byte store per plane
+            constexpr int RQ = (2 * kTSeg + 6) * CP / 4;   // float quads per row run
+            for (int e = tid; e < 7 * RQ; e += kTThreads) {
+                const int r = e / RQ, k = 4 * (e - r * RQ);
+                const int ih = 2 * oh - 3 + r;
+                float v[4] = {0.f, 0.f, 0.f, 0.f};
+                if ((unsigned)ih < (unsigned)H) {
+                    const long long f0 = (long long)iw0 * C + k;   // element of the row, may be < 0
+                    const float* row = a.x + (size_t)(b * H + ih) * W * C;
+                    if (f0 >= 0 && f0 + 4 <= (long long)W * C) {
+                        const float4 q4 = *(const float4*)(row + f0);
+                        v[0] = q4.x; v[1] = q4.y; v[2] = q4.z; v[3] = q4.w;
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            if (f0 + i >= 0 && f0 + i < (long long)W * C) v[i] = row[f0 + i];
+                    }
+                }
+                const int o = r * kTCols * CP + k;
+                u32x2 pk[3];
+#pragma unroll
+                for (int j = 0; j < 4; j += 2) {
+                    const float a0 = trunc16(v[j]), r0 = v[j] - a0, m0 = trunc16(r0);
+                    const float a1 = trunc16(v[j + 1]), r1 = v[j + 1] - a1, m1 = trunc16(r1);
+                    pk[0][j / 2] = hi16x2(a0, a1);
+                    pk[1][j / 2] = hi16x2(m0, m1);
+                    pk[2][j / 2] = hi16x2(r0 - m0, r1 - m1);
+                }
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) *(u32x2*)&xs[pl][o] = pk[pl];
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -423,9 +464,10 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
             bf16x8 fb[NB][3];
 #pragma unroll
             for (int ni = 0; ni < NB; ++ni) {
-                const int n0 = 16 * ni + 4 * p4, kw = n0 / CP, ci0 = n0 - kw * CP;
-                const int olo = (kh * kTCols + tr_xcol<CP>(2 * px + kw)) * CP + ci0;
-                const int ohi = (kh * kTCols + tr_xcol<CP>(2 * (px + 4) + kw)) * CP + ci0;
+                // n0 = kw·CP + ci0: element (2 px + kw)·CP + ci0 = 2 px·CP + n0 of the row
+                const int n0 = 16 * ni + 4 * p4;
+                const int olo = (kh * kTCols + 2 * px) * CP + n0;
+                const int ohi = (kh * kTCols + 2 * (px + 4)) * CP + n0;
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl) fb[ni][pl] = tr_pair(&xs[pl][olo], &xs[pl][ohi]);
             }
@@ -691,11 +733,11 @@ StemArgs plan(const md2_stem_desc* d) {
 // the transposed-read kernel (C = 3 / 6): 64-pixel chunks, all channel groups per block,
 // about two blocks per CU, at most 32 chunks (2048 pixels) per K split
 bool use_tr(const md2_stem_desc* d) {
-    static const bool tr = [] {   // MD2_STEM_WGRAD_TR=1: the transposed-read kernel (unverified: off)
-        const char* e = getenv("MD2_STEM_WGRAD_TR");
+    static const bool build = [] {   // A/B knob: MD2_STEM_WGRAD_BUILD=1 runs the im2col-build kernel
+        const char* e = getenv("MD2_STEM_WGRAD_BUILD");
         return e && e[0] == '1';
     }();
-    return tr && (d->channels == 3 || d->channels == 6);
+    return !build && (d->channels == 3 || d->channels == 6);
 }
 
 StemArgs plan_tr(const md2_stem_desc* d) {

@@ -3,9 +3,10 @@ split-bf16 MFMA (csrc/stem.hip, ABI `md2_stem_*`): forward and weight gradient.
 
 The stem reads the normalised frames, which are data: its backward is the weight
 gradient alone, MIOpen's igemm_wrw at ~125 us (C=3, depth encoder, B=12) and ~430 us
-(C=6, pose encoder, B=24) per step at 192x640.  stem_x6_wgrad_kernel (f32-class:
-three exact bf16 planes, six products) runs them in ~80 / ~380 us including its
-split reduction (rocprofv3, tools/stem_bench.py under tools/kstats.sh).  The forward
+(C=6, pose encoder, B=24) per step at 192x640.  stem_x6_wgrad_tr_kernel (f32-class:
+three exact bf16 planes, six products; the window taps read from the staged rows with
+transposing LDS reads) runs them in ~0.082 / ~0.21 ms including its split reduction
+(tools/stem_bench.py; the earlier im2col-build kernel: ~0.10 / ~0.40 ms).  The forward
 (MIOpen's igemm_fwd: 89 / 334 us) runs on stem_x6_fwd_kernel for C = 3 / 6 (the input
 windows read straight from the NHWC rows as MFMA fragments, FWD_ENABLED).  Same
 parameter (the torchvision `conv1.weight`), same semantics; any other case (an input

@@ -24,7 +24,7 @@ def _no_worse(ours, ref, exact, rel=1e-6):
 
 
 @pytest.mark.parametrize("B,C,H,W", [(2, 3, 64, 128), (3, 6, 30, 50), (1, 9, 17, 23), (2, 3, 192, 640),
-                                     (1, 6, 7, 9)])
+                                     (1, 6, 7, 9), (2, 6, 192, 640), (1, 6, 9, 300)])
 @pytest.mark.parametrize("w_cl", [True, False])
 def test_stem_wgrad_matches_conv_backward(B, C, H, W, w_cl):
     torch.manual_seed(7)
