@@ -9,6 +9,7 @@ convolutions.  GPU tensors only; `DepthDecoder` uses the eager chain on the CPU.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -137,28 +138,29 @@ def disp_head(P: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor:
     return _DispHead.apply(P, conv.weight, conv.bias)
 
 
-class _ConvBiasAct(torch.autograd.Function):
-    """[relu](conv2d(x, w) + b): the convolution bias-free on MIOpen, the bias (+ ReLU)
-    in one HIP pass each way (md2_bias_act_*)."""
+_POSE_MIOPEN = os.environ.get("MD2_POSE_MIOPEN", "0") == "1"   # A/B knob: the pose decoder's convs on MIOpen
+
+
+class _BiasAct(torch.autograd.Function):
+    """[relu](z + b) in place on the convolution's own output z, one HIP pass each way
+    (md2_bias_act_*); z's gradient goes back to the convolution's backward."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, padding, relu: bool):
-        z = F.conv2d(x, weight, None, stride, padding)
-        if not z.is_contiguous(memory_format=_CL):
-            z = z.contiguous(memory_format=_CL)
+    def forward(ctx, z, bias, relu: bool):
         B, C, H, W = z.shape
         d = _lib.BiasActDesc(B * H * W, C, _lib.BIAS_ACT_RELU if relu else 0)
         _lib.check(_lib.lib().md2_bias_act_fwd(ctypes.byref(d), z.data_ptr(), bias.data_ptr(), z.data_ptr(),
                                                _lib.stream(z.device)),
-                   "md2_bias_act_fwd")                      # in place: z is this op's own buffer
-        ctx.save_for_backward(x, weight, z if relu else None)
-        ctx.conf = (stride, padding, relu, d)
+                   "md2_bias_act_fwd")                      # in place: z is the convolution's fresh output
+        ctx.mark_dirty(z)
+        ctx.save_for_backward(z if relu else None)
+        ctx.conf = (relu, d)
         return z
 
     @staticmethod
     def backward(ctx, gy):
-        x, weight, y = ctx.saved_tensors
-        stride, padding, relu, d = ctx.conf
+        y, = ctx.saved_tensors
+        relu, d = ctx.conf
         gy = gy.contiguous(memory_format=_CL)
         gb = torch.empty(gy.shape[1], device=gy.device, dtype=torch.float32)
         gz = torch.empty_like(gy, memory_format=_CL) if relu else gy
@@ -168,20 +170,25 @@ class _ConvBiasAct(torch.autograd.Function):
                                       gz.data_ptr() if relu else None, gb.data_ptr(), ws.data_ptr(),
                                       _lib.stream(gy.device)),
                    "md2_bias_act_bwd")
-        gx, gw, _ = torch.ops.aten.convolution_backward(
-            gz, x, weight, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
-            [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
-        return gx, gw, gb, None, None, None
+        return gz, gb, None
 
 
 def conv_bias_act(conv: torch.nn.Conv2d, x: torch.Tensor, relu: bool) -> torch.Tensor:
-    """relu?(conv(x)) with the bias (+ ReLU) as one HIP pass each way when x is a CUDA
-    fp32 channels_last tensor (the pose decoder of the default build); else eager."""
+    """relu?(conv(x)) for the pose decoder (networks/pose_decoder.py:43-54): the
+    convolution bias-free on conv_ops (split-bf16 MFMA kernels chosen per shape against
+    MIOpen, forward and both gradients), the bias (+ ReLU) as one HIP pass each way, when
+    x is a CUDA fp32 channels_last tensor; else eager."""
     if (x.is_cuda and x.dtype == torch.float32 and conv.weight.dtype == torch.float32 and conv.bias is not None
             and x.is_contiguous(memory_format=_CL) and conv.weight.is_contiguous(memory_format=_CL)
             and conv.out_channels % 4 == 0 and conv.groups == 1 and tuple(conv.dilation) == (1, 1)
-            and conv.padding_mode == "zeros" and not torch.is_autocast_enabled() and torch.is_grad_enabled()):
-        return _ConvBiasAct.apply(x, conv.weight, conv.bias, tuple(conv.stride), tuple(conv.padding), relu)
+            and conv.padding_mode == "zeros" and not torch.is_autocast_enabled() and torch.is_grad_enabled()
+            and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]):
+        from .conv_ops import conv2d_w
+        z = (F.conv2d(x, conv.weight, None, conv.stride, conv.padding) if _POSE_MIOPEN
+             else conv2d_w(x, conv.weight, conv.stride[0], conv.padding[0]))
+        if not z.is_contiguous(memory_format=_CL):
+            z = z.contiguous(memory_format=_CL)
+        return _BiasAct.apply(z, conv.bias, relu)
     y = conv(x)
     return F.relu(y) if relu else y
 

@@ -190,18 +190,20 @@ def test_packed_pose_producer_matches_split():
 
 @pytest.mark.parametrize("cin,cout,k,relu", [(512, 256, 1, True), (256, 256, 3, True), (256, 12, 1, False)])
 def test_conv_bias_act_matches_eager(cin, cout, k, relu):
-    """decoder_ops.conv_bias_act (bias-free MIOpen conv + md2_bias_act_*) vs the pose
-    decoder's eager relu(conv(x)): values and the gradients w.r.t. x, weight, bias."""
+    """decoder_ops.conv_bias_act (bias-free conv_ops convolution — split-bf16 MFMA or
+    MIOpen, chosen per shape — + md2_bias_act_*) vs the pose decoder's eager
+    relu(conv(x)): values and the gradients w.r.t. x, weight, bias (f32-class sums in
+    different orders)."""
     from monodepth2_amd.decoder_ops import conv_bias_act
     torch.manual_seed(4)
     CL = torch.channels_last
     conv = torch.nn.Conv2d(cin, cout, k, 1, k // 2).cuda().to(memory_format=CL)
     x = torch.randn(6, cin, 6, 20, device="cuda").contiguous(memory_format=CL).requires_grad_(True)
     y = conv_bias_act(conv, x, relu)
-    assert y.grad_fn is not None and "ConvBiasAct" in type(y.grad_fn).__name__
+    assert y.grad_fn is not None and "BiasAct" in type(y.grad_fn).__name__
     ref = conv(x)
     ref = torch.relu(ref) if relu else ref
-    torch.testing.assert_close(y, ref, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5)
     g = torch.randn_like(ref)
     got = torch.autograd.grad(y, (x, conv.weight, conv.bias), g)
     exp = torch.autograd.grad(ref, (x, conv.weight, conv.bias), g)
