@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 18
+#define MD2_ABI_VERSION 19
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -206,6 +206,14 @@ int md2_decoder_pad_fwd(const md2_pad_desc* desc, const float* x, const float* s
                         float* out, void* stream);
 int md2_decoder_pad_bwd(const md2_pad_desc* desc, const float* x, const float* bias, const float* grad_out,
                         float* grad_x, float* grad_skip, float* grad_bias, void* workspace, void* stream);
+/* md2_decoder_pad_bwd of grad_out + grad_out2 (NULL = none; same shape and layout as
+ * grad_out, MD2_PAD_NHWC with channel counts multiple of 4 only): the padded input of
+ * upconv(i,1)'s output feeds both dispconv(i) and upconv(i-1,0) (depth_decoder.py:56-64),
+ * so its two gradients are summed as they are read instead of by a separate add.
+ * (ABI 19) */
+int md2_decoder_pad_bwd2(const md2_pad_desc* desc, const float* x, const float* bias, const float* grad_out,
+                         const float* grad_out2, float* grad_x, float* grad_skip, float* grad_bias, void* workspace,
+                         void* stream);
 
 /*
  * DepthDecoder disparity heads (networks/depth_decoder.py:63-64, layers.py:121-136):
@@ -475,6 +483,12 @@ int md2_maxpool3s2_bwd(const md2_pool_desc* desc, const uint32_t* idx, const voi
  * add pass. */
 int md2_maxpool3s2_bwd_add(const md2_pool_desc* desc, const uint32_t* idx, const void* grad_y, const void* grad_add,
                            void* grad_x, void* stream);
+/* ... and grad_y2 (NULL = none) a second gradient of the pooled map y, same shape and
+ * layout as grad_y, summed into it on load: y feeds both the first BasicBlock's conv1 and
+ * its identity shortcut (torchvision BasicBlock.forward, `identity = x`), so autograd
+ * would otherwise add the two gradients in a separate pass. (ABI 19) */
+int md2_maxpool3s2_bwd_multi(const md2_pool_desc* desc, const uint32_t* idx, const void* grad_y, const void* grad_y2,
+                             const void* grad_add, void* grad_x, void* stream);
 
 /*
  * fp32 convolutions as implicit GEMMs on f32 MFMA (csrc/conv.hip): the ResNet
@@ -531,6 +545,9 @@ typedef struct md2_wsplit_entry {
     void* planes_dgrad;         /* [3][ci][kt][co] bf16, taps flipped, or NULL    */
     int32_t co, kt, ci;         /* out channels, kernel_h * kernel_w, in channels */
     int32_t block0;             /* first grid block of this entry                 */
+    void* planes_col;           /* [3][kt][ci][co] bf16 (taps not flipped), or NULL: the
+                                   weight as the 1x1 GEMM operand of a strided input
+                                   gradient's column form (md2_conv_col2im; ABI 19) */
 } md2_wsplit_entry;
 int md2_conv_split_weights_multi(const md2_wsplit_entry* table, int n, int total_blocks, void* stream);
 int md2_conv_fwd(const md2_conv_desc* desc, const float* x, const float* weight, float* y, void* workspace,

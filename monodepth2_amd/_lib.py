@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -67,7 +67,7 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_conv_fwd", "md2_conv_workspace_bytes", "md2_conv_split_weights",
            "md2_conv_dgrad", "md2_conv_wgrad", "md2_conv_direct", "md2_conv_wgrad_direct",
            "md2_conv_wgrad_direct_workspace_bytes", "md2_conv_split_weights_multi", "md2_bn_fwd_mask",
-           "md2_bn_bwd_mask", "md2_build_id"]
+           "md2_bn_bwd_mask", "md2_build_id", "md2_maxpool3s2_bwd_multi", "md2_decoder_pad_bwd2"]
 
 DTYPE_F32 = 0    # md2_desc.disp_dtype
 DTYPE_BF16 = 1
@@ -130,7 +130,7 @@ class ConvDesc(ctypes.Structure):
 class WsplitEntry(ctypes.Structure):
     """include/md2hot.h md2_wsplit_entry (one weight of md2_conv_split_weights_multi)."""
     _fields_ = [("weight", _vp), ("planes_fwd", _vp), ("planes_dgrad", _vp), ("co", ctypes.c_int32),
-                ("kt", ctypes.c_int32), ("ci", ctypes.c_int32), ("block0", ctypes.c_int32)]
+                ("kt", ctypes.c_int32), ("ci", ctypes.c_int32), ("block0", ctypes.c_int32), ("planes_col", _vp)]
 
 
 class PoolDesc(ctypes.Structure):
@@ -224,6 +224,8 @@ def _declare(L):
     L.md2_decoder_pad_fwd.argtypes = [ctypes.POINTER(PadDesc), _vp, _vp, _vp, _vp, _vp]
     L.md2_decoder_pad_bwd.restype = ctypes.c_int
     L.md2_decoder_pad_bwd.argtypes = [ctypes.POINTER(PadDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.md2_decoder_pad_bwd2.restype = ctypes.c_int
+    L.md2_decoder_pad_bwd2.argtypes = [ctypes.POINTER(PadDesc)] + [_vp] * 9
     L.md2_encoder_input.restype = ctypes.c_int
     L.md2_encoder_input.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,
                                     ctypes.c_float, ctypes.c_float, _vp, _vp]
@@ -263,6 +265,8 @@ def _declare(L):
     L.md2_bn_bwd_mask.argtypes = [ctypes.POINTER(BnDesc)] + [_vp] * 14
     L.md2_maxpool3s2_bwd_add.restype = ctypes.c_int
     L.md2_maxpool3s2_bwd_add.argtypes = [ctypes.POINTER(PoolDesc)] + [_vp] * 5
+    L.md2_maxpool3s2_bwd_multi.restype = ctypes.c_int
+    L.md2_maxpool3s2_bwd_multi.argtypes = [ctypes.POINTER(PoolDesc)] + [_vp] * 6
     L.md2_timing_begin.restype = ctypes.c_int
     L.md2_timing_begin.argtypes = [ctypes.c_int]
     L.md2_timing_calls.restype = ctypes.c_int

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 from typing import Dict, Optional
 
 import torch
@@ -169,14 +170,19 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, residual: Optional[torch.Tensor]
     return (y,) * (aliases + 1) if aliases else y
 
 
+_ALIAS_SUM = os.environ.get("MD2_ALIAS_SUM", "1") != "0"
+
+
 class _MaxPool(torch.autograd.Function):
-    """MaxPool2d(3, 2, 1) on channels_last tensors (csrc/pool.hip).  with_alias: also
-    return the input itself (a view) for a second consumer; its gradient then comes
-    into this backward and is summed in the pool's gather (md2_maxpool3s2_bwd_add)
-    instead of by a separate add of the two gradients."""
+    """MaxPool2d(3, 2, 1) on channels_last tensors (csrc/pool.hip).  out_alias: also
+    return a view of the pooled map y for its second consumer (the first block's
+    identity shortcut); with_alias: also return the input itself (a view) for x's
+    second consumer (the decoder skip).  Every such gradient comes into this backward
+    and is summed in the pool's gather (md2_maxpool3s2_bwd_multi) instead of by
+    separate adds of the two gradients.  Outputs: (y[, y'][, x'])."""
 
     @staticmethod
-    def forward(ctx, x, with_alias: bool = False):
+    def forward(ctx, x, with_alias: bool = False, out_alias: bool = False):
         B, C, H, W = x.shape
         Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
         d = _lib.PoolDesc(B, C, H, W, _lib.POOL_BF16 if x.dtype == torch.bfloat16 else 0, 0)
@@ -188,26 +194,36 @@ class _MaxPool(torch.autograd.Function):
         ctx.save_for_backward(idx)
         ctx.desc = (B, C, H, W, d.flags, 0)
         ctx.xshape, ctx.dtype = x.shape, x.dtype
-        if with_alias:
-            ctx.set_materialize_grads(False)   # an unused alias brings None, not a zero tensor
-            return y, x.view_as(x)
-        return y
+        ctx.with_alias, ctx.out_alias = with_alias, out_alias
+        if not (with_alias or out_alias):
+            return y
+        ctx.set_materialize_grads(False)   # an unused output brings None, not a zero tensor
+        outs = (y,) + ((y.view_as(y),) if out_alias else ()) + ((x.view_as(x),) if with_alias else ())
+        return outs
 
     @staticmethod
-    def backward(ctx, gy, galias=None):
+    def backward(ctx, gy, *rest):
         (idx,) = ctx.saved_tensors
-        if gy is None:   # only the alias reached the loss: the pool adds nothing
-            return (galias.to(ctx.dtype) if galias is not None else None), None
+        rest = list(rest)
+        gy2 = rest.pop(0) if ctx.out_alias else None
+        galias = rest.pop(0) if ctx.with_alias else None
+        if gy is None:
+            gy, gy2 = gy2, None
+        if gy is None:   # only the input alias reached the loss: the pool adds nothing
+            return (galias.to(ctx.dtype) if galias is not None else None), None, None
         gy = gy.to(ctx.dtype).contiguous(memory_format=_CL)
+        if gy2 is not None:
+            gy2 = gy2.to(ctx.dtype).contiguous(memory_format=_CL)
         if galias is not None:
             galias = galias.to(ctx.dtype).contiguous(memory_format=_CL)
         gx = torch.empty(ctx.xshape, device=gy.device, dtype=ctx.dtype, memory_format=_CL)
         d = _lib.PoolDesc(*ctx.desc)
-        _lib.check(_lib.lib().md2_maxpool3s2_bwd_add(ctypes.byref(d), idx.data_ptr(), gy.data_ptr(),
-                                                     galias.data_ptr() if galias is not None else None,
-                                                     gx.data_ptr(), _lib.stream(gy.device)),
-                   "md2_maxpool3s2_bwd_add")
-        return gx, None
+        _lib.check(_lib.lib().md2_maxpool3s2_bwd_multi(ctypes.byref(d), idx.data_ptr(), gy.data_ptr(),
+                                                       gy2.data_ptr() if gy2 is not None else None,
+                                                       galias.data_ptr() if galias is not None else None,
+                                                       gx.data_ptr(), _lib.stream(gy.device)),
+                   "md2_maxpool3s2_bwd_multi")
+        return gx, None, None
 
 
 def _pool_ok(pool: nn.MaxPool2d, x: torch.Tensor) -> bool:
@@ -224,9 +240,15 @@ def max_pool_3x3s2(pool: nn.MaxPool2d, x: torch.Tensor) -> torch.Tensor:
     return pool(x)
 
 
-def max_pool_3x3s2_with_alias(pool: nn.MaxPool2d, x: torch.Tensor):
+def max_pool_3x3s2_with_alias(pool: nn.MaxPool2d, x: torch.Tensor, out_alias: bool = False):
     """(pool(x), x') with x' a view of x for x's other consumer (the decoder skip):
-    on the HIP path both gradients of x meet in the pool's backward gather."""
+    on the HIP path both gradients of x meet in the pool's backward gather.
+    out_alias: (y, y', x') with y' a view of the pooled map for its second consumer
+    (the first BasicBlock's identity shortcut), whose gradient meets y's there too."""
     if _pool_ok(pool, x) and torch.is_grad_enabled() and x.requires_grad:
-        return _MaxPool.apply(x, True)
-    return max_pool_3x3s2(pool, x), x
+        if out_alias and not _ALIAS_SUM:   # A/B knob MD2_ALIAS_SUM=0: autograd adds y's two gradients
+            y, xa = _MaxPool.apply(x, True, False)
+            return y, y, xa
+        return _MaxPool.apply(x, True, out_alias)
+    y = max_pool_3x3s2(pool, x)
+    return (y, y, x) if out_alias else (y, x)

@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import types
 from typing import Dict, Tuple
 
 import torch
@@ -135,13 +136,31 @@ def _dgrad_col(gy, x, w, stride, pad, flags):
     runs 1-, 2- and 4-tap GEMMs, the heaviest setting the time)."""
     N, C, KH, KW = w.shape
     B, _, H, W = x.shape
-    wcol = w.permute(2, 3, 1, 0).reshape(KH * KW * C, N, 1, 1).contiguous()
-    cols = _fwd(gy, wcol, 1, 0, flags)
+    pc = _bank.col_planes(w) if (_bank is not None and flags & X6 and _COL_BANK) else None
+    if pc is not None:   # refreshed with the step's other planes: no permute, no split
+        cols = _fwd_planes(gy, _col_shape(KH * KW * C, N), pc, 1, 0, flags)
+    else:
+        wcol = w.permute(2, 3, 1, 0).reshape(KH * KW * C, N, 1, 1).contiguous()
+        cols = _fwd(gy, wcol, 1, 0, flags)
     gx = torch.empty_like(x, memory_format=_CL)
     d = _lib.ConvDesc(B, H, W, C, N, KH, KW, stride, pad, 0)
     _lib.check(_lib.lib().md2_conv_col2im(ctypes.byref(d), cols.data_ptr(), gx.data_ptr(), _lib.stream(x.device)),
                "md2_conv_col2im")
     return gx
+
+
+_COL_BANK = os.environ.get("MD2_COL_PLANES", "1") != "0"   # A/B knob: 0 = permute + split per call
+
+
+def _col_shape(rows: int, n: int):
+    """Stands in for the column GEMM's (rows, n, 1, 1) weight where only its shape is
+    read (the descriptor); the operand itself is the bank's planes."""
+    return types.SimpleNamespace(shape=torch.Size((rows, n, 1, 1)))
+
+
+def _col_x(w):
+    """An input shape for a weight-only descriptor (the split reads channels and taps)."""
+    return types.SimpleNamespace(shape=torch.Size((1, w.shape[1], 8, 8)))
 
 
 def _x6_ok(x, w) -> bool:
@@ -180,12 +199,13 @@ class PlaneBank:
     and shape (parameters are updated in place, so both are stable)."""
 
     def __init__(self):
-        self.entries: Dict[tuple, list] = {}   # key -> [weight, planes_fwd, planes_dgrad or None]
+        self.entries: Dict[tuple, list] = {}   # key -> [weight, planes_fwd, planes_dgrad|None, planes_col|None]
         self.table = None                      # device md2_wsplit_entry array
         self.total_blocks = 0
         self.dirty = False
         self.fresh = False
         self._keep = []   # superseded tables / planes: a captured graph may still point at them
+        self._col_pending = set()   # keys whose column planes the next refresh fills first
 
     @staticmethod
     def _blocks(w: torch.Tensor) -> int:
@@ -196,10 +216,11 @@ class PlaneBank:
         ents = list(self.entries.values())
         arr = (_lib.WsplitEntry * len(ents))()
         blk = 0
-        for e, (w, pf, pd) in zip(arr, ents):
+        for e, (w, pf, pd, pc) in zip(arr, ents):
             co, ci, kh, kw = w.shape
             e.weight, e.planes_fwd = w.data_ptr(), pf.data_ptr()
             e.planes_dgrad = pd.data_ptr() if pd is not None else None
+            e.planes_col = pc.data_ptr() if pc is not None else None
             e.co, e.kt, e.ci, e.block0 = co, kh * kw, ci, blk
             blk += self._blocks(w)
         host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
@@ -222,6 +243,7 @@ class PlaneBank:
             _lib.check(_lib.lib().md2_conv_split_weights_multi(self.table.data_ptr(), len(self.entries),
                                                               self.total_blocks, _lib.stream(device)),
                        "md2_conv_split_weights_multi")
+        self._col_pending.clear()
         self.fresh = True
 
     def end_step(self):
@@ -240,9 +262,35 @@ class PlaneBank:
         pf, pd = _split_weights(x, w, stride, pad, need_dg or (e is not None and e[2] is not None))
         if e is not None:
             self._keep.append(e)
-        self.entries[k] = [w, pf, pd]
+        self.entries[k] = [w, pf, pd, e[3] if e is not None else None]
         self.dirty = True
         return pf, pd
+
+    def col_planes(self, w):
+        """The weight's planes as the column GEMM's 1x1 operand ([3][kh][kw][ci][co],
+        `_dgrad_col`) for this step, or None: a weight first asked for them gets them
+        allocated now and filled from the next refresh on (the caller permutes and
+        splits itself until then), never while a graph is being captured."""
+        if not self.fresh:
+            return None
+        k = (w.data_ptr(), tuple(w.shape))
+        e = self.entries.get(k)
+        if e is not None and e[3] is not None:
+            return None if k in self._col_pending else e[3]
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        pc = torch.empty(3 * w.numel(), dtype=torch.bfloat16, device=w.device)
+        if e is None:   # planes_fwd are part of every entry: split them now (once)
+            pf = torch.empty(3 * w.numel(), dtype=torch.bfloat16, device=w.device)
+            _lib.check(_lib.lib().md2_conv_split_weights(ctypes.byref(_desc(_col_x(w), w, 1, 0)), w.data_ptr(),
+                                                         pf.data_ptr(), None, _lib.stream(w.device)),
+                       "md2_conv_split_weights")
+            self.entries[k] = [w, pf, None, pc]
+        else:
+            e[3] = pc
+        self._col_pending.add(k)
+        self.dirty = True
+        return None
 
 
 _bank: PlaneBank | None = None

@@ -445,8 +445,8 @@ __device__ __forceinline__ void split_store(__bf16* out, int n, int i, float v) 
     out[n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, b) >> 16));
     out[2 * n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, c) >> 16));
 }
-__device__ __forceinline__ void wsplit_tile(const float* w, __bf16* fw, __bf16* dg, int Co, int KT, int Ci, int tap,
-                                            int co0, int ci0, float (*tile)[33]) {
+__device__ __forceinline__ void wsplit_tile(const float* w, __bf16* fw, __bf16* dg, __bf16* cl, int Co, int KT,
+                                            int Ci, int tap, int co0, int ci0, float (*tile)[33]) {
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
     const int n = Co * KT * Ci;
 #pragma unroll
@@ -460,12 +460,15 @@ __device__ __forceinline__ void wsplit_tile(const float* w, __bf16* fw, __bf16* 
         }
         tile[r][tx] = v;
     }
-    if (!dg) return;   // block-uniform
+    if (!dg && !cl) return;   // block-uniform
     __syncthreads();
 #pragma unroll
     for (int r = ty; r < 32; r += 8) {
         const int ci = ci0 + r, co = co0 + tx;
-        if (ci < Ci && co < Co) split_store(dg, n, (ci * KT + (KT - 1 - tap)) * Co + co, tile[tx][r]);
+        if (ci < Ci && co < Co) {
+            if (dg) split_store(dg, n, (ci * KT + (KT - 1 - tap)) * Co + co, tile[tx][r]);
+            if (cl) split_store(cl, n, (tap * Ci + ci) * Co + co, tile[tx][r]);   // [(tap, ci)][co], not flipped
+        }
     }
 }
 
@@ -487,14 +490,14 @@ __global__ __launch_bounds__(256) void conv_wsplit_multi_kernel(const md2_wsplit
     const int bx = t % nx;
     t /= nx;
     const int by = t % ny, tap = t / ny;
-    wsplit_tile(e.weight, (__bf16*)e.planes_fwd, (__bf16*)e.planes_dgrad, e.co, e.kt, e.ci, tap, by * 32, bx * 32,
-                tile);
+    wsplit_tile(e.weight, (__bf16*)e.planes_fwd, (__bf16*)e.planes_dgrad, (__bf16*)e.planes_col, e.co, e.kt, e.ci,
+                tap, by * 32, bx * 32, tile);
 }
 
 __global__ __launch_bounds__(256) void conv_wsplit_tile_kernel(const float* w, __bf16* fw, __bf16* dg, int Co,
                                                                int KT, int Ci) {
     __shared__ float tile[32][33];
-    wsplit_tile(w, fw, dg, Co, KT, Ci, blockIdx.z, blockIdx.y * 32, blockIdx.x * 32, tile);
+    wsplit_tile(w, fw, dg, nullptr, Co, KT, Ci, blockIdx.z, blockIdx.y * 32, blockIdx.x * 32, tile);
 }
 
 // Tiles BMX x BN.  NT threads: 8 waves (2 x 4 / 4 x 2 / 2 x 4, wave tiles 64/128 x 32)

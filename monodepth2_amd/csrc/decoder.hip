@@ -42,6 +42,7 @@ struct PadArgs {
     const float* skip;
     float* out;
     const float* gout;
+    const float* gout2;        // v4 bwd: a second gradient of the padded map (its other consumer), or null
     float* gx;
     float* gskip;
     const float* bias;         // (C,) fp32 bias of the conv that produced x, or null
@@ -194,8 +195,14 @@ __global__ __launch_bounds__(kThreads) void pad_fwd_v4_kernel(PadArgs a) {
 
 // fold() on quads: element offset g0 = (b, 0, 0, c) of the NHWC padded gradient
 template <typename T>
-__device__ __forceinline__ float4 fold4(const float* gout, size_t g0, int Wp, int H, int W, int yy, int xx, int Ct) {
-    auto G = [&](int y, int x) { return md2::ld4T<T>(gout, g0 + ((size_t)y * Wp + x) * Ct); };
+__device__ __forceinline__ float4 fold4(const float* gout, const float* gout2, size_t g0, int Wp, int H, int W,
+                                        int yy, int xx, int Ct) {
+    auto G = [&](int y, int x) {
+        const size_t o = g0 + ((size_t)y * Wp + x) * Ct;
+        float4 v = md2::ld4T<T>(gout, o);
+        if (gout2) v = add4(v, md2::ld4T<T>(gout2, o));   // summed per padded element, before the fold
+        return v;
+    };
     float4 s = G(yy + 1, xx + 1);
     const bool ry = (yy == 1), ry2 = (yy == H - 2), rx = (xx == 1), rx2 = (xx == W - 2);
     if (rx) s = add4(s, G(yy + 1, 0));
@@ -235,12 +242,12 @@ __global__ __launch_bounds__(kThreads) void pad_bwd_v4_kernel(PadArgs a) {
             const size_t g = (size_t)b * Hp * Wp * Ct + c;
             float4 s;
             if (UP) {
-                s = add4(add4(fold4<T>(a.gout, g, Wp, a.H, a.W, 2 * i, 2 * j, Ct),
-                              fold4<T>(a.gout, g, Wp, a.H, a.W, 2 * i, 2 * j + 1, Ct)),
-                         add4(fold4<T>(a.gout, g, Wp, a.H, a.W, 2 * i + 1, 2 * j, Ct),
-                              fold4<T>(a.gout, g, Wp, a.H, a.W, 2 * i + 1, 2 * j + 1, Ct)));
+                s = add4(add4(fold4<T>(a.gout, a.gout2, g, Wp, a.H, a.W, 2 * i, 2 * j, Ct),
+                              fold4<T>(a.gout, a.gout2, g, Wp, a.H, a.W, 2 * i, 2 * j + 1, Ct)),
+                         add4(fold4<T>(a.gout, a.gout2, g, Wp, a.H, a.W, 2 * i + 1, 2 * j, Ct),
+                              fold4<T>(a.gout, a.gout2, g, Wp, a.H, a.W, 2 * i + 1, 2 * j + 1, Ct)));
             } else {
-                s = fold4<T>(a.gout, g, Wp, a.H, a.W, i, j, Ct);
+                s = fold4<T>(a.gout, a.gout2, g, Wp, a.H, a.W, i, j, Ct);
             }
             if (ELU) {
                 float4 xv = md2::ld4T<T>(a.x, 4 * (size_t)idx);
@@ -257,7 +264,7 @@ __global__ __launch_bounds__(kThreads) void pad_bwd_v4_kernel(PadArgs a) {
             t /= a.W;
             const int yy = t % a.H;
             const int b = t / a.H;
-            md2::st4T<T>(a.gskip, 4 * (size_t)k, fold4<T>(a.gout, (size_t)b * Hp * Wp * Ct + a.C + c, Wp, a.H, a.W, yy, xx, Ct));
+            md2::st4T<T>(a.gskip, 4 * (size_t)k, fold4<T>(a.gout, a.gout2, (size_t)b * Hp * Wp * Ct + a.C + c, Wp, a.H, a.W, yy, xx, Ct));
         }
     }
     if (!a.gbias_part) return;   // uniform: every thread of the grid returns here together
@@ -385,8 +392,15 @@ int md2_decoder_pad_fwd(const md2_pad_desc* d, const float* x, const float* skip
 
 int md2_decoder_pad_bwd(const md2_pad_desc* d, const float* x, const float* bias, const float* grad_out,
                         float* grad_x, float* grad_skip, float* grad_bias, void* workspace, void* stream) {
+    return md2_decoder_pad_bwd2(d, x, bias, grad_out, nullptr, grad_x, grad_skip, grad_bias, workspace, stream);
+}
+
+int md2_decoder_pad_bwd2(const md2_pad_desc* d, const float* x, const float* bias, const float* grad_out,
+                         const float* grad_out2, float* grad_x, float* grad_skip, float* grad_bias, void* workspace,
+                         void* stream) {
     PadArgs a = {};
     if (!make_args(d, a) || !grad_out || !grad_x || (a.Cs > 0 && !grad_skip)) return MD2_ERR_ARG;
+    if (grad_out2 && !vec4(d)) return MD2_ERR_ARG;   // only the NHWC quad kernels sum a second gradient
     const bool elu = d->flags & MD2_PAD_ELU, up = d->flags & MD2_PAD_UPSAMPLE;
     if (elu && !x) return MD2_ERR_ARG;
     // bias: the NHWC float4 kernels, with C/4 dividing the block (per-thread channel quad)
@@ -394,6 +408,7 @@ int md2_decoder_pad_bwd(const md2_pad_desc* d, const float* x, const float* bias
     if (grad_bias && !workspace) return MD2_ERR_ARG;
     a.x = x;
     a.gout = grad_out;
+    a.gout2 = grad_out2;
     a.gx = grad_x;
     a.gskip = grad_skip;
     a.bias = bias;

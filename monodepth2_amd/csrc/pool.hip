@@ -70,8 +70,8 @@ __global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(PoolArgs p, const
 
 template <typename T>
 __global__ void __launch_bounds__(kThreads) maxpool_bwd_kernel(PoolArgs p, const uint32_t* __restrict__ idx,
-                                                               const void* __restrict__ gy, const void* __restrict__ ga,
-                                                               void* __restrict__ gx) {
+                                                               const void* __restrict__ gy, const void* __restrict__ gy2,
+                                                               const void* __restrict__ ga, void* __restrict__ gx) {
     const int C4 = p.C / 4;
     const int n = p.B * p.H * p.W * C4;
     for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
@@ -90,7 +90,11 @@ __global__ void __launch_bounds__(kThreads) maxpool_bwd_kernel(PoolArgs p, const
                 const size_t o = (((size_t)b * p.Ho + oy) * p.Wo + ox) * C4 + c4;
                 const uint32_t w = idx[o];
                 const int k = (iy - (2 * oy - 1)) * 3 + (ix - (2 * ox - 1));
-                const float4 g = md2::ld4T<T>(gy, 4 * o);
+                float4 g = md2::ld4T<T>(gy, 4 * o);
+                if (gy2) {
+                    const float4 h = md2::ld4T<T>(gy2, 4 * o);
+                    g.x += h.x; g.y += h.y; g.z += h.z; g.w += h.w;
+                }
                 if ((int)(w & 255u) == k) s[0] += g.x;
                 if ((int)((w >> 8) & 255u) == k) s[1] += g.y;
                 if ((int)((w >> 16) & 255u) == k) s[2] += g.z;
@@ -112,6 +116,7 @@ template <typename T>
 __global__ void __launch_bounds__(kThreads) maxpool_bwd_rows_kernel(PoolArgs p, int c4_shift,
                                                                     const uint32_t* __restrict__ idx,
                                                                     const void* __restrict__ gy,
+                                                                    const void* __restrict__ gy2,
                                                                     const void* __restrict__ ga, void* __restrict__ gx) {
     const int C4 = p.C / 4;
     const int j = blockIdx.x * kThreads + threadIdx.x;
@@ -126,7 +131,11 @@ __global__ void __launch_bounds__(kThreads) maxpool_bwd_rows_kernel(PoolArgs p, 
             const size_t o = (((size_t)b * p.Ho + oy) * p.Wo + ox) * C4 + c4;
             const uint32_t w = idx[o];
             const int k = (iy - (2 * oy - 1)) * 3 + (ix - (2 * ox - 1));
-            const float4 g = md2::ld4T<T>(gy, 4 * o);
+            float4 g = md2::ld4T<T>(gy, 4 * o);
+            if (gy2) {   // the pooled map's second consumer (the first block's shortcut)
+                const float4 h = md2::ld4T<T>(gy2, 4 * o);
+                g.x += h.x; g.y += h.y; g.z += h.z; g.w += h.w;
+            }
             if ((int)(w & 255u) == k) s[0] += g.x;
             if ((int)((w >> 8) & 255u) == k) s[1] += g.y;
             if ((int)((w >> 16) & 255u) == k) s[2] += g.z;
@@ -171,8 +180,8 @@ int md2_maxpool3s2_fwd(const md2_pool_desc* d, const void* x, void* y, uint32_t*
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }
 
-int md2_maxpool3s2_bwd_add(const md2_pool_desc* d, const uint32_t* idx, const void* grad_y, const void* grad_add,
-                           void* grad_x, void* stream) {
+int md2_maxpool3s2_bwd_multi(const md2_pool_desc* d, const uint32_t* idx, const void* grad_y, const void* grad_y2,
+                             const void* grad_add, void* grad_x, void* stream) {
     PoolArgs p;
     if (!make(d, p) || !idx || !grad_y || !grad_x)
         return md2_report_error(MD2_ERR_ARG, "maxpool: bad desc or NULL operand");
@@ -183,18 +192,23 @@ int md2_maxpool3s2_bwd_add(const md2_pool_desc* d, const uint32_t* idx, const vo
         while ((1 << sh) < C4) ++sh;
         auto k = (d->flags & MD2_POOL_BF16) ? maxpool_bwd_rows_kernel<uint16_t> : maxpool_bwd_rows_kernel<float>;
         hipLaunchKernelGGL(k, dim3((p.W * C4 + kThreads - 1) / kThreads, p.B * p.H), dim3(kThreads), 0,
-                           (hipStream_t)stream, p, sh, idx, grad_y, grad_add, grad_x);
+                           (hipStream_t)stream, p, sh, idx, grad_y, grad_y2, grad_add, grad_x);
     } else {
         auto k = (d->flags & MD2_POOL_BF16) ? maxpool_bwd_kernel<uint16_t> : maxpool_bwd_kernel<float>;
-        hipLaunchKernelGGL(k, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, p, idx, grad_y, grad_add,
-                           grad_x);
+        hipLaunchKernelGGL(k, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, p, idx, grad_y, grad_y2,
+                           grad_add, grad_x);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }
 
+int md2_maxpool3s2_bwd_add(const md2_pool_desc* d, const uint32_t* idx, const void* grad_y, const void* grad_add,
+                           void* grad_x, void* stream) {
+    return md2_maxpool3s2_bwd_multi(d, idx, grad_y, nullptr, grad_add, grad_x, stream);
+}
+
 int md2_maxpool3s2_bwd(const md2_pool_desc* d, const uint32_t* idx, const void* grad_y, void* grad_x, void* stream) {
-    return md2_maxpool3s2_bwd_add(d, idx, grad_y, nullptr, grad_x, stream);
+    return md2_maxpool3s2_bwd_multi(d, idx, grad_y, nullptr, nullptr, grad_x, stream);
 }
 
 }  // extern "C"

@@ -29,7 +29,7 @@ def _flags(elu: bool, upsample: bool, nhwc: bool, bf16: bool = False) -> int:
 class _ConvInput(torch.autograd.Function):
 
     @staticmethod
-    def forward(ctx, x, skip, bias, elu: bool, upsample: bool, nhwc: bool):
+    def forward(ctx, x, skip, bias, elu: bool, upsample: bool, nhwc: bool, alias: bool = False):
         fmt = _CL if nhwc else torch.contiguous_format
         x = x.contiguous(memory_format=fmt)
         skip = skip.contiguous(memory_format=fmt) if skip is not None else None
@@ -54,13 +54,23 @@ class _ConvInput(torch.autograd.Function):
         ctx.bias_dtype = None if bias is None else bias.dtype
         ctx.save_for_backward(x if elu else None, bias32)
         ctx.x_shape = x.shape
+        if alias:   # (out, out') for out's two consumers; an unused one brings None
+            ctx.set_materialize_grads(False)
+            return out, out.view_as(out)
         return out
 
     @staticmethod
-    def backward(ctx, gout):
+    def backward(ctx, gout, gout2=None):
         x, bias32 = ctx.saved_tensors
         fmt = _CL if ctx.nhwc else torch.contiguous_format
-        gout = gout.to(torch.bfloat16 if ctx.bf16 else torch.float32).contiguous(memory_format=fmt)
+        if gout is None:
+            gout, gout2 = gout2, None
+        if gout is None:
+            return None, None, None, None, None, None, None
+        dt = torch.bfloat16 if ctx.bf16 else torch.float32
+        gout = gout.to(dt).contiguous(memory_format=fmt)
+        if gout2 is not None:
+            gout2 = gout2.to(dt).contiguous(memory_format=fmt)
         B, C, h, w = ctx.x_shape
         gx = torch.empty(ctx.x_shape, device=gout.device, dtype=gout.dtype, memory_format=fmt)
         gskip = (torch.empty(ctx.skip_shape, device=gout.device, dtype=gout.dtype, memory_format=fmt)
@@ -72,17 +82,17 @@ class _ConvInput(torch.autograd.Function):
             gbias = torch.empty(C, device=gout.device, dtype=torch.float32)
             ws = torch.empty(_lib.lib().md2_decoder_pad_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
                              device=gout.device)
-        rc = _lib.lib().md2_decoder_pad_bwd(ctypes.byref(d), x.data_ptr() if x is not None else None,
-                                            bias32.data_ptr() if bias32 is not None else None,
-                                            gout.data_ptr(), gx.data_ptr(),
-                                            gskip.data_ptr() if gskip is not None else None,
-                                            gbias.data_ptr() if gbias is not None else None,
-                                            ws.data_ptr() if ws is not None else None,
-                                            _lib.stream(gout.device))
-        _lib.check(rc, "md2_decoder_pad_bwd")
+        rc = _lib.lib().md2_decoder_pad_bwd2(ctypes.byref(d), x.data_ptr() if x is not None else None,
+                                             bias32.data_ptr() if bias32 is not None else None,
+                                             gout.data_ptr(), gout2.data_ptr() if gout2 is not None else None,
+                                             gx.data_ptr(), gskip.data_ptr() if gskip is not None else None,
+                                             gbias.data_ptr() if gbias is not None else None,
+                                             ws.data_ptr() if ws is not None else None,
+                                             _lib.stream(gout.device))
+        _lib.check(rc, "md2_decoder_pad_bwd2")
         if gbias is not None and ctx.bias_dtype != torch.float32:
             gbias = gbias.to(ctx.bias_dtype)
-        return gx, gskip, gbias, None, None, None
+        return gx, gskip, gbias, None, None, None, None
 
 
 class _DispHead(torch.autograd.Function):
@@ -202,16 +212,30 @@ def supports_bias(channels: int, nhwc: bool) -> bool:
     return nhwc and channels % 4 == 0 and 256 % (channels // 4) == 0
 
 
+# A/B knob: MD2_ALIAS_SUM=0 leaves a shared padded map's two gradients to autograd's add
+ALIAS_SUM = os.environ.get("MD2_ALIAS_SUM", "1") != "0"
+
+
 def conv_input(x: torch.Tensor, skip: Optional[torch.Tensor] = None, elu: bool = False,
-               upsample: bool = False, nhwc: bool = False, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+               upsample: bool = False, nhwc: bool = False, bias: Optional[torch.Tensor] = None,
+               alias: bool = False):
     """ReflectionPad2d(1)(cat([upsample?(elu?(x + bias)), skip], 1)) in one fused pass.
     nhwc: tensors in (and out) channels_last, as the NHWC convolutions around it.
     bias: the bias of the conv that produced x (that conv then runs without one);
-    its gradient comes back from the same backward pass."""
+    its gradient comes back from the same backward pass.
+    alias: returns (P, P') with P' a view of P for its second consumer (dispconv beside
+    the next level's conv); in NHWC with channel counts multiple of 4 the two gradients
+    are summed as the backward reads them (md2_decoder_pad_bwd2), else P' is P."""
     if x.device.type != "cuda":
         raise RuntimeError("conv_input is a HIP kernel; use the eager chain on the CPU")
     if x.dtype != torch.float32 and not (x.dtype == torch.bfloat16 and supports_bf16(x, skip, nhwc)):
         raise ValueError("conv_input supports float32, and bfloat16 in NHWC with channel counts multiple of 4")
     if bias is not None and not supports_bias(x.shape[1], nhwc):
         raise ValueError("conv_input folds a bias only in NHWC with C/4 dividing 256")
-    return _ConvInput.apply(x, skip, bias, elu, upsample, nhwc)
+    if alias:
+        sc = 0 if skip is None else skip.shape[1]
+        if ALIAS_SUM and nhwc and x.shape[1] % 4 == 0 and sc % 4 == 0 and torch.is_grad_enabled():
+            return _ConvInput.apply(x, skip, bias, elu, upsample, nhwc, True)
+        P = _ConvInput.apply(x, skip, bias, elu, upsample, nhwc, False)
+        return P, P
+    return _ConvInput.apply(x, skip, bias, elu, upsample, nhwc, False)

@@ -74,13 +74,16 @@ class DepthDecoder(nn.Module):
             skip = input_features[i - 1] if (self.use_skips and i > 0) else None
             P = conv_input(y0, skip, elu=True, upsample=True, nhwc=cl, bias=b0)
             y1, b1 = conv(self.convs[("upconv", i, 1)], P)
-            P = conv_input(y1, None, elu=True, upsample=False, nhwc=cl, bias=b1)   # shared by dispconv and the next level
+            if i in self.scales and i > 0:   # shared by dispconv and the next level: a view each,
+                P, Ph = conv_input(y1, None, elu=True, upsample=False, nhwc=cl, bias=b1, alias=True)
+            else:                            # their gradients summed in the pad backward
+                P = Ph = conv_input(y1, None, elu=True, upsample=False, nhwc=cl, bias=b1)
             if i in self.scales:
                 head = self.convs[("dispconv", i)].conv
-                if self.fused_heads and supports_disp_head(P, head) and not torch.is_autocast_enabled():
-                    self.outputs[("disp", i)] = disp_head(P, head)
+                if self.fused_heads and supports_disp_head(Ph, head) and not torch.is_autocast_enabled():
+                    self.outputs[("disp", i)] = disp_head(Ph, head)
                 else:
-                    self.outputs[("disp", i)] = self.sigmoid(head(P))
+                    self.outputs[("disp", i)] = self.sigmoid(head(Ph))
         return self.outputs
 
     def forward(self, input_features):

@@ -196,9 +196,10 @@ class ResnetEncoder(nn.Module):
         """The encoder on an input already normalised by `prepare`."""
         e = self.encoder
         f0 = bn_act(e.bn1, stem_conv(e.conv1, x))   # weight gradient on f32 MFMA (stem_ops)
-        pooled, f0 = max_pool_3x3s2_with_alias(e.maxpool, f0)   # f0's two gradients meet in the pool backward
+        # f0's two gradients (layer1, decoder skip) and the pooled map's two (the first
+        # block's conv1 and shortcut) all meet in the pool backward
+        x, xs, f0 = max_pool_3x3s2_with_alias(e.maxpool, f0, out_alias=True)
         feats = [f0]
-        x, xs = pooled, pooled
         layers = [e.layer1, e.layer2, e.layer3, e.layer4]
         for li, layer in enumerate(layers):
             # every layer output but the last also feeds the decoder skip

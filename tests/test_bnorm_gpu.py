@@ -224,6 +224,37 @@ def test_maxpool_alias_only_gradient():
     torch.testing.assert_close(gx, ga, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("used", [(0, 1, 2), (0, 1), (1, 2), (0, 2), (1,), (2,)])
+def test_maxpool_out_alias_sums_all_gradients(used):
+    """out_alias: (y, y', x') — the pooled map's second consumer (the first block's
+    shortcut) and the input's (the decoder skip) are summed in the pool's gather
+    (md2_maxpool3s2_bwd_multi), for every subset of the three outputs that reaches
+    the loss; same gradient as autograd's sum over the consumers."""
+    torch.manual_seed(11)
+    pool = torch.nn.MaxPool2d(3, 2, 1)
+    x = torch.randn(2, 64, 24, 40, device="cuda").contiguous(memory_format=CL).requires_grad_(True)
+    outs = bn_ops.max_pool_3x3s2_with_alias(pool, x, out_alias=True)
+    assert len(outs) == 3 and torch.equal(outs[1], outs[0]) and torch.equal(outs[2], x)
+    grads = [torch.randn_like(o) for o in outs]
+    gx, = torch.autograd.grad([outs[i] for i in used], x, [grads[i] for i in used])
+    yr = pool(x)
+    refs = [yr, yr * 1.0, x * 1.0]
+    gxr, = torch.autograd.grad([refs[i] for i in used], x, [grads[i] for i in used])
+    torch.testing.assert_close(gx, gxr, rtol=1e-6, atol=1e-6)
+
+
+def test_maxpool_out_alias_bf16():
+    torch.manual_seed(12)
+    pool = torch.nn.MaxPool2d(3, 2, 1)
+    x = torch.randn(2, 64, 12, 20, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=CL)
+    x.requires_grad_(True)
+    y, y2, xa = bn_ops.max_pool_3x3s2_with_alias(pool, x, out_alias=True)
+    gy, gy2, ga = torch.randn_like(y), torch.randn_like(y), torch.randn_like(x)
+    gx, = torch.autograd.grad([y, y2, xa], x, [gy, gy2, ga])
+    gxr, = torch.autograd.grad([pool(x.float())], x, [(gy.float() + gy2.float())])
+    torch.testing.assert_close(gx.float(), (gxr.float() + ga.float()), rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("bf16", [False, True])
 @pytest.mark.parametrize("groups", [1, 2])
 @pytest.mark.parametrize("used", [(0, 1, 2), (0, 2), (1, 2)])

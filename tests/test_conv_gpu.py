@@ -284,6 +284,34 @@ def test_plane_bank_refresh_matches_per_call_split():
     bank.end_step()
 
 
+def test_plane_bank_column_planes(monkeypatch):
+    """PlaneBank.col_planes: the strided input gradient's column operand ([kh][kw][ci][co]
+    split planes) refreshed with the step's other planes is bitwise the per-call permute
+    + split, and _dgrad_col through it returns bitwise the same gradient."""
+    torch.manual_seed(7)
+    bank = conv_ops.PlaneBank()
+    monkeypatch.setattr(conv_ops, "_bank", bank)
+    B, C, N, H, W = 2, 64, 128, 24, 40
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    w = torch.randn(N, C, 3, 3, device="cuda").contiguous(memory_format=CL)
+    gy = torch.randn(B, N, H // 2, W // 2, device="cuda").contiguous(memory_format=CL)
+    flags = conv_ops.X6
+    bank.begin_step(torch.device("cuda", 0))
+    assert bank.col_planes(w) is None          # first request: registered, filled from the next refresh
+    g0 = conv_ops._dgrad_col(gy, x, w, 2, 1, flags)   # per-call permute + split meanwhile
+    assert bank.col_planes(w) is None          # still unfilled in this window
+    bank.end_step()
+    bank.begin_step(torch.device("cuda", 0))
+    pc = bank.col_planes(w)
+    assert pc is not None
+    wcol = w.permute(2, 3, 1, 0).reshape(9 * C, N, 1, 1).contiguous()
+    ref, _ = conv_ops._split_weights(gy, wcol, 1, 0, False)
+    assert torch.equal(pc, ref)
+    g1 = conv_ops._dgrad_col(gy, x, w, 2, 1, flags)
+    bank.end_step()
+    assert torch.equal(g0, g1)
+
+
 @pytest.mark.parametrize("B,C,N,p,H,W", [(2, 16, 16, 0, 20, 34), (2, 32, 16, 0, 12, 18), (2, 16, 32, 1, 9, 13),
                                          (1, 16, 16, 1, 7, 9), (3, 32, 16, 2, 5, 6), (2, 16, 16, 0, 70, 131),
                                          (1, 32, 16, 1, 9, 200)])
