@@ -60,7 +60,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0 # dense bf16; the split-bf16 convs issue 6 bf16 p
 ROUND = "r03"
 
 
-HOT_KERNELS = "pack_src8|photo_|smooth_fwd|finalize_fwd|disp_grad_kernel|grad_T_kernel"
+HOT_KERNELS = "pack_src8|photo_|smooth_fwd|finalize_fwd|disp_grad|grad_T_kernel"
 
 
 def pmc_traffic(args, S, timeout=150):

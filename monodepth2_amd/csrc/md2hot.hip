@@ -55,7 +55,7 @@ constexpr int kBwdCols = kWave - 4;  // output columns per backward strip
 #define MD2_BWD_MINB 2
 #endif
 constexpr int kRowsB = MD2_ROWS_B;   // output rows per backward work item
-constexpr int kSmoothChunk = 2048;   // pixels per smoothness partial
+constexpr int kSmoothChunk = 1024;   // pixels per smoothness partial (one pixel quad per thread)
 constexpr float kC1 = 0.0001f;       // 0.01 ** 2   layers.py:231
 constexpr float kC2 = 0.0009f;       // 0.03 ** 2   layers.py:232
 constexpr float kInv9 = 1.0f / 9.0f;
@@ -1459,6 +1459,7 @@ struct SmoothArgs {
     float* part[MD2_MAX_SCALES];        // [B][chunks][3]
     float* sgrad[MD2_MAX_SCALES];       // (B, hs, ws): the smoothness term's per-unit gradient
     int disp_bf16;
+    int quad;                           // every ws % 4 == 0: smooth_quad (float4 rows)
 };
 
 __device__ __forceinline__ float edge_weight(const float* img, int HW, int o0, int o1) {
@@ -1486,6 +1487,82 @@ __device__ __forceinline__ void block_sum3(float& a, float& b, float& c) {
     }
 }
 
+__device__ __forceinline__ float4 ldd4(const float* base, int idx, bool bf16) {   // idx % 4 == 0
+    if (bf16) {
+        const uint2 u = *(const uint2*)((const char*)base + ((uint32_t)idx << 1));
+        return make_float4(md2::bf2f((uint16_t)(u.x & 0xffffu)), md2::bf2f((uint16_t)(u.x >> 16)),
+                           md2::bf2f((uint16_t)(u.y & 0xffffu)), md2::bf2f((uint16_t)(u.y >> 16)));
+    }
+    return *(const float4*)((const char*)base + ((uint32_t)idx << 2));
+}
+
+__device__ __forceinline__ float f4at(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+
+// exp(-mean_c |a_c - b_c|) (layers.py:210-211 per edge), the channel mean as div3
+__device__ __forceinline__ float edge_w3(float a0, float b0, float a1, float b1, float a2, float b2) {
+    return expf(-div3(fabsf(a0 - b0) + fabsf(a1 - b1) + fabsf(a2 - b2)));
+}
+
+// One pixel quad (row i, columns j0..j0+3; ws % 4 == 0) of smooth_fwd: every load a
+// float4 row segment or one neighbour column, each horizontal edge's weight once.
+__device__ __forceinline__ void smooth_quad(const float* d, const float* img, bool bf, int hs, int ws, int i, int j0,
+                                            float cx, float cy, float* sg, float& sd, float& sx, float& sy) {
+    const int HW = hs * ws, p = i * ws + j0;
+    const bool up = i > 0, dn = i + 1 < hs, lf = j0 > 0, rt = j0 + 4 < ws;
+    // every load unconditional (border rows / columns clamped to the quad itself, their
+    // terms masked below): a conditional load is a branch the wave waits at, and the
+    // ~20 loads of a quad then paid ~20 serialised memory latencies (21 us per launch)
+    const int pu = up ? p - ws : p, pd = dn ? p + ws : p, pl = lf ? p - 1 : p, pr = rt ? p + 4 : p + 3;
+    const float4 dc = ldd4(d, p, bf);
+    const float4 du = ldd4(d, pu, bf);
+    const float4 dd = ldd4(d, pd, bf);
+    const float dl = ldd(d, pl, bf), dr = ldd(d, pr, bf);
+    float4 ic[3], iu[3], id[3];
+    float il[3], ir[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float* im = img + c * HW;
+        ic[c] = *(const float4*)(im + p);
+        iu[c] = *(const float4*)(im + pu);
+        id[c] = *(const float4*)(im + pd);
+        il[c] = im[pl];
+        ir[c] = im[pr];
+    }
+    // horizontal edges h[k] between columns j0+k-1 and j0+k, k = 0..4
+    auto col = [&](int c, int k) { return k < 0 ? il[c] : k > 3 ? ir[c] : f4at(ic[c], k); };
+    float h[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) h[k] = edge_w3(col(0, k - 1), col(0, k), col(1, k - 1), col(1, k), col(2, k - 1), col(2, k));
+    float g[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const float v = f4at(dc, m);
+        const float vl = m == 0 ? dl : f4at(dc, m - 1), vr = m == 3 ? dr : f4at(dc, m + 1);
+        sd += v;
+        float gx = 0.f, gy = 0.f;
+        if (m < 3 || rt) {
+            const float dv = v - vr;
+            sx += fabsf(dv) * h[m + 1];
+            gx += signf(dv) * h[m + 1];
+        }
+        if (m > 0 || lf) gx -= signf(vl - v) * h[m];
+        if (dn) {
+            const float e = edge_w3(f4at(ic[0], m), f4at(id[0], m), f4at(ic[1], m), f4at(id[1], m), f4at(ic[2], m),
+                                    f4at(id[2], m));
+            const float dv = v - f4at(dd, m);
+            sy += fabsf(dv) * e;
+            gy += signf(dv) * e;
+        }
+        if (up) {
+            const float e = edge_w3(f4at(iu[0], m), f4at(ic[0], m), f4at(iu[1], m), f4at(ic[1], m), f4at(iu[2], m),
+                                    f4at(ic[2], m));
+            gy -= signf(f4at(du, m) - v) * e;
+        }
+        g[m] = gx * cx + gy * cy;
+    }
+    *(float4*)(sg + p) = make_float4(g[0], g[1], g[2], g[3]);
+}
+
 __global__ __launch_bounds__(kBlock) void smooth_fwd_kernel(SmoothArgs a) {
     // consecutive chunks share their boundary rows (p + ws): keep them on one XCD's L2
     const int bid = xcd_contiguous_block(blockIdx.x, gridDim.x);
@@ -1505,6 +1582,14 @@ __global__ __launch_bounds__(kBlock) void smooth_fwd_kernel(SmoothArgs a) {
     // (disp_grad_kernel), so it never re-reads the target pyramid or the neighbours
     float* sg = a.sgrad[s] + (size_t)b * HW;
     const float cx = 1.0f / ((float)hs * (float)(ws - 1)), cy = 1.0f / ((float)(hs - 1) * (float)ws);
+    static_assert(kSmoothChunk == 4 * kBlock, "one pixel quad per thread");
+    if (a.quad) {   // block-uniform
+        const int p = p0 + 4 * threadIdx.x;
+        if (p < HW) {
+            const int i = p / ws;
+            smooth_quad(d, img, bf, hs, ws, i, p - i * ws, cx, cy, sg, sd, sx, sy);
+        }
+    } else
     for (int p = p0 + threadIdx.x; p < min(p0 + kSmoothChunk, HW); p += kBlock) {
         const int i = p / ws, j = p - i * ws;
         const float v = ldd(d, p, bf);
@@ -1589,22 +1674,55 @@ __global__ __launch_bounds__(kWave * kFinWaves) void finalize_fwd_kernel(FinalAr
             const int n = a.nphoto[sc];
             const float* p = a.photo_part[sc];
             double acc[4] = {0.0, 0.0, 0.0, 0.0};
-            int i = q * kWave + lane;
-            for (; i + 3 * 4 * kWave < n; i += 4 * 4 * kWave) {
+            // batches of 8 unconditional loads (clamped index, masked add): a load under
+            // a bound check is a branch the wave waits at, one memory latency per load
+            for (int i0 = q * kWave + lane; i0 < n; i0 += 8 * 4 * kWave) {
+                float v[8];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) acc[u] += (double)p[i + u * 4 * kWave];
+                for (int u = 0; u < 8; ++u) {
+                    const int i = i0 + u * 4 * kWave;
+                    v[u] = p[i < n ? i : 0];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (i0 + u * 4 * kWave < n) acc[u & 3] += (double)v[u];
             }
-            for (int u = 0; i < n; i += 4 * kWave, ++u) acc[u & 3] += (double)p[i];
             double v = wave_sum_d((acc[0] + acc[1]) + (acc[2] + acc[3]));
             if (lane == 0) photo[sc][q] = v;
         }
     }
-    for (int pi = wid; pi < a.num_scales * a.B; pi += kFinWaves) {
+    const int NP = a.num_scales * a.B;
+    constexpr int kPR = 4;   // (scale, image) pairs whose first 2 x 64 chunk partials load together
+    for (int p0 = wid; p0 < NP; p0 += kPR * kFinWaves) {
+        float v[kPR][2][3];
+#pragma unroll
+        for (int r = 0; r < kPR; ++r) {
+            const int pi = p0 + r * kFinWaves < NP ? p0 + r * kFinWaves : 0;
+            const int sc = pi / a.B, b = pi - sc * a.B, nch = a.chunks[sc];
+            const float* p = a.smooth_part[sc] + (size_t)b * nch * 3;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int k = lane + c * kWave < nch ? lane + c * kWave : 0;
+#pragma unroll
+                for (int e = 0; e < 3; ++e) v[r][c][e] = p[3 * k + e];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kPR; ++r) {
+        const int pi = p0 + r * kFinWaves;
+        if (pi >= NP) break;   // wave-uniform
         const int sc = pi / a.B, b = pi - sc * a.B;
         const int hs = a.hs[sc], ws = a.ws[sc], nch = a.chunks[sc];
         const float* p = a.smooth_part[sc] + (size_t)b * nch * 3;
         double sd = 0.0, sx = 0.0, sy = 0.0;
-        for (int k = lane; k < nch; k += kWave) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+            if (lane + c * kWave < nch) {
+                sd += v[r][c][0];
+                sx += v[r][c][1];
+                sy += v[r][c][2];
+            }
+        for (int k = lane + 2 * kWave; k < nch; k += kWave) {   // more than 128 chunks
             sd += p[3 * k];
             sx += p[3 * k + 1];
             sy += p[3 * k + 2];
@@ -1620,6 +1738,7 @@ __global__ __launch_bounds__(kWave * kFinWaves) void finalize_fwd_kernel(FinalAr
             st[1] = (float)sx;
             st[2] = (float)sy;
             st[3] = 0.f;
+        }
         }
     }
     __syncthreads();
@@ -1656,68 +1775,126 @@ struct DispGradArgs {
     float smoothness;
     float* out[MD2_MAX_SCALES];                   // (B, 1, hs, ws), fp32 or bf16 as disp
     int disp_bf16;
+    int quad;                                     // every ws % 4 == 0: disp_grad_quad
 };
 
-// One thread per native pixel; blocks own whole native rows: block_base[s] +
-// (b·hs + i)·bpr[s] + chunk (the (scale, image, row) decode is uniform per block).
-// Upsampled scales: the sum of the <= 2 x 2 backward items' partials that reach this
-// pixel (row blocks, then strips, ascending: fixed order); plus the smoothness gradient.
-__global__ __launch_bounds__(kBlock) void disp_grad_kernel(DispGradArgs a) {
-    // a block reads the rows above and below its own (smoothness stencil, edge
-    // weights): consecutive rows on one XCD, so its L2 serves those re-reads (blocks are
-    // dealt round-robin over the 8 XCDs otherwise — every row fetched three times)
-    const int bid = xcd_contiguous_block(blockIdx.x, gridDim.x);
-    int s = 0;
-    while (s + 1 < a.num_scales && bid >= a.block_base[s + 1]) ++s;
+// dL/d(disp) of native pixel (i, j) from the photometric term: the sum of the <= 2 x 2
+// backward items' partials that reach it (row blocks, then strips, ascending: fixed
+// order), or the full-resolution plane's value at scale 0 / v1
+__device__ __forceinline__ float disp_photo_acc(const DispGradArgs& a, int s, int b, int i, int j) {
     const int sh = a.upsh[s];
-    const int hs = a.hs[s], ws = a.ws[s], lh = a.lh[s], lw = a.lw[s], HWs = hs * ws;
-    const int rb = bid - a.block_base[s], bpr = a.bpr[s];
-    const int row = rb / bpr, chunk = rb - row * bpr;
-    const int b = row / hs, i = row - b * hs;
-    const int j = chunk * kBlock + threadIdx.x;
-    if (j >= ws) return;
-    const int p = i * ws + j;
-    float acc = 0.f;
-    if (sh == 0) {
-        acc = a.dfull[s][(size_t)b * lh * lw + i * lw + j];
-    } else {
-        const int kf = 1 << sh, half = kf >> 1;
-        const float sc = 1.0f / (float)kf;
-        const int NC = up_nc(sh), NR = up_nr(sh);
-        const int strips = a.strips[s], rowblocks = a.rowblocks[s];
-        // the full-resolution footprint of (i, j) (a superset of the weight-carrying rows /
-        // columns) and the items holding it
-        const int yf0 = max(0, kf * (i - 1) + half), yf1 = min(lh, kf * (i + 1) + half);
-        const int xf0 = max(0, kf * (j - 1) + half), xf1 = min(lw, kf * (j + 1) + half);
-        const int rb0 = yf0 / kRowsB, rb1 = (yf1 - 1) / kRowsB;
-        const int st0 = xf0 / kBwdCols, st1 = (xf1 - 1) / kBwdCols;
-        const float* base = a.upart[s] + (size_t)b * rowblocks * strips * NR * NC;
-        for (int r = rb0; r <= rb1; ++r) {
-            const int ic = i - up_src0(r * kRowsB, hs, sc);
-            if (ic < 0 || ic >= NR) continue;
-            for (int t = st0; t <= st1; ++t) {
-                const int jc = j - up_src0(t * kBwdCols, ws, sc);
-                if (jc < 0 || jc >= NC) continue;
-                acc += base[((size_t)r * strips + t) * NR * NC + ic * NC + jc];
-            }
-        }
+    const int hs = a.hs[s], ws = a.ws[s], lh = a.lh[s], lw = a.lw[s];
+    if (sh == 0) return a.dfull[s][(size_t)b * lh * lw + i * lw + j];
+    const int kf = 1 << sh, half = kf >> 1;
+    const float sc = 1.0f / (float)kf;
+    const int NC = up_nc(sh), NR = up_nr(sh);
+    const int strips = a.strips[s], rowblocks = a.rowblocks[s];
+    // the full-resolution footprint of (i, j) (a superset of the weight-carrying rows /
+    // columns) and the items holding it
+    const int yf0 = max(0, kf * (i - 1) + half), yf1 = min(lh, kf * (i + 1) + half);
+    const int xf0 = max(0, kf * (j - 1) + half), xf1 = min(lw, kf * (j + 1) + half);
+    const int rb0 = yf0 / kRowsB, rb1 = (yf1 - 1) / kRowsB;
+    const int st0 = xf0 / kBwdCols, st1 = (xf1 - 1) / kBwdCols;
+    const float* base = a.upart[s] + (size_t)b * rowblocks * strips * NR * NC;
+    // the footprint spans <= 2 row blocks and <= 2 strips (2^(s+1) <= kRowsB, kBwdCols):
+    // four candidate partials, all loaded unconditionally (an invalid one reads the
+    // image's first partial and adds nothing), summed rows then strips ascending
+    static_assert(kRowsB >= (2 << (MD2_MAX_SCALES - 1)) && kBwdCols >= (2 << (MD2_MAX_SCALES - 1)),
+                  "a native pixel's footprint spans at most two backward items per axis");
+    int idx[4];
+    bool ok[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int r = (u >> 1) ? rb1 : rb0, t = (u & 1) ? st1 : st0;
+        const int ic = i - up_src0(r * kRowsB, hs, sc), jc = j - up_src0(t * kBwdCols, ws, sc);
+        ok[u] = ic >= 0 && ic < NR && jc >= 0 && jc < NC && (!(u >> 1) || rb1 != rb0) && (!(u & 1) || st1 != st0);
+        idx[u] = ok[u] ? (r * strips + t) * NR * NC + ic * NC + jc : 0;
     }
-    // smoothness gradient on disp / (mean + 1e-7): the forward's per-unit stencil
-    // gradient scaled by dL/dloss_s, the weight / 2^s, 1/B and 1/mean, plus the term
-    // through the mean (trainer.py:486-490)
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ldf(base, idx[u]);
+    float acc = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (ok[u]) acc += v[u];
+    return acc;
+}
+
+// smoothness gradient on disp / (mean + 1e-7): the forward's per-unit stencil gradient
+// scaled by dL/dloss_s, the weight / 2^s, 1/B and 1/mean, plus the term through the
+// mean (trainer.py:486-490).  sg(x) = k1 * x - k0.
+struct SmoothScale {
+    float k1, k0;
+};
+__device__ __forceinline__ SmoothScale smooth_scale(const DispGradArgs& a, int s, int b) {
+    const int hs = a.hs[s], ws = a.ws[s];
     const float gl = a.grad_loss[s] + a.grad_loss[a.num_scales] / (float)a.num_scales;
     const float* st = a.stats + ((size_t)s * a.B + b) * 4;
     const float m = st[0];
     const float wsm = gl * a.smoothness / (float)(1 << s);
     const float ax = wsm / ((float)a.B * hs * (ws - 1)) / m;
     const float ay = wsm / ((float)a.B * (hs - 1) * ws) / m;
-    const bool bf = a.disp_bf16 != 0;
-    float sg = wsm / ((float)a.B * m) * a.sgrad[s][(size_t)b * HWs + p];
-    sg -= (ax * st[1] + ay * st[2]) / (m * (float)HWs);
+    return {wsm / ((float)a.B * m), (ax * st[1] + ay * st[2]) / (m * (float)(hs * ws))};
+}
+
+// One thread per native pixel; blocks own whole native rows: block_base[s] +
+// (b·hs + i)·bpr[s] + chunk (the (scale, image, row) decode is uniform per block).
+__device__ __forceinline__ void disp_grad_px(const DispGradArgs& a, int bid) {
+    int s = 0;
+    while (s + 1 < a.num_scales && bid >= a.block_base[s + 1]) ++s;
+    const int hs = a.hs[s], ws = a.ws[s], HWs = hs * ws;
+    const int rb = bid - a.block_base[s], bpr = a.bpr[s];
+    const int row = rb / bpr, chunk = rb - row * bpr;
+    const int b = row / hs, i = row - b * hs;
+    const int j = chunk * kBlock + threadIdx.x;
+    if (j >= ws) return;
+    const int p = i * ws + j;
+    const float acc = disp_photo_acc(a, s, b, i, j);
+    const SmoothScale k = smooth_scale(a, s, b);
+    float sg = k.k1 * a.sgrad[s][(size_t)b * HWs + p];
+    sg -= k.k0;
     // the gradient in the disparity's own dtype (bf16: round to nearest even, as the
     // cast-up's autograd backward would)
-    if (bf) ((uint16_t*)a.out[s])[(size_t)b * HWs + p] = (uint16_t)md2::f2bf(acc + sg);
+    if (a.disp_bf16) ((uint16_t*)a.out[s])[(size_t)b * HWs + p] = (uint16_t)md2::f2bf(acc + sg);
     else a.out[s][(size_t)b * HWs + p] = acc + sg;
+}
+
+// Every ws % 4 == 0 (a.quad): one thread per pixel quad of a row, blocks over the flat
+// quads of each scale (block_base in blocks of kBlock quads): float4 reads of the
+// smoothness plane (and the scale-0 plane), one 16-byte (bf16: 8-byte) store.
+__device__ __forceinline__ void disp_grad_quad(const DispGradArgs& a, int bid) {
+    int s = 0;
+    while (s + 1 < a.num_scales && bid >= a.block_base[s + 1]) ++s;
+    const int hs = a.hs[s], ws = a.ws[s], HWs = hs * ws, Q = HWs >> 2;
+    const int q = (bid - a.block_base[s]) * kBlock + threadIdx.x;
+    if (q >= a.B * Q) return;
+    const int b = q / Q, p = (q - b * Q) << 2;
+    const int i = p / ws, j0 = p - i * ws;
+    float acc[4];
+    if (a.upsh[s] == 0) {
+        const float4 v = *(const float4*)(a.dfull[s] + (size_t)b * HWs + p);   // lh, lw == hs, ws
+        acc[0] = v.x, acc[1] = v.y, acc[2] = v.z, acc[3] = v.w;
+    } else {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[m] = disp_photo_acc(a, s, b, i, j0 + m);
+    }
+    const SmoothScale k = smooth_scale(a, s, b);
+    const float4 g = *(const float4*)(a.sgrad[s] + (size_t)b * HWs + p);
+    float o[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        float sg = k.k1 * f4at(g, m);
+        sg -= k.k0;
+        o[m] = acc[m] + sg;
+    }
+    const size_t e = (size_t)b * HWs + p;
+    if (a.disp_bf16) {
+        const uint32_t lo = md2::f2bf(o[0]) | ((uint32_t)md2::f2bf(o[1]) << 16);
+        const uint32_t hi = md2::f2bf(o[2]) | ((uint32_t)md2::f2bf(o[3]) << 16);
+        *(uint2*)((uint16_t*)a.out[s] + e) = make_uint2(lo, hi);
+    } else {
+        *(float4*)(a.out[s] + e) = make_float4(o[0], o[1], o[2], o[3]);
+    }
 }
 
 // ----------------------------------------------------------------------------
@@ -1731,10 +1908,9 @@ struct DTArgs {
     float* grad_T;                          // (S,B,4,4) or (num_scales,S,B,4,4)
 };
 
-__global__ __launch_bounds__(kBlock) void grad_T_kernel(DTArgs a) {
+__device__ __forceinline__ void grad_T_block(const DTArgs& a, int id) {
     // one block per (tscale, f, b); every thread accumulates all 12 dP entries over
     // a strided share of the partials, then one fixed-order block reduction
-    int id = blockIdx.x;
     const int b = id % a.B;
     id /= a.B;
     const int f = id % a.S;
@@ -1746,12 +1922,41 @@ __global__ __launch_bounds__(kBlock) void grad_T_kernel(DTArgs a) {
     // dT = sum_s K_s^T [dP_s; 0] is linear in the partials: every thread maps its own
     // partials through K_s^T and sums over the scales, then ONE fixed-order block
     // reduction of the 16 entries (instead of one 12-entry reduction per scale)
-    for (int s = 0; s < a.num_scales; ++s) {
+    // first every scale's partial k = t, its 12 loads per scale issued together (a
+    // loop that waits for each scale's loads before the next pays ~4 memory latencies)
+    // (unconditional loads from clamped addresses; unused ones are masked afterwards)
+    float first[MD2_MAX_SCALES][12], Ks[MD2_MAX_SCALES][12];
+    bool use[MD2_MAX_SCALES];
+#pragma unroll
+    for (int s = 0; s < MD2_MAX_SCALES; ++s) {
+        const int sc = s < a.num_scales ? s : 0;
+        const int n = a.wpi[sc];
+        use[s] = s < a.num_scales && !(a.per_scale && s != ts) && t < n;
+        const float* base = a.dP_part[sc] + ((size_t)f * a.B * n + (size_t)b * n + (use[s] ? t : 0)) * 12;
+        const float* K = a.K[sc] + b * 16;
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            first[s][j] = base[j];
+            Ks[s][j] = K[j];
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < MD2_MAX_SCALES; ++s) {
+        if (!use[s]) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                dT[r * 4 + c] += (double)Ks[s][0 * 4 + r] * (double)first[s][0 * 4 + c] +
+                                 (double)Ks[s][1 * 4 + r] * (double)first[s][1 * 4 + c] +
+                                 (double)Ks[s][2 * 4 + r] * (double)first[s][2 * 4 + c];
+    }
+    for (int s = 0; s < a.num_scales; ++s) {   // the rest (more than kBlock partials per image)
         if (a.per_scale && s != ts) continue;
         const int n = a.wpi[s];
         const float* base = a.dP_part[s] + ((size_t)f * a.B * n + (size_t)b * n) * 12;
         const float* K = a.K[s] + b * 16;
-        for (int k = t; k < n; k += kBlock) {
+        for (int k = t + kBlock; k < n; k += kBlock) {
             double dP[12];
 #pragma unroll
             for (int j = 0; j < 12; ++j) dP[j] = (double)base[(size_t)k * 12 + j];
@@ -1770,6 +1975,23 @@ __global__ __launch_bounds__(kBlock) void grad_T_kernel(DTArgs a) {
         for (int j = 0; j < 16; ++j) v = (j == t) ? dT[j] : v;
         a.grad_T[(((size_t)ts * a.S + f) * a.B + b) * 16 + t] = (float)v;
     }
+}
+
+// The backward's tail in one launch: blocks [0, nTb) reduce dL/dT (nT·S·B of them
+// work, the rest of the 8-aligned prefix returns), the others write dL/d(disp) —
+// the 24 long fp64 reduction blocks run beside the short per-pixel ones instead of
+// after them.  nTb % 8 == 0 keeps disp_grad's XCD-contiguous block numbering.
+__global__ __launch_bounds__(kBlock) void disp_grad_T_kernel(DispGradArgs g, DTArgs ta, int nT, int nTb) {
+    const int bx = blockIdx.x;
+    if (bx < nTb) {
+        if (bx < nT) grad_T_block(ta, bx);
+        return;
+    }
+    // a block's pixels share partial grids with the neighbouring rows: consecutive
+    // blocks on one XCD, so its L2 serves those re-reads
+    const int bid = xcd_contiguous_block(bx - nTb, gridDim.x - nTb);
+    if (g.quad) disp_grad_quad(g, bid);
+    else disp_grad_px(g, bid);
 }
 
 // ----------------------------------------------------------------------------
@@ -2198,6 +2420,8 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
     }
     sa.block_base[L.nscales] = blocks;
     sa.disp_bf16 = d->disp_dtype == MD2_DTYPE_BF16;
+    sa.quad = 1;
+    for (int s = 0; s < L.nscales; ++s) sa.quad &= (L.ws[s] % 4 == 0) ? 1 : 0;
     hipLaunchKernelGGL(smooth_fwd_kernel, dim3(blocks), dim3(kBlock), 0, st, sa);
     if ((rc = hip_check("smooth_fwd_kernel"))) return rc;
 
@@ -2267,6 +2491,8 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
     g.smoothness = d->disparity_smoothness;
     g.disp_bf16 = d->disp_dtype == MD2_DTYPE_BF16;
     int gblocks = 0;
+    g.quad = 1;
+    for (int s = 0; s < L.nscales; ++s) g.quad &= (L.ws[s] % 4 == 0) ? 1 : 0;
     for (int s = 0; s < L.nscales; ++s) {   // all scales in one launch
         g.hs[s] = L.hs[s];
         g.ws[s] = L.ws[s];
@@ -2281,11 +2507,9 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
         g.out[s] = grad_disp[s];
         g.block_base[s] = gblocks;
         g.bpr[s] = (L.ws[s] + kBlock - 1) / kBlock;
-        gblocks += L.B * L.hs[s] * g.bpr[s];
+        gblocks += g.quad ? (L.B * L.hs[s] * L.ws[s] / 4 + kBlock - 1) / kBlock : L.B * L.hs[s] * g.bpr[s];
     }
     g.block_base[L.nscales] = gblocks;
-    hipLaunchKernelGGL(disp_grad_kernel, dim3(gblocks), dim3(kBlock), 0, st, g);
-    if ((rc = hip_check("disp_grad_kernel"))) return rc;
 
     DTArgs ta;
     memset(&ta, 0, sizeof(ta));
@@ -2299,12 +2523,13 @@ int md2_photometric_bwd(const md2_desc* d, const md2_tensors* t, const float* gr
         ta.K[s] = t->K[L.v1 ? s : 0];
     }
     ta.grad_T = grad_T;
-    const int nT = ta.per_scale ? L.nscales : 1;
+    const int nT = (ta.per_scale ? L.nscales : 1) * L.S * L.B, nTb = (nT + 7) / 8 * 8;
     if (c1)
-        hipExtLaunchKernelGGL(grad_T_kernel, dim3(nT * L.S * L.B), dim3(kBlock), 0, st, nullptr, c1, 0, ta);
+        hipExtLaunchKernelGGL(disp_grad_T_kernel, dim3(nTb + gblocks), dim3(kBlock), 0, st, nullptr, c1, 0, g, ta, nT,
+                              nTb);
     else
-        hipLaunchKernelGGL(grad_T_kernel, dim3(nT * L.S * L.B), dim3(kBlock), 0, st, ta);
-    return hip_check("grad_T_kernel");
+        hipLaunchKernelGGL(disp_grad_T_kernel, dim3(nTb + gblocks), dim3(kBlock), 0, st, g, ta, nT, nTb);
+    return hip_check("disp_grad_T_kernel");
 }
 
 int md2_generate_images(const md2_desc* d, const md2_tensors* t, float* const* depth_out, float* const* sample_out,

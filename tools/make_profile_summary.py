@@ -19,7 +19,7 @@ import shutil
 import sys
 
 VALU_ISSUE_PER_S = 256 * 4 * 0.5 * 2.4e9   # wave-instructions/s (SIMD32 issues a wave64 op per 2 clk)
-HOT = ("pack_src8", "photo_", "smooth_fwd", "finalize_fwd", "disp_grad_kernel", "grad_T_kernel")
+HOT = ("pack_src8", "photo_", "smooth_fwd", "finalize_fwd", "disp_grad", "grad_T_kernel")
 
 
 def short(n):
