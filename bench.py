@@ -212,13 +212,14 @@ def time_hot_kernels(trainer, batch, n=10):
     T = trainer._stacked_T(batch, outputs).detach().requires_grad_(True)
     disps = [outputs[("disp", s)].detach().requires_grad_(True) for s in range(hot.num_scales)]
     colors = trainer._colors(batch)
+    src8 = batch.get("color_src8")
     for _ in range(2):
-        loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=1)
+        loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=1, src8=src8)
         loss[hot.num_scales].backward()
     torch.cuda.synchronize()
     with _lib.KernelTimer(max_launches=4 * n + 8) as kt:
         for i in range(n):
-            loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=2 + i)
+            loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=2 + i, src8=src8)
             loss[hot.num_scales].backward()
     return kt
 

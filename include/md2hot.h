@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 19
+#define MD2_ABI_VERSION 20
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -99,6 +99,13 @@ typedef struct md2_tensors {
      * loss resolution (trainer.py:449-453), per scale packed back to back, scale s
      * shaped (B, S, h_s, w_s).  Multiplies each frame's reprojection loss. */
     const float* mask;
+    /* Optional (ABI 20): the source frames' scale-0 colours as 8-bit RGBx dwords,
+     * (S, B, H, W) uint32, byte c of a pixel = k with color[0][1+f][b][c][y][x] == k/255
+     * exactly — what the loader's to_tensor makes of 8-bit images (mono_dataset.py:
+     * 199-200), e.g. written by md2_aug_run2 as it decodes them.  NULL: the forward
+     * packs them from the fp32 planes itself and checks every colour (pack_src8).  The
+     * forward and the backward must see the same value. */
+    const uint32_t* src8;
 } md2_tensors;
 
 int md2_abi_version(void);
@@ -398,6 +405,12 @@ void md2_aug_plan_destroy(md2_aug_plan* plan);
  */
 int md2_aug_run(md2_aug_plan* plan, const uint8_t* frames, const md2_aug_item* items,
                 float* const* color, float* const* color_aug, void* stream);
+/* ... and (ABI 20) src8, device uint32 (F-1, B, height, width) or NULL: frames 1..F-1
+ * (the photometric sources, frame_ids[1:]) at scale 0 as RGBx dwords, byte c = the
+ * 8-bit colour whose k/255 is color[0] — md2_tensors.src8, so the hot path's forward
+ * does not re-pack them from the fp32 planes. */
+int md2_aug_run2(md2_aug_plan* plan, const uint8_t* frames, const md2_aug_item* items,
+                 float* const* color, float* const* color_aug, uint32_t* src8, void* stream);
 
 /*
  * Training-mode BatchNorm2d (+ residual add) (+ ReLU) on channels_last activations:

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -49,7 +49,8 @@ class Tensors(ctypes.Structure):
                 ("T", _vp),
                 ("noise", _vp),
                 ("seed_ptr", _vp),
-                ("mask", _vp)]
+                ("mask", _vp),
+                ("src8", _vp)]
 
 
 _lock = threading.Lock()
@@ -67,7 +68,7 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_conv_fwd", "md2_conv_workspace_bytes", "md2_conv_split_weights",
            "md2_conv_dgrad", "md2_conv_wgrad", "md2_conv_direct", "md2_conv_wgrad_direct",
            "md2_conv_wgrad_direct_workspace_bytes", "md2_conv_split_weights_multi", "md2_bn_fwd_mask",
-           "md2_bn_bwd_mask", "md2_build_id", "md2_maxpool3s2_bwd_multi", "md2_decoder_pad_bwd2"]
+           "md2_bn_bwd_mask", "md2_build_id", "md2_maxpool3s2_bwd_multi", "md2_decoder_pad_bwd2", "md2_aug_run2"]
 
 DTYPE_F32 = 0    # md2_desc.disp_dtype
 DTYPE_BF16 = 1
@@ -247,6 +248,8 @@ def _declare(L):
     L.md2_aug_plan_destroy.argtypes = [_vp]
     L.md2_aug_run.restype = ctypes.c_int
     L.md2_aug_run.argtypes = [_vp, _vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp]
+    L.md2_aug_run2.restype = ctypes.c_int
+    L.md2_aug_run2.argtypes = [_vp, _vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp]
     L.md2_bn_workspace_bytes.restype = ctypes.c_size_t
     L.md2_bn_workspace_bytes.argtypes = [ctypes.POINTER(BnDesc)]
     L.md2_bn_fwd.restype = ctypes.c_int

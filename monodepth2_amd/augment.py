@@ -135,9 +135,13 @@ class GpuAugment:
             color_aug.append(torch.empty(shp, device=self.device))
         cp = (ctypes.c_void_p * self.num_scales)(*[t.data_ptr() for t in color])
         ap = (ctypes.c_void_p * self.num_scales)(*[t.data_ptr() for t in color_aug])
+        # the photometric sources (frames 1..F-1) at scale 0 as 8-bit RGBx dwords too
+        self.src8 = torch.empty((F - 1, B, self.height, self.width), dtype=torch.int32,
+                                device=self.device) if F > 1 else None
         stream = _lib.stream(self.device)
-        _lib.check(_lib.lib().md2_aug_run(self._plan, frames.data_ptr(), ctypes.byref(items), cp, ap, stream),
-                   "md2_aug_run")
+        _lib.check(_lib.lib().md2_aug_run2(self._plan, frames.data_ptr(), ctypes.byref(items), cp, ap,
+                                           self.src8.data_ptr() if self.src8 is not None else None, stream),
+                   "md2_aug_run2")
         return color, color_aug
 
     def __call__(self, frames: torch.Tensor, draws: Sequence[ItemDraw], sides: Optional[Sequence[str]] = None
@@ -151,6 +155,8 @@ class GpuAugment:
             K, inv_K = self._K[s]
             inputs[("K", s)] = K
             inputs[("inv_K", s)] = inv_K
+        if self.src8 is not None:   # the hot path's 8-bit sources (md2_tensors.src8)
+            inputs["color_src8"] = self.src8
         if "s" in self.frame_ids:
             # mono_dataset.py:192-198: t_x = side_sign * baseline_sign * 0.1
             # the side comes from each split line (mono_dataset.py:136-140); no default:

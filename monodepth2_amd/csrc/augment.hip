@@ -89,7 +89,8 @@ __global__ void __launch_bounds__(kThreads) resize_v_kernel(const uint8_t* __res
                                                             uint8_t* __restrict__ dst, int N, int sh, int dh,
                                                             int w, const int2* __restrict__ bounds,
                                                             const int* __restrict__ kk, int ksize,
-                                                            float* __restrict__ color) {
+                                                            float* __restrict__ color, uint32_t* __restrict__ rgbx,
+                                                            int B) {
     const size_t total = (size_t)N * dh * w;
     const size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x;
     if (i >= total) return;
@@ -116,6 +117,8 @@ __global__ void __launch_bounds__(kThreads) resize_v_kernel(const uint8_t* __res
     c[0] = (float)o[0] / 255.f;
     c[hw] = (float)o[1] / 255.f;
     c[2 * hw] = (float)o[2] / 255.f;
+    if (rgbx && n >= (size_t)B)   // frames 1.. (the photometric sources) as RGBx dwords
+        rgbx[(n - B) * hw + (i - n * hw)] = (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16);
 }
 
 // Both LANCZOS passes of one pyramid level for a TW x TH output tile, through LDS:
@@ -164,7 +167,7 @@ __global__ void __launch_bounds__(kThreads) resize_fused_kernel(
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, float* __restrict__ color, int sh, int sw, int dh,
     int dw, const int2* __restrict__ bx, const int* __restrict__ kx, const int2* __restrict__ by,
     const int* __restrict__ ky, FusedLds L, const md2_aug_item* __restrict__ items, int B, int flip_level,
-    unsigned long long* __restrict__ sums) {
+    unsigned long long* __restrict__ sums, uint32_t* __restrict__ rgbx) {
     extern __shared__ __align__(16) uint8_t lds[];
     uint8_t* patch = lds + L.patch;
     uint32_t* inter = (uint32_t*)(lds + L.inter);
@@ -253,6 +256,8 @@ __global__ void __launch_bounds__(kThreads) resize_fused_kernel(
             c[0] = (float)v0 / 255.f;
             c[hw] = (float)v1 / 255.f;
             c[2 * hw] = (float)v2 / 255.f;
+            if (rgbx && n >= B)   // block-uniform: frames 1.. (the photometric sources) as RGBx dwords
+                rgbx[(size_t)(n - B) * hw + pix] = (uint32_t)v0 | ((uint32_t)v1 << 8) | ((uint32_t)v2 << 16);
             if (it.color_aug)
                 msum += (unsigned long long)contrast_gray(v0, v1, v2, order, it.brightness, it.contrast,
                                                           it.saturation, it.hue_shift, stop);
@@ -488,7 +493,8 @@ size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 // resize_fused_kernel instantiation for the two window sizes (2*ceil(3*max(scale,1))+1:
 // 7 up-scaling, 9/11/13 down to 2x), nullptr for wider windows (two-pass kernels).
 using FusedFn = void (*)(const uint8_t*, uint8_t*, float*, int, int, int, int, const int2*, const int*,
-                         const int2*, const int*, FusedLds, const md2_aug_item*, int, int, unsigned long long*);
+                         const int2*, const int*, FusedLds, const md2_aug_item*, int, int, unsigned long long*,
+                         uint32_t*);
 
 template <int KX>
 FusedFn fused_for_ky(int ky) {
@@ -654,6 +660,11 @@ void md2_aug_plan_destroy(md2_aug_plan* P) {
 
 int md2_aug_run(md2_aug_plan* P, const uint8_t* frames, const md2_aug_item* host_items, float* const* color,
                 float* const* color_aug, void* stream) {
+    return md2_aug_run2(P, frames, host_items, color, color_aug, nullptr, stream);
+}
+
+int md2_aug_run2(md2_aug_plan* P, const uint8_t* frames, const md2_aug_item* host_items, float* const* color,
+                 float* const* color_aug, uint32_t* src8, void* stream) {
     if (!P || !frames || !host_items || !color || !color_aug)
         return md2_report_error(MD2_ERR_ARG, "aug: plan/frames/items/color/color_aug is NULL");
     const md2_aug_desc& d = P->d;
@@ -687,13 +698,14 @@ int md2_aug_run(md2_aug_plan* P, const uint8_t* frames, const md2_aug_item* host
             const dim3 grid((P->w[s] + kTileW - 1) / kTileW, (P->h[s] + kTileH - 1) / kTileH, N);
             hipLaunchKernelGGL(fused_kernel(P->kx[s], P->ky[s]), grid, dim3(kThreads), P->lds[s].bytes, st, src,
                                P->pyr[s], color[s], P->sh[s], P->sw[s], P->h[s], P->w[s], P->bx[s], P->wx[s],
-                               P->by[s], P->wy[s], P->lds[s], items, B, s == 0 ? 1 : 0, P->sums + (size_t)s * N);
+                               P->by[s], P->wy[s], P->lds[s], items, B, s == 0 ? 1 : 0, P->sums + (size_t)s * N,
+                               s == 0 ? src8 : nullptr);
         } else {
             hipLaunchKernelGGL(resize_h_kernel, dim3(blocks_for((size_t)N * P->sh[s] * P->w[s])), dim3(kThreads), 0,
                                st, src, P->mid, N, P->sh[s], P->sw[s], P->w[s], P->bx[s], P->wx[s], P->kx[s], flip, B);
             hipLaunchKernelGGL(resize_v_kernel, dim3(blocks_for((size_t)N * P->h[s] * P->w[s])), dim3(kThreads), 0,
                                st, P->mid, P->pyr[s], N, P->sh[s], P->h[s], P->w[s], P->by[s], P->wy[s], P->ky[s],
-                               color[s]);
+                               color[s], s == 0 ? src8 : nullptr, B);
         }
     }
     Levels L{};

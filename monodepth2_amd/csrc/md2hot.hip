@@ -544,7 +544,7 @@ __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int 
     c.dbf16 = a.disp_bf16 != 0;
     c.disp = disp_off(a.disp[ls], (size_t)b * c.dh * c.dw, c.dbf16);
     c.src = a.src[f] + (size_t)b * 3 * HW;
-    c.src8 = (a.src8[f] && a.exact[f * a.B + b]) ? a.src8[f] + (size_t)b * HW : nullptr;
+    c.src8 = (a.src8[f] && (!a.exact || a.exact[f * a.B + b])) ? a.src8[f] + (size_t)b * HW : nullptr;
     c.h = a.h;
     c.w = a.w;
     c.sx = (float)a.w / (float)(a.w - 1);
@@ -2251,9 +2251,10 @@ void photo_args(const md2_desc* d, const md2_tensors* t, const Layout& L, int s_
     }
     a.ident = ws ? (float*)(ws + L.ident_off) : nullptr;
     if (ws && !L.v1) {
-        for (int f = 0; f < L.S; ++f)
-            a.src8[f] = (const uint32_t*)(ws + L.src8_off) + (size_t)f * L.B * L.lh[0] * L.lw[0];
-        a.exact = (const int*)(ws + L.exact_off);
+        // the caller's 8-bit copies (exact by contract: no flags) or the forward's pack
+        const uint32_t* s8 = t->src8 ? t->src8 : (const uint32_t*)(ws + L.src8_off);
+        for (int f = 0; f < L.S; ++f) a.src8[f] = s8 + (size_t)f * L.B * L.lh[0] * L.lw[0];
+        a.exact = t->src8 ? nullptr : (const int*)(ws + L.exact_off);
     }
 }
 
@@ -2378,7 +2379,7 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
         for (int f = 0; f < L.S; ++f) pk.src[f] = t->color[0][f + 1];
         pk.out = (uint32_t*)(ws + L.src8_off);
         pk.exact = (int*)(ws + L.exact_off);
-        if (hipMemsetAsync(pk.exact, 0x01, sizeof(int) * (size_t)L.S * L.B, st) != hipSuccess)
+        if (!t->src8 && hipMemsetAsync(pk.exact, 0x01, sizeof(int) * (size_t)L.S * L.B, st) != hipSuccess)
             return fail(MD2_ERR_HIP, "hipMemsetAsync failed");
         const int per_img = (pk.HW + 4 * kBlock - 1) / (4 * kBlock);
         timing_slot(2, &c0, &c1);   // the whole call: pack .. finalize
@@ -2390,7 +2391,9 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
         // and one launch per step); otherwise the identity pass writes them, and the
         // 8-bit copies too (it reads every source pixel anyway)
         a.ident_fused = (L.nscales == kWavesPerBlock && !(d->flags & MD2_NO_AUTOMASK)) ? 1 : 0;
-        if (!(d->flags & MD2_NO_AUTOMASK) && !a.ident_fused) {
+        if (t->src8) {   // the caller's copies: nothing to pack
+            if (c0 && hipEventRecord(c0, st) != hipSuccess) return fail(MD2_ERR_HIP, "hipEventRecord failed");
+        } else if (!(d->flags & MD2_NO_AUTOMASK) && !a.ident_fused) {
             a.pack8 = pk.out;
             a.pack_exact = pk.exact;
             if (c0 && hipEventRecord(c0, st) != hipSuccess) return fail(MD2_ERR_HIP, "hipEventRecord failed");

@@ -74,6 +74,24 @@ def _texture(gen: torch.Generator, batch: int, height: int, width: int,
     return out
 
 
+def pack_rgbx(colors: Sequence[torch.Tensor]) -> torch.Tensor:
+    """The photometric sources' 8-bit copies (md2_tensors.src8): (S, B, H, W) int32 RGBx
+    dwords, byte c = k of channel c, from (B, 3, H, W) colours that are exactly k/255
+    (what the loader's to_tensor makes of uint8 images; md2_aug_run2 writes the same
+    dwords as it decodes).  Raises if a colour is not k/255."""
+    out = []
+    for c in colors:
+        k = torch.round(c.float() * 255.0)
+        # checked on the host in float64 (exact k/255 rounded once to float32): a GPU
+        # float division need not be correctly rounded
+        kc = k.cpu().double()
+        if not torch.equal((kc / 255.0).float(), c.float().cpu()) or bool(((kc < 0) | (kc > 255)).any()):
+            raise ValueError("pack_rgbx: colours must be exactly k/255, k in 0..255")
+        k = k.to(torch.int32)
+        out.append(k[:, 0] | (k[:, 1] << 8) | (k[:, 2] << 16))
+    return torch.stack(out).contiguous()
+
+
 def synthetic_batch(batch_size: int, height: int, width: int,
                     frame_ids: Sequence[FrameId] = (0, -1, 1), num_scales: int = 4,
                     seed: int = 0, device: Union[str, torch.device] = "cpu",
@@ -82,7 +100,9 @@ def synthetic_batch(batch_size: int, height: int, width: int,
 
     eight_bit: colours quantised to k/255 at every scale, as the reference's loader
     delivers them (uint8 PIL images through to_tensor, datasets/mono_dataset.py:
-    199-200: float32 k / 255); default off to keep the committed fixtures' inputs.
+    199-200: float32 k / 255), plus "color_src8" — the sources' 8-bit copies
+    (pack_rgbx) the hot path reads instead of packing them per step; default off to
+    keep the committed fixtures' inputs.
     """
     gen = torch.Generator().manual_seed(int(seed))
     shifts = []
@@ -101,6 +121,8 @@ def synthetic_batch(batch_size: int, height: int, width: int,
             level = torch.round(cur * 255.0) / 255.0 if eight_bit else cur
             inputs[("color", f, s)] = level
             inputs[("color_aug", f, s)] = level
+    if eight_bit and len(frame_ids) > 1:
+        inputs["color_src8"] = pack_rgbx([inputs[("color", f, 0)] for f in frame_ids[1:]])
     for s in range(num_scales):
         K, inv_K = scaled_intrinsics(height, width, s)
         inputs[("K", s)] = torch.from_numpy(K).unsqueeze(0).repeat(batch_size, 1, 1)

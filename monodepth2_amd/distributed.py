@@ -120,6 +120,9 @@ def shard(batch: Dict, rank: int, world: int) -> Dict:
         if k == "stereo_T" or (isinstance(k, tuple) and k[0] in ("color", "color_aug", "K", "inv_K")):
             n = v.shape[0] // world
             out[k] = v[rank * n:(rank + 1) * n]
+        elif k == "color_src8":   # (S, B, H, W): the batch is the second axis
+            n = v.shape[1] // world
+            out[k] = v[:, rank * n:(rank + 1) * n].contiguous()
         else:
             out[k] = v
     return out

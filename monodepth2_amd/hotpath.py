@@ -98,9 +98,16 @@ class Operands:
     def __init__(self, cfg: HotPathConfig, colors: Sequence[Sequence[Optional[torch.Tensor]]],
                  K: Sequence[Optional[torch.Tensor]], inv_K: Sequence[Optional[torch.Tensor]],
                  noise: Optional[Dict[int, torch.Tensor]], device: torch.device,
-                 seed_tensor: Optional[torch.Tensor] = None):
+                 seed_tensor: Optional[torch.Tensor] = None, src8: Optional[torch.Tensor] = None):
         B, H, W, S = cfg.batch, cfg.height, cfg.width, cfg.num_src
         self.cfg = cfg
+        self.src8 = None
+        if src8 is not None and not cfg.v1_multiscale:   # (the v1 layout samples every scale's planes)
+            if (src8.device != device or src8.dtype != torch.int32 or tuple(src8.shape) != (S, B, H, W)
+                    or not src8.is_contiguous()):
+                raise ValueError(f"src8 must be a contiguous int32 {(S, B, H, W)} tensor on {device}, got "
+                                 f"{src8.dtype} {tuple(src8.shape)} on {src8.device}")
+            self.src8 = src8
         if seed_tensor is not None and (seed_tensor.device != device or seed_tensor.dtype != torch.int64
                                         or seed_tensor.numel() != 1):
             raise ValueError("seed_tensor must be a 1-element int64 tensor on " + str(device))
@@ -146,6 +153,7 @@ class Operands:
         st.noise = self.noise.data_ptr() if self.noise is not None else None
         st.seed_ptr = self.seed_tensor.data_ptr() if self.seed_tensor is not None else None
         st.mask = mask.data_ptr() if mask is not None else None
+        st.src8 = self.src8.data_ptr() if self.src8 is not None else None
         return st
 
 
@@ -196,7 +204,8 @@ class _PhotometricLoss(torch.autograd.Function):
 def photometric_loss(cfg: HotPathConfig, disps: Sequence[torch.Tensor], colors, K, inv_K, T: torch.Tensor,
                      noise: Optional[Dict[int, torch.Tensor]] = None, seed: int = 0,
                      seed_tensor: Optional[torch.Tensor] = None,
-                     mask: Optional[Dict[int, torch.Tensor]] = None):
+                     mask: Optional[Dict[int, torch.Tensor]] = None,
+                     src8: Optional[torch.Tensor] = None):
     """Fused hot path.  Returns (loss_vec, select).
 
     loss_vec[s] = losses["loss/s"], loss_vec[num_scales] = losses["loss"];
@@ -208,6 +217,9 @@ def photometric_loss(cfg: HotPathConfig, disps: Sequence[torch.Tensor], colors, 
     mask: with cfg.predictive_mask, {scale: (B,S,h,w)} predictive masks already
     upsampled to the loss resolution (trainer.py:449-455); differentiable.  The
     BCE weighting term (trainer.py:457-459) is the caller's.
+    src8: optional (S,B,H,W) int32 8-bit RGBx copies of the source frames at scale 0
+    (data.pack_rgbx / md2_aug_run2; the colours must be exactly k/255 — a contract,
+    not checked): the forward then reads them instead of packing them per call.
     """
     dev = T.device
     if dev.type != "cuda":
@@ -224,7 +236,7 @@ def photometric_loss(cfg: HotPathConfig, disps: Sequence[torch.Tensor], colors, 
             raise ValueError(f"disp[{s}] is {d.dtype}, disp[0] {disps[0].dtype}: one dtype for every scale")
     tshape = (cfg.num_scales, S, B, 4, 4) if cfg.t_per_scale else (S, B, 4, 4)
     _require(T, "T", tshape, dev)
-    ops = Operands(cfg, colors, K, inv_K, noise, dev, seed_tensor)
+    ops = Operands(cfg, colors, K, inv_K, noise, dev, seed_tensor, src8)
     packed = None
     if cfg.predictive_mask:
         if mask is None:

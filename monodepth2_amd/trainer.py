@@ -427,7 +427,8 @@ class Trainer:
                                                           for s in range(self.num_scales)})
         loss_vec, sel = photometric_loss(self.hot, [outputs[("disp", s)] for s in range(self.num_scales)],
                                          self._colors(inputs), K, inv_K, T, noise=self.noise_override,
-                                         seed=seed, seed_tensor=self.seed_tensor, mask=mask)
+                                         seed=seed, seed_tensor=self.seed_tensor, mask=mask,
+                                         src8=inputs.get("color_src8"))
         if bce is not None:   # trainer.py:457-459: loss/s += 0.2 * BCE(mask, 1)
             loss_vec = loss_vec + torch.cat([bce, bce.mean().view(1)])
         losses = {"loss/{}".format(s): loss_vec[s] for s in range(self.num_scales)}
@@ -487,6 +488,7 @@ class Trainer:
         self.seed_tensor = torch.zeros(1, dtype=torch.int64, device=self.device)
         snap = self._training_state()
         side = torch.cuda.Stream(self.device)
+        self.graph_stream = side   # an eager step after the capture belongs here too (its AccumulateGrad nodes)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             for _ in range(warmup):

@@ -44,7 +44,10 @@ def test_build_id_matches_tree(L):
 
 def test_struct_sizes():
     assert ctypes.sizeof(_lib.Desc) == 48
-    assert ctypes.sizeof(_lib.Tensors) == 8 * (4 + 16 + 4 + 4 + 4)
+    # disp[4], color[4][4], K[4], inv_K[4], T, noise, seed_ptr, mask, src8 (ABI 20)
+    assert ctypes.sizeof(_lib.Tensors) == 8 * (4 + 16 + 4 + 4 + 5)
+    # weight, planes_fwd, planes_dgrad, 4 x int32, planes_col (ABI 19)
+    assert ctypes.sizeof(_lib.WsplitEntry) == 48 and _lib.WsplitEntry.planes_col.offset == 40
 
 
 @pytest.mark.parametrize("B,H,W,S", [(12, 192, 640, 2), (8, 320, 1024, 2), (12, 192, 640, 3), (1, 32, 32, 1)])

@@ -41,6 +41,10 @@ def _check(aug, frames_np, draws, h, w, S, sides=None):
                 gaug = inputs[("color_aug", fid, s)][b].cpu().numpy()
                 assert np.array_equal(got, color[s]), (fid, b, s, int((got != color[s]).sum()))
                 assert np.array_equal(gaug, caug[s]), (fid, b, s, d, int((gaug != caug[s]).sum()))
+    # md2_aug_run2's RGBx copies of the sources (frames 1..) at scale 0 == pack_rgbx of color
+    from monodepth2_amd.data import pack_rgbx
+    if len(aug.frame_ids) > 1:
+        assert torch.equal(inputs["color_src8"], pack_rgbx([inputs[("color", f, 0)] for f in aug.frame_ids[1:]]))
     return inputs
 
 

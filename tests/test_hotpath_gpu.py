@@ -294,6 +294,47 @@ def test_eight_bit_sources_match_oracle(name):
 
 
 @pytest.mark.parametrize("name", ["mono_b2_64x128", "stereo_b2_64x128"])
+def test_caller_src8_matches_in_kernel_pack(name):
+    """md2_tensors.src8: the sources' 8-bit RGBx copies handed in by the caller
+    (data.pack_rgbx / md2_aug_run2) instead of packed by the forward — the same
+    dwords, so the losses, the selection and every gradient are bitwise those of the
+    in-kernel pack."""
+    from monodepth2_amd.hotpath import photometric_loss
+    from monodepth2_amd.data import pack_rgbx
+    from hotpath_case import case_config, case_operands
+    from monodepth2_amd.layers import transformation_from_parameters
+    case = Case(name)
+    for k, v in list(case.inputs.items()):
+        if isinstance(k, tuple) and k[0] in ("color", "color_aug"):
+            case.inputs[k] = torch.round(v * 255.0) / 255.0
+    cfg = case_config(case)
+    colors, K, inv_K, noise = case_operands(case, "cuda")
+    Ts, ti = [], 0
+    for f in case.frame_ids[1:]:
+        if f == "s":
+            Ts.append(case.inputs["stereo_T"].cuda())
+        else:
+            Ts.append(transformation_from_parameters(case.axisangle[ti].cuda(), case.translation[ti].cuda(),
+                                                     invert=(f < 0)))
+            ti += 1
+    src8 = pack_rgbx([colors[0][fi] for fi in range(1, cfg.num_src + 1)])
+    res = []
+    for s8 in (None, src8):
+        T = torch.stack(Ts).detach().requires_grad_(True)
+        disps = [case.disps[s].cuda().requires_grad_(True) for s in range(4)]
+        loss, sel = photometric_loss(cfg, disps, colors, K, inv_K, T, noise=noise, src8=s8)
+        loss[cfg.num_scales].backward()
+        torch.cuda.synchronize()
+        res.append((loss.clone(), sel.clone(), [d.grad.clone() for d in disps], T.grad.clone()))
+    (l0, s0, g0, t0), (l1, s1, g1, t1) = res
+    assert torch.equal(l0, l1) and torch.equal(s0, s1) and torch.equal(t0, t1)
+    assert all(torch.equal(a, b) for a, b in zip(g0, g1))
+    with pytest.raises(ValueError, match="src8"):
+        photometric_loss(cfg, [case.disps[s].cuda() for s in range(4)], colors, K, inv_K,
+                         torch.stack(Ts).detach(), noise=noise, src8=src8[:, :1].contiguous())
+
+
+@pytest.mark.parametrize("name", ["mono_b2_64x128", "stereo_b2_64x128"])
 def test_bf16_disparities_read_directly(name):
     """md2_desc.disp_dtype = bf16 (the depth decoder's output under bf16 autocast, C5):
     the kernels read the bf16 disparities as is.  bf16 -> fp32 is exact, so the losses

@@ -201,7 +201,10 @@ def test_hip_graph_replay_matches_eager_step():
     loss_graph = float(lg["loss"])
     params_graph = [p.detach().clone() for p in tr.nets.parameters()]
     restore(snap)
-    _, le = tr._step_body(tr.static_inputs)    # the same step, eagerly
+    side = tr.graph_stream   # the stream the parameters' AccumulateGrad nodes were created on
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        _, le = tr._step_body(tr.static_inputs)    # the same step, eagerly
     torch.cuda.synchronize()
     assert abs(loss_graph - float(le["loss"])) < 1e-6, (loss_graph, float(le["loss"]))
     worst = max(float((a - b).abs().max()) for a, b in zip(params_graph, tr.nets.parameters()))
