@@ -491,6 +491,181 @@ __device__ __forceinline__ void ssim_adjoint3(const H5P& a, const H5P& b, const 
 __device__ __forceinline__ C3 sign3(const C3& v) { return {f2v{signf(v.a.x), signf(v.a.y)}, signf(v.b)}; }
 
 // ----------------------------------------------------------------------------
+// smoothness (trainer.py:486-490, layers.py:202-215) — forward partial sums
+// ----------------------------------------------------------------------------
+struct SmoothArgs {
+    int B, num_scales;
+    int hs[MD2_MAX_SCALES], ws[MD2_MAX_SCALES], chunks[MD2_MAX_SCALES];
+    int block_base[MD2_MAX_SCALES + 1];
+    const float* disp[MD2_MAX_SCALES];
+    const float* img[MD2_MAX_SCALES];   // target colour at the native scale
+    float* part[MD2_MAX_SCALES];        // [B][chunks][3]
+    float* sgrad[MD2_MAX_SCALES];       // (B, hs, ws): the smoothness term's per-unit gradient
+    int disp_bf16;
+    int quad;                           // every ws % 4 == 0: smooth_quad (float4 rows)
+};
+
+__device__ __forceinline__ float edge_weight(const float* img, int HW, int o0, int o1) {
+    const float g = (fabsf(img[o0] - img[o1]) + fabsf(img[HW + o0] - img[HW + o1]) +
+                     fabsf(img[2 * HW + o0] - img[2 * HW + o1])) / 3.f;
+    return expf(-g);
+}
+
+__device__ __forceinline__ void block_sum3(float& a, float& b, float& c) {
+    __shared__ float red[3][kWavesPerBlock];
+    a = wave_sum(a);
+    b = wave_sum(b);
+    c = wave_sum(c);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[0][wid] = a;
+        red[1][wid] = b;
+        red[2][wid] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+        b = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        c = red[2][0] + red[2][1] + red[2][2] + red[2][3];
+    }
+}
+
+__device__ __forceinline__ float4 ldd4(const float* base, int idx, bool bf16) {   // idx % 4 == 0
+    if (bf16) {
+        const uint2 u = *(const uint2*)((const char*)base + ((uint32_t)idx << 1));
+        return make_float4(md2::bf2f((uint16_t)(u.x & 0xffffu)), md2::bf2f((uint16_t)(u.x >> 16)),
+                           md2::bf2f((uint16_t)(u.y & 0xffffu)), md2::bf2f((uint16_t)(u.y >> 16)));
+    }
+    return *(const float4*)((const char*)base + ((uint32_t)idx << 2));
+}
+
+__device__ __forceinline__ float f4at(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+
+// exp(-mean_c |a_c - b_c|) (layers.py:210-211 per edge), the channel mean as div3
+__device__ __forceinline__ float edge_w3(float a0, float b0, float a1, float b1, float a2, float b2) {
+    return expf(-div3(fabsf(a0 - b0) + fabsf(a1 - b1) + fabsf(a2 - b2)));
+}
+
+// One pixel quad (row i, columns j0..j0+3; ws % 4 == 0) of smooth_fwd: every load a
+// float4 row segment or one neighbour column, each horizontal edge's weight once.
+__device__ __forceinline__ void smooth_quad(const float* d, const float* img, bool bf, int hs, int ws, int i, int j0,
+                                            float cx, float cy, float* sg, float& sd, float& sx, float& sy) {
+    const int HW = hs * ws, p = i * ws + j0;
+    const bool up = i > 0, dn = i + 1 < hs, lf = j0 > 0, rt = j0 + 4 < ws;
+    // every load unconditional (border rows / columns clamped to the quad itself, their
+    // terms masked below): a conditional load is a branch the wave waits at, and the
+    // ~20 loads of a quad then paid ~20 serialised memory latencies (21 us per launch)
+    const int pu = up ? p - ws : p, pd = dn ? p + ws : p, pl = lf ? p - 1 : p, pr = rt ? p + 4 : p + 3;
+    const float4 dc = ldd4(d, p, bf);
+    const float4 du = ldd4(d, pu, bf);
+    const float4 dd = ldd4(d, pd, bf);
+    const float dl = ldd(d, pl, bf), dr = ldd(d, pr, bf);
+    float4 ic[3], iu[3], id[3];
+    float il[3], ir[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float* im = img + c * HW;
+        ic[c] = *(const float4*)(im + p);
+        iu[c] = *(const float4*)(im + pu);
+        id[c] = *(const float4*)(im + pd);
+        il[c] = im[pl];
+        ir[c] = im[pr];
+    }
+    // horizontal edges h[k] between columns j0+k-1 and j0+k, k = 0..4
+    auto col = [&](int c, int k) { return k < 0 ? il[c] : k > 3 ? ir[c] : f4at(ic[c], k); };
+    float h[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) h[k] = edge_w3(col(0, k - 1), col(0, k), col(1, k - 1), col(1, k), col(2, k - 1), col(2, k));
+    float g[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const float v = f4at(dc, m);
+        const float vl = m == 0 ? dl : f4at(dc, m - 1), vr = m == 3 ? dr : f4at(dc, m + 1);
+        sd += v;
+        float gx = 0.f, gy = 0.f;
+        if (m < 3 || rt) {
+            const float dv = v - vr;
+            sx += fabsf(dv) * h[m + 1];
+            gx += signf(dv) * h[m + 1];
+        }
+        if (m > 0 || lf) gx -= signf(vl - v) * h[m];
+        if (dn) {
+            const float e = edge_w3(f4at(ic[0], m), f4at(id[0], m), f4at(ic[1], m), f4at(id[1], m), f4at(ic[2], m),
+                                    f4at(id[2], m));
+            const float dv = v - f4at(dd, m);
+            sy += fabsf(dv) * e;
+            gy += signf(dv) * e;
+        }
+        if (up) {
+            const float e = edge_w3(f4at(iu[0], m), f4at(ic[0], m), f4at(iu[1], m), f4at(ic[1], m), f4at(iu[2], m),
+                                    f4at(ic[2], m));
+            gy -= signf(f4at(du, m) - v) * e;
+        }
+        g[m] = gx * cx + gy * cy;
+    }
+    *(float4*)(sg + p) = make_float4(g[0], g[1], g[2], g[3]);
+}
+
+// One block's chunk of the smoothness sums (block `bid` of the smoothness grid)
+__device__ __forceinline__ void smooth_block(const SmoothArgs& a, int bid) {
+    int s = 0;
+    while (s + 1 < a.num_scales && bid >= a.block_base[s + 1]) ++s;
+    const int local = bid - a.block_base[s];
+    const int b = local / a.chunks[s], chunk = local - b * a.chunks[s];
+    const int hs = a.hs[s], ws = a.ws[s], HW = hs * ws;
+    const bool bf = a.disp_bf16 != 0;
+    const float* d = disp_off(a.disp[s], (size_t)b * HW, bf);
+    const float* img = a.img[s] + (size_t)b * 3 * HW;
+    float sd = 0.f, sx = 0.f, sy = 0.f;
+    const int p0 = chunk * kSmoothChunk;
+    // per-unit gradient of the smoothness sums (layers.py:202-215): the sign stencil of
+    // |d_p - d_q| e_pq over the pixel's four edges, with the x / y means' normalisers
+    // folded in.  The backward scales it by dL/dloss_s, the weight and 1/mean
+    // (disp_grad_kernel), so it never re-reads the target pyramid or the neighbours
+    float* sg = a.sgrad[s] + (size_t)b * HW;
+    const float cx = 1.0f / ((float)hs * (float)(ws - 1)), cy = 1.0f / ((float)(hs - 1) * (float)ws);
+    static_assert(kSmoothChunk == 4 * kBlock, "one pixel quad per thread");
+    if (a.quad) {   // block-uniform
+        const int p = p0 + 4 * threadIdx.x;
+        if (p < HW) {
+            const int i = p / ws;
+            smooth_quad(d, img, bf, hs, ws, i, p - i * ws, cx, cy, sg, sd, sx, sy);
+        }
+    } else
+    for (int p = p0 + threadIdx.x; p < min(p0 + kSmoothChunk, HW); p += kBlock) {
+        const int i = p / ws, j = p - i * ws;
+        const float v = ldd(d, p, bf);
+        sd += v;
+        float gx = 0.f, gy = 0.f;
+        if (j + 1 < ws) {
+            const float dv = v - ldd(d, p + 1, bf), e = edge_weight(img, HW, p, p + 1);
+            sx += fabsf(dv) * e;
+            gx += signf(dv) * e;
+        }
+        if (j > 0) gx -= signf(ldd(d, p - 1, bf) - v) * edge_weight(img, HW, p - 1, p);
+        if (i + 1 < hs) {
+            const float dv = v - ldd(d, p + ws, bf), e = edge_weight(img, HW, p, p + ws);
+            sy += fabsf(dv) * e;
+            gy += signf(dv) * e;
+        }
+        if (i > 0) gy -= signf(ldd(d, p - ws, bf) - v) * edge_weight(img, HW, p - ws, p);
+        sg[p] = gx * cx + gy * cy;
+    }
+    block_sum3(sd, sx, sy);
+    if (threadIdx.x == 0) {
+        float* o = a.part[s] + ((size_t)b * a.chunks[s] + chunk) * 3;
+        o[0] = sd;
+        o[1] = sx;
+        o[2] = sy;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void smooth_fwd_kernel(SmoothArgs a) {
+    // consecutive chunks share their boundary rows (p + ws): keep them on one XCD's L2
+    smooth_block(a, xcd_contiguous_block(blockIdx.x, gridDim.x));
+}
+
+// ----------------------------------------------------------------------------
 // kernel arguments
 // ----------------------------------------------------------------------------
 struct PhotoArgs {
@@ -534,6 +709,10 @@ struct PhotoArgs {
     // the identity losses are computed inside photo_fwdall_kernel, by the four scale
     // waves of a block (one item) together, into LDS: no photo_ident_kernel, no planes
     int ident_fused;
+    // the forward walk's launch also runs the smoothness sums in blocks [fwd_blocks,
+    // fwd_blocks + smooth_blocks) (0: a separate smooth_fwd_kernel launch)
+    int fwd_blocks, smooth_blocks;
+    SmoothArgs sm;
 };
 
 __device__ __forceinline__ void make_ctx(const PhotoArgs& a, int ls, int f, int b, WarpCtx& c) {
@@ -905,7 +1084,12 @@ __global__ __launch_bounds__(kBlock, NS <= 2 ? MD2_FWD_MINB : 2) void photo_fwda
     __shared__ float idl_s[NS][kRowsP][kWave];   // ident_fused: the item's identity losses
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
     float (*dep)[kWave] = dep_s[wid];
-    const int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    if (a.smooth_blocks && (int)blockIdx.x >= a.fwd_blocks) {   // block-uniform: a smoothness block
+        // (fwd_blocks % 8 == 0: the XCD-contiguous numbering of the tail grid holds)
+        smooth_block(a.sm, xcd_contiguous_block((int)blockIdx.x - a.fwd_blocks, a.smooth_blocks));
+        return;
+    }
+    const int blk = xcd_contiguous_block(blockIdx.x, a.smooth_blocks ? a.fwd_blocks : (int)gridDim.x);
     const int wv = __builtin_amdgcn_readfirstlane(blk * kWavesPerBlock + wid);
     if (wv >= a.B * a.wpi * a.nsc) return;   // never with ident_fused (exact grid: no barrier skipped)
     const int ls = wv % a.nsc;   // scale fastest: the waves sharing a strip's rows run together
@@ -1444,177 +1628,6 @@ __global__ __launch_bounds__(kBlock, MD2_BWD_MINB) void photo_bwd_kernel(PhotoAr
         const int rb = t % a.rowblocks;
         const int b = t / a.rowblocks;
         bwd_item<NS, SSIM_ON, MASK>(a, b, ls, st, rb, lane, ddacc[threadIdx.x >> 6], dep[threadIdx.x >> 6]);
-    }
-}
-
-// ----------------------------------------------------------------------------
-// smoothness (trainer.py:486-490, layers.py:202-215) — forward partial sums
-// ----------------------------------------------------------------------------
-struct SmoothArgs {
-    int B, num_scales;
-    int hs[MD2_MAX_SCALES], ws[MD2_MAX_SCALES], chunks[MD2_MAX_SCALES];
-    int block_base[MD2_MAX_SCALES + 1];
-    const float* disp[MD2_MAX_SCALES];
-    const float* img[MD2_MAX_SCALES];   // target colour at the native scale
-    float* part[MD2_MAX_SCALES];        // [B][chunks][3]
-    float* sgrad[MD2_MAX_SCALES];       // (B, hs, ws): the smoothness term's per-unit gradient
-    int disp_bf16;
-    int quad;                           // every ws % 4 == 0: smooth_quad (float4 rows)
-};
-
-__device__ __forceinline__ float edge_weight(const float* img, int HW, int o0, int o1) {
-    const float g = (fabsf(img[o0] - img[o1]) + fabsf(img[HW + o0] - img[HW + o1]) +
-                     fabsf(img[2 * HW + o0] - img[2 * HW + o1])) / 3.f;
-    return expf(-g);
-}
-
-__device__ __forceinline__ void block_sum3(float& a, float& b, float& c) {
-    __shared__ float red[3][kWavesPerBlock];
-    a = wave_sum(a);
-    b = wave_sum(b);
-    c = wave_sum(c);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane == 0) {
-        red[0][wid] = a;
-        red[1][wid] = b;
-        red[2][wid] = c;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        a = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-        b = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-        c = red[2][0] + red[2][1] + red[2][2] + red[2][3];
-    }
-}
-
-__device__ __forceinline__ float4 ldd4(const float* base, int idx, bool bf16) {   // idx % 4 == 0
-    if (bf16) {
-        const uint2 u = *(const uint2*)((const char*)base + ((uint32_t)idx << 1));
-        return make_float4(md2::bf2f((uint16_t)(u.x & 0xffffu)), md2::bf2f((uint16_t)(u.x >> 16)),
-                           md2::bf2f((uint16_t)(u.y & 0xffffu)), md2::bf2f((uint16_t)(u.y >> 16)));
-    }
-    return *(const float4*)((const char*)base + ((uint32_t)idx << 2));
-}
-
-__device__ __forceinline__ float f4at(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
-
-// exp(-mean_c |a_c - b_c|) (layers.py:210-211 per edge), the channel mean as div3
-__device__ __forceinline__ float edge_w3(float a0, float b0, float a1, float b1, float a2, float b2) {
-    return expf(-div3(fabsf(a0 - b0) + fabsf(a1 - b1) + fabsf(a2 - b2)));
-}
-
-// One pixel quad (row i, columns j0..j0+3; ws % 4 == 0) of smooth_fwd: every load a
-// float4 row segment or one neighbour column, each horizontal edge's weight once.
-__device__ __forceinline__ void smooth_quad(const float* d, const float* img, bool bf, int hs, int ws, int i, int j0,
-                                            float cx, float cy, float* sg, float& sd, float& sx, float& sy) {
-    const int HW = hs * ws, p = i * ws + j0;
-    const bool up = i > 0, dn = i + 1 < hs, lf = j0 > 0, rt = j0 + 4 < ws;
-    // every load unconditional (border rows / columns clamped to the quad itself, their
-    // terms masked below): a conditional load is a branch the wave waits at, and the
-    // ~20 loads of a quad then paid ~20 serialised memory latencies (21 us per launch)
-    const int pu = up ? p - ws : p, pd = dn ? p + ws : p, pl = lf ? p - 1 : p, pr = rt ? p + 4 : p + 3;
-    const float4 dc = ldd4(d, p, bf);
-    const float4 du = ldd4(d, pu, bf);
-    const float4 dd = ldd4(d, pd, bf);
-    const float dl = ldd(d, pl, bf), dr = ldd(d, pr, bf);
-    float4 ic[3], iu[3], id[3];
-    float il[3], ir[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const float* im = img + c * HW;
-        ic[c] = *(const float4*)(im + p);
-        iu[c] = *(const float4*)(im + pu);
-        id[c] = *(const float4*)(im + pd);
-        il[c] = im[pl];
-        ir[c] = im[pr];
-    }
-    // horizontal edges h[k] between columns j0+k-1 and j0+k, k = 0..4
-    auto col = [&](int c, int k) { return k < 0 ? il[c] : k > 3 ? ir[c] : f4at(ic[c], k); };
-    float h[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) h[k] = edge_w3(col(0, k - 1), col(0, k), col(1, k - 1), col(1, k), col(2, k - 1), col(2, k));
-    float g[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const float v = f4at(dc, m);
-        const float vl = m == 0 ? dl : f4at(dc, m - 1), vr = m == 3 ? dr : f4at(dc, m + 1);
-        sd += v;
-        float gx = 0.f, gy = 0.f;
-        if (m < 3 || rt) {
-            const float dv = v - vr;
-            sx += fabsf(dv) * h[m + 1];
-            gx += signf(dv) * h[m + 1];
-        }
-        if (m > 0 || lf) gx -= signf(vl - v) * h[m];
-        if (dn) {
-            const float e = edge_w3(f4at(ic[0], m), f4at(id[0], m), f4at(ic[1], m), f4at(id[1], m), f4at(ic[2], m),
-                                    f4at(id[2], m));
-            const float dv = v - f4at(dd, m);
-            sy += fabsf(dv) * e;
-            gy += signf(dv) * e;
-        }
-        if (up) {
-            const float e = edge_w3(f4at(iu[0], m), f4at(ic[0], m), f4at(iu[1], m), f4at(ic[1], m), f4at(iu[2], m),
-                                    f4at(ic[2], m));
-            gy -= signf(f4at(du, m) - v) * e;
-        }
-        g[m] = gx * cx + gy * cy;
-    }
-    *(float4*)(sg + p) = make_float4(g[0], g[1], g[2], g[3]);
-}
-
-__global__ __launch_bounds__(kBlock) void smooth_fwd_kernel(SmoothArgs a) {
-    // consecutive chunks share their boundary rows (p + ws): keep them on one XCD's L2
-    const int bid = xcd_contiguous_block(blockIdx.x, gridDim.x);
-    int s = 0;
-    while (s + 1 < a.num_scales && bid >= a.block_base[s + 1]) ++s;
-    const int local = bid - a.block_base[s];
-    const int b = local / a.chunks[s], chunk = local - b * a.chunks[s];
-    const int hs = a.hs[s], ws = a.ws[s], HW = hs * ws;
-    const bool bf = a.disp_bf16 != 0;
-    const float* d = disp_off(a.disp[s], (size_t)b * HW, bf);
-    const float* img = a.img[s] + (size_t)b * 3 * HW;
-    float sd = 0.f, sx = 0.f, sy = 0.f;
-    const int p0 = chunk * kSmoothChunk;
-    // per-unit gradient of the smoothness sums (layers.py:202-215): the sign stencil of
-    // |d_p - d_q| e_pq over the pixel's four edges, with the x / y means' normalisers
-    // folded in.  The backward scales it by dL/dloss_s, the weight and 1/mean
-    // (disp_grad_kernel), so it never re-reads the target pyramid or the neighbours
-    float* sg = a.sgrad[s] + (size_t)b * HW;
-    const float cx = 1.0f / ((float)hs * (float)(ws - 1)), cy = 1.0f / ((float)(hs - 1) * (float)ws);
-    static_assert(kSmoothChunk == 4 * kBlock, "one pixel quad per thread");
-    if (a.quad) {   // block-uniform
-        const int p = p0 + 4 * threadIdx.x;
-        if (p < HW) {
-            const int i = p / ws;
-            smooth_quad(d, img, bf, hs, ws, i, p - i * ws, cx, cy, sg, sd, sx, sy);
-        }
-    } else
-    for (int p = p0 + threadIdx.x; p < min(p0 + kSmoothChunk, HW); p += kBlock) {
-        const int i = p / ws, j = p - i * ws;
-        const float v = ldd(d, p, bf);
-        sd += v;
-        float gx = 0.f, gy = 0.f;
-        if (j + 1 < ws) {
-            const float dv = v - ldd(d, p + 1, bf), e = edge_weight(img, HW, p, p + 1);
-            sx += fabsf(dv) * e;
-            gx += signf(dv) * e;
-        }
-        if (j > 0) gx -= signf(ldd(d, p - 1, bf) - v) * edge_weight(img, HW, p - 1, p);
-        if (i + 1 < hs) {
-            const float dv = v - ldd(d, p + ws, bf), e = edge_weight(img, HW, p, p + ws);
-            sy += fabsf(dv) * e;
-            gy += signf(dv) * e;
-        }
-        if (i > 0) gy -= signf(ldd(d, p - ws, bf) - v) * edge_weight(img, HW, p - ws, p);
-        sg[p] = gx * cx + gy * cy;
-    }
-    block_sum3(sd, sx, sy);
-    if (threadIdx.x == 0) {
-        float* o = a.part[s] + ((size_t)b * a.chunks[s] + chunk) * 3;
-        o[0] = sd;
-        o[1] = sx;
-        o[2] = sy;
     }
 }
 
@@ -2267,7 +2280,9 @@ void launch_fwd_t(const PhotoArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t 
         hipExtLaunchKernelGGL((photo_ident_kernel<NS, SSIM>), dim3(blocks), dim3(kBlock), 0, st, e0, nullptr, 0, a);
     }
     const int rblocks = (a.B * a.wpi * a.nsc + kWavesPerBlock - 1) / kWavesPerBlock;
-    hipExtLaunchKernelGGL((photo_fwdall_kernel<NS, SSIM, MASK>), dim3(rblocks), dim3(kBlock), 0, st,
+    // with the smoothness blocks behind the walk's (a.fwd_blocks = rblocks rounded up to 8)
+    const int grid = a.smooth_blocks ? a.fwd_blocks + a.smooth_blocks : rblocks;
+    hipExtLaunchKernelGGL((photo_fwdall_kernel<NS, SSIM, MASK>), dim3(grid), dim3(kBlock), 0, st,
                           ident_kernel ? nullptr : e0, e1, 0, a);
 }
 // number of workgroups that can be resident at once for a kernel (cached per
@@ -2362,6 +2377,34 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
     if (!loss_out || !select_out || !workspace) return fail(MD2_ERR_ARG, "loss_out/select_out/workspace is NULL");
     hipStream_t st = (hipStream_t)stream;
     uint8_t* ws = (uint8_t*)workspace;
+    SmoothArgs sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.B = L.B;
+    sa.num_scales = L.nscales;
+    int blocks = 0;
+    for (int s = 0; s < L.nscales; ++s) {
+        sa.hs[s] = L.hs[s];
+        sa.ws[s] = L.ws[s];
+        sa.chunks[s] = L.chunks[s];
+        sa.block_base[s] = blocks;
+        blocks += L.B * L.chunks[s];
+        sa.disp[s] = t->disp[s];
+        sa.img[s] = t->color[s][0];
+        sa.part[s] = (float*)(ws + L.smooth_off[s]);
+        sa.sgrad[s] = (float*)(ws + L.sgrad_off[s]);
+    }
+    sa.block_base[L.nscales] = blocks;
+    sa.disp_bf16 = d->disp_dtype == MD2_DTYPE_BF16;
+    sa.quad = 1;
+    for (int s = 0; s < L.nscales; ++s) sa.quad &= (L.ws[s] % 4 == 0) ? 1 : 0;
+    // the smoothness blocks ride behind the forward walk's in its launch (their ~12 us
+    // of latency-bound work fills the walk's tail instead of following it);
+    // MD2_SMOOTH_MERGE=0: a separate launch after it
+    static const bool merge_on = [] {
+        const char* e = getenv("MD2_SMOOTH_MERGE");
+        return !(e && e[0] == '0');
+    }();
+    const bool merged = merge_on && !L.v1;
     PhotoArgs a;
     hipEvent_t c0 = nullptr, c1 = nullptr;
     if (L.v1) {  // one launch per scale (each at its own resolution); not timed
@@ -2386,6 +2429,11 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
         hipEvent_t e0, e1;
         timing_slot(0, &e0, &e1);
         photo_args(d, t, L, 0, L.nscales, false, ws, select_out, a);
+        if (merged) {
+            a.fwd_blocks = ((L.B * a.wpi * a.nsc + kWavesPerBlock - 1) / kWavesPerBlock + 7) / 8 * 8;
+            a.smooth_blocks = blocks;
+            a.sm = sa;
+        }
         // four scales: the forward walk's blocks are (item, 4 scales) and compute the
         // identity losses themselves (no identity planes: round 4, -24 MB of traffic
         // and one launch per step); otherwise the identity pass writes them, and the
@@ -2405,28 +2453,10 @@ int md2_photometric_fwd(const md2_desc* d, const md2_tensors* t, float* loss_out
     }
     if ((rc = hip_check("photo forward kernels"))) return rc;
 
-    SmoothArgs sa;
-    memset(&sa, 0, sizeof(sa));
-    sa.B = L.B;
-    sa.num_scales = L.nscales;
-    int blocks = 0;
-    for (int s = 0; s < L.nscales; ++s) {
-        sa.hs[s] = L.hs[s];
-        sa.ws[s] = L.ws[s];
-        sa.chunks[s] = L.chunks[s];
-        sa.block_base[s] = blocks;
-        blocks += L.B * L.chunks[s];
-        sa.disp[s] = t->disp[s];
-        sa.img[s] = t->color[s][0];
-        sa.part[s] = (float*)(ws + L.smooth_off[s]);
-        sa.sgrad[s] = (float*)(ws + L.sgrad_off[s]);
+    if (!merged) {
+        hipLaunchKernelGGL(smooth_fwd_kernel, dim3(blocks), dim3(kBlock), 0, st, sa);
+        if ((rc = hip_check("smooth_fwd_kernel"))) return rc;
     }
-    sa.block_base[L.nscales] = blocks;
-    sa.disp_bf16 = d->disp_dtype == MD2_DTYPE_BF16;
-    sa.quad = 1;
-    for (int s = 0; s < L.nscales; ++s) sa.quad &= (L.ws[s] % 4 == 0) ? 1 : 0;
-    hipLaunchKernelGGL(smooth_fwd_kernel, dim3(blocks), dim3(kBlock), 0, st, sa);
-    if ((rc = hip_check("smooth_fwd_kernel"))) return rc;
 
     FinalArgs fa;
     memset(&fa, 0, sizeof(fa));
