@@ -1672,8 +1672,8 @@ __device__ __forceinline__ void block_sum_d(double (&v)[N]) {
 // One block of 16 waves, every assignment fixed (deterministic):
 //   photometric partials: wave w sums quarter w%4 of scale w/4's partials (four
 //   independent accumulators per lane, so the loads of a lane are in flight together);
-//   smoothness: wave w sums the chunk partials of (scale, image) pairs w, w+16, ...
-//   one chunk per lane;
+//   smoothness: 16-lane group g sums the chunk partials of (scale, image) pairs g,
+//   g+64, ... (see below);
 // then thread 0 combines everything in a fixed order.  (The first version used one
 // wave per scale and one thread per image: ~100 dependent load+add steps, 46 us.)
 constexpr int kFinWaves = 16;
@@ -1704,46 +1704,41 @@ __global__ __launch_bounds__(kWave * kFinWaves) void finalize_fwd_kernel(FinalAr
             if (lane == 0) photo[sc][q] = v;
         }
     }
+    // smoothness: 16 lanes per (scale, image) pair, every pair at once (48 pairs of 64
+    // groups at B = 12); each lane sums chunks gl, gl + 16, ... from batches of 8
+    // unconditional loads, then a 4-step xor butterfly inside the group.  (One wave per
+    // pair, three pairs in a row per wave, took 6.7 of the kernel's 10.9 us.)
     const int NP = a.num_scales * a.B;
-    constexpr int kPR = 4;   // (scale, image) pairs whose first 2 x 64 chunk partials load together
-    for (int p0 = wid; p0 < NP; p0 += kPR * kFinWaves) {
-        float v[kPR][2][3];
-#pragma unroll
-        for (int r = 0; r < kPR; ++r) {
-            const int pi = p0 + r * kFinWaves < NP ? p0 + r * kFinWaves : 0;
-            const int sc = pi / a.B, b = pi - sc * a.B, nch = a.chunks[sc];
-            const float* p = a.smooth_part[sc] + (size_t)b * nch * 3;
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const int k = lane + c * kWave < nch ? lane + c * kWave : 0;
-#pragma unroll
-                for (int e = 0; e < 3; ++e) v[r][c][e] = p[3 * k + e];
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < kPR; ++r) {
-        const int pi = p0 + r * kFinWaves;
-        if (pi >= NP) break;   // wave-uniform
+    constexpr int kGL = 16;
+    const int gl = t & (kGL - 1);
+    for (int pi = t / kGL; pi < NP; pi += kWave * kFinWaves / kGL) {   // uniform per 16-lane group
         const int sc = pi / a.B, b = pi - sc * a.B;
         const int hs = a.hs[sc], ws = a.ws[sc], nch = a.chunks[sc];
         const float* p = a.smooth_part[sc] + (size_t)b * nch * 3;
         double sd = 0.0, sx = 0.0, sy = 0.0;
+        for (int k0 = gl; k0 < nch; k0 += 8 * kGL) {
+            float v[8][3];
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
-            if (lane + c * kWave < nch) {
-                sd += v[r][c][0];
-                sx += v[r][c][1];
-                sy += v[r][c][2];
+            for (int u = 0; u < 8; ++u) {
+                const int k = k0 + u * kGL < nch ? k0 + u * kGL : 0;
+#pragma unroll
+                for (int e = 0; e < 3; ++e) v[u][e] = p[3 * k + e];
             }
-        for (int k = lane + 2 * kWave; k < nch; k += kWave) {   // more than 128 chunks
-            sd += p[3 * k];
-            sx += p[3 * k + 1];
-            sy += p[3 * k + 2];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (k0 + u * kGL < nch) {
+                    sd += v[u][0];
+                    sx += v[u][1];
+                    sy += v[u][2];
+                }
         }
-        sd = wave_sum_d(sd);
-        sx = wave_sum_d(sx);
-        sy = wave_sum_d(sy);
-        if (lane == 0) {
+#pragma unroll
+        for (int o = kGL / 2; o > 0; o >>= 1) {
+            sd += __shfl_xor(sd, o, kGL);
+            sx += __shfl_xor(sx, o, kGL);
+            sy += __shfl_xor(sy, o, kGL);
+        }
+        if (gl == 0) {
             const double m = sd / ((double)hs * ws) + 1e-7;
             smooth[sc][b] = sx / m / ((double)a.B * hs * (ws - 1)) + sy / m / ((double)a.B * (hs - 1) * ws);
             float* st = a.stats + ((size_t)sc * a.B + b) * 4;
@@ -1751,7 +1746,6 @@ __global__ __launch_bounds__(kWave * kFinWaves) void finalize_fwd_kernel(FinalAr
             st[1] = (float)sx;
             st[2] = (float)sy;
             st[3] = 0.f;
-        }
         }
     }
     __syncthreads();
