@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-ssim", action="store_true")
     ap.add_argument("--eight-bit", action="store_true", help="colours quantised to k/255 (loader output)")
+    ap.add_argument("--src8", action="store_true", help="with --eight-bit: hand the sources' 8-bit copies "
+                    "in (md2_tensors.src8, as the trainer does) instead of packing them per call")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, H, W, S = a.batch, a.height, a.width, a.src
@@ -51,8 +53,10 @@ def main():
     K = [inputs[("K", s)] for s in range(4)]
     iK = [inputs[("inv_K", s)] for s in range(4)]
 
+    src8 = inputs.get("color_src8") if (a.src8 and a.eight_bit) else None
+
     def step(i):
-        loss, _ = photometric_loss(cfg, disps, colors, K, iK, T, seed=i)
+        loss, _ = photometric_loss(cfg, disps, colors, K, iK, T, seed=i, src8=src8)
         loss[4].backward()
 
     for i in range(5):
