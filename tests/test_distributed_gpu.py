@@ -47,6 +47,10 @@ def _rank_flat(rank, world, port, backend="gloo"):
         from monodepth2_amd.data import synthetic_batch
         from monodepth2_amd.options import default_options
         from monodepth2_amd.trainer import Trainer
+        from monodepth2_amd import conv_ops
+        # the kernels are not under test here: fixed choices, none made from timings
+        # taken while both ranks share the one GPU
+        conv_ops.AUTOTUNE = False
         torch.manual_seed(0)
         tr = Trainer(default_options(batch_size=2, height=64, width=128, weights_init="scratch", grad_sync="flat",
                                      log_dir="/tmp/md2_ddp_gpu"), device=dev, rank=rank, world_size=world)
@@ -83,6 +87,10 @@ def _rank(rank, world, port, backend="gloo"):
         from monodepth2_amd.data import synthetic_batch
         from monodepth2_amd.options import default_options
         from monodepth2_amd.trainer import Trainer
+        from monodepth2_amd import conv_ops
+        # the kernels are not under test here: fixed choices, none made from timings
+        # taken while both ranks share the one GPU
+        conv_ops.AUTOTUNE = False
         torch.manual_seed(0)
         tr = Trainer(default_options(batch_size=2, height=64, width=128, weights_init="scratch",
                                      log_dir="/tmp/md2_ddp_gpu"), device=dev, rank=rank, world_size=world)
