@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "md2hot.h"
 
@@ -114,6 +115,58 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(HeadArgs a) {
             for (int o = L / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, L);
             if (sub == 0) a.disp[pp[u]] = 1.f / (1.f + expf(-(acc + bias)));
         }
+    }
+}
+
+// Column-walk form of the forward (the default): a block owns GPB = 256/L adjacent
+// output columns x R output rows of one image; each L-lane group owns one column and
+// loads the R + 2 padded rows of its 3-tap window once — (R + 2)·3 float4 loads per lane
+// for R pixels instead of 9 per pixel — all of them before any arithmetic, then the
+// same tap-ordered dot products, shuffle reduction, bias and sigmoid as head_fwd_kernel
+// (bitwise the same outputs).  MD2_HEAD_ROWWALK=1 keeps the pixel-walk kernel above.
+template <int L, int QL>
+__global__ __launch_bounds__(kThreads) void head_fwd_col_kernel(HeadArgs a) {
+    constexpr int Q = L * QL, GPB = kThreads / L, R = QL >= 4 ? 2 : 8 / QL;
+    const int Wp = a.w + 2, Hp = a.h + 2;
+    const int sub = threadIdx.x % L, grp = threadIdx.x / L;
+    const int ntx = (a.w + GPB - 1) / GPB, nty = (a.h + R - 1) / R;
+    int t = blockIdx.x;
+    const int tx = t % ntx;
+    t /= ntx;
+    const int ty = t % nty, b = t / nty;
+    const int x = tx * GPB + grp;
+    if (x >= a.w) return;   // whole L-lane groups exit together (L divides 64)
+    const int y0 = ty * R;
+    float4 wr[9][QL];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int k = 0; k < QL; ++k) wr[tap][k] = wt_quad(a, tap, sub + k * L);
+    const float bias = a.bias[0];
+    const float4* P4 = reinterpret_cast<const float4*>(a.P) + sub;
+    float4 v[R + 2][3][QL];
+#pragma unroll
+    for (int r = 0; r < R + 2; ++r) {
+        const int Y = y0 + r < Hp ? y0 + r : Hp - 1;   // rows past the image: loaded, not used
+        const unsigned base = ((unsigned)(b * Hp + Y) * Wp + x) * Q;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+            for (int k = 0; k < QL; ++k) v[r][kx][k] = P4[base + kx * Q + k * L];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (y0 + r >= a.h) break;   // block-uniform
+        float acc = 0.f;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+                for (int k = 0; k < QL; ++k) acc += dot4(v[r + ky][kx][k], wr[ky * 3 + kx][k]);
+#pragma unroll
+        for (int o = L / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, L);
+        if (sub == 0) a.disp[((unsigned)b * a.h + y0 + r) * a.w + x] = 1.f / (1.f + expf(-(acc + bias)));
     }
 }
 
@@ -290,6 +343,25 @@ int md2_disp_head_fwd(const md2_head_desc* d, const float* padded, const float* 
     long long want = (need + 3) / 4;                                // each group walks >= 4 pixels
     want = want < 8 ? 8 : (want > kFwdBlocks ? kFwdBlocks : want);
     const int grid = (int)((want + 7) / 8 * 8);                     // whole XCD rounds
+    static const bool rowwalk = [] {
+        const char* e = getenv("MD2_HEAD_ROWWALK");
+        return e && e[0] == '1';
+    }();
+    if (!rowwalk) {
+        const int QL = Q > 16 ? Q / 16 : 1, R = QL >= 4 ? 2 : 8 / QL, GPB = kThreads / L;
+        const long long tiles = (long long)((a.w + GPB - 1) / GPB) * ((a.h + R - 1) / R) * a.B;
+        void (*kc)(HeadArgs) = Q == 1    ? head_fwd_col_kernel<1, 1>
+                               : Q == 2  ? head_fwd_col_kernel<2, 1>
+                               : Q == 4  ? head_fwd_col_kernel<4, 1>
+                               : Q == 8  ? head_fwd_col_kernel<8, 1>
+                               : Q == 16 ? head_fwd_col_kernel<16, 1>
+                               : Q == 32 ? head_fwd_col_kernel<16, 2>
+                                         : head_fwd_col_kernel<16, 4>;
+        if (tiles < (1ll << 31)) {
+            hipLaunchKernelGGL(kc, dim3((unsigned)tiles), dim3(kThreads), 0, (hipStream_t)stream, a);
+            return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
+        }
+    }
     void (*k)(HeadArgs) = Q == 1    ? head_fwd_kernel<1, 1>
                           : Q == 2  ? head_fwd_kernel<2, 1>
                           : Q == 4  ? head_fwd_kernel<4, 1>
