@@ -88,7 +88,8 @@ def pmc_traffic(args, S, timeout=150):
                "--output-format", "csv", "--", sys.executable, os.path.join(REPO, "bench.py"),
                "--batch", str(args.batch), "--height", str(args.height), "--width", str(args.width),
                "--num_layers", str(args.num_layers), "--amp", args.amp, "--steps", "3", "--warmup", "2",
-               "--no-cpu-baseline", "--no-parity", "--pmc", "0", "--no-conv-roofline", "--graph", "0"] + \
+               "--no-cpu-baseline", "--no-parity", "--pmc", "0", "--no-conv-roofline", "--graph", "0",
+               "--src8", "0"] + \
               (["--stereo"] if args.stereo else [])
         env = dict(os.environ, TMPDIR="/tmp")
         p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env, start_new_session=True)
@@ -157,6 +158,9 @@ def parse():
     ap.add_argument("--miopen-find", type=str, default="fast", help="MIOPEN_FIND_MODE (fast|normal|...)")
     ap.add_argument("--amp", type=str, default="none", choices=["none", "bf16"],
                     help="bf16 autocast for the networks (config C5); the photometric loss stays fp32")
+    ap.add_argument("--src8", type=int, default=1,
+                    help="1: the batch carries the sources' 8-bit RGBx copies (color_src8), as the GPU input "
+                         "pipeline writes them; 0: the hot path packs them from the fp32 colours every step")
     ap.add_argument("--gpu-augment", type=int, default=0,
                     help="1: every step also runs the input pipeline (flip + LANCZOS pyramid + jitter, "
                          "md2_aug_run) from resident 375x1242 uint8 frames")
@@ -199,10 +203,11 @@ def loss_delta_vs_oracle(trainer, batch):
     return abs(float(loss[hot.num_scales]) - float(ref["loss"]))
 
 
-def time_hot_kernels(trainer, batch, n=10):
+def time_hot_kernels(trainer, batch, n=10, src8=True):
     """Stand-alone fwd+bwd of the fused hot path on the step's own tensors, with the
     photometric kernels HIP-event timed (used when the step runs as a hipGraph,
-    whose replays are not individually instrumented)."""
+    whose replays are not individually instrumented).  src8=False: without the
+    loader's 8-bit source copies, i.e. with the forward's own pack pass."""
     from monodepth2_amd import _lib
     from monodepth2_amd.hotpath import photometric_loss
     with torch.no_grad():
@@ -212,14 +217,14 @@ def time_hot_kernels(trainer, batch, n=10):
     T = trainer._stacked_T(batch, outputs).detach().requires_grad_(True)
     disps = [outputs[("disp", s)].detach().requires_grad_(True) for s in range(hot.num_scales)]
     colors = trainer._colors(batch)
-    src8 = batch.get("color_src8")
+    s8 = batch.get("color_src8") if src8 else None
     for _ in range(2):
-        loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=1, src8=src8)
+        loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=1, src8=s8)
         loss[hot.num_scales].backward()
     torch.cuda.synchronize()
     with _lib.KernelTimer(max_launches=4 * n + 8) as kt:
         for i in range(n):
-            loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=2 + i, src8=src8)
+            loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=2 + i, src8=s8)
             loss[hot.num_scales].backward()
     return kt
 
@@ -342,6 +347,8 @@ def main():
     # i.e. exactly k/255 (datasets/mono_dataset.py:199-200)
     batch = synthetic_batch(args.batch, args.height, args.width, frame_ids, 4, seed=100 + rank, device=device,
                             eight_bit=True)
+    if not args.src8:
+        batch.pop("color_src8", None)
     next_batch = lambda: batch   # noqa: E731
     if args.gpu_augment:
         next_batch = make_augmenting_source(args, frame_ids, device, rank)
@@ -416,11 +423,15 @@ def main():
         gbs = step_bytes / (hot_ms * 1e-3) / 1e9
         tfs = step_flops / (hot_ms * 1e-3) / 1e12
         hbm_frac, valu_frac = gbs / HBM_PEAK_GBS, tfs / F32_VALU_PEAK_TFLOPS
-        traffic, pmc_note, pmc_kernels = None, "skipped (--pmc 0 or N>1)", None
+        traffic, pmc_note, pmc_kernels, pack_traffic = None, "skipped (--pmc 0 or N>1)", None, None
         if args.pmc and world == 1:
             pmc_kernels, err = pmc_traffic(args, S)
             if pmc_kernels is not None:
-                traffic = sum(v["corrected"] for v in pmc_kernels.values())
+                # the PMC child runs without the loader's 8-bit copies (--src8 0), so its
+                # forward packs them (pack_src8_kernel); the other kernels read the same
+                # RGBx dwords either way
+                pack_traffic = sum(v["corrected"] for k, v in pmc_kernels.items() if k.startswith("pack_src8"))
+                traffic = sum(v["corrected"] for k, v in pmc_kernels.items() if not k.startswith("pack_src8"))
                 pmc_note = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in this run over a 3-step run of this "
                             "training step (bench.py --steps 3); per dispatch, summed over the hot path's kernels: "
                             "2*FETCH+WRITE (KB->B), the x2 calibrated for the 4/8/16-B-per-lane reads these kernels "
@@ -429,6 +440,24 @@ def main():
             else:
                 pmc_note = err
             log(f"pmc traffic: {traffic} B/step ({pmc_note[:80]})")
+        # the sources' RGBx copies: handed in with the batch (md2_aug_run2 writes them as it
+        # decodes; data.pack_rgbx for the resident bench batch), or packed by the forward
+        # from the reference's fp32 colours (mono_dataset.py:199-200's to_tensor output):
+        # that conversion timed beside the headline
+        pack = None
+        if "color_src8" in batch:
+            k0, k1 = time_hot_kernels(trainer, batch, src8=False), time_hot_kernels(trainer, batch)
+            pack_ms = max(k0.fwd_call_ms / max(k0.n_fwd_call, 1) - k1.fwd_call_ms / max(k1.n_fwd_call, 1), 0.0)
+            hot_pack = hot_ms + pack_ms
+            pack = {"src8": "loader", "pack_ms": round(pack_ms, 5),
+                    "pack_timing": "fwd call without the loader's copies (pack_src8_kernel + the walk) minus "
+                                   "the fwd call with them, stand-alone, same tensors",
+                    "pack_traffic": pack_traffic,
+                    "hot_path_ms_with_pack": round(hot_pack, 5),
+                    "valu_frac_with_pack": round(step_flops / (hot_pack * 1e-3) / 1e12 / F32_VALU_PEAK_TFLOPS, 5),
+                    "traffic_with_pack": (traffic + pack_traffic) if (traffic is not None and pack_traffic)
+                    else None}
+            log(f"src8 pack: {pack_ms:.4f} ms, {pack_traffic} B")
         head = ("valu", tfs, F32_VALU_PEAK_TFLOPS, "TFLOP/s", valu_frac) if valu_frac >= hbm_frac else \
             ("hbm", gbs, HBM_PEAK_GBS, "GB/s", hbm_frac)
         roof = {"bound": head[0], "kernel": "hot path: md2_photometric_fwd + md2_photometric_bwd (all their kernels)",
@@ -448,6 +477,10 @@ def main():
                 "photo_bwd": {"avg_launch_ms": round(bwd_ms, 5), "launches": kt.n_bwd,
                               "share_of_hot_path": round(bwd_ms / hot_ms, 3) if hot_ms else None},
                 "photo_fwd_kernels_ms": round(fwd_ms, 5)}
+        if pack is not None:
+            roof.update(pack)
+        else:
+            roof["src8"] = "packed in the forward (counted in the headline)"
         log(f"timed: {1e3 * dt / args.steps:.2f} ms/step, hot path {hot_ms:.3f} ms (fwd {fcall:.3f}, bwd {bcall:.3f};"
             f" photo_bwd {bwd_ms:.3f}), {tfs:.2f} TF = {valu_frac:.3f} of VALU peak, {gbs:.0f} GB/s, "
             f"adam table uploads {getattr(trainer.model_optimizer, 'rebuilds', '-')}")

@@ -394,6 +394,7 @@ def clear_choices():
     _pinned.clear()
     _times.clear()
     _names.clear()
+    _nondet.clear()
 
 
 _names: Dict[tuple, list] = {}    # (op, shape) -> candidate names, in candidate order
@@ -409,11 +410,52 @@ def _cached(op: str, key: tuple):
     return _choice.get((op,) + key)
 
 
+_nondet: Dict[tuple, list] = {}   # (op, shape) -> candidates whose repeated runs differed (never kept)
+
+
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def _same_bits(a, b) -> bool:
+    """Bitwise equality of two candidate outputs (NaN payloads and signed zeros included)."""
+    if a.shape != b.shape or a.dtype != b.dtype:
+        return False
+    if a.element_size() == 4:
+        return torch.equal(a.view(torch.int32), b.view(torch.int32))
+    if a.element_size() == 2:
+        return torch.equal(a.view(torch.int16), b.view(torch.int16))
+    return torch.equal(a, b)
+
+
+def _time_candidate(fn):
+    """One warm-up run and three timed runs of a candidate on the current stream:
+    (median ms, repeatable).  repeatable: the three timed runs' outputs are bitwise the
+    warm-up's — a kernel that is not (atomics, a race) would make two passes over the
+    same batch disagree, so the autotune never keeps one."""
+    y0 = fn()
+    ts, same = [], True
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        y = fn()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+        same = same and _same_bits(y0, y)
+    return sorted(ts)[1], same
+
+
 def _fastest(op: str, key: tuple, cands, names=None) -> int:
     """Time every candidate once per (op, shape) (3 runs each after a warm-up,
     median) and remember the fastest; the last candidate is MIOpen, kept unless
-    another beats it by >= 3 %.  Without AUTOTUNE: the first candidate.  Not while a
-    hipGraph is being captured: then the cached choice, or MIOpen."""
+    another beats it by >= 3 %.  A candidate whose repeated outputs are not bitwise
+    equal is never kept (`_nondet`).  Without AUTOTUNE: the first candidate.  Not while
+    a hipGraph is being captured: then the cached choice, or MIOpen.
+
+    No collective here: under data parallelism each rank times on its own (it may be
+    inside a forward, a backward or a rank-0-only evaluation), and the ranks line up on
+    rank 0's table at one known point, `agree_choices`."""
     k = (op,) + key
     if not AUTOTUNE:
         return 0
@@ -427,42 +469,53 @@ def _fastest(op: str, key: tuple, cands, names=None) -> int:
             raise RuntimeError(f"pinned conv choice {pin!r} for {k} is not a candidate here ({names})")
         _choice[k] = names.index(pin)
         return _choice[k]
-    if torch.cuda.is_current_stream_capturing():
+    if _capturing():
         return len(cands) - 1
-    times = []
+    times, rep = [], []
     for name, fn in zip(names, cands):
         if name in _EXCLUDE and name != names[-1]:
             times.append(float("inf"))
+            rep.append(False)
             continue
-        fn()
-        ts = []
-        for _ in range(3):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            fn()
-            e1.record()
-            e1.synchronize()
-            ts.append(e0.elapsed_time(e1))
-        times.append(sorted(ts)[1])
+        t, ok = _time_candidate(fn)
+        times.append(t)
+        rep.append(ok)
     _times[k] = dict(zip(names, times))
-    best = min(range(len(cands) - 1), key=lambda i: times[i]) if len(cands) > 1 else 0
-    _choice[k] = best if times[best] < 0.97 * times[-1] else len(cands) - 1
-    _choice[k] = _rank0_choice(_choice[k])
+    bad = [n for n, ok, t in zip(names, rep, times) if not ok and t != float("inf")]
+    if bad:
+        _nondet[k] = bad
+    ok = [i for i in range(len(cands) - 1) if rep[i]]
+    if not ok:
+        _choice[k] = len(cands) - 1
+    else:
+        best = min(ok, key=lambda i: times[i])
+        _choice[k] = best if (not rep[-1] or times[best] < 0.97 * times[-1]) else len(cands) - 1
     return _choice[k]
 
 
-def _rank0_choice(mine: int) -> int:
-    """Under data parallelism every rank runs rank 0's choice: the ranks' timings can
-    disagree, and different kernels round differently, so the replicas would drift
-    apart.  Every rank meets the same shapes in the same order (same networks and
-    batch shape), so one small broadcast per newly timed shape lines them up; a table
-    loaded with load_choices (the same file on every rank) needs none."""
+def agree_choices(group=None) -> int:
+    """Under data parallelism, every rank adopts rank 0's per-shape choices, so the
+    replicas run the same kernels (the same rounding) from here on.  ONE collective
+    (a broadcast of rank 0's table), to be called where every rank is present and none
+    is inside a forward or backward: the Trainer calls it after its first training step
+    (eager) or after the capture's warm-up steps (hipGraph).  Shapes rank 0 has timed
+    and this rank has not seen yet are pinned to rank 0's choice for when they appear.
+    Returns how many of this rank's choices changed."""
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
-        return mine
-    box = [mine]
-    dist.broadcast_object_list(box, src=0)
-    return int(box[0])
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1):
+        return 0
+    mine = {k: _names[k][i] for k, i in _choice.items() if k in _names}
+    box = [mine if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(box, src=0, group=group)
+    changed = 0
+    for k, name in box[0].items():
+        _pinned[k] = name
+        names = _names.get(k)
+        if names is not None and name in names:
+            i = names.index(name)
+            changed += int(_choice.get(k) != i)
+            _choice[k] = i
+    return changed
 
 
 _DIRECT = ((16, 16), (32, 16), (16, 32))   # (in, out) channels of md2_conv_direct

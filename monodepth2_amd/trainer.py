@@ -62,6 +62,36 @@ def _to_fp32(outputs, keep_disp: bool = True):
     return outputs
 
 
+def posecnn_transforms(disps, axisangle, translation, src_frames, stereo_T, height: int, width: int,
+                       min_depth: float, max_depth: float, v1_multiscale: bool) -> torch.Tensor:
+    """pose_model_type "posecnn" (trainer.py:366-375): cam_T_cam rebuilt at every scale
+    with the translation scaled by the mean inverse depth of that scale's depth map
+    (upsampled to the loss resolution unless v1_multiscale).  axisangle / translation:
+    (F,B,3) for the temporal source frames in frame order.  Returns the
+    (num_scales, S, B, 4, 4) stack the hot path takes with t_per_scale (stereo_T for an
+    "s" frame).  The mean inverse depth is formed as the reference forms it, 1 / (1 /
+    scaled disparity), then the transforms of a scale come from one md2_pose_fwd launch."""
+    temporal = [f for f in src_frames if f != "s"]
+    per_scale = []
+    for d in disps:
+        d = d.float()
+        if not v1_multiscale:
+            d = F.interpolate(d, [height, width], mode="bilinear", align_corners=False)
+        _, depth = disp_to_depth(d, min_depth, max_depth)
+        mean_inv_depth = (1 / depth).mean(3, True).mean(2, True)          # (B,1,1,1)
+        Tt = poses_to_transforms(axisangle, translation * mean_inv_depth[:, 0, 0].unsqueeze(0),
+                                 [f < 0 for f in temporal])
+        Ts, ti = [], 0
+        for f in src_frames:
+            if f == "s":
+                Ts.append(stereo_T)
+            else:
+                Ts.append(Tt[ti])
+                ti += 1
+        per_scale.append(torch.stack(Ts, 0))
+    return torch.stack(per_scale, 0)
+
+
 class _Networks(nn.Module):
     """All trainable networks behind one module so DDP sees a single graph."""
 
@@ -168,6 +198,7 @@ class Trainer:
             if ((world_size > 1 and (sync == "flat" or self.use_graph)) or explicit_flat) else None
         self.graph = None
         self.seed_tensor = None
+        self._choices_agreed = False
 
         # Adam (trainer.py:102): one HIP launch per step over every parameter (optim.py);
         # under hipGraph its capturable form: the lr is a device tensor that StepLR
@@ -369,28 +400,12 @@ class Trainer:
                             for i, t in enumerate(Ts))):
                 return T_all[0]    # the fused producer's (S,B,4,4) already is the stack
             return torch.stack(Ts, 0)
-        per_scale = []
-        for s in range(self.num_scales):
-            disp = outputs[("disp", s)].float()
-            if not self.opt.v1_multiscale:
-                disp = F.interpolate(disp, [self.opt.height, self.opt.width], mode="bilinear", align_corners=False)
-            scaled, _ = disp_to_depth(disp, self.opt.min_depth, self.opt.max_depth)
-            mean_inv_depth = scaled.mean(3, True).mean(2, True)          # (B,1,1,1)
-            temporal = [f for f in self.src_frames if f != "s"]
-            Tt = poses_to_transforms(
-                torch.stack([outputs[("axisangle", 0, f)][:, 0, 0] for f in temporal]),
-                torch.stack([outputs[("translation", 0, f)][:, 0, 0] * mean_inv_depth[:, 0, 0]
-                             for f in temporal]),
-                [f < 0 for f in temporal])
-            Ts, ti = [], 0
-            for f in self.src_frames:
-                if f == "s":
-                    Ts.append(inputs["stereo_T"])
-                else:
-                    Ts.append(Tt[ti])
-                    ti += 1
-            per_scale.append(torch.stack(Ts, 0))
-        return torch.stack(per_scale, 0)
+        temporal = [f for f in self.src_frames if f != "s"]
+        return posecnn_transforms([outputs[("disp", s)] for s in range(self.num_scales)],
+                                  torch.stack([outputs[("axisangle", 0, f)][:, 0, 0] for f in temporal]),
+                                  torch.stack([outputs[("translation", 0, f)][:, 0, 0] for f in temporal]),
+                                  self.src_frames, inputs.get("stereo_T"), self.opt.height, self.opt.width,
+                                  self.opt.min_depth, self.opt.max_depth, self.opt.v1_multiscale)
 
     def generate_images_pred(self, inputs, outputs):
         """Materialise what trainer.py:341-391 writes into `outputs` (no autograd)."""
@@ -476,6 +491,21 @@ class Trainer:
             self.seed_tensor.add_(1)
         return outputs, losses
 
+    def eager_step(self, inputs):
+        """One training step run eagerly (not replayed).  After a capture it runs on the
+        capture's stream: every parameter's AccumulateGrad node was created there (at the
+        warm-up) and keeps that stream, so a step issued on another stream would make
+        autograd accumulate across streams (its stream-mismatch warning)."""
+        side = getattr(self, "graph_stream", None)
+        if side is None:
+            return self._step_body(inputs)
+        cur = torch.cuda.current_stream(self.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            out = self._step_body(inputs)
+        cur.wait_stream(side)
+        return out
+
     def _capture(self, inputs, warmup: int = 3):
         """Capture one whole training step (networks, fused hot path, backward,
         all-reduce, Adam) into a hipGraph; later steps replay it.
@@ -488,12 +518,13 @@ class Trainer:
         self.seed_tensor = torch.zeros(1, dtype=torch.int64, device=self.device)
         snap = self._training_state()
         side = torch.cuda.Stream(self.device)
-        self.graph_stream = side   # an eager step after the capture belongs here too (its AccumulateGrad nodes)
+        self.graph_stream = side   # an eager step after the capture runs here too (eager_step)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             for _ in range(warmup):
                 self._step_body(self.static_inputs)
         torch.cuda.current_stream(self.device).wait_stream(side)
+        self._agree_conv_choices()   # before the capture: the graph holds rank 0's kernels
         self._restore_training_state(snap)
         self.graph = torch.cuda.CUDAGraph()
         dot = os.environ.get("MD2_GRAPH_DOT")
@@ -509,6 +540,15 @@ class Trainer:
             self.static_outputs, self.static_losses = self._step_body(self.static_inputs)
         if dot:
             self.graph.debug_dump(dot)
+
+    def _agree_conv_choices(self):
+        """Once, after the first step's convolution autotune (conv_ops._fastest times its
+        candidates on each rank without any collective): every rank adopts rank 0's
+        per-shape choices (conv_ops.agree_choices, one broadcast), at a point where every
+        rank is present and none is inside a forward or backward."""
+        if self.world_size > 1 and not self._choices_agreed:
+            conv_ops.agree_choices()
+            self._choices_agreed = True
 
     def _training_state(self):
         """Copies of every tensor a training step advances (see _capture)."""
@@ -555,6 +595,7 @@ class Trainer:
         if not self.use_graph:
             outputs, losses = self._step_body(inputs)
             self.step += 1
+            self._agree_conv_choices()
             return outputs, losses
         if self.graph is None:
             self._capture(inputs)

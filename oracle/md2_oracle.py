@@ -86,6 +86,17 @@ def project(points, K, T, h, w, eps=1e-7):
     return torch.stack([gx, gy], -1)
 
 
+def posecnn_cam_T(transform, axisangle, translation, depth, invert):
+    """trainer.py:366-375 (pose_model_type "posecnn"): T rebuilt at every scale with
+    the translation scaled by the mean inverse depth of that scale's depth map.
+    axisangle / translation are the pose network's outputs at frame 0, (B,1,3)
+    (`axisangle[:, 0]` of trainer.py:374); transform is transformation_from_parameters
+    (layers.py:28-45), passed in so the oracle needs no product module."""
+    inv_depth = 1 / depth
+    mean_inv_depth = inv_depth.mean(3, True).mean(2, True)
+    return transform(axisangle, translation * mean_inv_depth[:, 0], invert)
+
+
 def ssim_map(x, y):
     """layers.py:234-248."""
     x = F.pad(x, (1, 1, 1, 1), mode="reflect")
@@ -127,7 +138,8 @@ def hot_path(opt: HotPathOptions, disps: Dict[int, torch.Tensor], inputs: Dict,
 
     disps: {scale: (B,1,H/2^s,W/2^s)}; inputs: reference-keyed dict with
     ("color", f, s), ("K", s), ("inv_K", s); cam_T: {frame_id: (B,4,4)} (for "s"
-    pass inputs["stereo_T"]); noise: {scale: unit-normal tensor shaped like the
+    pass inputs["stereo_T"]; posecnn: a callable depth -> T evaluated per scale, see
+    posecnn_cam_T); noise: {scale: unit-normal tensor shaped like the
     identity losses} (trainer.py:468-469 multiplies it by 1e-5).
     selection: test-only {scale: (B,h,w) int64} pinning the per-pixel argmin of
     trainer.py:478 to given indices, so that gradients of two fp32
@@ -153,7 +165,7 @@ def hot_path(opt: HotPathOptions, disps: Dict[int, torch.Tensor], inputs: Dict,
         outputs[("depth", 0, s)] = depth
         h, w = depth.shape[2], depth.shape[3]
         for f in frames:
-            T = cam_T[f]
+            T = cam_T[f](depth) if callable(cam_T[f]) else cam_T[f]
             pts = cam_points(depth, inputs[("inv_K", src_s)])
             grid = project(pts, inputs[("K", src_s)], T, h, w)
             outputs[("sample", f, s)] = grid

@@ -61,6 +61,14 @@ CASES = {
     # checksums and identity-selection means only (the full planes would be ~8 MB)
     # (8-bit colours, as the loader and the bench deliver them)
     "c2_mono_b12_192x640": (12, 192, 640, [0, -1, 1], {"eight_bit": True}, 0.01, False, True),
+    # stereo-only training, the reference's "S" models (--use_stereo --frame_ids 0,
+    # experiments/stereo_experiments.sh:2-3): one source frame, T = stereo_T, no pose net
+    "stereo_only_b2_64x128": (2, 64, 128, [0, "s"], {}, 0.05, True),
+    "full_stereo_only_b2_192x640": (2, 192, 640, [0, "s"], {}, 0.01, False),
+    # pose_model_type posecnn: T rebuilt per scale with the translation scaled by the
+    # mean inverse depth (trainer.py:366-375)
+    "posecnn_b2_64x128": (2, 64, 128, [0, -1, 1], {"posecnn": True}, 0.05, True),
+    "full_posecnn_b2_192x640": (2, 192, 640, [0, -1, 1], {"posecnn": True}, 0.01, False),
 }
 
 
@@ -113,7 +121,8 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0, dtype=torch.float32, p
     opt = types.SimpleNamespace(
         scales=scales, frame_ids=list(frame_ids), height=H, width=W,
         v1_multiscale=flags.get("v1_multiscale", False), min_depth=0.1, max_depth=100.0,
-        pose_model_type="separate_resnet", disable_automasking=flags.get("disable_automasking", False),
+        pose_model_type="posecnn" if flags.get("posecnn") else "separate_resnet",
+        disable_automasking=flags.get("disable_automasking", False),
         no_ssim=flags.get("no_ssim", False), avg_reprojection=flags.get("avg_reprojection", False),
         predictive_mask=flags.get("predictive_mask", False), disparity_smoothness=1e-3, batch_size=B)
     self = types.SimpleNamespace(opt=opt, device=torch.device("cpu"), num_scales=len(scales))
@@ -146,6 +155,21 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0, dtype=torch.float32, p
         T.retain_grad()
         outputs[("cam_T_cam", 0, f)] = T
         camT[f] = T
+        if flags.get("posecnn"):
+            # the pose network's (B, frames=1, 1, 3) outputs (networks/pose_cnn.py:45-50):
+            # generate_images_pred reads axisangle[:, 0] / translation[:, 0]
+            outputs[("axisangle", 0, f)] = axis[i].unsqueeze(1)
+            outputs[("translation", 0, f)] = trans[i].unsqueeze(1)
+    # posecnn: the per-scale T of trainer.py:374-375, recorded as the reference builds
+    # them (scale-major, frame-minor) with their gradients
+    per_scale_T = []
+    real_tfp = ref_trainer.transformation_from_parameters
+
+    def recording_tfp(*a, **k):
+        T = real_tfp(*a, **k)
+        T.retain_grad()
+        per_scale_T.append(T)
+        return T
 
     # noise injection (trainer.py:468)
     gen = torch.Generator().manual_seed(seed + 12345)
@@ -176,6 +200,7 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0, dtype=torch.float32, p
 
     ref_trainer.torch.randn = fake_randn
     ref_trainer.torch.min = recording_min
+    ref_trainer.transformation_from_parameters = recording_tfp
     real_cuda = torch.Tensor.cuda
     torch.Tensor.cuda = lambda t, *a, **k: t     # trainer.py:458 calls .cuda(); CPU-only here
     try:
@@ -184,6 +209,7 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0, dtype=torch.float32, p
     finally:
         ref_trainer.torch.randn = real_randn
         ref_trainer.torch.min = real_min
+        ref_trainer.transformation_from_parameters = real_tfp
         torch.Tensor.cuda = real_cuda
     try:
         losses["loss"].backward()
@@ -201,14 +227,22 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0, dtype=torch.float32, p
     if len(argmins) == len(scales):
         for s, idx in zip(scales, argmins):
             rec[f"argmin_{s}"] = idx.numpy().astype(np.uint8)
-    rec["grad_axisangle"] = axis.grad.numpy()
-    rec["grad_translation"] = trans.grad.numpy()
+    if temporal:   # stereo-only: no pose parameters
+        rec["grad_axisangle"] = axis.grad.numpy()
+        rec["grad_translation"] = trans.grad.numpy()
     for s, m in masks.items():
         rec[f"mask_{s}"] = m.detach().numpy()
         rec[f"grad_mask_{s}"] = m.grad.numpy()
     for f in temporal:
-        rec[f"grad_T_{f}"] = camT[f].grad.numpy()
+        if camT[f].grad is not None:   # posecnn: the per-scale T below carry the gradient
+            rec[f"grad_T_{f}"] = camT[f].grad.numpy()
         rec[f"T_{f}"] = camT[f].detach().numpy()
+    if flags.get("posecnn"):
+        assert len(per_scale_T) == len(scales) * len(temporal), len(per_scale_T)
+        for j, T in enumerate(per_scale_T):
+            s, f = scales[j // len(temporal)], temporal[j % len(temporal)]
+            rec[f"T_{f}_{s}"] = T.detach().numpy()
+            rec[f"grad_T_{f}_{s}"] = T.grad.numpy()
     if keep_full:
         for s in scales:
             rec[f"disp_{s}"] = hp["disps"][s].numpy()
@@ -246,9 +280,10 @@ def run_case(ref_trainer, ref_layers, name, spec, seed=0, dtype=torch.float32, p
 
 
 # the full-size cases whose gradient parity is anchored on the fp64 floor
-FP64_CASES = ["full_mono_b2_192x640", "full_mono_b2_320x1024", "full_stereo_b2_192x640", "c2_mono_b12_192x640"]
+FP64_CASES = ["full_mono_b2_192x640", "full_mono_b2_320x1024", "full_stereo_b2_192x640", "c2_mono_b12_192x640",
+              "full_stereo_only_b2_192x640", "full_posecnn_b2_192x640"]
 F64_KEYS = ("loss", "loss_", "grad_disp_sum_", "grad_disp_abs_", "grad_disp_sq_", "grad_disp_abs_img_",
-            "grad_axisangle", "grad_translation")
+            "grad_axisangle", "grad_translation", "grad_T_")
 
 
 def add_fp64(ref_trainer, ref_layers, name):

@@ -34,6 +34,7 @@ class Case:
         self.checksums_only = "grad_disp_0" not in z.files   # large cases: scalars + checksums
         self.scales = [0, 1, 2, 3]
         self.temporal = [f for f in self.frame_ids[1:] if f != "s"]
+        self.posecnn = "posecnn" in self.flags   # per-scale T (trainer.py:366-375)
         if self.full:
             self._from_arrays()
         else:
@@ -79,3 +80,31 @@ class Case:
 
     def expected(self, key):
         return self.z[key]
+
+
+def oracle_cam_T(case: Case, axis, trans, stereo_T=None, record=None):
+    """The oracle's cam_T for a case: transformation_from_parameters per temporal frame
+    (trainer.py:294-295), or for posecnn a callable rebuilding T from each scale's depth
+    (oracle.md2_oracle.posecnn_cam_T, trainer.py:366-375).  record: a list that gets
+    (frame, T) for every T built (gradients retained), in the reference's order."""
+    from monodepth2_amd.layers import transformation_from_parameters as tfp
+    from oracle.md2_oracle import posecnn_cam_T
+    camT = {}
+    for i, f in enumerate(case.temporal):
+        if case.posecnn:
+            def per_scale(depth, i=i, f=f):
+                T = posecnn_cam_T(tfp, axis[i], trans[i], depth, f < 0)
+                if record is not None and T.requires_grad:
+                    T.retain_grad()
+                    record.append((f, T))
+                return T
+            camT[f] = per_scale
+        else:
+            T = tfp(axis[i], trans[i], invert=(f < 0))
+            if record is not None and T.requires_grad:
+                T.retain_grad()
+                record.append((f, T))
+            camT[f] = T
+    if "s" in case.frame_ids:
+        camT["s"] = stereo_T if stereo_T is not None else case.inputs["stereo_T"]
+    return camT

@@ -3,7 +3,9 @@ from __future__ import annotations
 
 import torch
 
-from golden_io import Case
+import numpy as np
+
+from golden_io import Case, oracle_cam_T
 from monodepth2_amd.hotpath import (HotPathConfig, generate_images, photometric_loss, predictive_mask_inputs,
                                     selection_maps)
 from monodepth2_amd.layers import transformation_from_parameters
@@ -14,7 +16,12 @@ def case_config(case: Case) -> HotPathConfig:
                          no_ssim="no_ssim" in case.flags, avg_reprojection="avg_reprojection" in case.flags,
                          disable_automasking="disable_automasking" in case.flags,
                          v1_multiscale="v1_multiscale" in case.flags,
-                         predictive_mask="predictive_mask" in case.flags)
+                         predictive_mask="predictive_mask" in case.flags, t_per_scale=case.posecnn)
+
+
+def _grad(t):
+    """a leaf's gradient as numpy; zeros for the empty pose parameters of stereo-only cases"""
+    return t.grad.cpu().numpy() if t.grad is not None else np.zeros(tuple(t.shape), np.float32)
 
 
 def case_operands(case: Case, device):
@@ -39,15 +46,23 @@ def run_hip(case: Case, device="cuda"):
     disps = [case.disps[s].to(device).clone().requires_grad_(True) for s in range(4)]
     axis = case.axisangle.to(device).clone().requires_grad_(True)
     trans = case.translation.to(device).clone().requires_grad_(True)
-    Ts = []
-    ti = 0
-    for f in case.frame_ids[1:]:
-        if f == "s":
-            Ts.append(case.inputs["stereo_T"].to(device))
-        else:
-            Ts.append(transformation_from_parameters(axis[ti], trans[ti], invert=(f < 0)))
-            ti += 1
-    T = torch.stack(Ts, 0)
+    if case.posecnn:
+        # the product's per-scale transforms (Trainer._stacked_T): mean inverse depth of
+        # each scale's upsampled depth, then one md2_pose_fwd launch per scale
+        from monodepth2_amd.trainer import posecnn_transforms
+        st = case.inputs["stereo_T"].to(device) if "stereo_T" in case.inputs else None
+        T = posecnn_transforms(disps, axis[:, :, 0], trans[:, :, 0], case.frame_ids[1:], st, case.H, case.W,
+                               cfg.min_depth, cfg.max_depth, cfg.v1_multiscale)
+    else:
+        Ts = []
+        ti = 0
+        for f in case.frame_ids[1:]:
+            if f == "s":
+                Ts.append(case.inputs["stereo_T"].to(device))
+            else:
+                Ts.append(transformation_from_parameters(axis[ti], trans[ti], invert=(f < 0)))
+                ti += 1
+        T = torch.stack(Ts, 0)
     T.retain_grad()
     masks, bce = None, None
     if cfg.predictive_mask:
@@ -60,7 +75,7 @@ def run_hip(case: Case, device="cuda"):
     loss[cfg.num_scales].backward()
     torch.cuda.synchronize()
     out = {"loss": loss.detach().cpu().numpy(), "grad_disp": [d.grad.cpu().numpy() for d in disps],
-           "grad_axis": axis.grad.cpu().numpy(), "grad_trans": trans.grad.cpu().numpy(),
+           "grad_axis": _grad(axis), "grad_trans": _grad(trans),
            "grad_T": T.grad.cpu().numpy(), "select": {s: v.cpu().numpy() for s, v in selection_maps(cfg, sel).items()}}
     if masks is not None:
         out["grad_mask"] = {s: m.grad.cpu().numpy() for s, m in masks.items()}
@@ -93,11 +108,7 @@ def run_oracle(case: Case, selection=None, device="cpu", dtype=torch.float32):
     trans = case.translation.to(dev, dtype).clone().requires_grad_(True)
     inputs = {k: (v.to(dev, dtype) if torch.is_tensor(v) and v.is_floating_point() else v)
               for k, v in case.inputs.items()}
-    camT = {}
-    for i, f in enumerate(case.temporal):
-        camT[f] = transformation_from_parameters(axis[i], trans[i], invert=(f < 0))
-    if "s" in case.frame_ids:
-        camT["s"] = inputs["stereo_T"]
+    camT = oracle_cam_T(case, axis, trans, stereo_T=inputs.get("stereo_T"))
     sel = None
     if selection is not None:
         sel = {s: torch.from_numpy(v).long().to(dev) for s, v in selection.items()}
@@ -106,7 +117,7 @@ def run_oracle(case: Case, selection=None, device="cpu", dtype=torch.float32):
     losses["loss"].backward()
     res = {"loss": [float(losses[f"loss/{s}"]) for s in range(4)] + [float(losses["loss"])],
            "grad_disp": [disps[s].grad.cpu().numpy() for s in range(4)],
-           "grad_axis": axis.grad.cpu().numpy(), "grad_trans": trans.grad.cpu().numpy(), "outputs": outputs}
+           "grad_axis": _grad(axis), "grad_trans": _grad(trans), "outputs": outputs}
     if masks:
         res["grad_mask"] = {s: m.grad.cpu().numpy() for s, m in masks.items()}
     return res

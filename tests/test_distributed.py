@@ -187,3 +187,87 @@ def test_flat_sync_sends_buckets_in_index_order():
     assert sent == [0, 1, 2, 3, 4, 5]    # the rest, in order (4 counts as zero)
     b4 = sync.buckets[4][0]
     assert torch.equal(b4.grad, torch.zeros_like(b4)) and torch.equal(sync.buckets[5][0].grad, torch.ones(4, 4))
+
+
+def _autotune_worker(rank, world, port, out_dir):
+    """The production conv-choice mechanism under data parallelism, host logic only (the
+    candidates are stand-ins with rank-dependent timings: the ranks disagree).  Each
+    rank autotunes inside its DDP forward and backward — rank 0 also runs an extra
+    no_grad evaluation first that meets shapes in a different order (bench.py's
+    rank-0-only parity check) — interleaved with DDP's bucket all-reduces; then
+    agree_choices lines every rank up on rank 0's table at one known point."""
+    import datetime
+    from monodepth2_amd import conv_ops
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    # a collective inside the autotune would pair with the other rank's DDP all-reduce
+    # or with a different shape's broadcast: fail fast instead of hanging
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    conv_ops.clear_choices()
+    conv_ops._time_candidate = lambda fn: fn()          # a candidate returns (ms, repeatable)
+    names = ["x6", "x6_256", "f32mfma", "miopen"]
+
+    def cands(shape):
+        # rank-dependent timings; on shape 1 the fastest candidate is not repeatable
+        base = [1.0 + 0.1 * ((i + shape + rank) % 4) for i in range(4)]
+        rep = [not (shape == 1 and i == int(min(range(3), key=lambda j: base[j]))) for i in range(4)]
+        return [(lambda t=t, r=r: (t, r)) for t, r in zip(base, rep)]
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = torch.nn.Linear(8, 8)
+
+        def forward(self, x, shapes):
+            for sh in shapes:
+                conv_ops._fastest("fwd", (sh,), cands(sh), names)
+            return self.lin(x)
+
+    torch.manual_seed(0)
+    net = Net()
+    ddp = torch.nn.parallel.DistributedDataParallel(net, bucket_cap_mb=1)
+
+    class Hook(torch.autograd.Function):   # autotune calls inside the backward too
+        @staticmethod
+        def forward(ctx, y):
+            return y
+
+        @staticmethod
+        def backward(ctx, g):
+            for sh in (5, 6):
+                conv_ops._fastest("wgrad", (sh,), cands(sh), names)
+            return g
+
+    if rank == 0:   # rank-0-only evaluation first, shapes in another order
+        with torch.no_grad():
+            net(torch.randn(2, 8), [3, 2, 9])
+    for step in range(2):
+        y = Hook.apply(ddp(torch.randn(4, 8), [0, 1, 2, 3, 4]))
+        y.square().sum().backward()
+        if step == 0:
+            changed = conv_ops.agree_choices()
+    table = {f"{k[0]} {k[1:]}": conv_ops._names[k][i] for k, i in conv_ops._choice.items()}
+    # a shape rank 0 timed alone is pinned here to rank 0's choice for when it appears
+    conv_ops._fastest("fwd", (9,), cands(9), names)
+    table["after fwd (9,)"] = conv_ops._names[("fwd", 9)][conv_ops._choice[("fwd", 9)]]
+    torch.save({"table": table, "changed": changed, "nondet": {str(k): v for k, v in conv_ops._nondet.items()}},
+               os.path.join(out_dir, f"tune_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_conv_autotune_no_collective_then_rank0_table(tmp_path):
+    port = _free_port()
+    mp.spawn(_autotune_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(os.path.join(tmp_path, "tune_0.pt"), weights_only=True)
+    r1 = torch.load(os.path.join(tmp_path, "tune_1.pt"), weights_only=True)
+    assert r0["changed"] == 0 and r1["changed"] > 0          # rank 1 timed differently
+    common = set(r0["table"]) & set(r1["table"])
+    assert {"fwd (0,)", "fwd (4,)", "wgrad (5,)", "after fwd (9,)"} <= common
+    for k in common:
+        assert r0["table"][k] == r1["table"][k], k
+    assert "fwd (9,)" not in r1["table"] or r1["table"]["fwd (9,)"] == r0["table"]["fwd (9,)"]
+    # the fastest candidate of shape 1 returned different bits on a rerun: never kept
+    for r in (r0, r1):
+        assert any("1" in k for k in r["nondet"])
+        assert r["table"]["fwd (1,)"] not in r["nondet"][next(k for k in r["nondet"] if "1" in k)]

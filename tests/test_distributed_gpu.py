@@ -28,7 +28,8 @@ def _init(rank, world, port, backend):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     # the local and the synced gradients come from two separate backward passes: the
     # convolutions MIOpen keeps must not use atomics (run-to-run rounding differences
-    # would read as averaging errors); our own kernels are deterministic anyway
+    # would read as averaging errors); the autotune keeps no candidate whose repeated
+    # outputs differ (conv_ops._time_candidate) either way
     torch.backends.cudnn.deterministic = True
     if backend == "nccl":
         torch.cuda.set_device(rank)
@@ -36,6 +37,31 @@ def _init(rank, world, port, backend):
         return torch.device("cuda", rank)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     return torch.device("cuda", 0)
+
+
+def _first_step(tr, batch, rank):
+    """The production convolution-choice path: rank 0 first runs a no_grad evaluation on
+    its own (as bench.py's parity check does), then one real training step — the
+    autotune times its candidates inside the forward and backward on each rank with no
+    collective, and the Trainer lines every rank up on rank 0's table after the step
+    (conv_ops.agree_choices).  Every rank then holds rank 0's choices, and no kept
+    candidate failed its repeatability check."""
+    from monodepth2_amd import conv_ops
+    assert conv_ops.AUTOTUNE
+    if rank == 0:
+        with torch.no_grad():
+            tr.nets(tr, batch)
+    tr.train_step(batch)
+    torch.cuda.synchronize()
+    assert tr._choices_agreed
+    mine = {k: conv_ops._names[k][i] for k, i in conv_ops._choice.items()}
+    box = [mine]
+    dist.broadcast_object_list(box, src=0)
+    for k, v in box[0].items():
+        assert k not in mine or mine[k] == v, (k, mine[k], v)
+    for k, bad in conv_ops._nondet.items():   # evidence: never kept (DESIGN.md §6)
+        print(f"rank {rank}: non-repeatable candidates {bad} for {k}", flush=True)
+        assert conv_ops._names[k][conv_ops._choice[k]] not in bad or not conv_ops.AUTOTUNE
 
 
 def _rank_flat(rank, world, port, backend="gloo"):
@@ -47,16 +73,13 @@ def _rank_flat(rank, world, port, backend="gloo"):
         from monodepth2_amd.data import synthetic_batch
         from monodepth2_amd.options import default_options
         from monodepth2_amd.trainer import Trainer
-        from monodepth2_amd import conv_ops
-        # the kernels are not under test here: fixed choices, none made from timings
-        # taken while both ranks share the one GPU
-        conv_ops.AUTOTUNE = False
         torch.manual_seed(0)
         tr = Trainer(default_options(batch_size=2, height=64, width=128, weights_init="scratch", grad_sync="flat",
                                      log_dir="/tmp/md2_ddp_gpu"), device=dev, rank=rank, world_size=world)
         assert tr.ddp is None and tr.flat_sync is not None and tr.flat_sync.overlap
         tr.set_train()
         batch = synthetic_batch(2, 64, 128, tr.opt.frame_ids, 4, seed=10 + rank, device=dev)
+        _first_step(tr, batch, rank)
         named = [(n, p) for n, p in tr.nets.named_parameters() if p.requires_grad and "fc." not in n]
         tr.flat_sync.zero()
         _, losses = tr.process_batch(batch)
@@ -87,16 +110,13 @@ def _rank(rank, world, port, backend="gloo"):
         from monodepth2_amd.data import synthetic_batch
         from monodepth2_amd.options import default_options
         from monodepth2_amd.trainer import Trainer
-        from monodepth2_amd import conv_ops
-        # the kernels are not under test here: fixed choices, none made from timings
-        # taken while both ranks share the one GPU
-        conv_ops.AUTOTUNE = False
         torch.manual_seed(0)
         tr = Trainer(default_options(batch_size=2, height=64, width=128, weights_init="scratch",
                                      log_dir="/tmp/md2_ddp_gpu"), device=dev, rank=rank, world_size=world)
         assert tr.ddp is not None and tr._pose_stream is not None
         tr.set_train()
         batch = synthetic_batch(2, 64, 128, tr.opt.frame_ids, 4, seed=10 + rank, device=dev)
+        _first_step(tr, batch, rank)
         params = [p for p in tr.nets.parameters() if p.requires_grad]
         names = [n for n, p in tr.nets.named_parameters() if p.requires_grad]
 

@@ -96,15 +96,33 @@ SMALL_T2_OVERRIDE = {("stereo_b2_64x128", 3): 3e-3}
 _FLOOR_TRIM = {"full_mono_b2_192x640": (5.78e-5, 7.36e-5, 9.50e-5, 9.12e-4),
                "full_mono_b2_320x1024": (1.10e-4, 2.01e-4, 1.48e-3, 4.41e-3),
                "full_stereo_b2_192x640": (6.25e-5, 7.07e-5, 8.56e-5, 9.48e-4),
-               "c2_mono_b12_192x640": (6.57e-5, 9.32e-5, 6.81e-4, 2.54e-3)}
+               "c2_mono_b12_192x640": (6.57e-5, 9.32e-5, 6.81e-4, 2.54e-3),
+               # round 5 (stereo-only S=1, posecnn per-scale T): the CPU-fp32 oracle's
+               # trimmed distance to the fp64 anchor, computed in the build container
+               "full_stereo_only_b2_192x640": (3.3e-5, 4.7e-5, 6.14e-4, 4.16e-3),
+               "full_posecnn_b2_192x640": (5.32e-5, 1.36e-4, 9.07e-5, 3.03e-3)}
+# the round-3 per-case bars (3x what HIP measured then): ADVICE r04 — the floor-anchored
+# bar must not loosen a case below what the implementation was already held to, so each
+# bar is the smaller of the two
+_MEASURED_T1 = {"full_mono_b2_192x640": (2e-4, 2.5e-4, 3e-4, 1.6e-3),
+                "full_mono_b2_320x1024": (2.5e-4, 3e-4, 2e-3, 7e-3),
+                "full_stereo_b2_192x640": (2e-4, 2e-4, 4.5e-4, 4.5e-3),
+                "c2_mono_b12_192x640": (2.5e-4, 1e-3, 6e-3, 1.2e-2)}
+_MEASURED_T2 = {"full_mono_b2_192x640": (2e-4, 2.5e-4, 3e-4, 2e-3),
+                "full_mono_b2_320x1024": (3e-4, 3.5e-4, 3.2e-3, 9.5e-3),
+                "full_stereo_b2_192x640": (2e-4, 2.5e-4, 3e-4, 6e-3),
+                "c2_mono_b12_192x640": (2.5e-4, 3.2e-4, 1.5e-3, 6.5e-3)}
+
+
 def _ceil2(x):
     """x rounded UP to two significant digits"""
     e = 10.0 ** (np.floor(np.log10(x)) - 1)
     return float(np.ceil(x / e - 1e-9) * e)
 
 
-FULL_T1 = {n: tuple(_ceil2(3 * 2 ** 0.5 * f) for f in v) for n, v in _FLOOR_TRIM.items()}
-FULL_T2 = FULL_T1
+_FLOOR_BAR = {n: tuple(_ceil2(3 * 2 ** 0.5 * f) for f in v) for n, v in _FLOOR_TRIM.items()}
+FULL_T1 = {n: tuple(min(a, b) for a, b in zip(v, _MEASURED_T1.get(n, v))) for n, v in _FLOOR_BAR.items()}
+FULL_T2 = {n: tuple(min(a, b) for a, b in zip(v, _MEASURED_T2.get(n, v))) for n, v in _FLOOR_BAR.items()}
 # fraction of pixels within 1e-4 max|ref| + 1e-3 |ref| (measured >= 0.9857 at 1024x320 s3)
 # (bar = 1 - 3x the measured out-of-tolerance fraction)
 FULL_IN_TOL = (0.9998, 0.996, 0.987, 0.955)
@@ -188,11 +206,19 @@ def test_hip_matches_reference(name):
             assert e <= FULL_T1[name][s], (s, e)
     # pose gradients sum over every pixel, flipped ones included (measured: small cases
     # <= 1.6e-4, stereo / full size <= 1.7e-3)
+    if not case.temporal:   # stereo-only: T = stereo_T, no pose parameters
+        return
     pose_bar = 5e-3 if (not case.full or name.startswith("stereo")) else 5e-4
     assert rel_l2(out["grad_axis"], case.expected("grad_axisangle")) <= pose_bar
     assert rel_l2(out["grad_trans"], case.expected("grad_translation")) <= pose_bar
     for i, f in enumerate(case.temporal):
-        assert rel_l2(out["grad_T"][case.frame_ids[1:].index(f)], case.expected(f"grad_T_{f}")) <= pose_bar
+        fi = case.frame_ids[1:].index(f)
+        if case.posecnn:   # the per-scale T of trainer.py:374-375 and dL/dT at each scale
+            for s in range(4):
+                e = rel_l2(out["grad_T"][s][fi], case.expected(f"grad_T_{f}_{s}"))
+                assert e <= pose_bar, (f, s, e)
+        else:
+            assert rel_l2(out["grad_T"][fi], case.expected(f"grad_T_{f}")) <= pose_bar
     for s, g in out.get("grad_mask", {}).items():
         assert rel_l2(g, case.expected(f"grad_mask_{s}")) <= SMALL_BAR, (s, rel_l2(g, case.expected(f"grad_mask_{s}")))
 
@@ -216,8 +242,9 @@ def test_hip_gradients_match_oracle_pinned_selection(name):
             assert e <= FULL_T2[name][s], (s, e)
             assert in_tol(g, r) >= FULL_IN_TOL[s], (s, in_tol(g, r))
     pose_bar = (6e-4 if name.startswith("stereo") else SMALL_BAR) if small else 5e-3
-    assert rel_l2(out["grad_axis"], ref["grad_axis"]) <= pose_bar
-    assert rel_l2(out["grad_trans"], ref["grad_trans"]) <= pose_bar
+    if case.temporal:
+        assert rel_l2(out["grad_axis"], ref["grad_axis"]) <= pose_bar
+        assert rel_l2(out["grad_trans"], ref["grad_trans"]) <= pose_bar
     for s, g in out.get("grad_mask", {}).items():
         assert rel_l2(g, ref["grad_mask"][s]) <= SMALL_BAR, s
 

@@ -10,8 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from golden_io import Case, case_names
-from monodepth2_amd.layers import transformation_from_parameters
+from golden_io import Case, case_names, oracle_cam_T
 from oracle.md2_oracle import HotPathOptions, hot_path
 
 
@@ -26,25 +25,20 @@ def run_oracle(case: Case, keep_images=True):
     disps = {s: d.clone().requires_grad_(True) for s, d in case.disps.items()}
     axis = case.axisangle.clone().requires_grad_(True)
     trans = case.translation.clone().requires_grad_(True)
-    camT = {}
-    for i, f in enumerate(case.temporal):
-        T = transformation_from_parameters(axis[i], trans[i], invert=(f < 0))
-        T.retain_grad()
-        camT[f] = T
-    if "s" in case.frame_ids:
-        camT["s"] = case.inputs["stereo_T"]
+    built = []
+    camT = oracle_cam_T(case, axis, trans, record=built)
     losses, outputs = hot_path(opt, disps, case.inputs, camT,
                                noise=case.noise if case.noise else None, keep_images=keep_images, masks=masks)
     losses["loss"].backward()
     outputs["_masks"] = masks
-    return losses, outputs, disps, axis, trans, camT
+    return losses, outputs, disps, axis, trans, built
 
 
 @pytest.mark.parametrize("name", case_names())
 def test_oracle_matches_reference(name):
     torch.set_num_threads(4)
     case = Case(name)
-    losses, outputs, disps, axis, trans, camT = run_oracle(case)
+    losses, outputs, disps, axis, trans, built = run_oracle(case)
     # losses: north_star bound is 1e-4; the restatement is op-for-op so it is much tighter
     for s in case.scales:
         assert abs(float(losses[f"loss/{s}"]) - float(case.expected(f"loss_{s}"))) < 1e-6
@@ -62,11 +56,20 @@ def test_oracle_matches_reference(name):
             continue
         np.testing.assert_allclose(disps[s].grad.numpy(), case.expected(f"grad_disp_{s}"),
                                    rtol=1e-4, atol=1e-9)
-    np.testing.assert_allclose(axis.grad.numpy(), case.expected("grad_axisangle"), rtol=1e-4, atol=1e-8)
-    np.testing.assert_allclose(trans.grad.numpy(), case.expected("grad_translation"), rtol=1e-4, atol=1e-8)
-    for f in case.temporal:
-        np.testing.assert_allclose(camT[f].detach().numpy(), case.expected(f"T_{f}"), atol=1e-7)
-        np.testing.assert_allclose(camT[f].grad.numpy(), case.expected(f"grad_T_{f}"), rtol=1e-4, atol=1e-8)
+    if case.temporal:   # stereo-only cases have no pose parameters
+        np.testing.assert_allclose(axis.grad.numpy(), case.expected("grad_axisangle"), rtol=1e-4, atol=1e-8)
+        np.testing.assert_allclose(trans.grad.numpy(), case.expected("grad_translation"), rtol=1e-4, atol=1e-8)
+    if case.posecnn:
+        # one T per (scale, frame), scale-major as the reference builds them (trainer.py:374)
+        assert len(built) == 4 * len(case.temporal)
+        for j, (f, T) in enumerate(built):
+            s = j // len(case.temporal)
+            np.testing.assert_allclose(T.detach().numpy(), case.expected(f"T_{f}_{s}"), rtol=1e-6, atol=1e-7)
+            np.testing.assert_allclose(T.grad.numpy(), case.expected(f"grad_T_{f}_{s}"), rtol=1e-4, atol=1e-8)
+    else:
+        for f, T in built:
+            np.testing.assert_allclose(T.detach().numpy(), case.expected(f"T_{f}"), atol=1e-7)
+            np.testing.assert_allclose(T.grad.numpy(), case.expected(f"grad_T_{f}"), rtol=1e-4, atol=1e-8)
     if outputs["_masks"]:
         for s, m in outputs["_masks"].items():
             np.testing.assert_allclose(m.grad.numpy(), case.expected(f"grad_mask_{s}"), rtol=1e-4, atol=1e-9)
@@ -120,5 +123,7 @@ def test_oracle_fp64_matches_reference_fp64(name):
             want = float(case.expected(f"f64_grad_disp_{key}_{s}"))
             assert abs(v - want) <= 1e-9 * max(abs(want), np.abs(g).sum() * 1e-3), (s, key, v, want)
         np.testing.assert_allclose(np.abs(g).sum((1, 2, 3)), case.expected(f"f64_grad_disp_abs_img_{s}"), rtol=1e-9)
-    np.testing.assert_allclose(ref["grad_axis"], case.expected("f64_grad_axisangle"), rtol=1e-8, atol=1e-14)
-    np.testing.assert_allclose(ref["grad_trans"], case.expected("f64_grad_translation"), rtol=1e-8, atol=1e-14)
+    if case.temporal:
+        np.testing.assert_allclose(ref["grad_axis"], case.expected("f64_grad_axisangle"), rtol=1e-8, atol=1e-14)
+        np.testing.assert_allclose(ref["grad_trans"], case.expected("f64_grad_translation"), rtol=1e-8,
+                                   atol=1e-14)

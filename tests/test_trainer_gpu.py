@@ -58,7 +58,7 @@ def test_train_step_runs_and_updates(name):
     assert changed > 0.8 * len(before)
 
 
-@pytest.mark.parametrize("name", ["mono", "stereo", "no_ssim", "avg_reprojection", "no_automask",
+@pytest.mark.parametrize("name", ["mono", "stereo", "stereo_only", "no_ssim", "avg_reprojection", "no_automask",
                                   "predictive_mask", "v1_multiscale", "posecnn", "mono_nchw", "amp_bf16"])
 def test_losses_match_oracle_on_same_outputs(name):
     """compute_losses (fused HIP) vs the oracle on identical network outputs + noise."""
@@ -201,10 +201,7 @@ def test_hip_graph_replay_matches_eager_step():
     loss_graph = float(lg["loss"])
     params_graph = [p.detach().clone() for p in tr.nets.parameters()]
     restore(snap)
-    side = tr.graph_stream   # the stream the parameters' AccumulateGrad nodes were created on
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):
-        _, le = tr._step_body(tr.static_inputs)    # the same step, eagerly
+    _, le = tr.eager_step(tr.static_inputs)    # the same step, eagerly (on the capture's stream)
     torch.cuda.synchronize()
     assert abs(loss_graph - float(le["loss"])) < 1e-6, (loss_graph, float(le["loss"]))
     worst = max(float((a - b).abs().max()) for a, b in zip(params_graph, tr.nets.parameters()))
@@ -218,16 +215,21 @@ def test_hip_graph_flat_sync_step_replays_eager_bitwise():
     stream's waits on the producing streams (pose network on its own stream), the
     bucket copies and the join back.  A replay must equal the same step run eagerly
     from the same state, bit for bit, and every gradient must be its bucket view."""
+    import warnings
     tr, batch = make("mono", hip_graph=True, grad_sync="flat")
     fs = tr.flat_sync
     assert fs is not None and fs.overlap and fs.comm is not None and len(fs.buckets) >= 1
     assert tr._pose_stream is not None
-    tr.train_step(batch)                       # capture (+ warm-up steps) and one replay
-    tr.train_step(batch)
-    for plist, views in zip(fs.buckets, fs.views):
-        for p, v in zip(plist, views):
-            assert p.grad is not None and p.grad.data_ptr() == v.data_ptr()
-    loss_g, loss_e, worst, delta = _replay_vs_eager(tr, batch)
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        tr.train_step(batch)                       # capture (+ warm-up steps) and one replay
+        tr.train_step(batch)
+        for plist, views in zip(fs.buckets, fs.views):
+            for p, v in zip(plist, views):
+                assert p.grad is not None and p.grad.data_ptr() == v.data_ptr()
+        loss_g, loss_e, worst, delta = _replay_vs_eager(tr, batch)
+    # every accumulation on the stream its AccumulateGrad node was created on
+    assert not [w for w in caught if "AccumulateGrad" in str(w.message)], [str(w.message) for w in caught]
     assert delta > 0
     assert loss_g == loss_e and worst == 0.0, (loss_g, loss_e, worst)
 
@@ -261,7 +263,7 @@ def test_hip_graph_first_step_is_one_step():
                 if torch.is_tensor(v):
                     v.zero_()
         tr.seed_tensor.zero_()
-    _, le = tr._step_body(tr.static_inputs)
+    _, le = tr.eager_step(tr.static_inputs)
     torch.cuda.synchronize()
     assert abs(loss_graph - float(le["loss"])) < 1e-6, (loss_graph, float(le["loss"]))
     for a, b in zip(params_g, tr.nets.parameters()):
@@ -297,7 +299,7 @@ def test_hip_graph_replay_sees_lr_schedule():
             for k, v in saved.items():
                 st[k].copy_(v)
         tr.seed_tensor.copy_(seed0)
-    tr._step_body(tr.static_inputs)
+    tr.eager_step(tr.static_inputs)
     torch.cuda.synchronize()
     delta = max(float((a - b).abs().max()) for a, b in zip(params_g, params0))
     worst = max(float((a - b).abs().max()) for a, b in zip(params_g, tr.nets.parameters()))
@@ -346,7 +348,7 @@ def _replay_vs_eager(tr, batch):
             for k, v in saved.items():
                 st[k].copy_(v)
         tr.seed_tensor.copy_(seed0)
-    _, le = tr._step_body(tr.static_inputs)
+    _, le = tr.eager_step(tr.static_inputs)
     torch.cuda.synchronize()
     delta = max(float((a - b).abs().max()) for a, b in zip(params_g, params0))
     worst = max(float((a - b).abs().max()) for a, b in zip(params_g, tr.nets.parameters()))

@@ -2,18 +2,18 @@
 # Build an A/B variant of libmd2hot.so: md2hot.hip (or another source given by
 # SRC=path) compiled with extra flags, linked with the in-tree objects of the other
 # sources.  Usage: tools/build_variant.sh NAME [-DFOO=1 ...]
-# Output: variants/NAME/libmd2hot.so (run with MD2_LIB=variants/NAME/libmd2hot.so).
+# Output: abx/NAME/libmd2hot.so (run with MD2_LIB=abx/NAME/libmd2hot.so).
 set -e
 name=$1; shift
 cd "$(dirname "$0")/.."
 SRC=${SRC:-monodepth2_amd/csrc/md2hot.hip}
-mkdir -p variants/$name
-obj=variants/$name/$(basename ${SRC%.hip}).o
+mkdir -p abx/$name
+obj=abx/$name/$(basename ${SRC%.hip}).o
 # the in-tree build flags (monodepth2_amd/build.py): -fno-slp-vectorize for md2hot.hip only
 slp=""
 [ "$(basename $SRC)" = "md2hot.hip" ] && slp="-fno-slp-vectorize"
 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -Iinclude $slp "$@" -c $SRC -o $obj
 others=$(ls monodepth2_amd/csrc/obj/*.o | grep -v "/$(basename ${SRC%.hip}).o$")
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared -o variants/$name/libmd2hot.so $obj $others
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared -o abx/$name/libmd2hot.so $obj $others
 rm -f $obj
-echo variants/$name/libmd2hot.so
+echo abx/$name/libmd2hot.so
