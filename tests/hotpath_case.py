@@ -63,7 +63,8 @@ def run_hip(case: Case, device="cuda"):
                 Ts.append(transformation_from_parameters(axis[ti], trans[ti], invert=(f < 0)))
                 ti += 1
         T = torch.stack(Ts, 0)
-    T.retain_grad()
+    if T.requires_grad:   # stereo-only: T = stereo_T, a constant
+        T.retain_grad()
     masks, bce = None, None
     if cfg.predictive_mask:
         masks = {s: m.to(device).clone().requires_grad_(True) for s, m in case.masks.items()}
@@ -76,7 +77,7 @@ def run_hip(case: Case, device="cuda"):
     torch.cuda.synchronize()
     out = {"loss": loss.detach().cpu().numpy(), "grad_disp": [d.grad.cpu().numpy() for d in disps],
            "grad_axis": _grad(axis), "grad_trans": _grad(trans),
-           "grad_T": T.grad.cpu().numpy(), "select": {s: v.cpu().numpy() for s, v in selection_maps(cfg, sel).items()}}
+           "grad_T": _grad(T), "select": {s: v.cpu().numpy() for s, v in selection_maps(cfg, sel).items()}}
     if masks is not None:
         out["grad_mask"] = {s: m.grad.cpu().numpy() for s, m in masks.items()}
     with torch.no_grad():
@@ -108,7 +109,8 @@ def run_oracle(case: Case, selection=None, device="cpu", dtype=torch.float32):
     trans = case.translation.to(dev, dtype).clone().requires_grad_(True)
     inputs = {k: (v.to(dev, dtype) if torch.is_tensor(v) and v.is_floating_point() else v)
               for k, v in case.inputs.items()}
-    camT = oracle_cam_T(case, axis, trans, stereo_T=inputs.get("stereo_T"))
+    built = []
+    camT = oracle_cam_T(case, axis, trans, stereo_T=inputs.get("stereo_T"), record=built)
     sel = None
     if selection is not None:
         sel = {s: torch.from_numpy(v).long().to(dev) for s, v in selection.items()}
@@ -118,6 +120,8 @@ def run_oracle(case: Case, selection=None, device="cpu", dtype=torch.float32):
     res = {"loss": [float(losses[f"loss/{s}"]) for s in range(4)] + [float(losses["loss"])],
            "grad_disp": [disps[s].grad.cpu().numpy() for s in range(4)],
            "grad_axis": _grad(axis), "grad_trans": _grad(trans), "outputs": outputs}
+    if case.posecnn:   # dL/dT of every per-scale T, scale-major (trainer.py:374)
+        res["T"] = [T.grad.cpu().numpy() for _, T in built]
     if masks:
         res["grad_mask"] = {s: m.grad.cpu().numpy() for s, m in masks.items()}
     return res

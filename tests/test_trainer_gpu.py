@@ -355,15 +355,18 @@ def _replay_vs_eager(tr, batch):
     return loss_g, float(le["loss"]), worst, delta
 
 
-def test_hip_graph_bf16_full_resolution_step():
+@pytest.mark.parametrize("Bf", [2, 32])
+def test_hip_graph_bf16_full_resolution_step(Bf):
     """Config C5's step (BASELINE configs[4]: bf16 autocast on the networks, the
     photometric loss in fp32, the whole step captured in one hipGraph) at the full
-    640x192 resolution: a replay equals the same step run eagerly from the same state,
-    and the replay's loss equals the CPU oracle (reference formulation,
-    trainer.py:341-496) on the replay's own network outputs within 1e-5."""
+    640x192 resolution, at B=2 and at C5's own 32 images per GPU: a replay equals the
+    same step run eagerly from the same state, and the replay's loss equals the CPU
+    oracle (reference formulation, trainer.py:341-496) on the replay's own network
+    outputs within 1e-5."""
     from oracle.md2_oracle import HotPathOptions, hot_path
     from monodepth2_amd.trainer import Trainer
-    Hf, Wf, Bf = 192, 640, 2
+    Hf, Wf = 192, 640
+    torch.set_num_threads(16)
     torch.manual_seed(0)
     tr = Trainer(default_options(batch_size=Bf, height=Hf, width=Wf, weights_init="scratch", log_dir="/tmp/md2_test",
                                  frame_ids=[0, -1, 1], amp="bf16", hip_graph=True), device=torch.device("cuda", 0))

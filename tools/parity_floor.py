@@ -29,7 +29,7 @@ def main():
     for name in fp64_cases():
         case = Case(name)
         _, out = run_hip(case)
-        r64, runs = floor_runs(case)
+        r64, runs = floor_runs(case, out["select"] if case.posecnn else None)
         rows = floor_metrics(case, out, runs, r64)
         for row in rows:
             row["hip_over_floor"] = row["hip_f64"] / row["floor"]
