@@ -34,14 +34,29 @@ def needs_build() -> bool:
     t = os.path.getmtime(LIB_PATH)
     deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(INCLUDE, "md2hot.h"),
                                                        os.path.join(CSRC, "md2_bf16.h")]
-    return any(os.path.getmtime(d) > t for d in deps)
+    if any(os.path.getmtime(d) > t for d in deps):
+        return True
+    try:   # per-source flags changed (they are part of the build id, not of any mtime)
+        import ctypes
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.md2_build_id.restype = ctypes.c_char_p
+        return lib.md2_build_id().decode() != source_hash()
+    except OSError:
+        return True
 
 
 # Per-source extra flags.  md2hot.hip: no SLP vectorisation — packed-f32 VALU
 # (v_pk_fma_f32 / v_pk_mul_f32) issues no faster than two scalar ops on gfx950 and the
 # register pairs it needs cost ~100 v_mov per row step of the photometric kernels;
 # measured: photo_bwd 0.306 -> 0.287 ms at B=12 640x192.
-FLAGS = {"md2hot.hip": ["-fno-slp-vectorize"]}
+# disphead.hip: also no SLP — the vectorised weight-gradient accumulation became
+# v_pk_fma_f32 whose src1 op_sel has the low lane read the pair's high dword, and those
+# instructions (taps 1 and 7, and only they) gave intermittently different low-lane
+# results when another process shared the GPU; tests/test_isa_guard.py
+# keeps that encoding out of the whole library (glue.hip's input normalisation had it
+# too, on an SGPR pair: no SLP there either).
+FLAGS = {"md2hot.hip": ["-fno-slp-vectorize"], "disphead.hip": ["-fno-slp-vectorize"],
+         "glue.hip": ["-fno-slp-vectorize"]}
 
 
 def source_hash() -> str:
