@@ -148,6 +148,9 @@ def parse():
     ap.add_argument("--pmc", type=int, default=1, help="measure the hot path's HBM traffic with rocprofv3 "
                     "PMC passes in this run (rank 0, N=1)")
     ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen exhaustive find per conv shape")
+    ap.add_argument("--deterministic", type=int, default=-1,
+                    help="MIOpen deterministic algorithms (1/0; default: MIOpen's own choice — its deterministic "
+                         "bf16 solvers take 9.4 s a step at B=32, DESIGN.md §6)")
     ap.add_argument("--channels-last", type=int, default=1, help="NHWC convolutions (1/0)")
     ap.add_argument("--pose-last", type=int, default=0,
                     help="1: pose network forward enqueued after the depth network (its backward first)")
@@ -336,6 +339,8 @@ def main():
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     torch.backends.cudnn.benchmark = args.cudnn_benchmark
+    if args.deterministic >= 0:
+        torch.backends.cudnn.deterministic = bool(args.deterministic)
     _lib.lib()
     log(f"world={world} device={torch.cuda.get_device_name(device)}")
 

@@ -355,14 +355,64 @@ def _replay_vs_eager(tr, batch):
     return loss_g, float(le["loss"]), worst, delta
 
 
+def _grads(tr):
+    return [None if p.grad is None else p.grad.detach().clone() for p in tr.nets.parameters()]
+
+
+def _rel_l2(a, b):
+    num = sum(float((x - y).double().square().sum()) for x, y in zip(a, b) if x is not None and y is not None)
+    den = sum(float(y.double().square().sum()) for x, y in zip(a, b) if x is not None and y is not None)
+    return (num / den) ** 0.5
+
+
+def _replay_eager_fp32(tr, batch):
+    """From one snapshot of the training state: the captured step (replay), the same
+    step eagerly, and the same step eagerly without autocast (fp32 networks); returns
+    the three losses and the three steps' gradients."""
+    torch.cuda.synchronize()
+    opt_state = [{k: v.detach().clone() for k, v in st.items()} for st in tr.model_optimizer.state.values()]
+    params0, bufs0 = _graph_state(tr)
+    seed0 = tr.seed_tensor.clone()
+
+    def restore():
+        with torch.no_grad():
+            for p, v in zip(tr.nets.parameters(), params0):
+                p.copy_(v)
+            for b, v in zip(tr.nets.buffers(), bufs0):
+                b.copy_(v)
+            for st, saved in zip(tr.model_optimizer.state.values(), opt_state):
+                for k, v in saved.items():
+                    st[k].copy_(v)
+            tr.seed_tensor.copy_(seed0)
+
+    _, lg = tr.train_step(batch)
+    torch.cuda.synchronize()
+    out = [(float(lg["loss"]), _grads(tr))]
+    for amp in ("bf16", "none"):
+        restore()
+        tr.opt.amp = amp
+        _, le = tr.eager_step(tr.static_inputs)
+        torch.cuda.synchronize()
+        out.append((float(le["loss"]), _grads(tr)))
+    tr.opt.amp = "bf16"
+    return out
+
+
 @pytest.mark.parametrize("Bf", [2, 32])
 def test_hip_graph_bf16_full_resolution_step(Bf):
     """Config C5's step (BASELINE configs[4]: bf16 autocast on the networks, the
     photometric loss in fp32, the whole step captured in one hipGraph) at the full
-    640x192 resolution, at B=2 and at C5's own 32 images per GPU: a replay equals the
-    same step run eagerly from the same state, and the replay's loss equals the CPU
-    oracle (reference formulation, trainer.py:341-496) on the replay's own network
-    outputs within 1e-5."""
+    640x192 resolution, at B=2 and at C5's own 32 images per GPU, and the replay's loss
+    equals the CPU oracle (reference formulation, trainer.py:341-496) on the replay's
+    own network outputs within 1e-5.
+
+    B=2: a replay equals the same step run eagerly from the same state.  B=32: MIOpen's
+    bf16 weight-gradient solvers at this batch are not deterministic (two replays of
+    the same graph from the same state differ by ~5% gradient rel-L2, the same size as
+    bf16 autocast's own error against the fp32 step; its deterministic solvers take 9.4 s
+    a step — DESIGN.md §6), so the replay and the eager step are each held against the
+    same step run in fp32 from the same state: both within bf16's measured error (0.052-0.064
+    over all parameters, bar 0.1), and their losses within 1e-5 (measured 1.3e-6)."""
     from oracle.md2_oracle import HotPathOptions, hot_path
     from monodepth2_amd.trainer import Trainer
     Hf, Wf = 192, 640
@@ -376,9 +426,16 @@ def test_hip_graph_bf16_full_resolution_step(Bf):
     tr.noise_override = {s: n.cuda() for s, n in noise.items()}
     tr.train_step(batch)       # warm-up + capture + first replay
     tr.train_step(batch)
-    loss_g, loss_e, worst, delta = _replay_vs_eager(tr, batch)
-    assert abs(loss_g - loss_e) < 1e-6, (loss_g, loss_e)
-    assert delta > 0 and worst < 1e-3 * delta + 1e-9, (worst, delta)
+    if Bf == 2:
+        loss_g, loss_e, worst, delta = _replay_vs_eager(tr, batch)
+        assert abs(loss_g - loss_e) < 1e-6, (loss_g, loss_e)
+        assert delta > 0 and worst < 1e-3 * delta + 1e-9, (worst, delta)
+    else:
+        (loss_g, g_g), (loss_e, g_e), (loss_f, g_f) = _replay_eager_fp32(tr, batch)
+        assert abs(loss_g - loss_e) < 1e-5, (loss_g, loss_e)
+        assert abs(loss_g - loss_f) < 1e-4, (loss_g, loss_f)
+        e_g, e_e = _rel_l2(g_g, g_f), _rel_l2(g_e, g_f)
+        assert e_g < 0.1 and e_e < 0.1, (e_g, e_e)
     # the replay's own outputs through the oracle
     _, lg = tr.train_step(batch)
     torch.cuda.synchronize()
