@@ -141,6 +141,9 @@ def parse():
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--num_layers", type=int, default=18)
     ap.add_argument("--stereo", action="store_true")
+    ap.add_argument("--frame-ids", type=str, default="0,-1,1",
+                    help="comma list (trainer --frame_ids): e.g. '0' with --stereo is the stereo-only step "
+                         "(no pose network; an experiment, not the headline)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
@@ -175,7 +178,7 @@ def make_trainer(args, device, rank, world):
     from monodepth2_amd.trainer import Trainer
     opt = default_options(batch_size=args.batch, height=args.height, width=args.width,
                           num_layers=args.num_layers, weights_init="scratch", use_stereo=args.stereo,
-                          frame_ids=[0, -1, 1], log_dir="/tmp/md2_bench",
+                          frame_ids=[int(f) for f in args.frame_ids.split(",")], log_dir="/tmp/md2_bench",
                           channels_last=bool(args.channels_last), hip_graph=bool(args.graph), amp=args.amp,
                           pose_streams=args.pose_stream)
     tr = Trainer(opt, device=device, rank=rank, world_size=world)

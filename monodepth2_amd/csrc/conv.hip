@@ -1209,7 +1209,7 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
 // wave tile BMW/2 x 32).  BMW = 128 rows (co) per tile, or 64 for the 64-channel
 // layers (half the MFMA work of a 128 tile there; only waves 0-1 stage gy, and two
 // blocks fit a CU).  ConvArgs: M = Co, N = KT*Ci, P = pixels, C = Ci, Cg = Co.
-template <int BMW>
+template <int BMW, bool XFAST>
 __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel(ConvArgs a) {
     constexpr int NT = 512, BNW = 128, TM = BMW / 64;
     constexpr int PA = BMW * XBK, PB = BNW * XBK;
@@ -1258,6 +1258,22 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
 #pragma unroll
         for (int e = 0; e < 16; ++e) tot[i][e] = 0.f;
 
+    // x side with Wo % 4 == 0 (every encoder layer): a micro-tile's 4 output pixels
+    // (p0 % 4 == 0) lie in one output row, so they share (b, oh) and their input
+    // offsets step by stride·C.  (b, oh, ow) of p0 is walked XBK pixels per chunk
+    // (load() is called for t = 0, 1, 2, ... in order) instead of two divisions and
+    // three 32-bit multiplies per pixel (quarter-rate v_mul_lo_u32 / v_mad_u64_u32: the
+    // x-staging waves issued ~1.6x the VALU of the gy-staging ones).
+    constexpr bool xfast = XFAST;   // the host checks Wo % 4 == 0
+    int wb = 0, woh = 0, wow = 0;
+    if (side == 1 && xfast) {
+        const int p = t0 * XBK + 4 * kq;
+        wb = fdiv(p, HoWo, rHoWo);
+        const int rem = p - wb * HoWo;
+        woh = fdiv(rem, a.Wo, rWo);
+        wow = rem - woh * a.Wo;
+    }
+    const int sC = a.stride * a.C;
     auto load = [&](auto side_c, int t, float4 (&V)[4]) {
         constexpr int SIDE = decltype(side_c)::value;
         const int p0 = (t0 + t) * XBK + 4 * kq;
@@ -1267,6 +1283,23 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
             for (int i = 0; i < 4; ++i) {
                 const int p = p0 + i;
                 V[i] = bload(gr, (live && p < a.P) ? (p * a.Cg + m0 + row) * 4 : kBad);
+            }
+        } else if constexpr (xfast) {
+            const int ih = woh * a.stride - a.pad + kh, iw0 = wow * a.stride - a.pad + kw;
+            const bool rowok = live && p0 < a.P && (unsigned)ih < (unsigned)a.H;
+            const int base = ((wb * a.H + ih) * a.W + iw0) * a.C + ci;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const bool ok = rowok && (unsigned)(iw0 + i * a.stride) < (unsigned)a.W;
+                V[i] = bload(xr, ok ? (base + i * sC) * 4 : kBad);
+            }
+            wow += XBK;
+            while (wow >= a.Wo) {
+                wow -= a.Wo;
+                if (++woh == a.Ho) {
+                    woh = 0;
+                    ++wb;
+                }
             }
         } else {
             int b = fdiv(p0, HoWo, rHoWo);
@@ -1325,12 +1358,18 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
             }
     };
     const int lr = lane & 31, h = lane >> 5;
-    auto mma = [&](int buf) {
-        const __bf16* L = lds[buf];
+    auto zero_acc = [&]() {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    };
+    auto fold = [&]() {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) tot[i] += acc[i];
+    };
+    auto mma = [&](int buf) {
+        const __bf16* L = lds[buf];
 #pragma unroll
         for (int s = 0; s < XBK / 16; ++s) {
             bf16x8 fa[TM][3], fb[3];
@@ -1353,8 +1392,6 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[0], acc[i], 0, 0, 0);
             }
         }
-#pragma unroll
-        for (int i = 0; i < TM; ++i) tot[i] += acc[i];
     };
 
     if (wid >= 4) __builtin_amdgcn_s_setprio(1);   // as in conv_x6_kernel
@@ -1372,14 +1409,18 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
         for (int t = 0; t < nchunks; t += 2) {
             load(side_c, t + 2, v0);
             split(v1);
+            zero_acc();
             mma(0);
+            fold();
             asm volatile("" ::: "memory");
             store(side_c, 1);
             __syncthreads();
             if (t + 1 >= nchunks) break;
             load(side_c, t + 3, v1);
             split(v0);
+            zero_acc();
             mma(1);
+            fold();
             asm volatile("" ::: "memory");
             store(side_c, 0);
             __syncthreads();
@@ -1389,10 +1430,14 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
         // waves 2-3 at BMW = 64: multiply only
         __syncthreads();
         for (int t = 0; t < nchunks; t += 2) {
+            zero_acc();
             mma(0);
+            fold();
             __syncthreads();
             if (t + 1 >= nchunks) break;
+            zero_acc();
             mma(1);
+            fold();
             __syncthreads();
         }
     } else if (side == 0) {
@@ -2233,8 +2278,10 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
         else hipLaunchKernelGGL(conv_x6pw_kernel<32>, grid, dim3(576), 0, st, a);
     } else if (use_x6(d, mode) && mode == MODE_WGRAD) {
         const dim3 grid(a.mblocks * a.nblocks * a.splits);
-        if (a.bm == 64) hipLaunchKernelGGL(conv_x6_wgrad_kernel<64>, grid, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL(conv_x6_wgrad_kernel<128>, grid, dim3(512), 0, st, a);
+        const bool xf = (a.Wo & 3) == 0;   // the x-side pixel walk (conv_x6_wgrad_kernel)
+        void (*k)(ConvArgs) = a.bm == 64 ? (xf ? conv_x6_wgrad_kernel<64, true> : conv_x6_wgrad_kernel<64, false>)
+                                         : (xf ? conv_x6_wgrad_kernel<128, true> : conv_x6_wgrad_kernel<128, false>);
+        hipLaunchKernelGGL(k, grid, dim3(512), 0, st, a);
     } else if (use_x6(d, mode)) {
         // B: the weights split into bf16 planes at the front of the workspace, or
         // already split by the caller (MD2_CONV_PRESPLIT: `weight` is the planes)
