@@ -189,7 +189,17 @@ class FlatGradSync:
         self.comm = torch.cuda.Stream(self.flat[0].device) if cuda else None
         self.pending = [dict() for _ in self.buckets]   # bucket -> {param: (grad, stream)}
         self.sent = [False] * len(self.buckets)
-        self.next_send = 0   # buckets go out strictly in index order (see _ready)
+        self.next_send = 0   # position in self.order (see _ready)
+        # send order: index order until calibrated.  At world > 1 the first step sends
+        # every bucket from sync(), in index order, and notes the order the buckets
+        # completed in; rank 0's order is broadcast once there (every rank present, no
+        # backward running, not capturing) and every later step sends in it — a bucket
+        # waits only for the buckets that finished before it on rank 0, not for every
+        # lower index (the pose network's buckets no longer wait behind the depth
+        # network's, nor the reverse)
+        self.order = list(range(len(self.buckets)))
+        self.calibrated = world <= 1
+        self.finished = []
         self.handles = [p.register_post_accumulate_grad_hook(self._ready) for plist in self.buckets for p in plist]
         self.works = []
 
@@ -205,6 +215,7 @@ class FlatGradSync:
         self.sent = [False] * len(self.buckets)
         self.next_send = 0
         self.works = []
+        self.finished = []
 
     def _ready(self, p):
         bi, _ = self.where[p]
@@ -212,13 +223,19 @@ class FlatGradSync:
             return
         stream = torch.cuda.current_stream(p.device) if p.is_cuda else None
         self.pending[bi][p] = (p.grad, stream)
+        if not self.calibrated:   # the calibration step: note the finish order, send from sync()
+            if len(self.pending[bi]) == len(self.buckets[bi]):
+                self.finished.append(bi)
+            return
         # RCCL needs the same collective order on every rank, and autograd's hook order
         # need not be the same everywhere (a parameter without a gradient, another
         # stream finishing first): a complete bucket waits until every bucket before it
-        # has gone out, as DDP's reducer launches its buckets in index order
-        while (self.next_send < len(self.buckets)
-               and len(self.pending[self.next_send]) == len(self.buckets[self.next_send])):
-            self._send(self.next_send)
+        # in self.order has gone out, as DDP's reducer launches its buckets in one order
+        while self.next_send < len(self.order):
+            b = self.order[self.next_send]
+            if len(self.pending[b]) != len(self.buckets[b]):
+                break
+            self._send(b)
             self.next_send += 1
 
     def _send(self, bi):
@@ -242,6 +259,18 @@ class FlatGradSync:
             if self.world > 1:
                 self.works.append(dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
 
+    def _calibrate(self):
+        """Rank 0's bucket finish order of this step (buckets that never completed
+        follow in index order), adopted by every rank: one broadcast, here in sync()."""
+        if self.flat and self.flat[0].is_cuda and torch.cuda.is_current_stream_capturing():
+            return   # not inside a capture: keep index order, try again on an eager step
+        seen = set(self.finished)
+        mine = list(self.finished) + [b for b in range(len(self.buckets)) if b not in seen]
+        box = [mine]
+        dist.broadcast_object_list(box, src=0, group=self.group)
+        self.order = [int(b) for b in box[0]]
+        self.calibrated = True
+
     @staticmethod
     def _fill(views, grads, missing):
         if views:
@@ -256,9 +285,11 @@ class FlatGradSync:
             for buf in self.flat:
                 dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.group)
             return
-        for bi in range(self.next_send, len(self.buckets)):   # in index order
-            self._send(bi)
-        self.next_send = len(self.buckets)
+        for i in range(self.next_send, len(self.order)):   # the rest, in send order
+            self._send(self.order[i])
+        self.next_send = len(self.order)
+        if not self.calibrated:
+            self._calibrate()
         if self.comm is not None:
             torch.cuda.current_stream(self.flat[0].device).wait_stream(self.comm)
         for w in self.works:   # CPU (gloo): the asynchronous all-reduces

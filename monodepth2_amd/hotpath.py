@@ -17,6 +17,7 @@ a ROCm device, otherwise this raises.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
@@ -87,6 +88,28 @@ def _require(t: torch.Tensor, name: str, shape, device, dtypes=(torch.float32,))
         raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
 
 
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def check_src8(src8: torch.Tensor, sources: Sequence[torch.Tensor]) -> None:
+    """The 8-bit contract of `src8` (photometric_loss): every packed channel k equals
+    round(255 * colour) and the colour is exactly k/255.  The kernels trust it (the
+    forward then skips its own exactness flags and reads only the 8-bit copies), so a
+    pipeline that edits the colours after md2_aug_run2 / pack_rgbx must drop
+    color_src8 from the batch.  MD2_CHECK_SRC8=1 runs this on every call (a debug
+    check: one pass over the sources and a host sync)."""
+    for fi, c in enumerate(sources):
+        p = src8[fi].cpu()
+        k = torch.stack([(p >> (8 * ch)) & 255 for ch in range(3)], 1).double()
+        # on the host in float64, as data.pack_rgbx checks (exact k/255 rounded once)
+        want = (k / 255.0).float()
+        got = c.float().cpu()
+        if not torch.equal(want, got):
+            raise ValueError(f"color_src8 frame {fi} does not match the fp32 source colours "
+                             f"({int((want != got).sum())} channels differ): drop color_src8 when the colours change")
+
+
 class Operands:
     """The non-differentiable operands of one call, validated and made contiguous.
 
@@ -129,6 +152,8 @@ class Operands:
                 _require(inv_K[s], f"inv_K[{s}]", (B, 4, 4), device)
                 self.K[s] = K[s].contiguous()
                 self.inv_K[s] = inv_K[s].contiguous()
+        if self.src8 is not None and os.environ.get("MD2_CHECK_SRC8") == "1" and not _capturing():
+            check_src8(self.src8, [self.colors[0][fi] for fi in range(1, S + 1)])
         self.noise = None
         if noise is not None:
             parts = []
@@ -218,8 +243,10 @@ def photometric_loss(cfg: HotPathConfig, disps: Sequence[torch.Tensor], colors, 
     upsampled to the loss resolution (trainer.py:449-455); differentiable.  The
     BCE weighting term (trainer.py:457-459) is the caller's.
     src8: optional (S,B,H,W) int32 8-bit RGBx copies of the source frames at scale 0
-    (data.pack_rgbx / md2_aug_run2; the colours must be exactly k/255 — a contract,
-    not checked): the forward then reads them instead of packing them per call.
+    (data.pack_rgbx / md2_aug_run2): the forward then reads them instead of packing
+    them per call.  Contract (not checked unless MD2_CHECK_SRC8=1, `check_src8`): the
+    same frames as the fp32 source colours, which are exactly k/255 — drop
+    color_src8 from a batch whose colours were edited after it was packed.
     """
     dev = T.device
     if dev.type != "cuda":

@@ -94,3 +94,19 @@ def test_product_path_has_no_cpu_fallback():
     T = torch.eye(4).view(1, 1, 4, 4)
     with pytest.raises(RuntimeError, match="GPU only"):
         photometric_loss(cfg, [torch.rand(1, 1, 32 >> s, 32 >> s) for s in range(4)], None, None, None, T)
+
+
+def test_src8_contract_check():
+    """hotpath.check_src8 (MD2_CHECK_SRC8=1): 8-bit copies that no longer match the
+    fp32 colours are refused (colours edited after packing)."""
+    import torch
+    from monodepth2_amd.data import pack_rgbx
+    from monodepth2_amd.hotpath import check_src8
+    g = torch.Generator().manual_seed(0)
+    cols = [torch.randint(0, 256, (2, 3, 4, 6), generator=g).float() / 255.0 for _ in range(2)]
+    s8 = pack_rgbx(cols)
+    check_src8(s8, cols)
+    edited = [c.clone() for c in cols]
+    edited[1][0, 2, 3, 5] = (edited[1][0, 2, 3, 5] * 255 + 1) % 256 / 255.0
+    with pytest.raises(ValueError, match="frame 1"):
+        check_src8(s8, edited)

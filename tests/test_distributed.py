@@ -189,6 +189,51 @@ def test_flat_sync_sends_buckets_in_index_order():
     assert torch.equal(b4.grad, torch.zeros_like(b4)) and torch.equal(sync.buckets[5][0].grad, torch.ones(4, 4))
 
 
+def _order_worker(rank, world, port, out_dir):
+    """FlatGradSync at world 2 (gloo, CPU): the first step sends from sync() in index
+    order and adopts rank 0's bucket finish order; later steps send in that order on
+    every rank, whatever order their own hooks fire in, and average correctly."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    params = [torch.nn.Parameter(torch.zeros(4, 4)) for _ in range(6)]
+    sync = FlatGradSync([(f"p{i}", p) for i, p in enumerate(params)], world=world, bucket_cap_mb=0)
+    sent = []
+    real_send = sync._send
+    sync._send = lambda bi: (sent.append(bi), real_send(bi))
+    fire = {0: (3, 0, 5, 1, 2), 1: (5, 4, 3, 2, 1, 0)}[rank]   # rank 0: bucket 4 gets no gradient
+    res = {}
+    for step in range(2):
+        sync.zero()
+        sent.clear()
+        for b in fire:
+            p = sync.buckets[b][0]
+            p.grad = torch.full_like(p, float(rank + 1 + b))
+            sync._ready(p)
+        res[f"before_sync_{step}"] = list(sent)
+        sync.sync()
+        res[f"sent_{step}"] = list(sent)
+        res[f"grads_{step}"] = [float(sync.buckets[b][0].grad[0, 0]) for b in range(6)]
+    res["order"] = sync.order
+    torch.save(res, os.path.join(out_dir, f"order_{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_flat_sync_adopts_rank0_finish_order(tmp_path):
+    port = _free_port()
+    mp.spawn(_order_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = (torch.load(os.path.join(tmp_path, f"order_{r}.pt"), weights_only=True) for r in range(2))
+    for r in (r0, r1):
+        assert r["before_sync_0"] == [] and r["sent_0"] == [0, 1, 2, 3, 4, 5]   # calibration step
+        assert r["order"] == [3, 0, 5, 1, 2, 4]                               # rank 0's finish order
+        assert r["sent_1"] == [3, 0, 5, 1, 2, 4]
+    # rank 1's hooks fire 5, 4, 3, ...: nothing goes out before bucket 3 is complete there
+    assert r1["before_sync_1"] == [3, 0, 5, 1, 2, 4][:len(r1["before_sync_1"])]
+    for step in (0, 1):
+        # mean of rank 0 (b + 1, or 0 for bucket 4 without a gradient) and rank 1 (b + 2)
+        want = [((b + 1 if b != 4 else 0) + b + 2) / 2 for b in range(6)]
+        assert r0[f"grads_{step}"] == want and r1[f"grads_{step}"] == want
+
+
 def _autotune_worker(rank, world, port, out_dir):
     """The production conv-choice mechanism under data parallelism, host logic only (the
     candidates are stand-ins with rank-dependent timings: the ranks disagree).  Each
