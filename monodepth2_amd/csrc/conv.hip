@@ -445,10 +445,58 @@ __device__ __forceinline__ void split_store(__bf16* out, int n, int i, float v) 
     out[n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, b) >> 16));
     out[2 * n + i] = __builtin_bit_cast(__bf16, (uint16_t)(__builtin_bit_cast(uint32_t, c) >> 16));
 }
+// A 32 (co) x 32 (ci) tile of one tap, split into the three bf16 planes of the
+// forward layout [co][tap][ci] and (through LDS) of the input-gradient layout
+// [ci][flipped tap][co] / the col layout [tap][ci][co].  With Ci and Co multiples of 4
+// (every x6 convolution) a thread handles 4 consecutive elements along the contiguous
+// index of each layout: one 16-byte load, and per plane one 8-byte store instead of
+// four 2-byte ones (the step's one split launch ran at ~60 % of HBM bandwidth on 2-byte
+// stores).  Same split (split3 = split_store's arithmetic), same bits.
 __device__ __forceinline__ void wsplit_tile(const float* w, __bf16* fw, __bf16* dg, __bf16* cl, int Co, int KT,
                                             int Ci, int tap, int co0, int ci0, float (*tile)[33]) {
-    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
     const int n = Co * KT * Ci;
+    if ((Ci & 3) == 0 && (Co & 3) == 0) {   // block-uniform
+        const int q = threadIdx.x & 7, r = threadIdx.x >> 3;   // 8 quads x 32 rows
+        {
+            const int co = co0 + r, ci = ci0 + 4 * q;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (co < Co && ci < Ci) {   // Ci % 4 == 0: the whole quad is in range
+                const int i = (co * KT + tap) * Ci + ci;
+                v = *(const float4*)(w + i);
+                bf16x4 p0, p1, p2;
+                split3(v, p0, p1, p2);
+                *(bf16x4*)(fw + i) = p0;
+                *(bf16x4*)(fw + n + i) = p1;
+                *(bf16x4*)(fw + 2 * n + i) = p2;
+            }
+            tile[r][4 * q] = v.x;
+            tile[r][4 * q + 1] = v.y;
+            tile[r][4 * q + 2] = v.z;
+            tile[r][4 * q + 3] = v.w;
+        }
+        if (!dg && !cl) return;   // block-uniform
+        __syncthreads();
+        const int ci = ci0 + r, co = co0 + 4 * q;
+        if (ci < Ci && co < Co) {
+            const float4 v = make_float4(tile[4 * q][r], tile[4 * q + 1][r], tile[4 * q + 2][r], tile[4 * q + 3][r]);
+            bf16x4 p0, p1, p2;
+            split3(v, p0, p1, p2);
+            if (dg) {
+                const int i = (ci * KT + (KT - 1 - tap)) * Co + co;
+                *(bf16x4*)(dg + i) = p0;
+                *(bf16x4*)(dg + n + i) = p1;
+                *(bf16x4*)(dg + 2 * n + i) = p2;
+            }
+            if (cl) {   // [(tap, ci)][co], not flipped
+                const int i = (tap * Ci + ci) * Co + co;
+                *(bf16x4*)(cl + i) = p0;
+                *(bf16x4*)(cl + n + i) = p1;
+                *(bf16x4*)(cl + 2 * n + i) = p2;
+            }
+        }
+        return;
+    }
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
 #pragma unroll
     for (int r = ty; r < 32; r += 8) {
         const int co = co0 + r, ci = ci0 + tx;
