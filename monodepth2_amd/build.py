@@ -55,7 +55,7 @@ def needs_build() -> bool:
 # results when another process shared the GPU; tests/test_isa_guard.py
 # keeps that encoding out of the whole library (glue.hip's input normalisation had it
 # too, on an SGPR pair: no SLP there either).
-# md2hot.hip also with LLVM's iterative ILP scheduler: forward 0.1252 -> 0.1240, backward
+# md2hot.hip also with LLVM's iterative ILP scheduler: forward 0.1259 -> 0.1240, backward
 # 0.2426 -> 0.2387 ms (means of three alternated tools/hot_bench.py runs; max-ilp,
 # max-memory-clause, iterative-minreg and iterative-maxocc measured slower or equal).
 FLAGS = {"md2hot.hip": ["-fno-slp-vectorize", "-mllvm", "--amdgpu-sched-strategy=iterative-ilp"],
