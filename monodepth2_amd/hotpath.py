@@ -199,6 +199,10 @@ class _PhotometricLoss(torch.autograd.Function):
         ctx.save_for_backward(T, *(([mask] if mask is not None else []) + list(disps)))
         ctx.cfg, ctx.ops, ctx.seed, ctx.ws, ctx.sel = cfg, ops, seed, ws, sel
         ctx.mark_non_differentiable(sel)
+        # no zero-filled gradient for the (non-differentiable, 1 byte per pixel and scale)
+        # selection map: backward gets None for it — a 5.9 MB fill at B=12 between the
+        # hot path's forward and backward, where both networks wait
+        ctx.set_materialize_grads(False)
         return loss, sel
 
     @staticmethod

@@ -174,6 +174,7 @@ class Trainer:
         # graph keeps the two branches independent.
         self._pose_stream = (torch.cuda.Stream(self.device)
                              if self.device.type == "cuda" and getattr(self.opt, "pose_streams", 1) else None)
+        self._in_step = False   # inside _step_body (compute_losses' logging maps go to the pose stream)
 
         # gradient averaging: DDP (hooks, overlapped with backward) for eager steps, flat
         # buckets + one RCCL all-reduce each (graph-capturable) for --hip_graph
@@ -449,9 +450,23 @@ class Trainer:
         losses = {"loss/{}".format(s): loss_vec[s] for s in range(self.num_scales)}
         losses["loss"] = loss_vec[self.num_scales]
         if not self.opt.disable_automasking:
-            # trainer.py:481-482, all scales in one compare + one cast over the packed map
+            # trainer.py:481-482, all scales in one compare + one cast over the packed map.
+            # Logging-only: inside a training step it runs on the pose stream, which idles
+            # here until the hot path's backward hands it dL/dT, instead of delaying that
+            # backward on the main stream (_step_body joins the pose stream after backward)
             C = self.hot.noise_channels()
-            for s, m in selection_maps(self.hot, sel.gt(C - 1).float()).items():
+            side = self._pose_stream if (self._in_step and self.use_pose_net) else None
+            if side is not None:
+                main = torch.cuda.current_stream(self.device)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    maps = selection_maps(self.hot, sel.gt(C - 1).float())
+                sel.record_stream(side)
+                for m in maps.values():
+                    m.record_stream(main)
+            else:
+                maps = selection_maps(self.hot, sel.gt(C - 1).float())
+            for s, m in maps.items():
                 outputs["identity_selection/{}".format(s)] = m
         return losses
 
@@ -474,6 +489,7 @@ class Trainer:
         bank = conv_ops.plane_bank() if self.device.type == "cuda" and conv_ops.PLANE_BANK else None
         if bank is not None:
             bank.begin_step(self.device)
+        self._in_step = True
         try:
             outputs, losses = self.process_batch(inputs)
             if self.flat_sync is not None:
@@ -481,7 +497,12 @@ class Trainer:
             else:
                 self.model_optimizer.zero_grad(set_to_none=True)
             losses["loss"].backward()
+            if self._pose_stream is not None and self.use_pose_net:
+                # the pose stream's work of this step (its backward, the logging maps of
+                # compute_losses) joined before anything reads it
+                torch.cuda.current_stream(self.device).wait_stream(self._pose_stream)
         finally:
+            self._in_step = False
             if bank is not None:
                 bank.end_step()
         if self.flat_sync is not None:
