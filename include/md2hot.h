@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 20
+#define MD2_ABI_VERSION 21
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -342,6 +342,16 @@ int md2_adam_step(const md2_adam_chunk* table, const int* chunk_start, int npara
 int md2_adam_step_dev(const md2_adam_chunk* table, const int* chunk_start, int nparams, const float* const* grads,
                       const double* lr, double beta1, double beta2, double eps, float* step, float* hyper,
                       void* stream);
+/* The capturable step in parts (ABI v21): md2_adam_hyper advances *step and writes the
+ * two factors to `hyper` (md2_adam_step_dev's first launch); md2_adam_apply_dev updates
+ * the parameters [k_begin, k_end) of the table with them.  Calls over disjoint ranges,
+ * each on a stream ordered after md2_adam_hyper and after its parameters' gradients,
+ * cover the step once (the trainer runs the pose network's parameters on the pose
+ * stream as soon as its backward is done).  grads is indexed like chunk_start. */
+int md2_adam_hyper(const double* lr, double beta1, double beta2, float* step, float* hyper, void* stream);
+int md2_adam_apply_dev(const md2_adam_chunk* table, const int* chunk_start, int k_begin, int k_end,
+                       const float* const* grads, double beta1, double beta2, double eps, const float* hyper,
+                       void* stream);
 
 /*
  * Fused pose producer: transformation_from_parameters

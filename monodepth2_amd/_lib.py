@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -59,7 +59,7 @@ _lib = None
 EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_select_bytes",
            "md2_photometric_fwd", "md2_photometric_bwd", "md2_generate_images", "md2_tiebreak_noise",
            "md2_timing_begin", "md2_timing_end", "md2_timing_calls", "md2_decoder_pad_fwd", "md2_decoder_pad_bwd",
-           "md2_decoder_pad_workspace_bytes", "md2_adam_step", "md2_adam_step_dev", "md2_encoder_input",
+           "md2_decoder_pad_workspace_bytes", "md2_adam_step", "md2_adam_step_dev", "md2_adam_hyper", "md2_adam_apply_dev", "md2_encoder_input",
            "md2_pose_fwd", "md2_pose_bwd", "md2_aug_plan_create", "md2_aug_plan_destroy", "md2_aug_run",
            "md2_bn_workspace_bytes", "md2_bn_fwd", "md2_bn_bwd", "md2_maxpool3s2_fwd", "md2_maxpool3s2_bwd",
            "md2_disp_head_workspace_bytes", "md2_disp_head_fwd", "md2_disp_head_bwd",
@@ -236,6 +236,11 @@ def _declare(L):
     L.md2_adam_step_dev.restype = ctypes.c_int
     L.md2_adam_step_dev.argtypes = [_vp, _vp, ctypes.c_int, _vp, _vp, ctypes.c_double, ctypes.c_double,
                                     ctypes.c_double, _vp, _vp, _vp]
+    L.md2_adam_hyper.restype = ctypes.c_int
+    L.md2_adam_hyper.argtypes = [_vp, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp]
+    L.md2_adam_apply_dev.restype = ctypes.c_int
+    L.md2_adam_apply_dev.argtypes = [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_double, ctypes.c_double,
+                                     ctypes.c_double, _vp, _vp]
     L.md2_decoder_pad_workspace_bytes.restype = ctypes.c_size_t
     L.md2_decoder_pad_workspace_bytes.argtypes = [ctypes.POINTER(PadDesc)]
     L.md2_pose_fwd.restype = ctypes.c_int

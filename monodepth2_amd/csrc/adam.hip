@@ -109,23 +109,38 @@ int md2_adam_step(const md2_adam_chunk* table, const int* chunk_start, int npara
     return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
 }
 
-int md2_adam_step_dev(const md2_adam_chunk* table, const int* chunk_start, int nparams, const float* const* grads,
-                      const double* lr, double beta1, double beta2, double eps, float* step, float* hyper,
-                      void* stream) {
-    if (!table || !chunk_start || !grads || nparams < 0 || !lr || !step || !hyper || !(eps > 0.0))
-        return MD2_ERR_ARG;
+int md2_adam_hyper(const double* lr, double beta1, double beta2, float* step, float* hyper, void* stream) {
+    if (!lr || !step || !hyper) return MD2_ERR_ARG;
     hipLaunchKernelGGL(adam_hyper_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step, lr, beta1, beta2, hyper);
-    for (int k0 = 0; k0 < nparams; k0 += kMaxParams) {
-        const int k1 = k0 + kMaxParams < nparams ? k0 + kMaxParams : nparams;
+    return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
+}
+
+int md2_adam_apply_dev(const md2_adam_chunk* table, const int* chunk_start, int k_begin, int k_end,
+                       const float* const* grads, double beta1, double beta2, double eps, const float* hyper,
+                       void* stream) {
+    if (!table || !chunk_start || !grads || k_begin < 0 || k_end < k_begin || !hyper || !(eps > 0.0))
+        return MD2_ERR_ARG;
+    for (int k0 = k_begin; k0 < k_end; k0 += kMaxParams) {
+        const int k1 = k0 + kMaxParams < k_end ? k0 + kMaxParams : k_end;
         GradPtrs gp = {};
         for (int k = k0; k < k1; ++k) gp.g[k - k0] = grads[k];
         const int c0 = chunk_start[k0], c1 = chunk_start[k1];
         if (c1 <= c0) continue;
         hipLaunchKernelGGL(adam_kernel<true>, dim3(c1 - c0), dim3(kThreads), 0, (hipStream_t)stream, table + c0, k0,
                            gp, (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), 0.f, 1.f,
-                           (float)eps, (const float*)hyper);
+                           (float)eps, hyper);
     }
     return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
+}
+
+int md2_adam_step_dev(const md2_adam_chunk* table, const int* chunk_start, int nparams, const float* const* grads,
+                      const double* lr, double beta1, double beta2, double eps, float* step, float* hyper,
+                      void* stream) {
+    if (!table || !chunk_start || !grads || nparams < 0 || !lr || !step || !hyper || !(eps > 0.0))
+        return MD2_ERR_ARG;
+    const int rc = md2_adam_hyper(lr, beta1, beta2, step, hyper, stream);
+    if (rc != MD2_OK) return rc;
+    return md2_adam_apply_dev(table, chunk_start, 0, nparams, grads, beta1, beta2, eps, hyper, stream);
 }
 
 }  // extern "C"

@@ -44,6 +44,8 @@ class FusedAdam(torch.optim.Adam):
         self._params = None   # the parameter list the table was built for
         self._step_t = None   # on the fast path every state's "step" is this one CPU tensor
         self.rebuilds = 0   # chunk-table uploads (a parameter or moment buffer moved)
+        self._hyper_ev = None   # prepare_step: the step's bias-correction factors are on the device
+        self.split = None       # (side stream, parameters): that tail of the parameters updates there
 
     def state_dict(self):
         """torch's layout, each parameter with its own step tensor (a reference Adam
@@ -162,6 +164,61 @@ class FusedAdam(torch.optim.Adam):
         self._grads = (ctypes.c_void_p * len(params))()
         self.rebuilds += 1
 
+    def prepare_step(self) -> bool:
+        """Capturable form: advance the device step counter and form this step's bias
+        corrections now (md2_adam_hyper, one thread), at the start of a training step, so
+        that `step()` can update part of the parameters on another stream (`split`)
+        without that stream waiting for this one's backward.  False (and nothing done)
+        where the split step does not apply; then `step()` does it all."""
+        if not (self.capturable and self._key is not None and self._step_t is not None and self._group_ok()):
+            return False
+        group = self.param_groups[0]
+        dev = group["params"][0].device
+        if self._hyper is None:
+            self._hyper = torch.empty(2, dtype=torch.float32, device=dev)
+        b1, b2 = group["betas"]
+        _lib.check(_lib.lib().md2_adam_hyper(group["lr"].data_ptr(), float(b1), float(b2), self._step_t.data_ptr(),
+                                             self._hyper.data_ptr(), _lib.stream(dev)), "md2_adam_hyper")
+        self._hyper_ev = torch.cuda.Event()
+        self._hyper_ev.record(torch.cuda.current_stream(dev))
+        return True
+
+    def _undo_prepare(self):
+        """A prepared step that falls back to torch's Adam: its counter goes back (torch
+        advances it itself)."""
+        if self._hyper_ev is not None:
+            self._hyper_ev = None
+            self._step_t.sub_(1)
+
+    def _step_split(self, params, group) -> bool:
+        """The rest of a prepared capturable step: the parameters of `split` (a tail of
+        this step's list) on the split's stream, the others here, both after the
+        factors prepare_step formed; this stream then waits for the split's."""
+        ev, self._hyper_ev = self._hyper_ev, None
+        side, tail = self.split if self.split is not None else (None, ())
+        ids = {id(p) for p in tail}
+        k = len(params)
+        while k > 0 and id(params[k - 1]) in ids:
+            k -= 1
+        if side is None or k == len(params) or any(id(p) in ids for p in params[:k]):
+            k = len(params)   # no contiguous tail: everything here
+        b1, b2 = group["betas"]
+        L = _lib.lib()
+        dev = params[0].device
+        cur = torch.cuda.current_stream(dev)
+        cur.wait_event(ev)
+        if k < len(params):
+            side.wait_event(ev)
+            _lib.check(L.md2_adam_apply_dev(self._table.data_ptr(), self._starts, k, len(params), self._grads,
+                                            float(b1), float(b2), float(group["eps"]), self._hyper.data_ptr(),
+                                            ctypes.c_void_p(side.cuda_stream)), "md2_adam_apply_dev")
+        _lib.check(L.md2_adam_apply_dev(self._table.data_ptr(), self._starts, 0, k, self._grads, float(b1),
+                                        float(b2), float(group["eps"]), self._hyper.data_ptr(), _lib.stream(dev)),
+                   "md2_adam_apply_dev")
+        if k < len(params):
+            cur.wait_stream(side)
+        return True
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -172,6 +229,7 @@ class FusedAdam(torch.optim.Adam):
         params = [p for p in group["params"] if p.grad is not None]
         fast = self._key is not None and self._fast_ok(params)
         if not fast and not self._eligible():
+            self._undo_prepare()
             self._key = None
             self._unshare_steps()
             return super().step()
@@ -192,6 +250,7 @@ class FusedAdam(torch.optim.Adam):
                 if (len({float(st["step"]) for st in states}) != 1
                         or any(st["exp_avg"].stride() != p.stride() or st["exp_avg_sq"].stride() != p.stride()
                                for p, st in zip(params, states))):
+                    self._undo_prepare()
                     self._key = None
                     self._unshare_steps()
                     return super().step()   # mixed step counts / layouts (e.g. a loaded partial state)
@@ -215,6 +274,16 @@ class FusedAdam(torch.optim.Adam):
         b1, b2 = group["betas"]
         for k, p in enumerate(params):
             self._grads[k] = p.grad.data_ptr()
+        if self.capturable and self._hyper_ev is not None:
+            if fast:   # the step prepared at its start (prepare_step): the update alone, split
+                self._step_split(params, group)
+                return loss
+            self._hyper_ev = None   # the table changed: prepare_step already advanced the counter
+            rc = _lib.lib().md2_adam_apply_dev(self._table.data_ptr(), self._starts, 0, len(params), self._grads,
+                                               float(b1), float(b2), float(group["eps"]), self._hyper.data_ptr(),
+                                               _lib.stream(params[0].device))
+            _lib.check(rc, "md2_adam_apply_dev")
+            return loss
         if self.capturable:
             # the kernel launch advances the device step counter itself
             if self._hyper is None:

@@ -208,8 +208,20 @@ class Trainer:
         if self.device.type == "cuda":
             self.model_optimizer = FusedAdam(self.parameters_to_train, self.opt.learning_rate,
                                              capturable=self.use_graph)
+            if (self.use_graph and world_size == 1 and self.flat_sync is None and self._pose_stream is not None
+                    and self.use_pose_net and self.opt.pose_model_type == "separate_resnet"
+                    and os.environ.get("MD2_ADAM_SPLIT", "1") != "0"):
+                # one GPU (no gradient averaging between the backward and the update): the
+                # pose networks' parameters — the tail of parameters_to_train — update on
+                # the stream that produced their gradients.  Not with FlatGradSync: its
+                # buckets are filled on the communication stream, which only the main
+                # stream joins (sync())
+                pose_params = [p for n in ("pose_encoder", "pose") if n in self.models
+                               for p in self.models[n].parameters()]
+                self.model_optimizer.split = (self._pose_stream, pose_params)
         else:
             self.model_optimizer = optim.Adam(self.parameters_to_train, self.opt.learning_rate)
+        self._adam_split = getattr(self.model_optimizer, "split", None) is not None
         self.model_lr_scheduler = optim.lr_scheduler.StepLR(self.model_optimizer, self.opt.scheduler_step_size, 0.1)
         if self.opt.load_weights_folder is not None:
             self.load_model()
@@ -490,6 +502,11 @@ class Trainer:
         if bank is not None:
             bank.begin_step(self.device)
         self._in_step = True
+        if self._adam_split:
+            # the optimizer's step counter and bias corrections first, so that the pose
+            # network's parameters update on the pose stream as soon as its backward is
+            # done, while the depth network's backward still runs (FusedAdam.split)
+            self.model_optimizer.prepare_step()
         try:
             outputs, losses = self.process_batch(inputs)
             if self.flat_sync is not None:

@@ -94,3 +94,37 @@ def test_fused_adam_shared_step_roundtrips_through_torch_adam():
     oc.load_state_dict(sd)   # in memory: the step tensors arrive aliased
     steps = [s["step"] for s in oc.state.values()]
     assert len({id(t) for t in steps}) == len(steps)
+
+
+def test_fused_adam_split_step_equals_single_launch():
+    """The split capturable step (prepare_step at the start of a training step, then a
+    tail of the parameters updated on another stream, FusedAdam.split) gives the
+    parameters and moments of the one-launch capturable step bit for bit, including
+    across an lr edit and on the first step (no table yet: prepare_step declines)."""
+    pa, pb = _params(4), _params(4)
+    oa = FusedAdam(pa, lr=1e-3, capturable=True)
+    ob = FusedAdam(pb, lr=1e-3, capturable=True)
+    side = torch.cuda.Stream()
+    oa.split = (side, pa[3:])
+    g = torch.Generator(device="cuda").manual_seed(5)
+    prepared = []
+    for step in range(5):
+        prepared.append(oa.prepare_step())
+        for a, b in zip(pa, pb):
+            gr = torch.randn(a.shape, device="cuda", generator=g)
+            if a.dim() == 4 and a.is_contiguous(memory_format=torch.channels_last):
+                gr = gr.contiguous(memory_format=torch.channels_last)
+            a.grad = gr.clone()
+            b.grad = gr.clone()
+        oa.step()
+        ob.step()
+        if step == 2:
+            for o in (oa, ob):
+                o.param_groups[0]["lr"].fill_(5e-4)
+    torch.cuda.synchronize()
+    assert prepared == [False, True, True, True, True]
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
+        assert torch.equal(oa.state[a]["exp_avg"], ob.state[b]["exp_avg"])
+        assert torch.equal(oa.state[a]["exp_avg_sq"], ob.state[b]["exp_avg_sq"])
+        assert float(oa.state[a]["step"]) == float(ob.state[b]["step"]) == 5.0
