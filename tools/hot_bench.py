@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--src", type=int, default=2)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--dump", default=None, help="save one seeded step's loss and gradients here (torch.save): "
+                    "bitwise A/B of builds run with MD2_LIB")
     ap.add_argument("--no-ssim", action="store_true")
     ap.add_argument("--eight-bit", action="store_true", help="colours quantised to k/255 (loader output)")
     ap.add_argument("--src8", action="store_true", help="with --eight-bit: hand the sources' 8-bit copies "
@@ -79,6 +81,13 @@ def main():
                       "step_ms": round(total, 4), "fwd_GBs": round(fwd_bytes / fwd / 1e6, 1),
                       "bwd_GBs": round(bwd_bytes / bwd / 1e6, 1),
                       "hot_path_img_per_s": round(B / total * 1e3, 1)}), flush=True)
+    if a.dump:
+        for d in disps:
+            d.grad = None
+        T.grad = None
+        loss, _ = photometric_loss(cfg, disps, colors, K, iK, T, seed=7, src8=src8)
+        loss[4].backward()
+        torch.save({"loss": loss.detach().cpu(), "disps": [d.grad.cpu() for d in disps], "T": T.grad.cpu()}, a.dump)
 
 
 if __name__ == "__main__":
