@@ -58,7 +58,11 @@ def needs_build() -> bool:
 # md2hot.hip also with LLVM's iterative ILP scheduler: forward 0.1259 -> 0.1240, backward
 # 0.2426 -> 0.2387 ms (means of three alternated tools/hot_bench.py runs; max-ilp,
 # max-memory-clause, iterative-minreg and iterative-maxocc measured slower or equal).
+# conv.hip (the x6 GEMMs) with LLVM's max-ILP scheduler: captured step 11.65 -> 11.54 ms
+# (three alternated runs each, pinned convolution choices; iterative-ilp equal to the
+# default there).
 FLAGS = {"md2hot.hip": ["-fno-slp-vectorize", "-mllvm", "--amdgpu-sched-strategy=iterative-ilp"],
+         "conv.hip": ["-mllvm", "--amdgpu-sched-strategy=max-ilp"],
          "disphead.hip": ["-fno-slp-vectorize"], "glue.hip": ["-fno-slp-vectorize"]}
 
 
