@@ -60,9 +60,12 @@ def needs_build() -> bool:
 # max-memory-clause, iterative-minreg and iterative-maxocc measured slower or equal).
 # conv.hip (the x6 GEMMs) with LLVM's max-ILP scheduler: captured step 11.65 -> 11.54 ms
 # (three alternated runs each, pinned convolution choices; iterative-ilp equal to the
-# default there).
+# default there); bnorm.hip + decoder.hip with it too: 11.721 -> 11.693 ms (three
+# alternated pairs, every pair faster); stem.hip and direct.hip were slower with it.
 FLAGS = {"md2hot.hip": ["-fno-slp-vectorize", "-mllvm", "--amdgpu-sched-strategy=iterative-ilp"],
          "conv.hip": ["-mllvm", "--amdgpu-sched-strategy=max-ilp"],
+         "bnorm.hip": ["-mllvm", "--amdgpu-sched-strategy=max-ilp"],
+         "decoder.hip": ["-mllvm", "--amdgpu-sched-strategy=max-ilp"],
          "disphead.hip": ["-fno-slp-vectorize"], "glue.hip": ["-fno-slp-vectorize"]}
 
 

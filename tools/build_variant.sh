@@ -12,7 +12,7 @@ obj=abx/$name/$(basename ${SRC%.hip}).o
 # the in-tree build flags of md2hot.hip (monodepth2_amd/build.py FLAGS)
 slp=""
 [ "$(basename $SRC)" = "md2hot.hip" ] && slp="-fno-slp-vectorize -mllvm --amdgpu-sched-strategy=iterative-ilp"
-[ "$(basename $SRC)" = "conv.hip" ] && slp="-mllvm --amdgpu-sched-strategy=max-ilp"
+case "$(basename $SRC)" in conv.hip|bnorm.hip|decoder.hip) slp="-mllvm --amdgpu-sched-strategy=max-ilp";; esac
 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -Iinclude $slp "$@" -c $SRC -o $obj
 others=$(ls monodepth2_amd/csrc/obj/*.o | grep -v "/$(basename ${SRC%.hip}).o$")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared -o abx/$name/libmd2hot.so $obj $others
