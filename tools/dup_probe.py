@@ -28,6 +28,10 @@ KINDS = {
     "conv_fwd": ("conv.hip", r"    return run\(d, MODE_FWD,.*?;\n"),
     "conv_dgrad": ("conv.hip", r"    return run\(d, MODE_DGRAD,.*?;\n"),
     "conv_wgrad": ("conv.hip", r"    return run\(d, MODE_WGRAD,.*?;\n"),
+    "pad_fwd": ("decoder.hip", r"hipLaunchKernelGGL\(k, dim3\(grid_for\(n / 4\)\).*?;\n"),
+    "pad_bwd": ("decoder.hip", r"hipLaunchKernelGGL\(k, dim3\(G\).*?;\n"),
+    "pool": ("pool.hip", r"hipLaunchKernelGGL\(k, dim3\((?:grid_for\(n\)|\(p\.W).*?;\n"),
+    "photo_bwd": ("md2hot.hip", r"hipLaunchKernelGGL\(\(photo_bwd_kernel<NS, SSIM, MASK>\).*?;\n"),
 }
 
 
