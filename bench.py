@@ -31,6 +31,10 @@ Extra fields:
                   the reference), a bounded sample of steps at batch 4 (configs[0]).
   loss_delta_vs_oracle — |loss_GPU - loss_oracle| on identical inputs, weights and
                   tie-break noise (first step).
+  eager_aten_hot_path_ms — configs[1]'s own comparison: the reference's hot path
+                  (generate_images_pred + compute_losses, trainer.py:341-496) as eager
+                  ATen ops on the same GPU, fwd+bwd on the step's own outputs; the
+                  ratio to the HIP hot path is context, never the target.
 """
 from __future__ import annotations
 
@@ -88,7 +92,7 @@ def pmc_traffic(args, S, timeout=150):
                "--output-format", "csv", "--", sys.executable, os.path.join(REPO, "bench.py"),
                "--batch", str(args.batch), "--height", str(args.height), "--width", str(args.width),
                "--num_layers", str(args.num_layers), "--amp", args.amp, "--steps", "3", "--warmup", "2",
-               "--no-cpu-baseline", "--no-parity", "--pmc", "0", "--no-conv-roofline", "--graph", "0",
+               "--no-cpu-baseline", "--no-parity", "--pmc", "0", "--no-conv-roofline", "--no-eager-aten", "--graph", "0",
                "--src8", "0"] + \
               (["--stereo"] if args.stereo else [])
         env = dict(os.environ, TMPDIR="/tmp")
@@ -148,6 +152,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-conv-roofline", action="store_true")
+    ap.add_argument("--no-eager-aten", action="store_true",
+                    help="skip timing the reference's eager ATen hot path beside the HIP one")
     ap.add_argument("--pmc", type=int, default=1, help="measure the hot path's HBM traffic with rocprofv3 "
                     "PMC passes in this run (rank 0, N=1)")
     ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen exhaustive find per conv shape")
@@ -233,6 +239,70 @@ def time_hot_kernels(trainer, batch, n=10, src8=True):
             loss, _ = photometric_loss(hot, disps, colors, K, iK, T, seed=2 + i, src8=s8)
             loss[hot.num_scales].backward()
     return kt
+
+
+def eager_aten_hot_path(trainer, batch, n=5):
+    """configs[1]'s own comparison ("HIP warp+SSIM kernels vs PyTorch-ROCm
+    grid_sample"): the reference's hot path as the reference writes it —
+    generate_images_pred + compute_losses (trainer.py:341-496): per scale the bilinear
+    upsample, disp_to_depth, BackprojectDepth / Project3D (bmm), F.grid_sample with
+    border padding, the 3x3 SSIM of layers.py:218-248 + L1 for every reprojected AND
+    every identity candidate (recomputed per scale, trainer.py:432-439), the 1e-5 randn
+    tie-break, cat + torch.min, the mean-normalised smoothness — forward and backward to
+    the disparities and the transforms, eagerly on PyTorch-ROCm (ATen's kernels), on the
+    same GPU, the step's own network outputs, intrinsics and colours.  The layer objects
+    are this package's restatement of the reference's layers.py (same signatures, same
+    ATen ops), not the fused path.  HIP-event timed on torch's current stream (every op
+    runs there); returns ms per fwd+bwd."""
+    import torch.nn.functional as F
+    from monodepth2_amd.layers import SSIM, BackprojectDepth, Project3D, disp_to_depth, get_smooth_loss
+    o = trainer.opt
+    with torch.no_grad():
+        outputs = trainer.nets(trainer, batch)
+    dev = batch[("color", 0, 0)].device
+    B = batch[("color", 0, 0)].shape[0]
+    nsc = trainer.num_scales
+    ssim = SSIM().to(dev)
+    backproject = BackprojectDepth(B, o.height, o.width).to(dev)
+    project = Project3D(B, o.height, o.width).to(dev)
+    T = trainer._stacked_T(batch, outputs).detach().requires_grad_(True)
+    disps = [outputs[("disp", s)].detach().float().requires_grad_(True) for s in range(nsc)]
+    srcs = trainer.src_frames
+
+    def reproj_loss(pred, target):                                     # trainer.py:393-405
+        l1 = (target - pred).abs().mean(1, True)
+        return 0.85 * ssim(pred, target).mean(1, True) + 0.15 * l1
+
+    def fwd_bwd():
+        total = 0
+        target = batch[("color", 0, 0)]
+        for s in range(nsc):
+            disp = F.interpolate(disps[s], [o.height, o.width], mode="bilinear", align_corners=False)
+            _, depth = disp_to_depth(disp, o.min_depth, o.max_depth)  # trainer.py:350-354
+            reproj = []
+            for i, f in enumerate(srcs):                               # trainer.py:358-387
+                pix = project(backproject(depth, batch[("inv_K", 0)]), batch[("K", 0)], T[i])
+                warped = F.grid_sample(batch[("color", f, 0)], pix, padding_mode="border", align_corners=False)
+                reproj.append(reproj_loss(warped, target))
+            ident = torch.cat([reproj_loss(batch[("color", f, 0)], target) for f in srcs], 1)
+            ident = ident + torch.randn(ident.shape, device=dev) * 0.00001   # trainer.py:468-469
+            to_opt, _ = torch.min(torch.cat((ident, torch.cat(reproj, 1)), 1), dim=1)
+            loss = to_opt.mean()
+            norm = disps[s] / (disps[s].mean(2, True).mean(3, True) + 1e-7)  # trainer.py:486-490
+            loss = loss + o.disparity_smoothness * get_smooth_loss(norm, batch[("color", 0, s)]) / (2 ** s)
+            total = total + loss
+        (total / nsc).backward()
+
+    for _ in range(2):
+        fwd_bwd()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fwd_bwd()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n
 
 
 def conv_mfma_roofline(device):
@@ -349,7 +419,13 @@ def main():
 
     if args.graph < 0:
         args.graph = 1 if world == 1 else 0
-    trainer = make_trainer(args, device, rank, world)
+    try:
+        trainer = make_trainer(args, device, rank, world)
+    except ValueError as e:   # e.g. --graph 1 at N > 1 on a non-RCCL backend (Trainer refuses it)
+        log(f"cannot run this configuration: {e}")
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(2)
     frame_ids = trainer.opt.frame_ids
     # colours as the reference's loader delivers them: uint8 frames through to_tensor,
     # i.e. exactly k/255 (datasets/mono_dataset.py:199-200)
@@ -492,6 +568,10 @@ def main():
         log(f"timed: {1e3 * dt / args.steps:.2f} ms/step, hot path {hot_ms:.3f} ms (fwd {fcall:.3f}, bwd {bcall:.3f};"
             f" photo_bwd {bwd_ms:.3f}), {tfs:.2f} TF = {valu_frac:.3f} of VALU peak, {gbs:.0f} GB/s, "
             f"adam table uploads {getattr(trainer.model_optimizer, 'rebuilds', '-')}")
+        eager_ms = None
+        if not args.no_eager_aten:
+            eager_ms = eager_aten_hot_path(trainer, batch)
+            log(f"eager ATen hot path (reference formulation): {eager_ms:.3f} ms fwd+bwd vs HIP {hot_ms:.3f} ms")
         conv_roof = None
         if not args.no_conv_roofline:
             conv_roof = conv_mfma_roofline(device)
@@ -516,6 +596,15 @@ def main():
                            "parallelism": f"dp{world}",
                            "step": "hipgraph replay" if trainer.graph is not None else "eager"},
                 "roofline": roof, "conv_roofline": conv_roof, "cpu_baseline": cpu,
+                "eager_aten_hot_path_ms": round(eager_ms, 4) if eager_ms is not None else None,
+                "eager_aten_vs_hip_hot_path": ({
+                    "eager_ms": round(eager_ms, 4), "hip_ms": round(hot_ms, 5),
+                    "ratio": round(eager_ms / hot_ms, 2),
+                    "what": "configs[1]'s comparison, context only (never the target): the reference's "
+                            "generate_images_pred + compute_losses (trainer.py:341-496) as ATen ops "
+                            "(grid_sample, avg_pool SSIM, min, smoothness) fwd+bwd on PyTorch-ROCm vs the HIP "
+                            "hot path (roofline.avg_ms_per_step), same GPU, same run, same B=%d inputs, the "
+                            "step's own disparities and transforms" % B} if eager_ms is not None else None),
                 "loss_delta_vs_oracle": delta, "final_loss": round(final_loss, 6),
                 "host_enqueue_ms_per_step": round(host_ms, 3)}
         print(json.dumps(line), flush=True)

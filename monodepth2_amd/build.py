@@ -36,13 +36,29 @@ def needs_build() -> bool:
                                                        os.path.join(CSRC, "md2_bf16.h")]
     if any(os.path.getmtime(d) > t for d in deps):
         return True
-    try:   # per-source flags changed (they are part of the build id, not of any mtime)
-        import ctypes
-        lib = ctypes.CDLL(LIB_PATH)
-        lib.md2_build_id.restype = ctypes.c_char_p
-        return lib.md2_build_id().decode() != source_hash()
+    # per-source flags changed (they are part of the build id, not of any mtime).  The
+    # id is read from the file's bytes, NOT by loading the library: a dlopen here would
+    # pin this copy in the process, and after a rebuild os.replace()s the file a later
+    # _lib.lib() would get the stale mapping back from dlopen's cache
+    return built_id(LIB_PATH) != source_hash()
+
+
+def built_id(path: str):
+    """The MD2_BUILD_ID baked into a built library (glue.hip stores it behind a marker
+    string), read from the file without loading it; None if absent."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
     except OSError:
-        return True
+        return None
+    i = data.find(BUILD_ID_MARKER)
+    if i < 0:
+        return None
+    i += len(BUILD_ID_MARKER)
+    return data[i:i + 16].decode("ascii", errors="replace")
+
+
+BUILD_ID_MARKER = b"md2-build-id:"
 
 
 # Per-source extra flags.  md2hot.hip: no SLP vectorisation — packed-f32 VALU

@@ -395,6 +395,7 @@ def clear_choices():
     _times.clear()
     _names.clear()
     _nondet.clear()
+    _agreed_keys.clear()
 
 
 _names: Dict[tuple, list] = {}    # (op, shape) -> candidate names, in candidate order
@@ -493,23 +494,40 @@ def _fastest(op: str, key: tuple, cands, names=None) -> int:
     return _choice[k]
 
 
+_agreed_keys: set = set()   # shapes whose choice every rank already holds (agree_choices)
+
+
+def new_choices_since_agree() -> int:
+    """Shapes this rank has chosen a kernel for since the last agree_choices."""
+    return sum(1 for k in _choice if k not in _agreed_keys)
+
+
 def agree_choices(group=None) -> int:
-    """Under data parallelism, every rank adopts rank 0's per-shape choices, so the
-    replicas run the same kernels (the same rounding) from here on.  ONE collective
-    (a broadcast of rank 0's table), to be called where every rank is present and none
-    is inside a forward or backward: the Trainer calls it after its first training step
-    (eager) or after the capture's warm-up steps (hipGraph).  Shapes rank 0 has timed
-    and this rank has not seen yet are pinned to rank 0's choice for when they appear.
-    Returns how many of this rank's choices changed."""
+    """Under data parallelism, every rank adopts ONE per-shape table, so the replicas run
+    the same kernels (the same rounding) from here on.  The table is the union of every
+    rank's choices: a shape rank 0 has chosen for keeps rank 0's choice, a shape only
+    other ranks have met keeps the lowest such rank's choice.  ONE collective (an
+    all_gather of the ranks' tables; every rank forms the same union from it), to be
+    called where every rank is present and none is inside a forward or backward: the
+    Trainer calls it after its first training step (eager) or after the capture's
+    warm-up steps (hipGraph), and again at the end of every epoch (run_epoch) so that
+    shapes first met later (another batch shape, an evaluation on every rank) line up
+    too.  Shapes this rank has not met yet are pinned for when they appear.  Returns
+    how many of this rank's choices changed."""
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1):
         return 0
     mine = {k: _names[k][i] for k, i in _choice.items() if k in _names}
-    box = [mine if dist.get_rank() == 0 else None]
-    dist.broadcast_object_list(box, src=0, group=group)
+    tables = [None] * dist.get_world_size(group)
+    dist.all_gather_object(tables, mine, group=group)
+    union = {}
+    for t in tables:                      # rank order: the lowest rank that met a shape wins
+        for k, name in t.items():
+            union.setdefault(k, name)
     changed = 0
-    for k, name in box[0].items():
+    for k, name in union.items():
         _pinned[k] = name
+        _agreed_keys.add(k)
         names = _names.get(k)
         if names is not None and name in names:
             i = names.index(name)

@@ -86,8 +86,10 @@ __global__ __launch_bounds__(kThreads) void encoder_input_v4_kernel(InputArgs a)
 
 extern "C" {
 
-// the source hash monodepth2_amd/build.py bakes in (see md2hot.h)
-const char* md2_build_id(void) { return MD2_BUILD_ID; }
+// the source hash monodepth2_amd/build.py bakes in (see md2hot.h), stored behind a
+// marker so that build.py can read it from the file without loading the library
+static const char kBuildIdTagged[] = "md2-build-id:" MD2_BUILD_ID;
+const char* md2_build_id(void) { return kBuildIdTagged + 13; }
 
 int md2_encoder_input(int groups, int batch, int slots, int height, int width, const float* const* src, float mean,
                       float std_, float* out, void* stream) {

@@ -147,7 +147,12 @@ class FlatGradSync:
     events, so it can sit inside a captured hipGraph of the whole training step.
     Parameters that never get a gradient (the encoders' fc heads) are left out.
     `overlap=False`: the round-2 form (views of pre-zeroed buckets, one all-reduce per
-    bucket after the backward), kept for comparison."""
+    bucket after the backward), kept for comparison.
+
+    The send order is calibrated on the first step at world > 1 (see `order` below):
+    that step sends every bucket from sync(), after the backward, so it has no overlap.
+    `recalibrate()` starts that over (the Trainer calls it before every capture's
+    warm-up, so a re-capture or a changed stream layout measures its own order)."""
 
     def __init__(self, named_params, world: int, group=None, bucket_cap_mb: int = BUCKET_CAP_MB,
                  overlap: bool = True):
@@ -202,6 +207,14 @@ class FlatGradSync:
         self.finished = []
         self.handles = [p.register_post_accumulate_grad_hook(self._ready) for plist in self.buckets for p in plist]
         self.works = []
+
+    def recalibrate(self):
+        """Forget the adopted send order: the next step (at world > 1) sends in index
+        order from sync() and measures the finish order again."""
+        if self.overlap:
+            self.order = list(range(len(self.buckets)))
+            self.calibrated = self.world <= 1
+            self.finished = []
 
     def zero(self):
         if not self.overlap:

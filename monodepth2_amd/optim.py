@@ -267,10 +267,13 @@ class FusedAdam(torch.optim.Adam):
         if not fast:
             # a parameter without a gradient this step keeps its own counter (torch's
             # Adam leaves its step alone)
+            # (a step prepared at its start has already advanced the shared counter:
+            # such a parameter keeps the value from before this step)
+            prepared = self.capturable and self._hyper_ev is not None
             live = {id(st) for st in states}
             for st in self.state.values():
                 if id(st) not in live and st.get("step") is self._step_t:
-                    st["step"] = self._step_t.clone()
+                    st["step"] = self._step_t.clone().sub_(1) if prepared else self._step_t.clone()
         b1, b2 = group["betas"]
         for k, p in enumerate(params):
             self._grads[k] = p.grad.data_ptr()

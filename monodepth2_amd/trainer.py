@@ -92,6 +92,23 @@ def posecnn_transforms(disps, axisangle, translation, src_frames, stereo_T, heig
     return torch.stack(per_scale, 0)
 
 
+def _check_graph_backend(hip_graph: bool, world_size: int) -> None:
+    """A captured step at world size > 1 holds the gradient all-reduce inside the
+    hipGraph (FlatGradSync on its communication stream), which only RCCL ("nccl") can
+    enqueue under stream capture: gloo's host-side all-reduce raises
+    hipErrorStreamCaptureUnsupported in the middle of the capture.  Refuse the
+    combination up front, before any network is built (trainer.py:201-210 is the
+    reference's single-process step this distributes)."""
+    if not hip_graph or world_size <= 1:
+        return
+    backend = dist.get_backend() if (dist.is_available() and dist.is_initialized()) else None
+    if backend != "nccl":
+        raise ValueError(
+            f"--hip_graph at world size {world_size} needs the RCCL process group (backend 'nccl'); "
+            f"got {backend!r}: a {backend} all-reduce cannot be captured into a hipGraph.  "
+            "Run the eager step (hip_graph off / bench.py --graph 0) on this backend.")
+
+
 class _Networks(nn.Module):
     """All trainable networks behind one module so DDP sees a single graph."""
 
@@ -113,6 +130,7 @@ class Trainer:
             raise RuntimeError("the MI355X build has no CPU training path: the hot path is HIP-only")
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.rank, self.world_size = rank, world_size
+        _check_graph_backend(bool(getattr(self.opt, "hip_graph", False)), world_size)
 
         self.num_scales = len(self.opt.scales)
         if list(self.opt.scales) != list(range(self.num_scales)):
@@ -555,6 +573,8 @@ class Trainer:
         self.static_inputs = {k: v.to(self.device).clone() for k, v in inputs.items()}
         self.seed_tensor = torch.zeros(1, dtype=torch.int64, device=self.device)
         snap = self._training_state()
+        if self.flat_sync is not None:
+            self.flat_sync.recalibrate()   # the warm-up's first step measures the send order
         side = torch.cuda.Stream(self.device)
         self.graph_stream = side   # an eager step after the capture runs here too (eager_step)
         side.wait_stream(torch.cuda.current_stream(self.device))
@@ -579,12 +599,15 @@ class Trainer:
         if dot:
             self.graph.debug_dump(dot)
 
-    def _agree_conv_choices(self):
-        """Once, after the first step's convolution autotune (conv_ops._fastest times its
-        candidates on each rank without any collective): every rank adopts rank 0's
-        per-shape choices (conv_ops.agree_choices, one broadcast), at a point where every
-        rank is present and none is inside a forward or backward."""
-        if self.world_size > 1 and not self._choices_agreed:
+    def _agree_conv_choices(self, again: bool = False):
+        """After the first step's convolution autotune (conv_ops._fastest times its
+        candidates on each rank without any collective): every rank adopts one per-shape
+        table (conv_ops.agree_choices: the union of the ranks' choices, rank 0's first),
+        at a point where every rank is present and none is inside a forward or backward.
+        `again` (the end of every epoch, run_epoch): once more, for shapes any rank met
+        after the first agreement — one all_gather of small tables, never inside a
+        capture."""
+        if self.world_size > 1 and (again or not self._choices_agreed):
             conv_ops.agree_choices()
             self._choices_agreed = True
 
@@ -656,6 +679,7 @@ class Trainer:
                 self.log_time(batch_idx, time.time() - t0, loss)
         self.model_lr_scheduler.step()
         self.epoch += 1
+        self._agree_conv_choices(again=True)
 
     def compute_depth_losses(self, inputs, outputs, losses):
         """trainer.py:498-526 (monitoring only)."""

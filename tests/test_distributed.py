@@ -316,3 +316,83 @@ def test_conv_autotune_no_collective_then_rank0_table(tmp_path):
     for r in (r0, r1):
         assert any("1" in k for k in r["nondet"])
         assert r["table"]["fwd (1,)"] not in r["nondet"][next(k for k in r["nondet"] if "1" in k)]
+
+
+def _union_worker(rank, world, port, out_dir):
+    """agree_choices forms ONE table from every rank's choices: rank 0's choice where it
+    has one, otherwise the lowest rank that met the shape.  A shape only rank 1 has met
+    is pinned on rank 0 to rank 1's choice for when rank 0 meets it; a second agreement
+    (run_epoch's) picks up shapes first met after the first one."""
+    from monodepth2_amd import conv_ops
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    conv_ops.clear_choices()
+    conv_ops._time_candidate = lambda fn: fn()
+    names = ["x6", "x6_256", "f32mfma", "miopen"]
+
+    def cands(shape):
+        # rank- and shape-dependent fastest candidate: the ranks disagree on every shape
+        return [(lambda i=i: (1.0 + 0.1 * ((i + shape + 2 * rank) % 3), True)) for i in range(4)]
+
+    def pick(shape):
+        return names[conv_ops._fastest("fwd", (shape,), cands(shape), names)]
+
+    met = {0: [0, 1], 1: [1, 7]}[rank]
+    own = {sh: pick(sh) for sh in met}
+    res = {"own": own, "new_before": conv_ops.new_choices_since_agree()}
+    res["changed1"] = conv_ops.agree_choices()
+    res["new_after"] = conv_ops.new_choices_since_agree()
+    res["seven"] = pick(7)                      # rank 0 meets rank 1's shape now: pinned
+    later = 11 if rank == 1 else None           # a shape rank 1 alone meets after the agreement
+    if later is not None:
+        res["eleven_own"] = pick(later)
+    res["changed2"] = conv_ops.agree_choices()
+    res["eleven"] = pick(11)
+    res["table"] = {str(k): conv_ops._names[k][i] for k, i in conv_ops._choice.items()}
+    res["pinned"] = {str(k): v for k, v in conv_ops._pinned.items()}
+    torch.save(res, os.path.join(out_dir, f"union_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_agree_choices_takes_the_union_of_every_ranks_shapes(tmp_path):
+    port = _free_port()
+    mp.spawn(_union_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = (torch.load(os.path.join(tmp_path, f"union_{r}.pt"), weights_only=True) for r in range(2))
+    assert r0["new_before"] == 2 and r1["new_before"] == 2
+    assert r0["new_after"] == 0 and r1["new_after"] == 0
+    assert r0["own"][1] != r1["own"][1]                    # the ranks timed shape 1 differently
+    assert r0["pinned"] == r1["pinned"]                    # one table on every rank
+    common = set(r0["table"]) & set(r1["table"])
+    assert common == {"('fwd', 1)", "('fwd', 7)", "('fwd', 11)"}
+    assert all(r0["table"][k] == r1["table"][k] for k in common)
+    assert r1["pinned"]["('fwd', 0)"] == r0["own"][0]      # rank 0's shape pinned on rank 1
+    assert r1["table"]["('fwd', 1)"] == r0["own"][1]       # rank 0's choice wins a shared shape
+    assert r0["seven"] == r1["own"][7] == r1["seven"]      # rank 1's shape pinned on rank 0
+    assert r0["eleven"] == r1["eleven_own"] == r1["eleven"]   # the second agreement
+    assert r0["changed1"] == 0 and r1["changed1"] == 1
+
+
+def _graph_guard_worker(rank, world, port, out_dir):
+    """Trainer(hip_graph=True) at world size 2 on gloo: refused at construction with a
+    message naming the backend, before any network is built or any step captured."""
+    from monodepth2_amd.options import default_options
+    from monodepth2_amd.trainer import Trainer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    msg = None
+    try:
+        Trainer(default_options(batch_size=2, height=64, width=64, hip_graph=True, log_dir=str(out_dir)),
+                device=torch.device("cpu"), rank=rank, world_size=world)
+    except ValueError as e:
+        msg = str(e)
+    torch.save({"msg": msg}, os.path.join(out_dir, f"guard_{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_hip_graph_on_gloo_is_refused_before_capture(tmp_path):
+    port = _free_port()
+    mp.spawn(_graph_guard_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        msg = torch.load(os.path.join(tmp_path, f"guard_{r}.pt"), weights_only=True)["msg"]
+        assert msg is not None and "nccl" in msg and "gloo" in msg, msg
