@@ -35,11 +35,6 @@ def test_fused_adam_matches_torch_adam():
                 gr = gr.contiguous(memory_format=torch.channels_last)   # grads follow their params
             a.grad = gr.clone()
             b.grad = gr.clone()
-        # the split's contract (md2_adam_apply_dev): the tail's update is ordered after
-        # its parameters' gradients — in the Trainer they are produced on the side (pose)
-        # stream itself; here they were written on the current stream, so the side stream
-        # waits for it before the step enqueues the tail there
-        side.wait_stream(torch.cuda.current_stream())
         oa.step()
         ob.step()
         if step == 1:   # the scheduler's lr edit reaches the kernel
