@@ -125,6 +125,12 @@ _FLOOR_TRIM = {"full_mono_b2_192x640": (5.78e-5, 7.36e-5, 9.50e-5, 9.12e-4),
 # computed in the build container), [scale][frame -1, 1]; bar 3 sqrt(2) x that floor
 _POSECNN_T_FLOOR = {"full_posecnn_b2_192x640": ((2.93e-4, 8.29e-4), (8.31e-3, 1.33e-3), (8.50e-4, 2.36e-3),
                                                 (3.12e-3, 8.74e-3))}
+# tier 1 of the per-scale dL/dT (each implementation on its own argmin, against the
+# golden): the larger of the reference formulation's distances on the host CPU and with
+# ATen on the GPU, per (scale, temporal frame) — profiles/r06/parity_floor.json
+# "grad_T_tier1" (tools/parity_floor.py; HIP measured 0.45-1.4x of it)
+_POSECNN_T1_FLOOR = {"full_posecnn_b2_192x640": ((4.53e-3, 3.56e-3), (9.19e-3, 3.26e-3), (4.03e-3, 1.17e-2),
+                                                 (3.10e-3, 1.16e-2))}
 # the round-3 per-case bars (3x what HIP measured then): ADVICE r04 — the floor-anchored
 # bar must not loosen a case below what the implementation was already held to, so each
 # bar is the smaller of the two
@@ -240,10 +246,12 @@ def test_hip_matches_reference(name):
         if case.posecnn:   # the per-scale T of trainer.py:374-375 and dL/dT at each scale
             for s in range(4):
                 e = rel_l2(out["grad_T"][s][fi], case.expected(f"grad_T_{f}_{s}"))
-                # unpinned: an argmin flip anywhere in the scale moves that scale's dL/dT
-                # (measured 5.7e-3 / 1.14e-2 at full size, scale 2, two runs); the
-                # argmin-pinned comparison (tier 2) holds it to 3 sqrt(2) x the fp32 floor
-                bar = 2e-2 if name in _POSECNN_T_FLOOR else small_pose_bar(name, "trans", pose_bar)
+                # unpinned: an argmin flip anywhere in the scale moves that scale's dL/dT,
+                # so the bar is 3x the reference formulation's own unpinned distance to the
+                # golden on the two fp32 platforms (_POSECNN_T1_FLOOR); the argmin-pinned
+                # comparison (tier 2) holds it to 3 sqrt(2) x the pinned fp32 floor
+                t1 = _POSECNN_T1_FLOOR.get(name)
+                bar = _ceil2(3 * t1[s][i]) if t1 else small_pose_bar(name, "trans", pose_bar)
                 assert e <= bar, (f, s, e, bar)
         else:
             assert rel_l2(out["grad_T"][fi], case.expected(f"grad_T_{f}")) <= pose_bar

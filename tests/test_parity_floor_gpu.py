@@ -33,17 +33,33 @@ from test_hotpath_gpu import FLIP_FRAC, flip_footprint, rel_l2, trimmed_rel_l2
 pytestmark = pytest.mark.gpu
 
 K_FLOOR = 3.0
-# Whether an fp32 platform hits a bilinear cell boundary at a scale is chance: on
+# Whether an fp32 platform hits a bilinear cell boundary at a scale is chance.  On
 # full_posecnn_b2_192x640 the CPU and ATen fp32 runs hit none at scale 0 (untrimmed
-# floor 7.2e-5) while the HIP path hit a handful (1.8e-3 untrimmed, trimmed 0.99x the
-# floor).  The untrimmed bar therefore never falls below K_FLOOR x the smallest untrimmed
-# fp32 floor measured at that scale on the four separate-pose full-size cases
-# (profiles/r05/parity_floor.json): one cell flip's size at that scale.
-CELL_FLOOR = (1.72e-3, 2.46e-3, 1.14e-2, 3.82e-3)
+# floor 7.2e-5) and only a small one at scale 2 (7.8e-4), while the HIP path hit a
+# handful there (1.8e-3 / 2.4e-3 untrimmed).  For exactly those cells (profiles/r06/
+# parity_floor.json) the untrimmed bar is K_FLOOR x one cell flip's size at that scale —
+# the smallest untrimmed fp32 floor measured at that scale on the separate-pose full-size
+# cases, where the platforms did hit flips — AND the excess must be a handful of pixels:
+# with the max(3, 1e-5 n) largest differences left out (`cut_rel_l2`) the HIP path is
+# within K_FLOOR x the case's own untrimmed floor (measured 0.97x / 0.86x of it).  Every
+# other (case, scale) is held to K_FLOOR x its own floor.
+CELL_FLOOR = {("full_posecnn_b2_192x640", 0): 1.72e-3, ("full_posecnn_b2_192x640", 2): 1.14e-2}
 
 
 def fp64_cases():
     return [n for n in case_names() if "f64_loss" in Case(n).z.files]
+
+
+def cut_rel_l2(g, r):
+    """relative L2 with the few largest absolute differences left out: max(3, 1e-5 n) of
+    them — a handful of bilinear cell flips, far fewer than trimmed_rel_l2's 0.1 %"""
+    g = np.asarray(g, np.float64).ravel()
+    r = np.asarray(r, np.float64).ravel()
+    d = np.abs(g - r)
+    n = min(d.size - 1, max(3, int(np.ceil(1e-5 * d.size))))
+    keep = np.ones(d.size, bool)
+    keep[np.argpartition(d, -n)[-n:]] = False
+    return rel_l2(g[keep], r[keep])
 
 
 def in_tol(g, r):
@@ -63,9 +79,11 @@ def floor_metrics(case, hip_out, runs, r64):
         for k, g in [("hip", hip_out["grad_disp"][s])] + [(k, v["grad_disp"][s]) for k, v in runs.items()]:
             row[f"{k}_f64"] = rel_l2(g[keep], r)
             row[f"{k}_f64_trim"] = trimmed_rel_l2(g[keep], r)
+            row[f"{k}_f64_cut"] = cut_rel_l2(g[keep], r)
             row[f"{k}_f64_in_tol"] = in_tol(g[keep], r)
         row["floor"] = max(row[f"{k}_f64"] for k in runs)
         row["floor_trim"] = max(row[f"{k}_f64_trim"] for k in runs)
+        row["floor_cut"] = max(row[f"{k}_f64_cut"] for k in runs)
         rows.append(row)
     return rows
 
@@ -91,7 +109,12 @@ def test_hip_gradients_within_fp32_floor(name):
         assert abs(out["loss"][s] - r64["loss"][s]) <= 2e-6, (s, out["loss"][s], r64["loss"][s])
     for s, m in enumerate(floor_metrics(case, out, runs, r64)):
         assert m["flips"] <= max(3, FLIP_FRAC * out["select"][s].size), (s, m)
-        assert m["hip_f64"] <= K_FLOOR * max(m["floor"], CELL_FLOOR[s]), (s, m)
+        cell = CELL_FLOOR.get((name, s))
+        if cell is None:
+            assert m["hip_f64"] <= K_FLOOR * m["floor"], (s, m)
+        else:   # a platform without a flip at this scale: the flips' own bar (see CELL_FLOOR)
+            assert m["hip_f64"] <= K_FLOOR * max(m["floor"], cell), (s, m)
+            assert m["hip_f64_cut"] <= K_FLOOR * m["floor"], (s, m)
         assert m["hip_f64_trim"] <= K_FLOOR * m["floor_trim"], (s, m)
     for key in (("grad_axis", "grad_trans") if case.temporal else ()):
         e_hip = rel_l2(out[key], r64[key])
