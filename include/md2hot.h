@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 21
+#define MD2_ABI_VERSION 22
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -542,6 +542,14 @@ int md2_maxpool3s2_bwd_multi(const md2_pool_desc* desc, const uint32_t* idx, con
                                         in one launch, no K split                           */
 #define MD2_CONV_WS        (1u << 10) /* x6 forward / stride-1 input gradient, 128-wide tiles: the
                                          warp-specialised kernel (4 MFMA + 4 staging waves) */
+#define MD2_CONV_BF16      (1u << 11) /* ABI 22: a bf16 autocast convolution (config C5): x, y,
+                                         grad_y, grad_x are bf16 NHWC; `weight` of md2_conv_fwd /
+                                         md2_conv_dgrad is ONE bf16 plane of
+                                         md2_conv_bf16_weights; grad_weight stays fp32, holding
+                                         bf16-rounded values (the autocast cast's backward).
+                                         f32 accumulation, output rounded to nearest even,
+                                         deterministic (fixed-order K split).  fwd: in_channels
+                                         % 8; dgrad: stride 1, out_channels % 8 */
 
 typedef struct md2_conv_desc {
     int32_t batch, height, width, in_channels; /* input */
@@ -573,6 +581,14 @@ typedef struct md2_wsplit_entry {
                                    gradient's column form (md2_conv_col2im; ABI 19) */
 } md2_wsplit_entry;
 int md2_conv_split_weights_multi(const md2_wsplit_entry* table, int n, int total_blocks, void* stream);
+/* MD2_CONV_BF16 operands (ABI 22): the fp32 weight rounded to bf16 (nearest even) in the
+ * forward layout w_fwd [Co][KH*KW][Ci] and (nullable) the input gradient's w_dgrad
+ * [Ci][KH*KW][Co] with the taps flipped — what autocast's bf16 cast of the weight feeds a
+ * bf16 convolution, in the two GEMM layouts.  The _multi form converts a whole table of
+ * weights in one launch (md2_wsplit_entry: planes_fwd / planes_dgrad receive the one
+ * plane each, planes_col unused). */
+int md2_conv_bf16_weights(const md2_conv_desc* desc, const float* weight, void* w_fwd, void* w_dgrad, void* stream);
+int md2_conv_bf16_weights_multi(const md2_wsplit_entry* table, int n, int total_blocks, void* stream);
 int md2_conv_fwd(const md2_conv_desc* desc, const float* x, const float* weight, float* y, void* workspace,
                  void* stream);
 /* grad_x (batch, height, width, in_channels) from grad_y (batch, Ho, Wo, out_channels):

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -68,7 +68,8 @@ EXPORTS = ["md2_abi_version", "md2_last_error", "md2_workspace_bytes", "md2_sele
            "md2_conv_fwd", "md2_conv_workspace_bytes", "md2_conv_split_weights",
            "md2_conv_dgrad", "md2_conv_wgrad", "md2_conv_direct", "md2_conv_wgrad_direct",
            "md2_conv_wgrad_direct_workspace_bytes", "md2_conv_split_weights_multi", "md2_bn_fwd_mask",
-           "md2_bn_bwd_mask", "md2_build_id", "md2_maxpool3s2_bwd_multi", "md2_decoder_pad_bwd2", "md2_aug_run2"]
+           "md2_bn_bwd_mask", "md2_build_id", "md2_maxpool3s2_bwd_multi", "md2_decoder_pad_bwd2", "md2_aug_run2",
+           "md2_conv_bf16_weights", "md2_conv_bf16_weights_multi"]
 
 DTYPE_F32 = 0    # md2_desc.disp_dtype
 DTYPE_BF16 = 1
@@ -119,6 +120,7 @@ CONV_PRESPLIT = 1 << 7
 CONV_PATCH = 1 << 8
 CONV_S2_ONE = 1 << 9
 CONV_WS = 1 << 10
+CONV_BF16 = 1 << 11   # ABI 22: bf16 operands (autocast convolutions, config C5)
 
 
 class ConvDesc(ctypes.Structure):
@@ -185,6 +187,10 @@ def _declare(L):
     L.md2_conv_split_weights.argtypes = [ctypes.POINTER(ConvDesc)] + [_vp] * 4
     L.md2_conv_split_weights_multi.restype = ctypes.c_int
     L.md2_conv_split_weights_multi.argtypes = [_vp, ctypes.c_int, ctypes.c_int, _vp]
+    L.md2_conv_bf16_weights.restype = ctypes.c_int
+    L.md2_conv_bf16_weights.argtypes = [ctypes.POINTER(ConvDesc)] + [_vp] * 4
+    L.md2_conv_bf16_weights_multi.restype = ctypes.c_int
+    L.md2_conv_bf16_weights_multi.argtypes = [_vp, ctypes.c_int, ctypes.c_int, _vp]
     L.md2_conv_workspace_bytes.restype = ctypes.c_size_t
     L.md2_conv_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc)]
     L.md2_stem_wgrad_workspace_bytes.restype = ctypes.c_size_t

@@ -185,6 +185,18 @@ def _split_weights(x, w, stride, pad, dgrad: bool):
     return pf, pd
 
 
+def _bf16_weights(x, w, stride, pad, dgrad: bool):
+    """The weight rounded to bf16 in the forward and (nullable) input-gradient layouts,
+    one launch (md2_conv_bf16_weights)."""
+    n = w.numel()
+    pf = torch.empty(n, dtype=torch.bfloat16, device=w.device)
+    pd = torch.empty(n, dtype=torch.bfloat16, device=w.device) if dgrad else None
+    _lib.check(_lib.lib().md2_conv_bf16_weights(ctypes.byref(_desc(x, w, stride, pad)), w.data_ptr(), pf.data_ptr(),
+                                                pd.data_ptr() if pd is not None else None, _lib.stream(w.device)),
+               "md2_conv_bf16_weights")
+    return pf, pd
+
+
 class PlaneBank:
     """Persistent split-bf16 planes of every conv weight a training step multiplies on
     the x6 path, refreshed by ONE md2_conv_split_weights_multi launch at the start of
@@ -198,7 +210,10 @@ class PlaneBank:
     captured: then it keeps the per-call split).  Keys: the weight's storage address
     and shape (parameters are updated in place, so both are stable)."""
 
-    def __init__(self):
+    def __init__(self, bf16: bool = False):
+        # bf16 (config C5's autocast convolutions): ONE bf16 plane per layout, the weight
+        # rounded to nearest even (md2_conv_bf16_weights[_multi]), no column planes
+        self.bf16 = bf16
         self.entries: Dict[tuple, list] = {}   # key -> [weight, planes_fwd, planes_dgrad|None, planes_col|None]
         self.table = None                      # device md2_wsplit_entry array
         self.total_blocks = 0
@@ -240,9 +255,9 @@ class PlaneBank:
         if self.dirty:
             self._upload(device)
         if self.entries:
-            _lib.check(_lib.lib().md2_conv_split_weights_multi(self.table.data_ptr(), len(self.entries),
-                                                              self.total_blocks, _lib.stream(device)),
-                       "md2_conv_split_weights_multi")
+            fn = "md2_conv_bf16_weights_multi" if self.bf16 else "md2_conv_split_weights_multi"
+            _lib.check(getattr(_lib.lib(), fn)(self.table.data_ptr(), len(self.entries), self.total_blocks,
+                                               _lib.stream(device)), fn)
         self._col_pending.clear()
         self.fresh = True
 
@@ -259,7 +274,8 @@ class PlaneBank:
             return e[1], e[2]
         if torch.cuda.is_current_stream_capturing():
             return None
-        pf, pd = _split_weights(x, w, stride, pad, need_dg or (e is not None and e[2] is not None))
+        split = _bf16_weights if self.bf16 else _split_weights
+        pf, pd = split(x, w, stride, pad, need_dg or (e is not None and e[2] is not None))
         if e is not None:
             self._keep.append(e)
         self.entries[k] = [w, pf, pd, e[3] if e is not None else None]
@@ -294,6 +310,7 @@ class PlaneBank:
 
 
 _bank: PlaneBank | None = None
+_bank_bf: PlaneBank | None = None
 
 
 def plane_bank() -> PlaneBank:
@@ -302,6 +319,26 @@ def plane_bank() -> PlaneBank:
     if _bank is None:
         _bank = PlaneBank()
     return _bank
+
+
+def plane_bank_bf16() -> PlaneBank:
+    """The bf16 counterpart (autocast steps): one rounded plane per weight and layout."""
+    global _bank_bf
+    if _bank_bf is None:
+        _bank_bf = PlaneBank(bf16=True)
+    return _bank_bf
+
+
+def begin_step(device: torch.device, bf16: bool = False):
+    """Open the step window of the plane bank the step's convolutions use (one weight-
+    conversion launch for all of them); end_step() closes it."""
+    (plane_bank_bf16() if bf16 else plane_bank()).begin_step(device)
+
+
+def end_step():
+    for b in (_bank, _bank_bf):
+        if b is not None:
+            b.end_step()
 
 
 def _planes_for(x, w, stride, pad, need_dg: bool):
@@ -685,6 +722,126 @@ class _Conv(torch.autograd.Function):
         return gx, gw, None, None
 
 
+# ---------------------------------------------------------------------------------------
+# bf16 autocast convolutions (config C5: `--amp bf16`).  Autocast would hand F.conv2d the
+# activations and the weight cast to bf16 and run MIOpen's bf16 kernels, whose weight
+# gradients are not deterministic at C5's batch (two replays of one captured step 4-6 %
+# apart).  Here the same operands — the input cast to bf16, the weight
+# rounded to nearest even (md2_conv_bf16_weights, refreshed once per step by the bf16
+# PlaneBank) — go to the per-tap GEMMs in their bf16 form (MD2_CONV_BF16: one bf16 plane,
+# one MFMA per fragment pair, f32 accumulation, fixed-order K split, output rounded to
+# bf16), chosen per shape against MIOpen by the same autotune, which never keeps a
+# candidate whose repeated outputs differ.  The weight gradient leaves as fp32 values
+# rounded to bf16, as the autocast cast's backward would hand them to the parameter.
+# Reference: networks/resnet_encoder.py:87-98, networks/depth_decoder.py:50-65 under
+# torch.autocast (BASELINE configs[4]).
+# ---------------------------------------------------------------------------------------
+BF16_ENABLED = os.environ.get("MD2_CONV_BF16", "1") != "0"
+BF = _lib.CONV_BF16
+_FLAGS_BF = (BF, BF | BM256, BF | NO_SPLIT, BF | BM256 | NO_SPLIT)
+_NAMES_BF = ("bf16", "bf16_256", "bf16_ns", "bf16_256_ns")
+
+
+def _bf_flags(n_out: int):
+    """bf16 tile variants: the 256-row tile needs the 128-wide one (more than 64 columns)"""
+    if n_out > 64:
+        return _FLAGS_BF, _NAMES_BF
+    return (_FLAGS_BF[0], _FLAGS_BF[2]), (_NAMES_BF[0], _NAMES_BF[2])
+
+
+def _bf_planes_for(x, w, stride, pad, need_dg: bool):
+    if _bank_bf is not None:
+        got = _bank_bf.planes(x, w, stride, pad, need_dg)
+        if got is not None:
+            return got
+    return _bf16_weights(x, w, stride, pad, need_dg)
+
+
+def _fwd_bf(x, w, plane, stride, pad, flags):
+    B, _, H, W = x.shape
+    N, _, KH, KW = w.shape
+    y = torch.empty(B, N, (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1, device=x.device,
+                    dtype=torch.bfloat16, memory_format=_CL)
+    _call("md2_conv_fwd", x, w, stride, pad, flags, x.data_ptr(), plane.data_ptr(), y.data_ptr(), x.device)
+    return y
+
+
+def _dgrad_bf(gy, x, w, plane, pad, flags):
+    gx = torch.empty_like(x, memory_format=_CL)
+    _call("md2_conv_dgrad", x, w, 1, pad, flags, gy.data_ptr(), plane.data_ptr(), gx.data_ptr(), x.device)
+    return gx
+
+
+def _wgrad_bf(gy, x, w, stride, pad):
+    gw = torch.empty_like(w, memory_format=_CL)
+    _call("md2_conv_wgrad", x, w, stride, pad, BF, x.data_ptr(), gy.data_ptr(), gw.data_ptr(), x.device)
+    return gw
+
+
+class _ConvBF16(torch.autograd.Function):
+    """y = conv2d(x_bf16, bf16(weight)) with autocast's dtypes: x and y bf16, weight the
+    fp32 parameter (its gradient fp32, holding bf16-rounded values)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, pad: int):
+        ctx.stride, ctx.pad = stride, pad
+        ctx.key = (tuple(x.shape), tuple(weight.shape), stride, pad)
+        Co, Ci = weight.shape[0], weight.shape[1]
+        need_dg = stride == 1 and Co % 8 == 0
+        ours = Ci % 8 == 0
+        fl, nm = _bf_flags(Co) if ours else ((), ())
+        pf, pd = _bf_planes_for(x, weight, stride, pad, need_dg) if (ours or need_dg) else (None, None)
+        cands = [(lambda f=f: _fwd_bf(x, weight, pf, stride, pad, f)) for f in fl] + \
+            [lambda: F.conv2d(x, weight.to(torch.bfloat16), None, stride, pad)]
+        i = _fastest("fwd_bf16", ctx.key, cands, list(nm) + ["miopen"])
+        y = cands[i]()
+        ctx.save_for_backward(x, weight, pd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, pd = ctx.saved_tensors
+        s, p = ctx.stride, ctx.pad
+        gy = gy.contiguous(memory_format=_CL)
+        gx = gw = None
+        wb = None
+        if ctx.needs_input_grad[0]:
+            if pd is not None:
+                fl, nm = _bf_flags(w.shape[1])
+                cands = [(lambda f=f: _dgrad_bf(gy, x, w, pd, p, f)) for f in fl]
+            else:
+                fl, nm, cands = (), (), []
+            wb = w.to(torch.bfloat16)
+            cands.append(lambda: _miopen_bwd(gy, x, wb, s, p, (True, False, False))[0])
+            gx = cands[_fastest("dgrad_bf16", ctx.key, cands, list(nm) + ["miopen"])]()
+        if ctx.needs_input_grad[1]:
+            if wb is None:
+                wb = w.to(torch.bfloat16)
+            cands = [lambda: _wgrad_bf(gy, x, w, s, p),
+                     lambda: _miopen_bwd(gy, x, wb, s, p, (False, True, False))[1].float()]
+            gw = cands[_fastest("wgrad_bf16", ctx.key, cands, ["bf16", "miopen"])]()
+        return gx, gw, None, None
+
+
+def _bf16_autocast() -> bool:
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
+def _bf16_ok(x: torch.Tensor, weight: torch.Tensor, stride: int, pad: int) -> bool:
+    return (ENABLED and BF16_ENABLED and x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)
+            and weight.dtype == torch.float32 and weight.shape[2] == weight.shape[3]
+            and _fits(weight.shape[1], weight.shape[0]) and x.is_contiguous(memory_format=_CL)
+            and weight.is_contiguous(memory_format=_CL) and stride >= 1 and 0 <= pad < weight.shape[2]
+            and _sizes_ok(x, weight, stride, pad) and _bf16_autocast())
+
+
+def conv2d_bf16(x: torch.Tensor, weight: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
+    """The bf16 autocast convolution of x (cast to bf16 as autocast would) with weight."""
+    xb = x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
+    with torch.autocast("cuda", enabled=False):
+        return _ConvBF16.apply(xb, weight, stride, pad)
+
+
 def _sizes_ok(x: torch.Tensor, weight: torch.Tensor, stride: int, pad: int) -> bool:
     """csrc/conv.hip valid(): input, output and weight each < 2^29 elements."""
     B, _, H, W = x.shape
@@ -710,10 +867,19 @@ def supports(conv: nn.Conv2d, x: torch.Tensor) -> bool:
             and _shape_ok(x, conv.weight, s[0], p[0]))
 
 
+def _module_ok(conv: nn.Conv2d) -> bool:
+    k, s, p = conv.kernel_size, conv.stride, conv.padding
+    return (conv.bias is None and conv.groups == 1 and tuple(conv.dilation) == (1, 1)
+            and conv.padding_mode == "zeros" and k[0] == k[1] and s[0] == s[1] and p[0] == p[1] and p[0] < k[0])
+
+
 def conv2d(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
-    """conv(x), on the MFMA kernels when supports(conv, x) (and faster, see _fastest)."""
+    """conv(x), on the MFMA kernels when supports(conv, x) (and faster, see _fastest);
+    under bf16 autocast on their bf16 form (conv2d_bf16)."""
     if supports(conv, x):
         return _Conv.apply(x, conv.weight, conv.stride[0], conv.padding[0])
+    if _module_ok(conv) and _bf16_ok(x, conv.weight, conv.stride[0], conv.padding[0]):
+        return conv2d_bf16(x, conv.weight, conv.stride[0], conv.padding[0])
     return conv(x)
 
 
@@ -722,6 +888,8 @@ def conv2d_w(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad: int = 
     bias is folded elsewhere), on the MFMA kernels when the shape fits."""
     if _shape_ok(x, weight, stride, pad):
         return _Conv.apply(x, weight, stride, pad)
+    if _bf16_ok(x, weight, stride, pad):
+        return conv2d_bf16(x, weight, stride, pad)
     return F.conv2d(x, weight, None, stride, pad)
 
 

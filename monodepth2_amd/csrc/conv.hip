@@ -32,6 +32,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "md2hot.h"
 
@@ -80,6 +81,10 @@ struct ConvArgs {
     const float* a;          // fwd: x; dgrad: gy; wgrad: x
     const float* b;          // fwd / dgrad: weight; wgrad: gy
     float* y;                // output [M][N], or partials [splits][M][N]
+    // MD2_CONV_BF16 (ABI 22): bf16 activations / one bf16 weight plane; the output is
+    // written as bf16 (ybf16 = 1, fwd / dgrad) or as fp32 rounded to bf16 values (ybf16 =
+    // 2, wgrad) when there is no K split (else the reduction does it)
+    int ybf16;
 };
 
 __device__ __forceinline__ int xcd_contiguous_block(int bid, int n) {
@@ -93,6 +98,20 @@ __device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, int byte_off) 
 }
 
 constexpr int kBad = 0x7fffffff;   // a byte offset past every buffer: the load returns zeros
+
+// 8 bytes (four bf16) from a buffer
+__device__ __forceinline__ uint2 bload8(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0));
+}
+// fp32 -> bf16 bits, round to nearest even (finite values; NaN stays a NaN)
+__device__ __forceinline__ uint16_t f2bf16(float v) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, v);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf16_round(float v) {
+    return __builtin_bit_cast(float, (uint32_t)f2bf16(v) << 16);
+}
 
 // n / d for 0 <= n < 2^24, d >= 1, from a float reciprocal (rd = 1.0f / d) and one
 // correction step each way: ~6 VALU instead of the ~30 of an integer division
@@ -452,8 +471,28 @@ __device__ __forceinline__ void split_store(__bf16* out, int n, int i, float v) 
 // index of each layout: one 16-byte load, and per plane one 8-byte store instead of
 // four 2-byte ones (the step's one split launch ran at ~60 % of HBM bandwidth on 2-byte
 // stores).  Same split (split3 = split_store's arithmetic), same bits.
+// bf (MD2_CONV_BF16, md2_conv_bf16_weights): ONE plane per layout, the weight rounded to
+// bf16 (nearest even) — the operand a bf16 autocast convolution multiplies
+__device__ __forceinline__ bf16x4 rne4(float4 v) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 q;
+    q.x = (uint32_t)f2bf16(v.x) | ((uint32_t)f2bf16(v.y) << 16);
+    q.y = (uint32_t)f2bf16(v.z) | ((uint32_t)f2bf16(v.w) << 16);
+    return __builtin_bit_cast(bf16x4, q);
+}
+__device__ __forceinline__ void planes_store4(__bf16* out, int n, int i, float4 v, bool bf) {
+    if (bf) {
+        *(bf16x4*)(out + i) = rne4(v);
+        return;
+    }
+    bf16x4 p0, p1, p2;
+    split3(v, p0, p1, p2);
+    *(bf16x4*)(out + i) = p0;
+    *(bf16x4*)(out + n + i) = p1;
+    *(bf16x4*)(out + 2 * n + i) = p2;
+}
 __device__ __forceinline__ void wsplit_tile(const float* w, __bf16* fw, __bf16* dg, __bf16* cl, int Co, int KT,
-                                            int Ci, int tap, int co0, int ci0, float (*tile)[33]) {
+                                            int Ci, int tap, int co0, int ci0, float (*tile)[33], bool bf = false) {
     const int n = Co * KT * Ci;
     if ((Ci & 3) == 0 && (Co & 3) == 0) {   // block-uniform
         const int q = threadIdx.x & 7, r = threadIdx.x >> 3;   // 8 quads x 32 rows
@@ -463,11 +502,7 @@ __device__ __forceinline__ void wsplit_tile(const float* w, __bf16* fw, __bf16* 
             if (co < Co && ci < Ci) {   // Ci % 4 == 0: the whole quad is in range
                 const int i = (co * KT + tap) * Ci + ci;
                 v = *(const float4*)(w + i);
-                bf16x4 p0, p1, p2;
-                split3(v, p0, p1, p2);
-                *(bf16x4*)(fw + i) = p0;
-                *(bf16x4*)(fw + n + i) = p1;
-                *(bf16x4*)(fw + 2 * n + i) = p2;
+                planes_store4(fw, n, i, v, bf);
             }
             tile[r][4 * q] = v.x;
             tile[r][4 * q + 1] = v.y;
@@ -479,20 +514,8 @@ __device__ __forceinline__ void wsplit_tile(const float* w, __bf16* fw, __bf16* 
         const int ci = ci0 + r, co = co0 + 4 * q;
         if (ci < Ci && co < Co) {
             const float4 v = make_float4(tile[4 * q][r], tile[4 * q + 1][r], tile[4 * q + 2][r], tile[4 * q + 3][r]);
-            bf16x4 p0, p1, p2;
-            split3(v, p0, p1, p2);
-            if (dg) {
-                const int i = (ci * KT + (KT - 1 - tap)) * Co + co;
-                *(bf16x4*)(dg + i) = p0;
-                *(bf16x4*)(dg + n + i) = p1;
-                *(bf16x4*)(dg + 2 * n + i) = p2;
-            }
-            if (cl) {   // [(tap, ci)][co], not flipped
-                const int i = (tap * Ci + ci) * Co + co;
-                *(bf16x4*)(cl + i) = p0;
-                *(bf16x4*)(cl + n + i) = p1;
-                *(bf16x4*)(cl + 2 * n + i) = p2;
-            }
+            if (dg) planes_store4(dg, n, (ci * KT + (KT - 1 - tap)) * Co + co, v, bf);
+            if (cl) planes_store4(cl, n, (tap * Ci + ci) * Co + co, v, bf);   // [(tap, ci)][co], not flipped
         }
         return;
     }
@@ -523,7 +546,7 @@ __device__ __forceinline__ void wsplit_tile(const float* w, __bf16* fw, __bf16* 
 // md2_conv_split_weights_multi: the tile kernel's work for every weight of the step in
 // one grid.  Block b belongs to the last entry whose block0 <= b (entries ascending;
 // a binary search over <= a few hundred entries held in the kernel's scalar path).
-__global__ __launch_bounds__(256) void conv_wsplit_multi_kernel(const md2_wsplit_entry* tab, int n) {
+__global__ __launch_bounds__(256) void conv_wsplit_multi_kernel(const md2_wsplit_entry* tab, int n, int bf = 0) {
     __shared__ float tile[32][33];
     const int b = blockIdx.x;
     int lo = 0, hi = n - 1;
@@ -539,13 +562,13 @@ __global__ __launch_bounds__(256) void conv_wsplit_multi_kernel(const md2_wsplit
     t /= nx;
     const int by = t % ny, tap = t / ny;
     wsplit_tile(e.weight, (__bf16*)e.planes_fwd, (__bf16*)e.planes_dgrad, (__bf16*)e.planes_col, e.co, e.kt, e.ci,
-                tap, by * 32, bx * 32, tile);
+                tap, by * 32, bx * 32, tile, bf != 0);
 }
 
 __global__ __launch_bounds__(256) void conv_wsplit_tile_kernel(const float* w, __bf16* fw, __bf16* dg, int Co,
-                                                               int KT, int Ci) {
+                                                               int KT, int Ci, int bf = 0) {
     __shared__ float tile[32][33];
-    wsplit_tile(w, fw, dg, nullptr, Co, KT, Ci, blockIdx.z, blockIdx.y * 32, blockIdx.x * 32, tile);
+    wsplit_tile(w, fw, dg, nullptr, Co, KT, Ci, blockIdx.z, blockIdx.y * 32, blockIdx.x * 32, tile, bf != 0);
 }
 
 // Tiles BMX x BN.  NT threads: 8 waves (2 x 4 / 4 x 2 / 2 x 4, wave tiles 64/128 x 32)
@@ -585,16 +608,21 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, int v
 // (buffer_load_dwordx4 ... lds: no VGPRs, no ds_write), one chunk ahead.  Forward
 // and stride-1 input gradient alike (ConvArgs as the f32 path builds them; b = the
 // planes).
-template <int BN, int BMX>
+// BF (MD2_CONV_BF16): A holds bf16 activations and B ONE bf16 weight plane (the
+// operands of a bf16 autocast convolution, config C5): A quads are 8-byte bf16 loads
+// stored to LDS as they are (no split), one MFMA per fragment pair, f32 accumulation,
+// the output rounded to bf16 (RNE) — the same tiles, pipeline and swizzles.
+template <int BN, int BMX, bool BF = false>
 __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void conv_x6_kernel(ConvArgs a_) {
     using G = X6Geo<BN, BMX>;
     constexpr int NT = G::NT, TM = G::TM;
-    constexpr int AQ = BMX * XBK / 4 / NT;         // f32 quads of A per thread
-    constexpr int NW = NT / 64, PIECES = 3 * BN / 16;   // B: 1 KiB DMA pieces per chunk
+    constexpr int NP = BF ? 1 : 3;                 // bf16 planes per operand
+    constexpr int AQ = BMX * XBK / 4 / NT;         // 4-element quads of A per thread
+    constexpr int NW = NT / 64, PIECES = NP * BN / 16;   // B: 1 KiB DMA pieces per chunk
     constexpr int BQ = (PIECES + NW - 1) / NW;          // pieces per wave (the last j partial)
     constexpr int PA = BMX * XBK, PB = BN * XBK;   // bf16 elements per plane
     static_assert(AQ * NT * 4 == BMX * XBK, "A staging must tile the chunk");
-    __shared__ __bf16 lds[2][3 * (PA + PB)];
+    __shared__ __bf16 lds[2][NP * (PA + PB)];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / G::WN, wn = wid % G::WN;
@@ -635,7 +663,8 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
     // A staging: rows ra + (NT/8) j of the tile, f32 quad qa (k = 4 qa .. 4 qa + 3)
     const int qa = tid & 7, ra = tid >> 3;
     int aih[AQ], aiw[AQ], apb[AQ];
-    const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ar =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * (BF ? 2 : 4), 0x00020000);
 #pragma unroll
     for (int j = 0; j < AQ; ++j) {
         const int m = m0 + ra + (NT / 8) * j;
@@ -666,7 +695,7 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
         const int n = n0 + r;
         bk8[j] = 8 * q;
         bsrc[j] = n < a.N ? ((pl * a.N + n) * KT) * a.C + 8 * q : -1;
-        bdst[j] = (3 * PA + pl * PB + rb * 16 * XBK) * 2;   // bytes into the buffer (wave-uniform)
+        bdst[j] = (NP * PA + pl * PB + rb * 16 * XBK) * 2;   // bytes into the buffer (wave-uniform)
     }
 
     constexpr int NACC = G::MT == 16 ? 4 : 16;
@@ -677,8 +706,9 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
 #pragma unroll
         for (int e = 0; e < NACC; ++e) acc[i][e] = 0.f;
 
-    float4 fa0[AQ], fa1[AQ];
-    auto load = [&](int t, float4 (&RA)[AQ]) {
+    using AReg = typename std::conditional<BF, uint2, float4>::type;   // one quad of A
+    AReg fa0[AQ], fa1[AQ];
+    auto load = [&](int t, AReg (&RA)[AQ]) {
         const int tt = t0 + t;
         const bool live = t < nchunks;
         int kh, kw, off;
@@ -707,7 +737,8 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
 #pragma unroll
         for (int j = 0; j < AQ; ++j) {
             const bool ok = cok && (unsigned)(aih[j] + kh) < (unsigned)a.H && (unsigned)(aiw[j] + kw) < (unsigned)a.W;
-            RA[j] = bload(ar, ok ? (apb[j] + off) * 4 : kBad);
+            if constexpr (BF) RA[j] = bload8(ar, ok ? (apb[j] + off) * 2 : kBad);
+            else RA[j] = bload(ar, ok ? (apb[j] + off) * 4 : kBad);
         }
     };
     // B of chunk t into LDS buffer `buf` (wave-uniform skip past the last chunk)
@@ -732,10 +763,13 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
             dma16(br, base + bdst[j], ok ? (bsrc[j] + kofs) * 2 : kBad);
         }
     };
-    bf16x4 sa[AQ][3];
-    auto split = [&](const float4 (&RA)[AQ]) {
+    bf16x4 sa[AQ][NP];
+    auto split = [&](const AReg (&RA)[AQ]) {
 #pragma unroll
-        for (int j = 0; j < AQ; ++j) split3(RA[j], sa[j][0], sa[j][1], sa[j][2]);
+        for (int j = 0; j < AQ; ++j) {
+            if constexpr (BF) sa[j][0] = __builtin_bit_cast(bf16x4, RA[j]);
+            else split3(RA[j], sa[j][0], sa[j][1], sa[j][2]);
+        }
     };
     auto store = [&](int buf) {
         __bf16* L = lds[buf];
@@ -743,7 +777,7 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
         for (int j = 0; j < AQ; ++j) {
             const int e = xsw<G::MT>(ra + (NT / 8) * j, 4 * qa);
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) *(bf16x4*)(L + pl * PA + e) = sa[j][pl];
+            for (int pl = 0; pl < NP; ++pl) *(bf16x4*)(L + pl * PA + e) = sa[j][pl];
         }
     };
     const int lr = lane & 31, h = lane >> 5;
@@ -752,43 +786,51 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
         if constexpr (G::MT == 16) {
             // 16x16x32: lane l holds row / column l & 15, k = 8 (l >> 4) .. + 7
             const int l16 = lane & 15, kq = lane >> 4;
-            bf16x8 fb[3];
+            bf16x8 fb[NP];
             const int eb = xsw<16>(wn * 16 + l16, 8 * kq);
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
+            for (int pl = 0; pl < NP; ++pl) fb[pl] = *(const bf16x8*)(L + NP * PA + pl * PB + eb);
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                bf16x8 fa[3];
+                bf16x8 fa[NP];
                 const int e = xsw<16>(wm * (TM * 16) + 16 * i + l16, 8 * kq);
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(L + pl * PA + e);
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[1], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[2], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[0], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[1], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+                for (int pl = 0; pl < NP; ++pl) fa[pl] = *(const bf16x8*)(L + pl * PA + e);
+                if constexpr (BF) {
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+                } else {
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[1], acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[2], acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[0], acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[1], acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+                }
             }
         } else {
 #pragma unroll
             for (int s = 0; s < XBK / 16; ++s) {
-                bf16x8 fb[3];
+                bf16x8 fb[NP];
                 const int eb = xidx(wn * 32 + lr, 16 * s + 8 * h);
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
+                for (int pl = 0; pl < NP; ++pl) fb[pl] = *(const bf16x8*)(L + NP * PA + pl * PB + eb);
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
-                    bf16x8 fa[3];
+                    bf16x8 fa[NP];
                     const int e = xidx(wm * (TM * 32) + 32 * i + lr, 16 * s + 8 * h);
 #pragma unroll
-                    for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(L + pl * PA + e);
-                    // small terms first: x2y0, x1y1, x0y2, x1y0, x0y1, x0y0
-                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
-                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[i], 0, 0, 0);
-                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc[i], 0, 0, 0);
-                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[i], 0, 0, 0);
-                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[i], 0, 0, 0);
-                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+                    for (int pl = 0; pl < NP; ++pl) fa[pl] = *(const bf16x8*)(L + pl * PA + e);
+                    if constexpr (BF) {
+                        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+                    } else {
+                        // small terms first: x2y0, x1y1, x0y2, x1y0, x0y1, x0y0
+                        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
+                        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[i], 0, 0, 0);
+                        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc[i], 0, 0, 0);
+                        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[i], 0, 0, 0);
+                        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[i], 0, 0, 0);
+                        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+                    }
                 }
             }
         }
@@ -840,6 +882,12 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
         const int hw = a.Ho * a.Wo, b = m / hw, rem = m - b * hw, oh = rem / a.Wo, ow = rem - oh * a.Wo;
         return (b * a.oHf + 2 * oh + a.py) * a.oWf + 2 * ow + a.px;
     };
+    // BF without a K split: the bf16 output itself (round to nearest even)
+    const bool obf = BF && a.ybf16 == 1 && a.splits == 1;
+    auto put = [&](int m, int n, float v) {
+        if (obf) ((uint16_t*)a.y)[orow(m) * a.N + n] = f2bf16(v);
+        else out[orow(m) * a.N + n] = v;
+    };
     if constexpr (G::MT == 16) {
         // 16x16 D: lane l holds column l & 15, rows 4 (l >> 4) .. + 3
         const int n = n0 + wn * 16 + (lane & 15);
@@ -849,7 +897,7 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int m = m0 + wm * (TM * 16) + 16 * i + 4 * (lane >> 4) + e;
-                    if (m < a.M) out[orow(m) * a.N + n] = acc[i][e];
+                    if (m < a.M) put(m, n, acc[i][e]);
                 }
         }
     } else {
@@ -860,7 +908,7 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), (X6Geo<BN, BMX>::MINB)) void 
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
                     const int m = m0 + wm * (TM * 32) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
-                    if (m < a.M) out[orow(m) * a.N + n] = acc[i][e];
+                    if (m < a.M) put(m, n, acc[i][e]);
                 }
         }
     }
@@ -1257,12 +1305,18 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
 // wave tile BMW/2 x 32).  BMW = 128 rows (co) per tile, or 64 for the 64-channel
 // layers (half the MFMA work of a 128 tile there; only waves 0-1 stage gy, and two
 // blocks fit a CU).  ConvArgs: M = Co, N = KT*Ci, P = pixels, C = Ci, Cg = Co.
-template <int BMW, bool XFAST>
+// BF (MD2_CONV_BF16): x and gy are bf16 — a micro-tile is four 8-byte loads, repacked
+// (not split) into one plane; one MFMA per fragment pair; the weight gradient (fp32
+// accumulation, two-level as above) leaves as fp32 values rounded to bf16 (a bf16
+// autocast convolution's weight gradient) — here without a K split, else in the
+// reduction.
+template <int BMW, bool XFAST, bool BF = false>
 __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel(ConvArgs a) {
     constexpr int NT = 512, BNW = 128, TM = BMW / 64;
+    constexpr int NP = BF ? 1 : 3;
     constexpr int PA = BMW * XBK, PB = BNW * XBK;
     static_assert(BMW == 64 || BMW == 128, "wgrad row tile");
-    __shared__ __bf16 lds[2][3 * (PA + PB)];
+    __shared__ __bf16 lds[2][NP * (PA + PB)];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 2, wn = wid & 3;
     int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
@@ -1293,8 +1347,9 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
         kh = tap / a.KW;
         kw = tap - kh * a.KW;
     }
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * 4, 0x00020000);
+    constexpr int ES = BF ? 2 : 4;   // operand element bytes
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * ES, 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * ES, 0x00020000);
 
     // two-level accumulation: the MFMAs sum one chunk (32 pixels x 6 products) into
     // `acc`, which is then added into `tot` with rounded f32 adds — K here runs over
@@ -1322,7 +1377,12 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
         wow = rem - woh * a.Wo;
     }
     const int sC = a.stride * a.C;
-    auto load = [&](auto side_c, int t, float4 (&V)[4]) {
+    using VReg = typename std::conditional<BF, uint2, float4>::type;   // 4 channels of one pixel
+    auto ld = [&](__amdgpu_buffer_rsrc_t r, int elem) -> VReg {
+        if constexpr (BF) return bload8(r, elem == kBad ? kBad : elem * 2);
+        else return bload(r, elem == kBad ? kBad : elem * 4);
+    };
+    auto load = [&](auto side_c, int t, VReg (&V)[4]) {
         constexpr int SIDE = decltype(side_c)::value;
         const int p0 = (t0 + t) * XBK + 4 * kq;
         const bool live = t < nchunks && rok;
@@ -1330,7 +1390,7 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int p = p0 + i;
-                V[i] = bload(gr, (live && p < a.P) ? (p * a.Cg + m0 + row) * 4 : kBad);
+                V[i] = ld(gr, (live && p < a.P) ? p * a.Cg + m0 + row : kBad);
             }
         } else if constexpr (xfast) {
             const int ih = woh * a.stride - a.pad + kh, iw0 = wow * a.stride - a.pad + kw;
@@ -1339,7 +1399,7 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const bool ok = rowok && (unsigned)(iw0 + i * a.stride) < (unsigned)a.W;
-                V[i] = bload(xr, ok ? (base + i * sC) * 4 : kBad);
+                V[i] = ld(xr, ok ? base + i * sC : kBad);
             }
             wow += XBK;
             while (wow >= a.Wo) {
@@ -1357,7 +1417,7 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
             for (int i = 0; i < 4; ++i) {
                 const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
                 const bool ok = live && p0 + i < a.P && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-                V[i] = bload(xr, ok ? (((b * a.H + ih) * a.W + iw) * a.C + ci) * 4 : kBad);
+                V[i] = ld(xr, ok ? ((b * a.H + ih) * a.W + iw) * a.C + ci : kBad);
                 if (++ow == a.Wo) {
                     ow = 0;
                     if (++oh == a.Ho) {
@@ -1368,8 +1428,20 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
             }
         }
     };
-    uint32_t pk[3][4][2];   // plane, channel j, (k0k1, k2k3) packed bf16 pairs
-    auto split = [&](const float4 (&V)[4]) {
+    uint32_t pk[NP][4][2];   // plane, channel j, (k0k1, k2k3) packed bf16 pairs
+    auto split = [&](const VReg (&V)[4]) {
+        if constexpr (BF) {
+            // channel j of pixels (0, 1) and (2, 3): the low / high halves of dword j / 2
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t sel = (j & 1) ? 0x07060302u : 0x05040100u;
+                const uint32_t d0 = (j < 2) ? V[0].x : V[0].y, d1 = (j < 2) ? V[1].x : V[1].y;
+                const uint32_t d2 = (j < 2) ? V[2].x : V[2].y, d3 = (j < 2) ? V[3].x : V[3].y;
+                pk[0][j][0] = __builtin_amdgcn_perm(d1, d0, sel);
+                pk[0][j][1] = __builtin_amdgcn_perm(d3, d2, sel);
+            }
+            return;
+        } else {
         float c[3][4][4];   // plane, pixel i, channel j
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1389,14 +1461,15 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
                 pk[pl][j][0] = hi16x2(c[pl][0][j], c[pl][1][j]);
                 pk[pl][j][1] = hi16x2(c[pl][2][j], c[pl][3][j]);
             }
+        }
     };
     auto store = [&](auto side_c, int buf) {
         constexpr int SIDE = decltype(side_c)::value;
-        __bf16* L = lds[buf] + (SIDE ? 3 * PA : 0);
+        __bf16* L = lds[buf] + (SIDE ? NP * PA : 0);
         constexpr int P = SIDE ? PB : PA;
         typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
+        for (int pl = 0; pl < NP; ++pl)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 u32x2 q;
@@ -1420,24 +1493,29 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
         const __bf16* L = lds[buf];
 #pragma unroll
         for (int s = 0; s < XBK / 16; ++s) {
-            bf16x8 fa[TM][3], fb[3];
+            bf16x8 fa[TM][NP], fb[NP];
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 const int e = xidx2(wm * (TM * 32) + 32 * i + lr, 16 * s + 8 * h);
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) fa[i][pl] = *(const bf16x8*)(L + pl * PA + e);
+                for (int pl = 0; pl < NP; ++pl) fa[i][pl] = *(const bf16x8*)(L + pl * PA + e);
             }
             const int eb = xidx2(wn * 32 + lr, 16 * s + 8 * h);
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
+            for (int pl = 0; pl < NP; ++pl) fb[pl] = *(const bf16x8*)(L + NP * PA + pl * PB + eb);
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
+                if constexpr (BF) {
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[0], acc[i], 0, 0, 0);
+                    continue;
+                } else {
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[0], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[1], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[2], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[0], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[1], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[0], acc[i], 0, 0, 0);
+                }
             }
         }
     };
@@ -1448,7 +1526,7 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
     // the scheduler can interleave (the MFMA shadows hide the split VALU), as in
     // conv_x6pw_kernel's per-role loops
     auto run = [&](auto side_c) {
-        float4 v0[4], v1[4];
+        VReg v0[4], v1[4];
         load(side_c, 0, v0);
         load(side_c, 1, v1);
         split(v0);
@@ -1502,7 +1580,7 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const int m = m0 + wm * (TM * 32) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
-                if (m < a.M) out[m * a.N + n] = tot[i][e];
+                if (m < a.M) out[m * a.N + n] = (BF && a.splits == 1) ? bf16_round(tot[i][e]) : tot[i][e];
             }
     }
 }
@@ -1730,7 +1808,9 @@ constexpr int kRedOut = 64, kRedLanes = 256 / kRedOut;
 // OUT outputs per block, 256 / OUT lanes each: 64 for wide partials with few splits,
 // 16 (sixteen lanes, each every 16th split) for the weight gradients' narrow ones with
 // many splits, which at 64 per block ran a few dozen blocks of long serial chains
-template <int OUT>
+// OM: the output as fp32 (0), as bf16 bits (1: a bf16 convolution's activations, RNE)
+// or as fp32 rounded to bf16 values (2: a bf16 convolution's weight gradient)
+template <int OUT, int OM = 0>
 __global__ __launch_bounds__(256) void conv_reduce_kernel(const float4* part, float4* y, int n4, int splits) {
     constexpr int LANES = 256 / OUT;
     __shared__ float4 red[LANES][OUT];
@@ -1758,16 +1838,29 @@ __global__ __launch_bounds__(256) void conv_reduce_kernel(const float4* part, fl
             s.z += v.z;
             s.w += v.w;
         }
-        y[i] = s;
+        if constexpr (OM == 1) {
+            ((uint2*)y)[i] = make_uint2((uint32_t)f2bf16(s.x) | ((uint32_t)f2bf16(s.y) << 16),
+                                        (uint32_t)f2bf16(s.z) | ((uint32_t)f2bf16(s.w) << 16));
+        } else if constexpr (OM == 2) {
+            y[i] = make_float4(bf16_round(s.x), bf16_round(s.y), bf16_round(s.z), bf16_round(s.w));
+        } else {
+            y[i] = s;
+        }
     }
 }
 
-void launch_reduce(const float4* part, float4* y, int n4, int splits, hipStream_t st) {
+template <int OM>
+void launch_reduce_om(const float4* part, float4* y, int n4, int splits, hipStream_t st) {
     if (splits >= 16 && (n4 + kRedOut - 1) / kRedOut < 512)
-        hipLaunchKernelGGL(conv_reduce_kernel<16>, dim3((n4 + 15) / 16), dim3(256), 0, st, part, y, n4, splits);
+        hipLaunchKernelGGL((conv_reduce_kernel<16, OM>), dim3((n4 + 15) / 16), dim3(256), 0, st, part, y, n4, splits);
     else
-        hipLaunchKernelGGL(conv_reduce_kernel<kRedOut>, dim3((n4 + kRedOut - 1) / kRedOut), dim3(256), 0, st, part, y,
-                           n4, splits);
+        hipLaunchKernelGGL((conv_reduce_kernel<kRedOut, OM>), dim3((n4 + kRedOut - 1) / kRedOut), dim3(256), 0, st,
+                           part, y, n4, splits);
+}
+void launch_reduce(const float4* part, float4* y, int n4, int splits, hipStream_t st, int om = 0) {
+    if (om == 1) launch_reduce_om<1>(part, y, n4, splits, st);
+    else if (om == 2) launch_reduce_om<2>(part, y, n4, splits, st);
+    else launch_reduce_om<0>(part, y, n4, splits, st);
 }
 
 // conv_reduce_kernel for a stride-2 parity class: class-ordered partials [splits][M][N]
@@ -1970,12 +2063,25 @@ void launch(const ConvArgs& a, int BN, hipStream_t st) {
 int min_chunks_of(int mode) { return mode == MODE_WGRAD ? 8 : 6; }
 
 bool use_x6(const md2_conv_desc* d, int mode) {
+    if (d->flags & MD2_CONV_BF16) return false;
     if (!((d->flags & MD2_CONV_X6) && d->in_channels % 8 == 0 && d->out_channels % 8 == 0)) return false;
     if (mode == MODE_WGRAD) {   // fdiv() of the pixel index needs it below 2^24
         const Shape s = shape_of(d);
         if ((long long)s.B * s.Ho * s.Wo + 64 >= (1ll << 24)) return false;
     }
     return true;
+}
+
+// MD2_CONV_BF16 (ABI 22): the per-tap GEMMs on bf16 operands.  The forward's B rows
+// run along in_channels and the input gradient's along out_channels (16-byte LDS-DMA
+// pieces: multiples of 8); the A quads are 4 channels (multiples of 4); the input
+// gradient is stride 1 only; the weight gradient walks its pixels with fdiv (< 2^24).
+bool use_bf(const md2_conv_desc* d, int mode) {
+    if (!(d->flags & MD2_CONV_BF16)) return false;
+    if (mode == MODE_FWD) return d->in_channels % 8 == 0;
+    if (mode == MODE_DGRAD) return d->stride == 1 && d->out_channels % 8 == 0;
+    const Shape s = shape_of(d);
+    return (long long)s.B * s.Ho * s.Wo + 64 < (1ll << 24);
 }
 
 // the weight gradient's x6 GEMM: rows co, columns (tap, ci), K = output pixels
@@ -2008,6 +2114,16 @@ void flat_k(ConvArgs& a, int mode) {
         a.flatk = 1;
         a.nchunks = (a.KH * a.KW * a.C + XBK - 1) / XBK;
     }
+}
+
+void launch_bf(const ConvArgs& a, hipStream_t st) {
+    const dim3 grid(a.mblocks * a.nblocks * a.splits);
+    if (a.bm == 256) hipLaunchKernelGGL((conv_x6_kernel<128, 256, true>), grid, dim3(X6Geo<128, 256>::NT), 0, st, a);
+    else if (a.bn == 128)
+        hipLaunchKernelGGL((conv_x6_kernel<128, 128, true>), grid, dim3(X6Geo<128, 128>::NT), 0, st, a);
+    else if (a.bn == 64) hipLaunchKernelGGL((conv_x6_kernel<64, 128, true>), grid, dim3(X6Geo<64, 128>::NT), 0, st, a);
+    else if (a.bn == 32) hipLaunchKernelGGL((conv_x6_kernel<32, 128, true>), grid, dim3(X6Geo<32, 128>::NT), 0, st, a);
+    else hipLaunchKernelGGL((conv_x6_kernel<16, 128, true>), grid, dim3(X6Geo<16, 128>::NT), 0, st, a);
 }
 
 void launch_x6(const ConvArgs& a, hipStream_t st, bool ws = false) {
@@ -2304,8 +2420,41 @@ __global__ __launch_bounds__(256) void conv_col2im_kernel(const float4* __restri
     }
 }
 
+// MD2_CONV_BF16: A / out are bf16 (the weight gradient's out fp32), B the one bf16
+// weight plane (fwd / dgrad: md2_conv_bf16_weights) or grad_y (wgrad)
+int run_bf(const md2_conv_desc* d, int mode, const void* A, const void* B, void* out, void* ws, void* stream,
+           const char* name) {
+    if (!use_bf(d, mode))
+        return md2_report_error(MD2_ERR_ARG, "conv bf16: fwd in_channels % 8; dgrad stride 1, out_channels % 8; "
+                                             "wgrad fewer than 2^24 output pixels");
+    ConvArgs a = mode == MODE_WGRAD ? args_x6_wgrad(d) : args_of(d, mode);
+    flat_k(a, mode);
+    plan_x6(a, d->flags, mode == MODE_WGRAD);
+    a.a = (const float*)A;
+    a.b = (const float*)B;
+    a.ybf16 = mode == MODE_WGRAD ? 2 : 1;
+    if (mode != MODE_WGRAD) a.b_elems = d->out_channels * d->kernel_h * d->kernel_w * d->in_channels;
+    if (a.splits > 1 && !ws) return md2_report_error(MD2_ERR_ARG, name);
+    a.y = a.splits > 1 ? (float*)ws : (float*)out;
+    const hipStream_t st = (hipStream_t)stream;
+    if (mode == MODE_WGRAD) {
+        const dim3 grid(a.mblocks * a.nblocks * a.splits);
+        const bool xf = (a.Wo & 3) == 0;
+        void (*k)(ConvArgs) = a.bm == 64
+                                  ? (xf ? conv_x6_wgrad_kernel<64, true, true> : conv_x6_wgrad_kernel<64, false, true>)
+                                  : (xf ? conv_x6_wgrad_kernel<128, true, true> : conv_x6_wgrad_kernel<128, false, true>);
+        hipLaunchKernelGGL(k, grid, dim3(512), 0, st, a);
+    } else {
+        launch_bf(a, st);
+    }
+    if (a.splits > 1) launch_reduce((const float4*)a.y, (float4*)out, a.M * a.N / 4, a.splits, st, a.ybf16);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
 int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float* out, void* ws, void* stream,
         const char* name) {
+    if (d->flags & MD2_CONV_BF16) return run_bf(d, mode, A, B, out, ws, stream, name);
     ConvArgs a = (mode == MODE_WGRAD && use_x6(d, mode)) ? args_x6_wgrad(d) : args_of(d, mode);
     if (use_x6(d, mode)) flat_k(a, mode);
     const bool patch = use_x6p(d, mode, a);
@@ -2355,6 +2504,13 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
 }
 
 size_t ws_bytes(const md2_conv_desc* d, int mode) {
+    if (d->flags & MD2_CONV_BF16) {   // the K split's fp32 partials only (the weight plane is the caller's)
+        if (!use_bf(d, mode)) return 0;
+        ConvArgs a = mode == MODE_WGRAD ? args_x6_wgrad(d) : args_of(d, mode);
+        flat_k(a, mode);
+        plan_x6(a, d->flags, mode == MODE_WGRAD);
+        return a.splits > 1 ? sizeof(float) * (size_t)a.splits * a.M * a.N : 0;
+    }
     if (mode == MODE_DGRAD && use_x6_s2(d)) {
         size_t part = 0;
         for (int py = 0; py < 2; ++py)
@@ -2405,6 +2561,23 @@ int md2_conv_split_weights(const md2_conv_desc* d, const float* weight, void* pl
     hipLaunchKernelGGL(conv_wsplit_tile_kernel, grid, dim3(256), 0, (hipStream_t)stream, weight,
                        (__bf16*)planes_fwd, (__bf16*)planes_dgrad, d->out_channels, d->kernel_h * d->kernel_w,
                        d->in_channels);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
+int md2_conv_bf16_weights(const md2_conv_desc* d, const float* weight, void* w_fwd, void* w_dgrad, void* stream) {
+    if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "conv_bf16_weights: channels % 4, pad < kernel, sizes < 2^29");
+    if (!weight || !w_fwd) return md2_report_error(MD2_ERR_ARG, "conv_bf16_weights: NULL operand");
+    const dim3 grid((d->in_channels + 31) / 32, (d->out_channels + 31) / 32, d->kernel_h * d->kernel_w);
+    hipLaunchKernelGGL(conv_wsplit_tile_kernel, grid, dim3(256), 0, (hipStream_t)stream, weight, (__bf16*)w_fwd,
+                       (__bf16*)w_dgrad, d->out_channels, d->kernel_h * d->kernel_w, d->in_channels, 1);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
+}
+
+int md2_conv_bf16_weights_multi(const md2_wsplit_entry* table, int n, int total_blocks, void* stream) {
+    if (!table || n <= 0 || total_blocks <= 0) return md2_report_error(MD2_ERR_ARG, "conv_bf16_weights_multi: empty");
+    hipLaunchKernelGGL(conv_wsplit_multi_kernel, dim3(total_blocks), dim3(256), 0, (hipStream_t)stream, table, n, 1);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));
 }

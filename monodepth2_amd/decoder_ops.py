@@ -199,6 +199,16 @@ def conv_bias_act(conv: torch.nn.Conv2d, x: torch.Tensor, relu: bool) -> torch.T
         if not z.is_contiguous(memory_format=_CL):
             z = z.contiguous(memory_format=_CL)
         return _BiasAct.apply(z, conv.bias, relu)
+    from . import conv_ops
+    if (conv.bias is not None and conv.groups == 1 and tuple(conv.dilation) == (1, 1) and conv.padding_mode == "zeros"
+            and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
+            and conv_ops._bf16_ok(x, conv.weight, conv.stride[0], conv.padding[0])):
+        # bf16 autocast (config C5): the bias-free bf16 convolution (conv_ops.conv2d_bf16,
+        # deterministic weight gradient), the bf16-cast bias added as autocast's conv
+        # would, then the ReLU
+        z = conv_ops.conv2d_bf16(x, conv.weight, conv.stride[0], conv.padding[0])
+        z = z + conv.bias.to(torch.bfloat16).view(1, -1, 1, 1)
+        return F.relu(z) if relu else z
     y = conv(x)
     return F.relu(y) if relu else y
 

@@ -26,6 +26,8 @@ from . import _lib
 _CL = torch.channels_last
 ENABLED = True       # the x6 weight gradient (tests flip it to compare with MIOpen)
 FWD_ENABLED = os.environ.get("MD2_STEM_FWD", "1") != "0"   # the x6 forward (C = 3 / 6); 0: MIOpen's (A/B)
+# bf16 autocast: the weight gradient on md2_stem_wgrad (deterministic) instead of MIOpen's bf16 one
+BF16_ENABLED = os.environ.get("MD2_CONV_BF16", "1") != "0"
 
 
 def _fwd(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
@@ -69,6 +71,48 @@ class _StemConv(torch.autograd.Function):
         return None, gw
 
 
+class _StemConvBF16(torch.autograd.Function):
+    """The stem under bf16 autocast (config C5): the forward is autocast's — x and the
+    weight cast to bf16, MIOpen's bf16 convolution — and the weight gradient, which MIOpen
+    computes non-deterministically in bf16, runs on md2_stem_wgrad (f32-class split-bf16
+    products, fixed-order reduction) over the exact fp32 values of the bf16 operands, then
+    rounded to bf16 as the autocast cast's backward would hand it to the parameter."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        xb = x.to(torch.bfloat16)
+        ctx.save_for_backward(xb)
+        ctx.w_cl = weight.is_contiguous(memory_format=_CL)
+        ctx.w_shape = weight.shape
+        with torch.autocast("cuda", enabled=False):
+            return F.conv2d(xb, weight.to(torch.bfloat16), None, 2, 3)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xb, = ctx.saved_tensors
+        x = xb.float().contiguous(memory_format=_CL)
+        gy = gy.float().contiguous(memory_format=_CL)
+        B, C, H, W = x.shape
+        d = _lib.StemDesc(B, C, H, W, _lib.STEM_WEIGHT_CL if ctx.w_cl else 0)
+        gw = torch.empty(ctx.w_shape, device=x.device, dtype=torch.float32,
+                         memory_format=_CL if ctx.w_cl else torch.contiguous_format)
+        L = _lib.lib()
+        ws = torch.empty(L.md2_stem_wgrad_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=x.device)
+        _lib.check(L.md2_stem_wgrad(ctypes.byref(d), x.data_ptr(), gy.data_ptr(), gw.data_ptr(), ws.data_ptr(),
+                                    _lib.stream(x.device)), "md2_stem_wgrad")
+        return None, gw.to(torch.bfloat16).to(torch.float32)
+
+
+def supports_stem_bf16(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    from .conv_ops import _bf16_autocast
+    return (BF16_ENABLED and x.is_cuda and x.dtype == torch.float32 and conv.weight.dtype == torch.float32
+            and not x.requires_grad and x.dim() == 4 and x.shape[1] in (3, 6, 9)
+            and x.is_contiguous(memory_format=_CL) and conv.out_channels == 64
+            and tuple(conv.kernel_size) == (7, 7) and tuple(conv.stride) == (2, 2) and tuple(conv.padding) == (3, 3)
+            and tuple(conv.dilation) == (1, 1) and conv.groups == 1 and conv.bias is None
+            and conv.padding_mode == "zeros" and _bf16_autocast() and x.numel() < 2 ** 31)
+
+
 def supports_stem(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     return (x.is_cuda and x.dtype == torch.float32 and conv.weight.dtype == torch.float32 and not x.requires_grad
             and x.dim() == 4 and x.shape[1] in (3, 6, 9) and x.is_contiguous(memory_format=_CL)
@@ -85,4 +129,6 @@ def stem_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
         if torch.is_grad_enabled() and conv.weight.requires_grad:
             return _StemConv.apply(x, conv.weight)
         return _fwd(x, conv.weight.detach())
+    if ENABLED and torch.is_grad_enabled() and conv.weight.requires_grad and supports_stem_bf16(conv, x):
+        return _StemConvBF16.apply(x, conv.weight)
     return conv(x)

@@ -515,10 +515,11 @@ class Trainer:
     def _step_body(self, inputs):
         """process_batch + backward + gradient averaging + Adam (trainer.py:205-209).
         The conv weights' split-bf16 planes are refreshed once for the whole step
-        (conv_ops.PlaneBank, one launch) and valid until the optimizer step."""
-        bank = conv_ops.plane_bank() if self.device.type == "cuda" and conv_ops.PLANE_BANK else None
-        if bank is not None:
-            bank.begin_step(self.device)
+        (conv_ops.PlaneBank, one launch) and valid until the optimizer step — under
+        --amp bf16 the bf16-rounded weights of the bf16 convolutions likewise."""
+        bank = self.device.type == "cuda" and conv_ops.PLANE_BANK
+        if bank:
+            conv_ops.begin_step(self.device, bf16=getattr(self.opt, "amp", "none") == "bf16")
         self._in_step = True
         if self._adam_split:
             # the optimizer's step counter and bias corrections first, so that the pose
@@ -538,8 +539,8 @@ class Trainer:
                 torch.cuda.current_stream(self.device).wait_stream(self._pose_stream)
         finally:
             self._in_step = False
-            if bank is not None:
-                bank.end_step()
+            if bank:
+                conv_ops.end_step()
         if self.flat_sync is not None:
             self.flat_sync.sync()
         self.model_optimizer.step()
