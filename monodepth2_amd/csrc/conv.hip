@@ -1865,6 +1865,7 @@ void launch_reduce(const float4* part, float4* y, int n4, int splits, hipStream_
 
 // conv_reduce_kernel for a stride-2 parity class: class-ordered partials [splits][M][N]
 // summed the same way, each output quad written to its gx pixel
+template <int OM = 0>   // OM 1: bf16 output (MD2_CONV_BF16)
 __global__ __launch_bounds__(256) void conv_reduce_scatter_kernel(const float4* part, float4* y, int n4, int splits,
                                                                    int N4, int Hc, int Wc, int oHf, int oWf, int py,
                                                                    int px) {
@@ -1894,7 +1895,12 @@ __global__ __launch_bounds__(256) void conv_reduce_scatter_kernel(const float4* 
         }
         const int m = i / N4, q = i - m * N4, hw = Hc * Wc, b = m / hw, rem = m - b * hw, oh = rem / Wc,
                   ow = rem - oh * Wc;
-        y[((size_t)(b * oHf + 2 * oh + py) * oWf + 2 * ow + px) * N4 + q] = s;
+        const size_t o = ((size_t)(b * oHf + 2 * oh + py) * oWf + 2 * ow + px) * N4 + q;
+        if constexpr (OM == 1)
+            ((uint2*)y)[o] = make_uint2((uint32_t)f2bf16(s.x) | ((uint32_t)f2bf16(s.y) << 16),
+                                        (uint32_t)f2bf16(s.z) | ((uint32_t)f2bf16(s.w) << 16));
+        else
+            y[o] = s;
     }
 }
 
@@ -2299,12 +2305,23 @@ bool dgrad_s2_class(const md2_conv_desc* d, int py, int px, ConvArgs& a, uint32_
 bool use_x6_s2(const md2_conv_desc* d) {
     return d->stride == 2 && use_x6(d, MODE_DGRAD) && d->out_channels >= XBK;
 }
+// the same parity-class input gradient on bf16 operands (MD2_CONV_BF16): the flipped
+// [Ci][KT][Co] plane rows run along out_channels
+bool use_bf_s2(const md2_conv_desc* d) {
+    return (d->flags & MD2_CONV_BF16) && d->stride == 2 && d->out_channels % 8 == 0 && d->out_channels >= XBK;
+}
 
 int run_dgrad_s2(const md2_conv_desc* d, const float* gy, const float* w, float* gx, void* ws, void* stream) {
     if (!ws) return md2_report_error(MD2_ERR_ARG, "conv_dgrad (stride 2): workspace required");
     const hipStream_t st = (hipStream_t)stream;
-    __bf16* planes = (d->flags & MD2_CONV_PRESPLIT) ? (__bf16*)w : (__bf16*)ws;
-    if (!(d->flags & MD2_CONV_PRESPLIT)) {
+    const bool bf = (d->flags & MD2_CONV_BF16) != 0;   // bf16 gy / gx, `w` the one bf16 plane
+    __bf16* planes = (bf || (d->flags & MD2_CONV_PRESPLIT)) ? (__bf16*)w : (__bf16*)ws;
+    const size_t part_off = bf ? 0 : x6_planes_bytes(d);
+    auto go = [&](const ConvArgs& a) {
+        if (bf) launch_bf(a, st);
+        else launch_x6(a, st);
+    };
+    if (!bf && !(d->flags & MD2_CONV_PRESPLIT)) {
         const int nw = d->out_channels * d->kernel_h * d->kernel_w * d->in_channels;
         hipLaunchKernelGGL(conv_wsplit_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, w, planes, d->out_channels,
                            d->kernel_h * d->kernel_w, d->in_channels, 1);
@@ -2318,7 +2335,7 @@ int run_dgrad_s2(const md2_conv_desc* d, const float* gy, const float* w, float*
             if (dgrad_s2_class(d, py, px, a) && a.nchunks == 0) tapless = true;
         }
     if (tapless) {
-        const hipError_t me = hipMemsetAsync(gx, 0, sizeof(float) * (size_t)d->batch * d->height * d->width *
+        const hipError_t me = hipMemsetAsync(gx, 0, (bf ? 2 : 4) * (size_t)d->batch * d->height * d->width *
                                                         d->in_channels, st);
         if (me != hipSuccess) return md2_report_error(MD2_ERR_HIP, hipGetErrorString(me));
     }
@@ -2357,7 +2374,11 @@ int run_dgrad_s2(const md2_conv_desc* d, const float* gy, const float* w, float*
             m.a = gy;
             m.b = (const float*)planes;
             m.y = gx;
-            launch_x6(m, st);
+            if (bf) {
+                m.ybf16 = 1;
+                m.b_elems /= 3;
+            }
+            go(m);
         }
     } else {
     for (int py = 0; py < 2; ++py)
@@ -2366,13 +2387,17 @@ int run_dgrad_s2(const md2_conv_desc* d, const float* gy, const float* w, float*
             if (!dgrad_s2_class(d, py, px, a) || a.nchunks == 0) continue;
             a.a = gy;
             a.b = (const float*)planes;
-            a.y = a.splits > 1 ? (float*)((char*)ws + x6_planes_bytes(d)) : gx;
-            launch_x6(a, st);
+            a.y = a.splits > 1 ? (float*)((char*)ws + part_off) : gx;
+            if (bf) {
+                a.ybf16 = 1;
+                a.b_elems /= 3;
+            }
+            go(a);
             if (a.splits > 1) {
                 const int n4 = a.M * a.N / 4;
-                hipLaunchKernelGGL(conv_reduce_scatter_kernel, dim3((n4 + kRedOut - 1) / kRedOut), dim3(256), 0, st,
-                                   (const float4*)a.y, (float4*)gx, n4, a.splits, a.N / 4, a.Ho, a.Wo, a.oHf, a.oWf,
-                                   py, px);
+                hipLaunchKernelGGL(bf ? conv_reduce_scatter_kernel<1> : conv_reduce_scatter_kernel<0>,
+                                   dim3((n4 + kRedOut - 1) / kRedOut), dim3(256), 0, st, (const float4*)a.y,
+                                   (float4*)gx, n4, a.splits, a.N / 4, a.Ho, a.Wo, a.oHf, a.oWf, py, px);
             }
         }
     }
@@ -2505,6 +2530,16 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
 
 size_t ws_bytes(const md2_conv_desc* d, int mode) {
     if (d->flags & MD2_CONV_BF16) {   // the K split's fp32 partials only (the weight plane is the caller's)
+        if (mode == MODE_DGRAD && use_bf_s2(d)) {
+            size_t part = 0;
+            for (int py = 0; py < 2; ++py)
+                for (int px = 0; px < 2; ++px) {
+                    ConvArgs c;
+                    if (dgrad_s2_class(d, py, px, c) && c.splits > 1)
+                        part = std::max(part, sizeof(float) * (size_t)c.splits * c.M * c.N);
+                }
+            return part;
+        }
         if (!use_bf(d, mode)) return 0;
         ConvArgs a = mode == MODE_WGRAD ? args_x6_wgrad(d) : args_of(d, mode);
         flat_k(a, mode);
@@ -2547,7 +2582,7 @@ extern "C" {
 size_t md2_conv_workspace_bytes(const md2_conv_desc* d) {
     if (!valid(d)) return 0;
     size_t m = ws_bytes(d, MODE_FWD);
-    if (d->stride == 1 || use_x6_s2(d)) m = m > ws_bytes(d, MODE_DGRAD) ? m : ws_bytes(d, MODE_DGRAD);
+    if (d->stride == 1 || use_x6_s2(d) || use_bf_s2(d)) m = m > ws_bytes(d, MODE_DGRAD) ? m : ws_bytes(d, MODE_DGRAD);
     const size_t w = ws_bytes(d, MODE_WGRAD);
     return m > w ? m : w;
 }
@@ -2598,7 +2633,7 @@ int md2_conv_fwd(const md2_conv_desc* d, const float* x, const float* weight, fl
 
 int md2_conv_dgrad(const md2_conv_desc* d, const float* grad_y, const float* weight, float* grad_x,
                    void* workspace, void* stream) {
-    if (!valid(d) || (d->stride != 1 && !use_x6_s2(d)))
+    if (!valid(d) || (d->stride != 1 && !use_x6_s2(d) && !use_bf_s2(d)))
         return md2_report_error(MD2_ERR_ARG, "conv_dgrad: stride 1 (stride 2: MD2_CONV_X6, channels % 8, >= 32 "
                                              "output channels), channels % 4, pad < kernel, sizes < 2^29");
     if (!grad_y || !weight || !grad_x) return md2_report_error(MD2_ERR_ARG, "conv_dgrad: NULL operand");
