@@ -742,11 +742,21 @@ _FLAGS_BF = (BF, BF | BM256, BF | NO_SPLIT, BF | BM256 | NO_SPLIT)
 _NAMES_BF = ("bf16", "bf16_256", "bf16_ns", "bf16_256_ns")
 
 
-def _bf_flags(n_out: int):
-    """bf16 tile variants: the 256-row tile needs the 128-wide one (more than 64 columns)"""
-    if n_out > 64:
-        return _FLAGS_BF, _NAMES_BF
-    return (_FLAGS_BF[0], _FLAGS_BF[2]), (_NAMES_BF[0], _NAMES_BF[2])
+_PFLAGS_BF = (BF | PATCH, BF | PATCH | NO_SPLIT, BF | PATCH | BM256, BF | PATCH | BM256 | NO_SPLIT)
+_PNAMES_BF = ("bf16p", "bf16p_ns", "bf16p_256", "bf16p_256_ns")
+
+
+def _bf_flags(n_out: int, gemm_c: int = 0, k: int = 0, stride: int = 0):
+    """bf16 variants of a forward / stride-1 input gradient: the per-tap GEMM (the 256-row
+    tile needs the 128-wide one, more than 64 columns) and, for 3x3 stride 1 with GEMM
+    channels % 32 and more than 16 columns, the patch-staged one (csrc/conv.hip use_bfp)"""
+    wide = n_out > 64
+    fl = _FLAGS_BF if wide else (_FLAGS_BF[0], _FLAGS_BF[2])
+    nm = _NAMES_BF if wide else (_NAMES_BF[0], _NAMES_BF[2])
+    if k == 3 and stride == 1 and gemm_c % 32 == 0 and n_out > 16:
+        fl = fl + (_PFLAGS_BF if wide else _PFLAGS_BF[:2])
+        nm = nm + (_PNAMES_BF if wide else _PNAMES_BF[:2])
+    return fl, nm
 
 
 def _bf_planes_for(x, w, stride, pad, need_dg: bool):
@@ -772,9 +782,9 @@ def _dgrad_bf(gy, x, w, plane, pad, flags, stride=1):
     return gx
 
 
-def _wgrad_bf(gy, x, w, stride, pad):
+def _wgrad_bf(gy, x, w, stride, pad, flags=BF):
     gw = torch.empty_like(w, memory_format=_CL)
-    _call("md2_conv_wgrad", x, w, stride, pad, BF, x.data_ptr(), gy.data_ptr(), gw.data_ptr(), x.device)
+    _call("md2_conv_wgrad", x, w, stride, pad, flags, x.data_ptr(), gy.data_ptr(), gw.data_ptr(), x.device)
     return gw
 
 
@@ -791,7 +801,7 @@ class _ConvBF16(torch.autograd.Function):
         # stride 2 runs as four output-parity classes (csrc/conv.hip use_bf_s2)
         need_dg = Co % 8 == 0 and (stride == 1 or (stride == 2 and Co >= 32))
         ours = Ci % 8 == 0
-        fl, nm = _bf_flags(Co) if ours else ((), ())
+        fl, nm = _bf_flags(Co, Ci, weight.shape[2], stride) if ours else ((), ())
         pf, pd = _bf_planes_for(x, weight, stride, pad, need_dg) if (ours or need_dg) else (None, None)
         cands = [(lambda f=f: _fwd_bf(x, weight, pf, stride, pad, f)) for f in fl] + \
             [lambda: F.conv2d(x, weight.to(torch.bfloat16), None, stride, pad)]
@@ -809,7 +819,7 @@ class _ConvBF16(torch.autograd.Function):
         wb = None
         if ctx.needs_input_grad[0]:
             if pd is not None and s == 1:
-                fl, nm = _bf_flags(w.shape[1])
+                fl, nm = _bf_flags(w.shape[1], w.shape[0], w.shape[2], 1)
                 cands = [(lambda f=f: _dgrad_bf(gy, x, w, pd, p, f)) for f in fl]
             elif pd is not None:
                 fl, nm = (BF, BF | S2_ONE), ("bf16_s2", "bf16_s2one")
@@ -822,8 +832,12 @@ class _ConvBF16(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             # ours only: MIOpen's bf16 weight gradients are not deterministic (atomics);
             # a repeat check over a few timing runs does not always catch it (C5's
-            # replay-vs-replay diagnosis kept MIOpen on one decoder shape)
-            gw = _wgrad_bf(gy, x, w, s, p)
+            # replay-vs-replay diagnosis kept MIOpen on one decoder shape).  3x3 stride 1:
+            # the per-tap GEMM or the patch-staged one (the input rows of a 32-pixel
+            # segment staged once for the nine taps), whichever is faster
+            pw = w.shape[2] == 3 and w.shape[3] == 3 and s == 1
+            cands = [lambda: _wgrad_bf(gy, x, w, s, p)] + ([lambda: _wgrad_bf(gy, x, w, s, p, BF | PATCH)] if pw else [])
+            gw = cands[_fastest("wgrad_bf16", ctx.key, cands, ["bf16"] + (["bf16pw"] if pw else []))]()
         return gx, gw, None, None
 
 

@@ -1127,17 +1127,20 @@ __device__ __forceinline__ int pidx16(int pix, int pr, int pc, int k) {
 // behind tap 0's MFMAs and split / stored after tap 8.  A tiles of 128 or 256 pixels
 // as TR x TC with TC in {16, 32, 64} chosen per shape (the least padding); outputs
 // outside the image are not stored.  K splits run over channel chunks.
-template <int BN, int BMX, int TC>
+// BF (MD2_CONV_BF16): bf16 activations staged as they are (8-byte quads, one plane), one
+// bf16 weight plane, one MFMA per fragment pair, the output rounded to bf16.
+template <int BN, int BMX, int TC, bool BF = false>
 __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvArgs a) {
     using G = X6Geo<BN, BMX>;
     static_assert(G::MT == 32, "patch kernel: 32x32x16 MFMA tiles");
     constexpr int NT = G::NT, TM = G::TM;
+    constexpr int NP = BF ? 1 : 3;
     constexpr int TR = BMX / TC, PW = TC + 2, PH = TR + 2, PP = PH * PW;
-    constexpr int AQP = (PP * 8 + NT - 1) / NT;          // f32 quads of the patch per thread
-    constexpr int NW = NT / 64, PIECES = 3 * BN / 16;
+    constexpr int AQP = (PP * 8 + NT - 1) / NT;          // 4-channel quads of the patch per thread
+    constexpr int NW = NT / 64, PIECES = NP * BN / 16;
     constexpr int BQ = (PIECES + NW - 1) / NW;
     constexpr int PA = PP * XBK, PB = BN * XBK;          // bf16 elements per plane
-    __shared__ __bf16 lds[3 * PA + 2 * 3 * PB];
+    __shared__ __bf16 lds[NP * PA + 2 * NP * PB];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / G::WN, wn = wid % G::WN;
@@ -1154,7 +1157,8 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
 
     // A: patch float4 f = tid + NT j -> pixel f / 8 (row-major PH x PW), channel quad f % 8
     int aofs[AQP];
-    const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ar =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * (BF ? 2 : 4), 0x00020000);
 #pragma unroll
     for (int j = 0; j < AQP; ++j) {
         const int f = tid + NT * j, pix = f >> 3, q = f & 7;
@@ -1174,7 +1178,7 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
         const int n = n0 + r;
         bk8[j] = 8 * q;
         bsrc[j] = n < a.N ? ((pl * a.N + n) * KT) * a.C + 8 * q : -1;
-        bdst[j] = (3 * PA + pl * PB + rb * 16 * XBK) * 2;
+        bdst[j] = (NP * PA + pl * PB + rb * 16 * XBK) * 2;
     }
     f32x16 acc[TM];
 #pragma unroll
@@ -1182,11 +1186,15 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
 
-    float4 RA[AQP];
+    using AReg = typename std::conditional<BF, uint2, float4>::type;
+    AReg RA[AQP];
     auto load = [&](int t) {   // the patch of channel chunk t (zeros outside the image)
         const int c0 = (t0 + t) * XBK;
 #pragma unroll
-        for (int j = 0; j < AQP; ++j) RA[j] = bload(ar, aofs[j] >= 0 ? (aofs[j] + c0) * 4 : kBad);
+        for (int j = 0; j < AQP; ++j) {
+            if constexpr (BF) RA[j] = bload8(ar, aofs[j] >= 0 ? (aofs[j] + c0) * 2 : kBad);
+            else RA[j] = bload(ar, aofs[j] >= 0 ? (aofs[j] + c0) * 4 : kBad);
+        }
     };
     auto store_patch = [&]() {
 #pragma unroll
@@ -1194,7 +1202,8 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
             const int f = tid + NT * j;
             if (PP * 8 % NT && f >= PP * 8) break;
             bf16x4 p0, p1, p2;
-            split3(RA[j], p0, p1, p2);
+            if constexpr (BF) p0 = __builtin_bit_cast(bf16x4, RA[j]);
+            else split3(RA[j], p0, p1, p2);
             int e;
             if constexpr (TC == 16) {
                 const int pix = f >> 3, pr = pix / PW;
@@ -1203,13 +1212,15 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
                 e = xidx(f >> 3, 4 * (f & 7));
             }
             *(bf16x4*)(lds + e) = p0;
-            *(bf16x4*)(lds + PA + e) = p1;
-            *(bf16x4*)(lds + 2 * PA + e) = p2;
+            if constexpr (!BF) {
+                *(bf16x4*)(lds + PA + e) = p1;
+                *(bf16x4*)(lds + 2 * PA + e) = p2;
+            }
         }
     };
     auto dma = [&](int t, int tap, int buf) {   // B of (chunk t, tap) into buffer buf
         const int kofs = tap * a.C + (t0 + t) * XBK, klim = tap * a.C + a.C;
-        char* base = (char*)lds + buf * 3 * PB * 2;
+        char* base = (char*)lds + buf * NP * PB * 2;
 #pragma unroll
         for (int j = 0; j < BQ; ++j) {
             if (PIECES % NW && wid + NW * j >= PIECES) break;   // wave-uniform
@@ -1227,27 +1238,32 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
         acol[i] = c;
     }
     auto mma = [&](int buf, int tap) {
-        const __bf16* LB = lds + 3 * PA + buf * 3 * PB;
+        const __bf16* LB = lds + NP * PA + buf * NP * PB;
         const int th = tap / 3, tw = tap - 3 * th, toff = th * PW + tw;
 #pragma unroll
         for (int s = 0; s < XBK / 16; ++s) {
-            bf16x8 fb[3];
+            bf16x8 fb[NP];
             const int eb = xidx(wn * 32 + lr, 16 * s + 8 * h);
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(LB + pl * PB + eb);
+            for (int pl = 0; pl < NP; ++pl) fb[pl] = *(const bf16x8*)(LB + pl * PB + eb);
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                bf16x8 fa[3];
+                bf16x8 fa[NP];
                 const int e = TC == 16 ? pidx16(abase[i] + toff, arow[i] + th, acol[i] + tw, 16 * s + 8 * h)
                                        : xidx(abase[i] + toff, 16 * s + 8 * h);
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(lds + pl * PA + e);
+                for (int pl = 0; pl < NP; ++pl) fa[pl] = *(const bf16x8*)(lds + pl * PA + e);
+                if constexpr (BF) {
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+                    continue;
+                } else {
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+                }
             }
         }
     };
@@ -1290,7 +1306,11 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
             for (int e = 0; e < 16; ++e) {
                 const int ml = wm * (TM * 32) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
                 const int r = ml / TC, c = ml - r * TC, oh = oh0 + r, ow = ow0 + c;
-                if (oh < a.Ho && ow < a.Wo) out[((size_t)(b * a.Ho + oh) * a.Wo + ow) * a.N + n] = acc[i][e];
+                if (oh < a.Ho && ow < a.Wo) {
+                    const size_t o = ((size_t)(b * a.Ho + oh) * a.Wo + ow) * a.N + n;
+                    if (BF && a.ybf16 == 1 && a.splits == 1) ((uint16_t*)a.y)[o] = f2bf16(acc[i][e]);
+                    else out[o] = acc[i][e];
+                }
             }
     }
 }
@@ -1598,11 +1618,14 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
 // K splits run over the chunks; output and partials as conv_x6_wgrad_kernel.
 // ConvArgs: M = Co, N = 9 Ci, C = Ci, Cg = Co, nblocks = 32-channel groups of Ci,
 // ptc = 32-column segments per output row, nchunks = B Ho ptc.
-template <int BMW>
+// BF (MD2_CONV_BF16): bf16 x / gy, one plane (repacked, not split), one MFMA per
+// fragment pair, the output rounded to bf16 values (as conv_x6_wgrad_kernel's BF form).
+template <int BMW, bool BF = false>
 __global__ __launch_bounds__(576, 1) void conv_x6pw_kernel(ConvArgs a) {
     constexpr int TM = BMW / 32;
+    constexpr int NP = BF ? 1 : 3;
     constexpr int PA = BMW * XBK, PT = 32 * XBK;   // bf16 per A plane / per B tile plane
-    constexpr int BUF = 3 * PA + 27 * PT;
+    constexpr int BUF = NP * PA + 9 * NP * PT;
     static_assert(BMW == 32 || BMW == 64, "wgrad patch row tile");
     __shared__ __bf16 lds[2 * BUF];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1619,8 +1642,9 @@ __global__ __launch_bounds__(576, 1) void conv_x6pw_kernel(ConvArgs a) {
     // faster than keeping the three waves that share a SIMD, 0 / 4 / 8, free of staging)
     const int rr = wid, g = lane & 7, q = lane >> 3;        // x: input row rr, columns 4g .., channels 4q ..
     const int u = tid - 192, kq = u & 7, mq = u >> 3;       // gy: pixels 4kq .., channels 4mq ..
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * 4, 0x00020000);
+    constexpr int ES = BF ? 2 : 4;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * ES, 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * ES, 0x00020000);
 
     // the loader's chunk position (b, oh, seg), advanced one chunk at a time
     int pc = t0, pseg, poh, pb;
@@ -1640,7 +1664,21 @@ __global__ __launch_bounds__(576, 1) void conv_x6pw_kernel(ConvArgs a) {
             }
         }
     };
-    float4 V[6];
+    using VReg = typename std::conditional<BF, uint2, float4>::type;   // 4 channels of one pixel
+    VReg V[6];
+    auto ld = [&](__amdgpu_buffer_rsrc_t r, bool ok, int elem) -> VReg {
+        if constexpr (BF) return bload8(r, ok ? elem * 2 : kBad);
+        else return bload(r, ok ? elem * 4 : kBad);
+    };
+    // channel j of pixels i and i + 1 as one bf16 pair (BF)
+    auto pair16 = [&](int j, int i) -> uint32_t {
+        if constexpr (BF) {
+            const uint32_t d0 = (j < 2) ? V[i].x : V[i].y, d1 = (j < 2) ? V[i + 1].x : V[i + 1].y;
+            return __builtin_amdgcn_perm(d1, d0, (j & 1) ? 0x07060302u : 0x05040100u);
+        } else {
+            return 0u;
+        }
+    };
     // loads of the loader's chunk (zeros past the split's last chunk: no branch)
     auto load_x = [&]() {
         const int ih = poh - a.pad + rr, iw0 = pseg * 32 - a.pad + 4 * g;
@@ -1649,7 +1687,7 @@ __global__ __launch_bounds__(576, 1) void conv_x6pw_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const int iw = iw0 + i;
-            V[i] = bload(xr, rok && (unsigned)iw < (unsigned)a.W ? (base + iw * a.C) * 4 : kBad);
+            V[i] = ld(xr, rok && (unsigned)iw < (unsigned)a.W, base + iw * a.C);
         }
     };
     auto load_g = [&]() {
@@ -1657,9 +1695,25 @@ __global__ __launch_bounds__(576, 1) void conv_x6pw_kernel(ConvArgs a) {
         const bool ok = pc < t0 + nchunks && m0 + 4 * mq < a.M;
         const int base = ((pb * a.Ho + poh) * a.Wo) * a.Cg + m0 + 4 * mq;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) V[i] = bload(gr, ok && ow0 + i < a.Wo ? (base + (ow0 + i) * a.Cg) * 4 : kBad);
+        for (int i = 0; i < 4; ++i) V[i] = ld(gr, ok && ow0 + i < a.Wo, base + (ow0 + i) * a.Cg);
     };
     auto store_x = [&](__bf16* L) {
+        if constexpr (BF) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t w[5];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) w[k] = pair16(j, k);
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) {
+                    u32x2 v;
+                    v.x = w[kw];
+                    v.y = w[kw + 2];
+                    *(u32x2*)(L + PA + (kw * 3 + rr) * PT + xidx2(4 * q + j, 4 * g)) = v;
+                }
+            }
+            return;
+        } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             float c[3][6];
@@ -1685,8 +1739,19 @@ __global__ __launch_bounds__(576, 1) void conv_x6pw_kernel(ConvArgs a) {
                 }
             }
         }
+        }
     };
     auto store_g = [&](__bf16* L) {
+        if constexpr (BF) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                u32x2 v;
+                v.x = pair16(j, 0);
+                v.y = pair16(j, 2);
+                *(u32x2*)(L + xidx2(4 * mq + j, 4 * kq)) = v;
+            }
+            return;
+        } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             float c[3][4];
@@ -1706,6 +1771,7 @@ __global__ __launch_bounds__(576, 1) void conv_x6pw_kernel(ConvArgs a) {
                 *(u32x2*)(L + pl * PA + xidx2(4 * mq + j, 4 * kq)) = v;
             }
         }
+        }
     };
 
     const int lr = lane & 31, h = lane >> 5;
@@ -1717,26 +1783,31 @@ __global__ __launch_bounds__(576, 1) void conv_x6pw_kernel(ConvArgs a) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
-    const int boff = 3 * PA + (kw * 3 + kh) * 3 * PT;
+    const int boff = NP * PA + (kw * 3 + kh) * NP * PT;
     auto mma = [&](const __bf16* L) {
 #pragma unroll
         for (int s = 0; s < XBK / 16; ++s) {
-            bf16x8 fb[3];
+            bf16x8 fb[NP];
             const int eb = boff + xidx2(lr, 16 * s + 8 * h);
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + pl * PT + eb);
+            for (int pl = 0; pl < NP; ++pl) fb[pl] = *(const bf16x8*)(L + pl * PT + eb);
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                bf16x8 fa[3];
+                bf16x8 fa[NP];
                 const int e = xidx2(32 * i + lr, 16 * s + 8 * h);
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(L + pl * PA + e);
+                for (int pl = 0; pl < NP; ++pl) fa[pl] = *(const bf16x8*)(L + pl * PA + e);
+                if constexpr (BF) {
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+                    continue;
+                } else {
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[i], 0, 0, 0);
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[i], 0, 0, 0);
+                }
             }
         }
     };
@@ -1795,7 +1866,7 @@ __global__ __launch_bounds__(576, 1) void conv_x6pw_kernel(ConvArgs a) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const int m = m0 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
-                if (m < a.M) out[m * a.N + n] = acc[i][e];
+                if (m < a.M) out[m * a.N + n] = (BF && a.splits == 1) ? bf16_round(acc[i][e]) : acc[i][e];
             }
     }
 }
@@ -2090,6 +2161,19 @@ bool use_bf(const md2_conv_desc* d, int mode) {
     return (long long)s.B * s.Ho * s.Wo + 64 < (1ll << 24);
 }
 
+// the patch-staged forward / stride-1 input gradient on bf16 operands (MD2_CONV_BF16 |
+// MD2_CONV_PATCH): 3x3, GEMM channels % 32, more than 16 GEMM columns (as use_x6p)
+bool use_bfp(const md2_conv_desc* d, int mode, const ConvArgs& a) {
+    return (d->flags & MD2_CONV_PATCH) && use_bf(d, mode) && mode != MODE_WGRAD && a.KH == 3 && a.KW == 3 &&
+           a.stride == 1 && a.C % XBK == 0 && a.N > 16 && !a.flatk;
+}
+
+// the patch-staged weight gradient on bf16 operands (MD2_CONV_BF16 | MD2_CONV_PATCH): 3x3 stride 1
+bool use_bfpw(const md2_conv_desc* d) {
+    return (d->flags & MD2_CONV_PATCH) && use_bf(d, MODE_WGRAD) && d->kernel_h == 3 && d->kernel_w == 3 &&
+           d->stride == 1;
+}
+
 // the weight gradient's x6 GEMM: rows co, columns (tap, ci), K = output pixels
 ConvArgs args_x6_wgrad(const md2_conv_desc* d) {
     const Shape s = shape_of(d);
@@ -2200,21 +2284,22 @@ void plan_x6p(ConvArgs& a, uint32_t flags) {
     a.flatk = best_tc;   // carried to launch_x6p (the kernel itself does not read flatk)
 }
 
-template <int BN, int BMX>
+template <int BN, int BMX, bool BF = false>
 void launch_x6p_tc(const ConvArgs& a, hipStream_t st) {
     const dim3 grid(a.mblocks * a.nblocks * a.splits), block(X6Geo<BN, BMX>::NT);
     ConvArgs b = a;
     b.flatk = 0;
-    if (a.flatk == 64) hipLaunchKernelGGL((conv_x6p_kernel<BN, BMX, 64>), grid, block, 0, st, b);
-    else if (a.flatk == 32) hipLaunchKernelGGL((conv_x6p_kernel<BN, BMX, 32>), grid, block, 0, st, b);
-    else hipLaunchKernelGGL((conv_x6p_kernel<BN, BMX, 16>), grid, block, 0, st, b);
+    if (a.flatk == 64) hipLaunchKernelGGL((conv_x6p_kernel<BN, BMX, 64, BF>), grid, block, 0, st, b);
+    else if (a.flatk == 32) hipLaunchKernelGGL((conv_x6p_kernel<BN, BMX, 32, BF>), grid, block, 0, st, b);
+    else hipLaunchKernelGGL((conv_x6p_kernel<BN, BMX, 16, BF>), grid, block, 0, st, b);
 }
 
+template <bool BF = false>
 void launch_x6p(const ConvArgs& a, hipStream_t st) {
-    if (a.bm == 256) launch_x6p_tc<128, 256>(a, st);
-    else if (a.bn == 128) launch_x6p_tc<128, 128>(a, st);
-    else if (a.bn == 64) launch_x6p_tc<64, 128>(a, st);
-    else launch_x6p_tc<32, 128>(a, st);
+    if (a.bm == 256) launch_x6p_tc<128, 256, BF>(a, st);
+    else if (a.bn == 128) launch_x6p_tc<128, 128, BF>(a, st);
+    else if (a.bn == 64) launch_x6p_tc<64, 128, BF>(a, st);
+    else launch_x6p_tc<32, 128, BF>(a, st);
 }
 
 // Patch weight gradient (MD2_CONV_X6 | MD2_CONV_PATCH): 3x3 stride 1, any Ci % 8 (the
@@ -2453,8 +2538,12 @@ int run_bf(const md2_conv_desc* d, int mode, const void* A, const void* B, void*
         return md2_report_error(MD2_ERR_ARG, "conv bf16: fwd in_channels % 8; dgrad stride 1, out_channels % 8; "
                                              "wgrad fewer than 2^24 output pixels");
     ConvArgs a = mode == MODE_WGRAD ? args_x6_wgrad(d) : args_of(d, mode);
+    const bool pw = mode == MODE_WGRAD && use_bfpw(d);
     flat_k(a, mode);
-    plan_x6(a, d->flags, mode == MODE_WGRAD);
+    const bool patch = use_bfp(d, mode, a);
+    if (pw) plan_x6pw(a, d->flags);
+    else if (patch) plan_x6p(a, d->flags);
+    else plan_x6(a, d->flags, mode == MODE_WGRAD);
     a.a = (const float*)A;
     a.b = (const float*)B;
     a.ybf16 = mode == MODE_WGRAD ? 2 : 1;
@@ -2462,13 +2551,19 @@ int run_bf(const md2_conv_desc* d, int mode, const void* A, const void* B, void*
     if (a.splits > 1 && !ws) return md2_report_error(MD2_ERR_ARG, name);
     a.y = a.splits > 1 ? (float*)ws : (float*)out;
     const hipStream_t st = (hipStream_t)stream;
-    if (mode == MODE_WGRAD) {
+    if (pw) {
+        const dim3 grid(a.mblocks * a.nblocks * a.splits);
+        if (a.bm == 64) hipLaunchKernelGGL((conv_x6pw_kernel<64, true>), grid, dim3(576), 0, st, a);
+        else hipLaunchKernelGGL((conv_x6pw_kernel<32, true>), grid, dim3(576), 0, st, a);
+    } else if (mode == MODE_WGRAD) {
         const dim3 grid(a.mblocks * a.nblocks * a.splits);
         const bool xf = (a.Wo & 3) == 0;
         void (*k)(ConvArgs) = a.bm == 64
                                   ? (xf ? conv_x6_wgrad_kernel<64, true, true> : conv_x6_wgrad_kernel<64, false, true>)
                                   : (xf ? conv_x6_wgrad_kernel<128, true, true> : conv_x6_wgrad_kernel<128, false, true>);
         hipLaunchKernelGGL(k, grid, dim3(512), 0, st, a);
+    } else if (patch) {
+        launch_x6p<true>(a, st);
     } else {
         launch_bf(a, st);
     }
@@ -2543,7 +2638,9 @@ size_t ws_bytes(const md2_conv_desc* d, int mode) {
         if (!use_bf(d, mode)) return 0;
         ConvArgs a = mode == MODE_WGRAD ? args_x6_wgrad(d) : args_of(d, mode);
         flat_k(a, mode);
-        plan_x6(a, d->flags, mode == MODE_WGRAD);
+        if (mode == MODE_WGRAD && use_bfpw(d)) plan_x6pw(a, d->flags);
+        else if (use_bfp(d, mode, a)) plan_x6p(a, d->flags);
+        else plan_x6(a, d->flags, mode == MODE_WGRAD);
         return a.splits > 1 ? sizeof(float) * (size_t)a.splits * a.M * a.N : 0;
     }
     if (mode == MODE_DGRAD && use_x6_s2(d)) {

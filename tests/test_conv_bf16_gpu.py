@@ -21,7 +21,6 @@ pytestmark = pytest.mark.gpu
 
 CL = torch.channels_last
 BF = conv_ops.BF
-VARIANTS = [BF, BF | conv_ops.NO_SPLIT, BF | conv_ops.BM256, BF | conv_ops.BM256 | conv_ops.NO_SPLIT]
 
 SHAPES = [  # (B, Cin, Cout, k, stride, pad, H, W)
     (2, 64, 64, 3, 1, 1, 24, 40),      # ResNet layer1
@@ -70,7 +69,7 @@ def test_bf16_kernels_match_fp64(B, C, N, k, s, p, H, W):
                                                      (0, 0), 1, (True, True, False))[:2]
     pf, pd = conv_ops._bf16_weights(x, w, s, p, N % 8 == 0 and (s == 1 or N >= 32))
     assert torch.equal(pf.view(N, k, k, C).permute(0, 3, 1, 2), wb)   # the weight rounded to nearest even
-    flags = VARIANTS if N > 64 else VARIANTS[:2]
+    flags = list(conv_ops._bf_flags(N, C, k, s)[0])
     if C % 8 == 0:
         for f in flags:
             y = conv_ops._fwd_bf(x, w, pf, s, p, f)
@@ -78,16 +77,18 @@ def test_bf16_kernels_match_fp64(B, C, N, k, s, p, H, W):
             _check(y, y64, ("fwd", f))
             assert torch.equal(y, conv_ops._fwd_bf(x, w, pf, s, p, f)), ("fwd repeat", f)
     if pd is not None:   # stride 2: the four output-parity classes, per-class launches or one
-        dflags = (VARIANTS if C > 64 else VARIANTS[:2]) if s == 1 else (BF, BF | conv_ops.S2_ONE)
+        dflags = list(conv_ops._bf_flags(C, N, k, 1)[0]) if s == 1 else [BF, BF | conv_ops.S2_ONE]
         for f in dflags:
             gx = conv_ops._dgrad_bf(gy, x, w, pd, p, f, s)
             assert gx.dtype == torch.bfloat16
             _check(gx, gx64, ("dgrad", f))
             assert torch.equal(gx, conv_ops._dgrad_bf(gy, x, w, pd, p, f, s)), ("dgrad repeat", f)
-    gw = conv_ops._wgrad_bf(gy, x, w, s, p)
-    assert gw.dtype == torch.float32 and torch.equal(gw, gw.to(torch.bfloat16).float())   # bf16 values
-    _check(gw, gw64, "wgrad")
-    assert torch.equal(gw, conv_ops._wgrad_bf(gy, x, w, s, p)), "wgrad repeat"
+    wflags = [BF] + ([BF | conv_ops.PATCH] if (k == 3 and s == 1) else [])   # per-tap / patch-staged
+    for f in wflags:
+        gw = conv_ops._wgrad_bf(gy, x, w, s, p, f)
+        assert gw.dtype == torch.float32 and torch.equal(gw, gw.to(torch.bfloat16).float())   # bf16 values
+        _check(gw, gw64, ("wgrad", f))
+        assert torch.equal(gw, conv_ops._wgrad_bf(gy, x, w, s, p, f)), ("wgrad repeat", f)
     # MIOpen's bf16 convolution of the same operands, for scale (its own summation order)
     ym = F.conv2d(x, wb, None, s, p).double()
     assert float((ym - y64).norm() / y64.norm()) <= 5e-3
