@@ -42,6 +42,7 @@ def bn_groups(n: int):
 
 _CL = torch.channels_last
 _workspaces: Dict[int, torch.Tensor] = {}
+_workspaces_keep = []
 
 
 def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
@@ -51,6 +52,8 @@ def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
     key = _lib.stream(device)
     ws = _workspaces.get(key)
     if ws is None or ws.numel() < nbytes:
+        if ws is not None:   # never freed: a captured hipGraph may still use it (conv_ops._workspace)
+            _workspaces_keep.append(ws)
         with torch.cuda.stream(torch.cuda.current_stream(device)):
             ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
         _workspaces[key] = ws

@@ -77,11 +77,19 @@ def _x6_flags(gemm_c: int, k: int, stride: int, n_out: int):
     return flags, names
 
 
+_ws_keep = []   # superseded workspaces: a captured hipGraph may still write into them
+
+
 def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
-    """K-split partials, one buffer per HIP stream (the pose network runs on its own)."""
+    """K-split partials, one buffer per HIP stream (the pose network runs on its own).
+    A buffer that grows is never freed: a graph captured while it was current keeps its
+    address, and an eager step after the capture (e.g. a larger shape, or fp32 after a
+    bf16 capture) must not hand that memory to other tensors the replays would overwrite."""
     key = (device.index, _lib.stream(device))
     ws = _ws.get(key)
     if ws is None or ws.numel() < nbytes:
+        if ws is not None:
+            _ws_keep.append(ws)
         ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
         _ws[key] = ws
     return ws
