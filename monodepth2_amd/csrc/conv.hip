@@ -1605,6 +1605,225 @@ __global__ __launch_bounds__(512, (BMW == 64 ? 2 : 1)) void conv_x6_wgrad_kernel
     }
 }
 
+// Warp-specialised split-bf16 weight gradient (MD2_CONV_X6 | MD2_CONV_WS, 128-row tiles).
+// conv_x6_wgrad_kernel<128> has all 8 waves stage AND multiply between two barriers, so a
+// SIMD's two waves split, store and wait on their loads in the same window as their MFMAs
+// (profiles/r06: MFMA busy 0.35, a third of its wave cycles waiting).  Here waves 0-3
+// only multiply (2 x 2, wave tile 64 x 64: per 16 k, 4 fragment triples for 24 MFMAs —
+// 0.5 reads per MFMA instead of 0.75) and waves 4-7 (one per SIMD) stage both operands:
+// each thread the gy AND the x micro-tile of conv_x6_wgrad_kernel's two staging sides.
+// The staging waves keep two register sets: chunk t+2's loads are issued before chunk
+// t+1 is split and stored (a whole chunk of MFMAs between a load and its use; three sets,
+// loads two chunks ahead, measured 2-10 % slower per shape); one barrier per chunk hands
+// the double-buffered LDS over.  Same tiles, swizzle, products,
+// product order and two-level accumulation per output as conv_x6_wgrad_kernel<128>:
+// bitwise equal results (tests/test_conv_gpu.py).
+template <bool XFAST>
+__global__ __launch_bounds__(512, 1) void conv_x6wws_kernel(ConvArgs a) {
+    constexpr int BMW = 128, BNW = 128;
+    constexpr int PA = BMW * XBK, PB = BNW * XBK;
+    __shared__ __bf16 lds[2][3 * (PA + PB)];
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool mfma_wave = wid < 4;
+    int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int nb = blk % a.nblocks;
+    blk /= a.nblocks;
+    const int mb = blk % a.mblocks, ks = blk / a.mblocks;
+    const int m0 = mb * BMW, n0 = nb * BNW;
+    const int t0 = ks * a.chunks_per_split;
+    const int nchunks = min(a.chunks_per_split, a.nchunks - t0);
+    const int HoWo = a.Ho * a.Wo;
+    const float rHoWo = 1.0f / (float)HoWo, rWo = 1.0f / (float)a.Wo;
+
+    // ---- staging waves: micro-tile rows 4 mq .. 4 mq + 3 of both operands, pixels 4 kq .. ----
+    const int st = tid - 256, kq = st & 7, mq = st >> 3, row = 4 * mq;
+    const bool rokA = m0 + row < a.M;
+    const int nrow = n0 + row;
+    const bool rokB = nrow < a.N;
+    const int tap = nrow / a.C, ci = nrow - tap * a.C;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * 4, 0x00020000);
+    int wb = 0, woh = 0, wow = 0;   // (b, oh, ow) of this thread's first pixel of the next x load
+    if (XFAST && !mfma_wave) {
+        const int p = t0 * XBK + 4 * kq;
+        wb = fdiv(p, HoWo, rHoWo);
+        const int rem = p - wb * HoWo;
+        woh = fdiv(rem, a.Wo, rWo);
+        wow = rem - woh * a.Wo;
+    }
+    const int sC = a.stride * a.C;
+    // chunk t's gy quads (G) and x quads (X); called for t = 0, 1, 2, ... in order
+    auto load = [&](int t, float4 (&G)[4], float4 (&X)[4]) {
+        const int p0 = (t0 + t) * XBK + 4 * kq;
+        const bool live = t < nchunks;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int p = p0 + i;
+            G[i] = bload(gr, (live && rokA && p < a.P) ? (p * a.Cg + m0 + row) * 4 : kBad);
+        }
+        if constexpr (XFAST) {
+            const int ih = woh * a.stride - a.pad + kh, iw0 = wow * a.stride - a.pad + kw;
+            const bool rowok = live && rokB && p0 < a.P && (unsigned)ih < (unsigned)a.H;
+            const int base = ((wb * a.H + ih) * a.W + iw0) * a.C + ci;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const bool ok = rowok && (unsigned)(iw0 + i * a.stride) < (unsigned)a.W;
+                X[i] = bload(xr, ok ? (base + i * sC) * 4 : kBad);
+            }
+            wow += XBK;
+            while (wow >= a.Wo) {
+                wow -= a.Wo;
+                if (++woh == a.Ho) {
+                    woh = 0;
+                    ++wb;
+                }
+            }
+        } else {
+            int b = fdiv(p0, HoWo, rHoWo);
+            const int rem = p0 - b * HoWo;
+            int oh = fdiv(rem, a.Wo, rWo), ow = rem - oh * a.Wo;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
+                const bool ok = live && rokB && p0 + i < a.P && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+                X[i] = bload(xr, ok ? (((b * a.H + ih) * a.W + iw) * a.C + ci) * 4 : kBad);
+                if (++ow == a.Wo) {
+                    ow = 0;
+                    if (++oh == a.Ho) {
+                        oh = 0;
+                        ++b;
+                    }
+                }
+            }
+        }
+    };
+    // split a 4-pixel x 4-channel micro-tile into 3 planes and store it transposed (per
+    // plane and channel one 8-byte run of 4 consecutive k) — conv_x6_wgrad_kernel's split
+    auto split_store = [&](const float4 (&V)[4], __bf16* L, int P) {
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        float c[3][4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float x[4] = {V[i].x, V[i].y, V[i].z, V[i].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float a0 = trunc16(x[j]), r1 = x[j] - a0, a1 = trunc16(r1);
+                c[0][i][j] = a0;
+                c[1][i][j] = a1;
+                c[2][i][j] = r1 - a1;
+            }
+        }
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                u32x2 q;
+                q.x = hi16x2(c[pl][0][j], c[pl][1][j]);
+                q.y = hi16x2(c[pl][2][j], c[pl][3][j]);
+                *(u32x2*)(L + pl * P + xidx2(row + j, 4 * kq)) = q;
+            }
+    };
+    auto stage = [&](int buf, const float4 (&G)[4], const float4 (&X)[4]) {
+        split_store(G, lds[buf], PA);
+        split_store(X, lds[buf] + 3 * PA, PB);
+    };
+
+    // ---- MFMA waves: 2 x 2, wave tile 64 x 64 ----
+    const int wm = wid >> 1, wn = wid & 1, lr = lane & 31, h = lane >> 5;
+    f32x16 acc[2][2], tot[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) tot[i][jn][e] = 0.f;
+    auto mma = [&](int buf) {
+        const __bf16* L = lds[buf];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
+#pragma unroll
+        for (int s = 0; s < XBK / 16; ++s) {
+            bf16x8 fb[2][3];
+#pragma unroll
+            for (int jn = 0; jn < 2; ++jn) {
+                const int eb = xidx2(wn * 64 + 32 * jn + lr, 16 * s + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fb[jn][pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                bf16x8 fa[3];
+                const int e = xidx2(wm * 64 + 32 * i + lr, 16 * s + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fa[pl] = *(const bf16x8*)(L + pl * PA + e);
+#pragma unroll
+                for (int jn = 0; jn < 2; ++jn) {
+                    // conv_x6_wgrad_kernel's order: x2y0, x1y1, x0y2, x1y0, x0y1, x0y0
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[jn][0], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[jn][1], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[jn][2], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[jn][0], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[jn][1], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[jn][0], acc[i][jn], 0, 0, 0);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int jn = 0; jn < 2; ++jn) tot[i][jn] += acc[i][jn];
+    };
+
+    if (mfma_wave) {
+        lds_sync();   // chunk 0 staged
+        for (int t = 0; t < nchunks; ++t) {
+            mma(t & 1);
+            lds_sync();
+        }
+        float* out = a.y + (size_t)ks * a.M * a.N;
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn) {
+            const int n = n0 + wn * 64 + 32 * jn + lr;
+            if (n >= a.N) continue;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int m = m0 + wm * 64 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    if (m < a.M) out[(size_t)m * a.N + n] = tot[i][jn][e];
+                }
+        }
+        return;
+    }
+    // staging: register set c & 1 holds chunk c; the loop body is unrolled by two so the
+    // sets are static
+    float4 g0[4], x0[4], g1[4], x1[4];
+    load(0, g0, x0);
+    load(1, g1, x1);
+    stage(0, g0, x0);
+    lds_sync();
+    for (int t = 0; t < nchunks; t += 2) {
+        // MFMA waves on chunk t (buffer 0); chunk t+1 into buffer 1, chunk t+2's loads first
+        if (t + 1 < nchunks) {
+            load(t + 2, g0, x0);
+            stage(1, g1, x1);
+        }
+        lds_sync();
+        if (t + 1 >= nchunks) break;
+        // chunk t+1 (buffer 1) being multiplied; chunk t+2 into buffer 0
+        if (t + 2 < nchunks) {
+            load(t + 3, g1, x1);
+            stage(0, g0, x0);
+        }
+        lds_sync();
+    }
+}
+
 // Patch-staged split-bf16 weight gradient (MD2_CONV_X6 | MD2_CONV_PATCH; 3x3, stride 1).
 // conv_x6_wgrad_kernel stages x once per (tap, ci) column, so every activation is
 // fetched and split nine times.  Here a K chunk is one 32-pixel segment of one output
@@ -2598,6 +2817,8 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
         const bool xf = (a.Wo & 3) == 0;   // the x-side pixel walk (conv_x6_wgrad_kernel)
         void (*k)(ConvArgs) = a.bm == 64 ? (xf ? conv_x6_wgrad_kernel<64, true> : conv_x6_wgrad_kernel<64, false>)
                                          : (xf ? conv_x6_wgrad_kernel<128, true> : conv_x6_wgrad_kernel<128, false>);
+        if (a.bm == 128 && (d->flags & MD2_CONV_WS))   // warp-specialised, same results
+            k = xf ? conv_x6wws_kernel<true> : conv_x6wws_kernel<false>;
         hipLaunchKernelGGL(k, grid, dim3(512), 0, st, a);
     } else if (use_x6(d, mode)) {
         // B: the weights split into bf16 planes at the front of the workspace, or

@@ -222,7 +222,9 @@ def test_x6_split_bf16_is_f32_class(B, C, N, k, s, p, H, W):
 def test_x6_warp_specialised_is_bitwise_the_per_tap_kernel(B, C, N, k, s, p, H, W):
     """MD2_CONV_WS (4 MFMA waves + 4 staging waves per block) computes the same products
     in the same order per output as conv_x6_kernel with the same tile height: forward and
-    stride-1 input gradient bitwise equal, K splits, M / N tails, stride 2 included."""
+    stride-1 input gradient bitwise equal, K splits, M / N tails, stride 2 included.  The
+    weight gradient's warp-specialised kernel (conv_x6wws_kernel) likewise against
+    conv_x6_wgrad_kernel<128>, with and without its K split and pixel walk (Wo % 4)."""
     torch.manual_seed(3 + C + N + H)
     x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
     w = (torch.randn(N, C, k, k, device="cuda") / (C * k * k) ** 0.5).contiguous(memory_format=CL)
@@ -232,6 +234,12 @@ def test_x6_warp_specialised_is_bitwise_the_per_tap_kernel(B, C, N, k, s, p, H, 
         if s == 1:
             gy = torch.randn(conv_ops._fwd(x, w, s, p, base).shape, device="cuda").contiguous(memory_format=CL)
             assert torch.equal(conv_ops._dgrad(gy, x, w, p, base | conv_ops.WS), conv_ops._dgrad(gy, x, w, p, base)), extra
+    gy = torch.randn(conv_ops._fwd(x, w, s, p, conv_ops.X6).shape, device="cuda").contiguous(memory_format=CL)
+    for extra in (0, conv_ops.NO_SPLIT):
+        base = conv_ops.X6 | extra
+        gw = conv_ops._wgrad(gy, x, w, s, p, base | conv_ops.WS)
+        assert torch.equal(gw, conv_ops._wgrad(gy, x, w, s, p, base)), ("wgrad", extra)
+        assert torch.equal(gw, conv_ops._wgrad(gy, x, w, s, p, base | conv_ops.WS)), ("wgrad repeat", extra)
 
 
 def test_x6_presplit_planes_match_in_call_split():
