@@ -712,15 +712,17 @@ class _Conv(torch.autograd.Function):
             x6 = _x6_ok(x, w)
             # the patch-staged weight gradient: 3x3, stride 1 (csrc/conv.hip use_x6pw)
             pw = x6 and w.shape[2] == 3 and w.shape[3] == 3 and s == 1
-            # the warp-specialised form of the 128-row x6 tile (csrc/conv.hip conv_x6wws_kernel)
+            # the warp-specialised forms of the 128-row x6 tile, 128 or 256 columns wide
+            # (csrc/conv.hip conv_x6wws_kernel / conv_x6wws256_kernel)
             wsw = x6 and w.shape[0] > 64
             cands = ([lambda: _wgrad(gy, x, w, s, p, X6)] if x6 else []) + \
-                ([lambda: _wgrad(gy, x, w, s, p, X6 | WS)] if wsw else []) + \
+                ([lambda: _wgrad(gy, x, w, s, p, X6 | WS), lambda: _wgrad(gy, x, w, s, p, X6 | WS | BM256)]
+                 if wsw else []) + \
                 ([lambda: _wgrad(gy, x, w, s, p, X6 | PATCH)] if pw else []) + [lambda: _wgrad(gy, x, w, s, p)] + \
                 ([lambda: _direct_wgrad(gy, x, w, p), lambda: _direct_wgrad(gy, x, w, p, X6)] if direct else []) + \
                 [lambda: _miopen_bwd(gy, x, w, s, p, (False, True, False))[1]]
             i = _fastest("wgrad", ctx.key, cands,
-                         (["x6"] if x6 else []) + (["x6ws"] if wsw else []) + (["x6pw"] if pw else []) + ["f32mfma"] +
+                         (["x6"] if x6 else []) + (["x6ws", "x6ws_256"] if wsw else []) + (["x6pw"] if pw else []) + ["f32mfma"] +
                          (["direct", "direct_x6"] if direct else []) + ["miopen"])
             if i < len(cands) - 1:
                 gw = cands[i]()

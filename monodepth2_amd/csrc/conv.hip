@@ -1824,6 +1824,222 @@ __global__ __launch_bounds__(512, 1) void conv_x6wws_kernel(ConvArgs a) {
     }
 }
 
+// Warp-specialised weight gradient with a 256-wide tile (MD2_CONV_X6 | MD2_CONV_WS |
+// MD2_CONV_BM256; more than 64 output channels): a block covers 128 output channels x 256
+// (tap, ci) columns — two taps of a 128-channel layer — so each gy micro-tile staged
+// feeds twice the MFMAs (48 KB fetched per 384 MFMAs instead of 32 KB per 192) and each
+// barrier / pipe drain twice the work.  4 MFMA waves, wave tile 64 x 128 (per 16 k, 6
+// fragment triples for 48 MFMAs: 0.375 reads per MFMA); 4 staging waves, each thread one
+// gy and two x micro-tiles per chunk.  The wave tile's 8 accumulators fill 128 VGPRs, so
+// there is no second accumulation level: the MFMAs sum a whole K split, which the host
+// caps at 64 chunks (2,048 pixels, 128 MFMA k-steps; plan_x6w256) — f32-class against
+// fp64 like the others (tests/test_conv_gpu.py), deterministic, not bitwise the
+// two-level kernels.  LDS: 2 x 72 KB.
+template <bool XFAST>
+__global__ __launch_bounds__(512, 1) void conv_x6wws256_kernel(ConvArgs a) {
+    constexpr int BMW = 128, BNW = 256;
+    constexpr int PA = BMW * XBK, PB = BNW * XBK;
+    __shared__ __bf16 lds[2][3 * (PA + PB)];
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool mfma_wave = wid < 4;
+    int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
+    const int nb = blk % a.nblocks;
+    blk /= a.nblocks;
+    const int mb = blk % a.mblocks, ks = blk / a.mblocks;
+    const int m0 = mb * BMW, n0 = nb * BNW;
+    const int t0 = ks * a.chunks_per_split;
+    const int nchunks = min(a.chunks_per_split, a.nchunks - t0);
+    const int HoWo = a.Ho * a.Wo;
+    const float rHoWo = 1.0f / (float)HoWo, rWo = 1.0f / (float)a.Wo;
+
+    // ---- staging waves: gy rows 4 mq .., x rows 4 mq .. and 128 + 4 mq .., pixels 4 kq .. ----
+    const int st = tid - 256, kq = st & 7, mq = st >> 3, row = 4 * mq;
+    const bool rokA = m0 + row < a.M;
+    bool rokB[2];
+    int ci[2], kh[2], kw[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int nrow = n0 + row + 128 * u;
+        rokB[u] = nrow < a.N;
+        const int tap = nrow / a.C;
+        ci[u] = nrow - tap * a.C;
+        kh[u] = tap / a.KW;
+        kw[u] = tap - kh[u] * a.KW;
+    }
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * 4, 0x00020000);
+    int wb = 0, woh = 0, wow = 0;
+    if (XFAST && !mfma_wave) {
+        const int p = t0 * XBK + 4 * kq;
+        wb = fdiv(p, HoWo, rHoWo);
+        const int rem = p - wb * HoWo;
+        woh = fdiv(rem, a.Wo, rWo);
+        wow = rem - woh * a.Wo;
+    }
+    const int sC = a.stride * a.C;
+    auto load = [&](int t, float4 (&G)[4], float4 (&X)[2][4]) {
+        const int p0 = (t0 + t) * XBK + 4 * kq;
+        const bool live = t < nchunks;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int p = p0 + i;
+            G[i] = bload(gr, (live && rokA && p < a.P) ? (p * a.Cg + m0 + row) * 4 : kBad);
+        }
+        if constexpr (XFAST) {
+            const int oh_s = woh * a.stride - a.pad, ow_s = wow * a.stride - a.pad;
+            const bool pok = live && p0 < a.P;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int ih = oh_s + kh[u], iw0 = ow_s + kw[u];
+                const bool rowok = pok && rokB[u] && (unsigned)ih < (unsigned)a.H;
+                const int base = ((wb * a.H + ih) * a.W + iw0) * a.C + ci[u];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const bool ok = rowok && (unsigned)(iw0 + i * a.stride) < (unsigned)a.W;
+                    X[u][i] = bload(xr, ok ? (base + i * sC) * 4 : kBad);
+                }
+            }
+            wow += XBK;
+            while (wow >= a.Wo) {
+                wow -= a.Wo;
+                if (++woh == a.Ho) {
+                    woh = 0;
+                    ++wb;
+                }
+            }
+        } else {
+            int b = fdiv(p0, HoWo, rHoWo);
+            const int rem = p0 - b * HoWo;
+            int oh = fdiv(rem, a.Wo, rWo), ow = rem - oh * a.Wo;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int ih = oh * a.stride - a.pad + kh[u], iw = ow * a.stride - a.pad + kw[u];
+                    const bool ok = live && rokB[u] && p0 + i < a.P && (unsigned)ih < (unsigned)a.H &&
+                                    (unsigned)iw < (unsigned)a.W;
+                    X[u][i] = bload(xr, ok ? (((b * a.H + ih) * a.W + iw) * a.C + ci[u]) * 4 : kBad);
+                }
+                if (++ow == a.Wo) {
+                    ow = 0;
+                    if (++oh == a.Ho) {
+                        oh = 0;
+                        ++b;
+                    }
+                }
+            }
+        }
+    };
+    auto split_store = [&](const float4 (&V)[4], __bf16* L, int P, int r0) {
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        float c[3][4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float x[4] = {V[i].x, V[i].y, V[i].z, V[i].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float a0 = trunc16(x[j]), r1 = x[j] - a0, a1 = trunc16(r1);
+                c[0][i][j] = a0;
+                c[1][i][j] = a1;
+                c[2][i][j] = r1 - a1;
+            }
+        }
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                u32x2 q;
+                q.x = hi16x2(c[pl][0][j], c[pl][1][j]);
+                q.y = hi16x2(c[pl][2][j], c[pl][3][j]);
+                *(u32x2*)(L + pl * P + xidx2(r0 + j, 4 * kq)) = q;
+            }
+    };
+    auto stage = [&](int buf, const float4 (&G)[4], const float4 (&X)[2][4]) {
+        split_store(G, lds[buf], PA, row);
+        split_store(X[0], lds[buf] + 3 * PA, PB, row);
+        split_store(X[1], lds[buf] + 3 * PA, PB, row + 128);
+    };
+
+    // ---- MFMA waves: 2 x 2, wave tile 64 x 128, one accumulation level ----
+    const int wm = wid >> 1, wn = wid & 1, lr = lane & 31, h = lane >> 5;
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
+    auto mma = [&](int buf) {
+        const __bf16* L = lds[buf];
+#pragma unroll
+        for (int s = 0; s < XBK / 16; ++s) {
+            bf16x8 fa[2][3];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int e = xidx2(wm * 64 + 32 * i + lr, 16 * s + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fa[i][pl] = *(const bf16x8*)(L + pl * PA + e);
+            }
+#pragma unroll
+            for (int jn = 0; jn < 4; ++jn) {
+                bf16x8 fb[3];
+                const int eb = xidx2(wn * 128 + 32 * jn + lr, 16 * s + 8 * h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[0], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[1], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[2], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[0], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[1], acc[i][jn], 0, 0, 0);
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[0], acc[i][jn], 0, 0, 0);
+                }
+            }
+        }
+    };
+
+    if (mfma_wave) {
+        lds_sync();   // chunk 0 staged
+        for (int t = 0; t < nchunks; ++t) {
+            mma(t & 1);
+            lds_sync();
+        }
+        float* out = a.y + (size_t)ks * a.M * a.N;
+#pragma unroll
+        for (int jn = 0; jn < 4; ++jn) {
+            const int n = n0 + wn * 128 + 32 * jn + lr;
+            if (n >= a.N) continue;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int m = m0 + wm * 64 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    if (m < a.M) out[(size_t)m * a.N + n] = acc[i][jn][e];
+                }
+        }
+        return;
+    }
+    float4 g0[4], x0[2][4], g1[4], x1[2][4];
+    load(0, g0, x0);
+    load(1, g1, x1);
+    stage(0, g0, x0);
+    lds_sync();
+    for (int t = 0; t < nchunks; t += 2) {
+        if (t + 1 < nchunks) {
+            load(t + 2, g0, x0);
+            stage(1, g1, x1);
+        }
+        lds_sync();
+        if (t + 1 >= nchunks) break;
+        if (t + 2 < nchunks) {
+            load(t + 3, g1, x1);
+            stage(0, g0, x0);
+        }
+        lds_sync();
+    }
+}
+
 // Patch-staged split-bf16 weight gradient (MD2_CONV_X6 | MD2_CONV_PATCH; 3x3, stride 1).
 // conv_x6_wgrad_kernel stages x once per (tap, ci) column, so every activation is
 // fetched and split nine times.  Here a K chunk is one 32-pixel segment of one output
@@ -2316,14 +2532,18 @@ double split_launch_cost() {
 // autotune tries both); K split by the wave-quantisation model.  The weight-gradient
 // kernel is 128 wide, 64 or 128 rows (co) tall.
 void plan_x6(ConvArgs& a, uint32_t flags, bool wgrad = false) {
-    const int BN = wgrad ? 128 : (a.N <= 16 ? 16 : (a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128)));
+    // the weight gradient's 256-wide warp-specialised tile (conv_x6wws256_kernel): one
+    // accumulation level, so at most 64 chunks per K split
+    const bool w256 = wgrad && a.M > 64 && (flags & MD2_CONV_WS) && (flags & MD2_CONV_BM256) && !(flags & MD2_CONV_BF16);
+    const int BN = wgrad ? (w256 ? 256 : 128) : (a.N <= 16 ? 16 : (a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128)));
     const int BMX = wgrad ? (a.M <= 64 ? 64 : 128) : ((BN == 128 && (flags & MD2_CONV_BM256)) ? 256 : 128);
     const int mblocks = (a.M + BMX - 1) / BMX, nblocks = (a.N + BN - 1) / BN;
     const int base = mblocks * nblocks, res = resident_blocks_x6(BN, BMX);
     int best_s = 1;
     double best_t = 1e30;
-    const int smax = (flags & MD2_CONV_NO_SPLIT) ? 1 : (a.nchunks / 6 > 1 ? a.nchunks / 6 : 1);
-    for (int sp = 1; sp <= smax && sp <= 64; ++sp) {
+    const int smin = w256 ? (a.nchunks + 63) / 64 : 1;
+    const int smax = std::max(smin, (flags & MD2_CONV_NO_SPLIT) ? 1 : (a.nchunks / 6 > 1 ? a.nchunks / 6 : 1));
+    for (int sp = smin; sp <= smax && sp <= std::max(64, smin); ++sp) {
         const int per = (a.nchunks + sp - 1) / sp;
         const int splits = (a.nchunks + per - 1) / per;
         const int rounds = (base * splits + res - 1) / res;
@@ -2331,7 +2551,7 @@ void plan_x6(ConvArgs& a, uint32_t flags, bool wgrad = false) {
         // (splits + 1) M x N floats at ~2.4 KB/cycle chip-wide
         const double red = splits > 1 ? (double)(splits + 1) * a.M * a.N * 4.0 / 2400.0 / 1536.0 + split_launch_cost()
                                       : 0.0;
-        const double t = (double)rounds * per * (BMX / 128.0) + red;
+        const double t = (double)rounds * per * (BMX / 128.0) * (BN / 128 > 1 ? BN / 128 : 1) + red;
         if (t < best_t - 1e-9) {
             best_t = t;
             best_s = splits;
@@ -2819,6 +3039,7 @@ int run(const md2_conv_desc* d, int mode, const float* A, const float* B, float*
                                          : (xf ? conv_x6_wgrad_kernel<128, true> : conv_x6_wgrad_kernel<128, false>);
         if (a.bm == 128 && (d->flags & MD2_CONV_WS))   // warp-specialised, same results
             k = xf ? conv_x6wws_kernel<true> : conv_x6wws_kernel<false>;
+        if (a.bn == 256) k = xf ? conv_x6wws256_kernel<true> : conv_x6wws256_kernel<false>;   // 256-wide tile
         hipLaunchKernelGGL(k, grid, dim3(512), 0, st, a);
     } else if (use_x6(d, mode)) {
         // B: the weights split into bf16 planes at the front of the workspace, or

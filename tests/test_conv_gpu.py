@@ -242,6 +242,33 @@ def test_x6_warp_specialised_is_bitwise_the_per_tap_kernel(B, C, N, k, s, p, H, 
         assert torch.equal(gw, conv_ops._wgrad(gy, x, w, s, p, base | conv_ops.WS)), ("wgrad repeat", extra)
 
 
+@pytest.mark.parametrize("B,C,N,k,s,p,H,W", [(2, 128, 128, 3, 1, 1, 24, 40), (2, 256, 256, 3, 1, 1, 12, 20),
+                                             (2, 64, 128, 3, 2, 1, 23, 39), (2, 64, 128, 1, 2, 0, 24, 40),
+                                             (1, 96, 136, 3, 1, 1, 7, 9), (2, 512, 256, 3, 1, 0, 8, 22),
+                                             (12, 128, 128, 3, 1, 1, 24, 80)])
+def test_x6_wgrad_256_wide_tile_is_f32_class(B, C, N, k, s, p, H, W):
+    """The weight gradient's 256-wide warp-specialised tile (MD2_CONV_WS | MD2_CONV_BM256:
+    two taps of a 128-channel layer per block, one accumulation level over K splits of at
+    most 64 chunks) against fp64: within 3x MIOpen's f32 error and below 2e-6, with and
+    without the split model's choice (NO_SPLIT still splits past 64 chunks), M / N tails,
+    stride 2, the pixel walk off (Wo % 4); bitwise repeatable."""
+    torch.manual_seed(5 + C + N + H)
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=CL)
+    w = (torch.randn(N, C, k, k, device="cuda") / (C * k * k) ** 0.5).contiguous(memory_format=CL)
+    gy = torch.randn(F.conv2d(x, w, None, s, p).shape, device="cuda").contiguous(memory_format=CL)
+    wref = torch.ops.aten.convolution_backward(gy.double().cpu(), x.double().cpu(), w.double().cpu(), None, (s, s),
+                                               (p, p), (1, 1), False, (0, 0), 1, (False, True, False))[1]
+    w_mi = torch.ops.aten.convolution_backward(gy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
+                                               (False, True, False))[1].double().cpu()
+    e_mi = _rel(w_mi, wref)
+    for extra in (0, conv_ops.NO_SPLIT):
+        fl = conv_ops.X6 | conv_ops.WS | conv_ops.BM256 | extra
+        gw = conv_ops._wgrad(gy, x, w, s, p, fl)
+        e = _rel(gw.double().cpu(), wref)
+        assert e < max(3 * e_mi, 1e-7) and e < 2e-6, (extra, e, e_mi)
+        assert torch.equal(gw, conv_ops._wgrad(gy, x, w, s, p, fl)), ("repeat", extra)
+
+
 def test_x6_presplit_planes_match_in_call_split():
     """md2_conv_split_weights (both layouts in one pass) + MD2_CONV_PRESPLIT gives
     bitwise the result of the x6 calls that split the weight themselves."""

@@ -17,7 +17,7 @@ import torch.nn.functional as F  # noqa: E402
 from conv_bench import CL, SHAPES, timeit, wgrad, rel  # noqa: E402
 from monodepth2_amd import _lib  # noqa: E402
 
-X6, P, WS = _lib.CONV_X6, _lib.CONV_PATCH, _lib.CONV_WS
+X6, P, WS, B256 = _lib.CONV_X6, _lib.CONV_PATCH, _lib.CONV_WS, _lib.CONV_BM256
 EXTRA = [("pose.layer2", 24, 128, 128, 3, 1, 1, 24, 80), ("pose.layer4", 24, 512, 512, 3, 1, 1, 6, 20)]
 
 
@@ -34,7 +34,7 @@ def main():
         mi = lambda: torch.ops.aten.convolution_backward(gy, x, w, None, (s, s), (p, p), (1, 1), False, (0, 0), 1,
                                                          (False, True, False))[1]
         ref = mi()
-        tags = [("x6", X6)] + ([("x6ws", X6 | WS)] if N > 64 else []) + ([("x6pw", X6 | P)] if k == 3 and s == 1 else [])
+        tags = [("x6", X6)] + ([("x6ws", X6 | WS), ("x6ws_256", X6 | WS | B256)] if N > 64 else []) + ([("x6pw", X6 | P)] if k == 3 and s == 1 else [])
         for tag, fl in tags:
             row[tag] = round(gf / timeit(lambda: wgrad(gy, x, w, s, p, fl)), 1)
             row["err_" + tag] = float(rel(wgrad(gy, x, w, s, p, fl), ref))
