@@ -849,8 +849,11 @@ class _ConvBF16(torch.autograd.Function):
             # the per-tap GEMM or the patch-staged one (the input rows of a 32-pixel
             # segment staged once for the nine taps), whichever is faster
             pw = w.shape[2] == 3 and w.shape[3] == 3 and s == 1
-            cands = [lambda: _wgrad_bf(gy, x, w, s, p)] + ([lambda: _wgrad_bf(gy, x, w, s, p, BF | PATCH)] if pw else [])
-            gw = cands[_fastest("wgrad_bf16", ctx.key, cands, ["bf16"] + (["bf16pw"] if pw else []))]()
+            w256 = w.shape[0] > 64   # the 256-wide warp-specialised tile (conv_x6wws256_kernel)
+            cands = [lambda: _wgrad_bf(gy, x, w, s, p)] + ([lambda: _wgrad_bf(gy, x, w, s, p, BF | PATCH)] if pw else []) + \
+                ([lambda: _wgrad_bf(gy, x, w, s, p, BF | WS | BM256)] if w256 else [])
+            gw = cands[_fastest("wgrad_bf16", ctx.key, cands,
+                                ["bf16"] + (["bf16pw"] if pw else []) + (["bf16ws_256"] if w256 else []))]()
         return gx, gw, None, None
 
 

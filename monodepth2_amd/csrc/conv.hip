@@ -1834,12 +1834,18 @@ __global__ __launch_bounds__(512, 1) void conv_x6wws_kernel(ConvArgs a) {
 // there is no second accumulation level: the MFMAs sum a whole K split, which the host
 // caps at 64 chunks (2,048 pixels, 128 MFMA k-steps; plan_x6w256) — f32-class against
 // fp64 like the others (tests/test_conv_gpu.py), deterministic, not bitwise the
-// two-level kernels.  LDS: 2 x 72 KB.
-template <bool XFAST>
+// two-level kernels.  LDS: 2 x 72 KB.  BF (MD2_CONV_BF16, config C5): bf16 x / gy
+// repacked into one plane, one MFMA per fragment pair, the output rounded to bf16
+// values (as conv_x6_wgrad_kernel's BF form; tests/test_conv_bf16_gpu.py).
+template <bool XFAST, bool BF = false>
 __global__ __launch_bounds__(512, 1) void conv_x6wws256_kernel(ConvArgs a) {
     constexpr int BMW = 128, BNW = 256;
+    constexpr int NP = BF ? 1 : 3;   // bf16 planes per operand
     constexpr int PA = BMW * XBK, PB = BNW * XBK;
-    __shared__ __bf16 lds[2][3 * (PA + PB)];
+    // chunks per barrier (KS = 2 for bf16 measured 0-8 % slower: the bf16 form is bound
+    // by its LDS traffic — one MFMA per fragment pair — not by the barriers)
+    constexpr int KS = 1, SUB = NP * (PA + PB);
+    __shared__ __bf16 lds[2][KS * SUB];
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool mfma_wave = wid < 4;
     int blk = xcd_contiguous_block(blockIdx.x, gridDim.x);
@@ -1866,8 +1872,14 @@ __global__ __launch_bounds__(512, 1) void conv_x6wws256_kernel(ConvArgs a) {
         kh[u] = tap / a.KW;
         kw[u] = tap - kh[u] * a.KW;
     }
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * 4, 0x00020000);
+    constexpr int ES = BF ? 2 : 4;   // operand element bytes
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.a, 0, a.a_elems * ES, 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc((void*)a.b, 0, a.b_elems * ES, 0x00020000);
+    using VReg = typename std::conditional<BF, uint2, float4>::type;   // 4 channels of one pixel
+    auto ld = [&](__amdgpu_buffer_rsrc_t r, bool ok, int elem) -> VReg {
+        if constexpr (BF) return bload8(r, ok ? elem * 2 : kBad);
+        else return bload(r, ok ? elem * 4 : kBad);
+    };
     int wb = 0, woh = 0, wow = 0;
     if (XFAST && !mfma_wave) {
         const int p = t0 * XBK + 4 * kq;
@@ -1877,13 +1889,13 @@ __global__ __launch_bounds__(512, 1) void conv_x6wws256_kernel(ConvArgs a) {
         wow = rem - woh * a.Wo;
     }
     const int sC = a.stride * a.C;
-    auto load = [&](int t, float4 (&G)[4], float4 (&X)[2][4]) {
+    auto load = [&](int t, VReg (&G)[4], VReg (&X)[2][4]) {
         const int p0 = (t0 + t) * XBK + 4 * kq;
         const bool live = t < nchunks;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int p = p0 + i;
-            G[i] = bload(gr, (live && rokA && p < a.P) ? (p * a.Cg + m0 + row) * 4 : kBad);
+            G[i] = ld(gr, live && rokA && p < a.P, p * a.Cg + m0 + row);
         }
         if constexpr (XFAST) {
             const int oh_s = woh * a.stride - a.pad, ow_s = wow * a.stride - a.pad;
@@ -1896,7 +1908,7 @@ __global__ __launch_bounds__(512, 1) void conv_x6wws256_kernel(ConvArgs a) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const bool ok = rowok && (unsigned)(iw0 + i * a.stride) < (unsigned)a.W;
-                    X[u][i] = bload(xr, ok ? (base + i * sC) * 4 : kBad);
+                    X[u][i] = ld(xr, ok, base + i * sC);
                 }
             }
             wow += XBK;
@@ -1918,7 +1930,7 @@ __global__ __launch_bounds__(512, 1) void conv_x6wws256_kernel(ConvArgs a) {
                     const int ih = oh * a.stride - a.pad + kh[u], iw = ow * a.stride - a.pad + kw[u];
                     const bool ok = live && rokB[u] && p0 + i < a.P && (unsigned)ih < (unsigned)a.H &&
                                     (unsigned)iw < (unsigned)a.W;
-                    X[u][i] = bload(xr, ok ? (((b * a.H + ih) * a.W + iw) * a.C + ci[u]) * 4 : kBad);
+                    X[u][i] = ld(xr, ok, ((b * a.H + ih) * a.W + iw) * a.C + ci[u]);
                 }
                 if (++ow == a.Wo) {
                     ow = 0;
@@ -1930,8 +1942,22 @@ __global__ __launch_bounds__(512, 1) void conv_x6wws256_kernel(ConvArgs a) {
             }
         }
     };
-    auto split_store = [&](const float4 (&V)[4], __bf16* L, int P, int r0) {
+    auto split_store = [&](const VReg (&V)[4], __bf16* L, int P, int r0) {
         typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        if constexpr (BF) {
+            // channel j of pixels (0, 1) and (2, 3): the low / high halves of dword j / 2
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t sel = (j & 1) ? 0x07060302u : 0x05040100u;
+                const uint32_t d0 = (j < 2) ? V[0].x : V[0].y, d1 = (j < 2) ? V[1].x : V[1].y;
+                const uint32_t d2 = (j < 2) ? V[2].x : V[2].y, d3 = (j < 2) ? V[3].x : V[3].y;
+                u32x2 q;
+                q.x = __builtin_amdgcn_perm(d1, d0, sel);
+                q.y = __builtin_amdgcn_perm(d3, d2, sel);
+                *(u32x2*)(L + xidx2(r0 + j, 4 * kq)) = q;
+            }
+            return;
+        } else {
         float c[3][4][4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1953,11 +1979,21 @@ __global__ __launch_bounds__(512, 1) void conv_x6wws256_kernel(ConvArgs a) {
                 q.y = hi16x2(c[pl][2][j], c[pl][3][j]);
                 *(u32x2*)(L + pl * P + xidx2(r0 + j, 4 * kq)) = q;
             }
+        }
     };
-    auto stage = [&](int buf, const float4 (&G)[4], const float4 (&X)[2][4]) {
-        split_store(G, lds[buf], PA, row);
-        split_store(X[0], lds[buf] + 3 * PA, PB, row);
-        split_store(X[1], lds[buf] + 3 * PA, PB, row + 128);
+    // step j = chunks KS j .. KS j + KS - 1 (zeros past the split's last chunk)
+    auto load_step = [&](int j, VReg (&G)[KS][4], VReg (&X)[KS][2][4]) {
+#pragma unroll
+        for (int u = 0; u < KS; ++u) load(KS * j + u, G[u], X[u]);
+    };
+    auto stage = [&](int buf, const VReg (&G)[KS][4], const VReg (&X)[KS][2][4]) {
+#pragma unroll
+        for (int u = 0; u < KS; ++u) {
+            __bf16* L = lds[buf] + u * SUB;
+            split_store(G[u], L, PA, row);
+            split_store(X[u][0], L + NP * PA, PB, row);
+            split_store(X[u][1], L + NP * PA, PB, row + 128);
+        }
     };
 
     // ---- MFMA waves: 2 x 2, wave tile 64 x 128, one accumulation level ----
@@ -1970,38 +2006,45 @@ __global__ __launch_bounds__(512, 1) void conv_x6wws256_kernel(ConvArgs a) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
     auto mma = [&](int buf) {
-        const __bf16* L = lds[buf];
 #pragma unroll
-        for (int s = 0; s < XBK / 16; ++s) {
-            bf16x8 fa[2][3];
+        for (int su = 0; su < KS * XBK / 16; ++su) {
+            const __bf16* L = lds[buf] + (su / (XBK / 16)) * SUB;
+            const int s = su % (XBK / 16);
+            bf16x8 fa[2][NP];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int e = xidx2(wm * 64 + 32 * i + lr, 16 * s + 8 * h);
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) fa[i][pl] = *(const bf16x8*)(L + pl * PA + e);
+                for (int pl = 0; pl < NP; ++pl) fa[i][pl] = *(const bf16x8*)(L + pl * PA + e);
             }
 #pragma unroll
             for (int jn = 0; jn < 4; ++jn) {
-                bf16x8 fb[3];
+                bf16x8 fb[NP];
                 const int eb = xidx2(wn * 128 + 32 * jn + lr, 16 * s + 8 * h);
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) fb[pl] = *(const bf16x8*)(L + 3 * PA + pl * PB + eb);
+                for (int pl = 0; pl < NP; ++pl) fb[pl] = *(const bf16x8*)(L + NP * PA + pl * PB + eb);
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
+                    if constexpr (BF) {
+                        acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[0], acc[i][jn], 0, 0, 0);
+                        continue;
+                    } else {
                     acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[0], acc[i][jn], 0, 0, 0);
                     acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[1], acc[i][jn], 0, 0, 0);
                     acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[2], acc[i][jn], 0, 0, 0);
                     acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[0], acc[i][jn], 0, 0, 0);
                     acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[1], acc[i][jn], 0, 0, 0);
                     acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[0], acc[i][jn], 0, 0, 0);
+                    }
                 }
             }
         }
     };
 
+    const int nsteps = (nchunks + KS - 1) / KS;
     if (mfma_wave) {
-        lds_sync();   // chunk 0 staged
-        for (int t = 0; t < nchunks; ++t) {
+        lds_sync();   // step 0 staged
+        for (int t = 0; t < nsteps; ++t) {
             mma(t & 1);
             lds_sync();
         }
@@ -2015,25 +2058,25 @@ __global__ __launch_bounds__(512, 1) void conv_x6wws256_kernel(ConvArgs a) {
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
                     const int m = m0 + wm * 64 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
-                    if (m < a.M) out[(size_t)m * a.N + n] = acc[i][jn][e];
+                    if (m < a.M) out[(size_t)m * a.N + n] = (BF && a.splits == 1) ? bf16_round(acc[i][jn][e]) : acc[i][jn][e];
                 }
         }
         return;
     }
-    float4 g0[4], x0[2][4], g1[4], x1[2][4];
-    load(0, g0, x0);
-    load(1, g1, x1);
+    VReg g0[KS][4], x0[KS][2][4], g1[KS][4], x1[KS][2][4];
+    load_step(0, g0, x0);
+    load_step(1, g1, x1);
     stage(0, g0, x0);
     lds_sync();
-    for (int t = 0; t < nchunks; t += 2) {
-        if (t + 1 < nchunks) {
-            load(t + 2, g0, x0);
+    for (int t = 0; t < nsteps; t += 2) {
+        if (t + 1 < nsteps) {
+            load_step(t + 2, g0, x0);
             stage(1, g1, x1);
         }
         lds_sync();
-        if (t + 1 >= nchunks) break;
-        if (t + 2 < nchunks) {
-            load(t + 3, g1, x1);
+        if (t + 1 >= nsteps) break;
+        if (t + 2 < nsteps) {
+            load_step(t + 3, g1, x1);
             stage(0, g0, x0);
         }
         lds_sync();
@@ -2534,7 +2577,7 @@ double split_launch_cost() {
 void plan_x6(ConvArgs& a, uint32_t flags, bool wgrad = false) {
     // the weight gradient's 256-wide warp-specialised tile (conv_x6wws256_kernel): one
     // accumulation level, so at most 64 chunks per K split
-    const bool w256 = wgrad && a.M > 64 && (flags & MD2_CONV_WS) && (flags & MD2_CONV_BM256) && !(flags & MD2_CONV_BF16);
+    const bool w256 = wgrad && a.M > 64 && (flags & MD2_CONV_WS) && (flags & MD2_CONV_BM256);
     const int BN = wgrad ? (w256 ? 256 : 128) : (a.N <= 16 ? 16 : (a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128)));
     const int BMX = wgrad ? (a.M <= 64 ? 64 : 128) : ((BN == 128 && (flags & MD2_CONV_BM256)) ? 256 : 128);
     const int mblocks = (a.M + BMX - 1) / BMX, nblocks = (a.N + BN - 1) / BN;
@@ -3000,6 +3043,7 @@ int run_bf(const md2_conv_desc* d, int mode, const void* A, const void* B, void*
         void (*k)(ConvArgs) = a.bm == 64
                                   ? (xf ? conv_x6_wgrad_kernel<64, true, true> : conv_x6_wgrad_kernel<64, false, true>)
                                   : (xf ? conv_x6_wgrad_kernel<128, true, true> : conv_x6_wgrad_kernel<128, false, true>);
+        if (a.bn == 256) k = xf ? conv_x6wws256_kernel<true, true> : conv_x6wws256_kernel<false, true>;   // 256-wide
         hipLaunchKernelGGL(k, grid, dim3(512), 0, st, a);
     } else if (patch) {
         launch_x6p<true>(a, st);

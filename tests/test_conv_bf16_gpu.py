@@ -83,7 +83,8 @@ def test_bf16_kernels_match_fp64(B, C, N, k, s, p, H, W):
             assert gx.dtype == torch.bfloat16
             _check(gx, gx64, ("dgrad", f))
             assert torch.equal(gx, conv_ops._dgrad_bf(gy, x, w, pd, p, f, s)), ("dgrad repeat", f)
-    wflags = [BF] + ([BF | conv_ops.PATCH] if (k == 3 and s == 1) else [])   # per-tap / patch-staged
+    wflags = [BF] + ([BF | conv_ops.PATCH] if (k == 3 and s == 1) else []) + \
+        ([BF | conv_ops.WS | conv_ops.BM256] if N > 64 else [])   # per-tap / patch-staged / 256-wide
     for f in wflags:
         gw = conv_ops._wgrad_bf(gy, x, w, s, p, f)
         assert gw.dtype == torch.float32 and torch.equal(gw, gw.to(torch.bfloat16).float())   # bf16 values
