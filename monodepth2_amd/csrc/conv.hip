@@ -1140,7 +1140,11 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
     constexpr int NW = NT / 64, PIECES = NP * BN / 16;
     constexpr int BQ = (PIECES + NW - 1) / NW;
     constexpr int PA = PP * XBK, PB = BN * XBK;          // bf16 elements per plane
-    __shared__ __bf16 lds[NP * PA + 2 * NP * PB];
+    // taps per barrier: the bf16 form (one MFMA per fragment pair) multiplies three taps'
+    // weight tiles per LDS hand-over (a tap alone is ~128 MFMA cycles per wave, less
+    // than the barrier and DMA round trip around it); the three-plane form one
+    constexpr int TPS = BF ? 3 : 1, NGR = 9 / TPS;
+    __shared__ __bf16 lds[NP * PA + 2 * TPS * NP * PB];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / G::WN, wn = wid % G::WN;
@@ -1218,9 +1222,9 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
             }
         }
     };
-    auto dma = [&](int t, int tap, int buf) {   // B of (chunk t, tap) into buffer buf
+    auto dma = [&](int t, int tap, int slot) {   // B of (chunk t, tap) into B slot `slot`
         const int kofs = tap * a.C + (t0 + t) * XBK, klim = tap * a.C + a.C;
-        char* base = (char*)lds + buf * NP * PB * 2;
+        char* base = (char*)lds + slot * NP * PB * 2;
 #pragma unroll
         for (int j = 0; j < BQ; ++j) {
             if (PIECES % NW && wid + NW * j >= PIECES) break;   // wave-uniform
@@ -1237,8 +1241,13 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
         arow[i] = r;
         acol[i] = c;
     }
-    auto mma = [&](int buf, int tap) {
-        const __bf16* LB = lds + NP * PA + buf * NP * PB;
+    // the TPS taps of group g of chunk t into buffer buf (slots buf TPS ..)
+    auto dma_group = [&](int t, int g, int buf) {
+#pragma unroll
+        for (int u = 0; u < TPS; ++u) dma(t, g * TPS + u, buf * TPS + u);
+    };
+    auto mma = [&](int slot, int tap) {
+        const __bf16* LB = lds + NP * PA + slot * NP * PB;
         const int th = tap / 3, tw = tap - 3 * th, toff = th * PW + tw;
 #pragma unroll
         for (int s = 0; s < XBK / 16; ++s) {
@@ -1271,22 +1280,23 @@ __global__ __launch_bounds__((X6Geo<BN, BMX>::NT), 1) void conv_x6p_kernel(ConvA
     if (NT == 512 && wid >= 4) __builtin_amdgcn_s_setprio(1);   // as conv_x6_kernel
     if (nchunks > 0) {
         load(0);
-        dma(0, 0, 0);
+        dma_group(0, 0, 0);
         store_patch();
         wait_vm<0>();
         lds_sync();
     }
     int buf = 0;
     for (int t = 0; t < nchunks; ++t) {
-        for (int tap = 0; tap < KT; ++tap) {
-            const bool more = tap + 1 < KT || t + 1 < nchunks;
-            if (more) dma(tap + 1 < KT ? t : t + 1, tap + 1 < KT ? tap + 1 : 0, buf ^ 1);
-            // the next patch behind tap 0 (issued after the DMA: waiting for the DMA at the
-            // end of this tap leaves these loads in flight)
-            if (tap == 0 && t + 1 < nchunks) load(t + 1);
-            mma(buf, tap);
+        for (int g = 0; g < NGR; ++g) {
+            const bool more = g + 1 < NGR || t + 1 < nchunks;
+            if (more) dma_group(g + 1 < NGR ? t : t + 1, g + 1 < NGR ? g + 1 : 0, buf ^ 1);
+            // the next patch behind group 0 (issued after the DMA: waiting for the DMA at the
+            // end of this group leaves these loads in flight)
+            if (g == 0 && t + 1 < nchunks) load(t + 1);
+#pragma unroll
+            for (int u = 0; u < TPS; ++u) mma(buf * TPS + u, g * TPS + u);
             asm volatile("" ::: "memory");
-            if (tap == 0 && t + 1 < nchunks) wait_vm<AQP>();
+            if (g == 0 && t + 1 < nchunks) wait_vm<AQP>();
             else wait_vm<0>();
             lds_sync();
             buf ^= 1;
