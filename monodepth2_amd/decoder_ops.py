@@ -130,11 +130,12 @@ class _DispHead(torch.autograd.Function):
         return gP, gw, gb
 
 
-def supports_disp_head(P: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
+def supports_disp_head(P: torch.Tensor, conv: torch.nn.Conv2d, bf16_input: bool = False) -> bool:
     """The fused head takes fp32 NHWC inputs, one output channel, C % 4 == 0,
-    C/4 dividing 256, C <= 256."""
+    C/4 dividing 256, C <= 256 (bf16_input: P is bf16, to be cast up by the caller)."""
     C = P.shape[1]
-    return (P.is_cuda and P.dtype == torch.float32 and conv.weight.dtype == torch.float32
+    want = torch.bfloat16 if bf16_input else torch.float32
+    return (P.is_cuda and P.dtype == want and conv.weight.dtype == torch.float32
             and P.is_contiguous(memory_format=_CL) and conv.out_channels == 1 and conv.bias is not None
             and tuple(conv.kernel_size) == (3, 3) and tuple(conv.padding) == (0, 0)
             and tuple(conv.stride) == (1, 1) and C % 4 == 0 and C <= 256 and 256 % (C // 4) == 0)

@@ -14,6 +14,12 @@ import torch.nn.functional as F
 
 from ..layers import Conv3x3, ConvBlock, upsample
 
+import os
+
+# bf16 autocast: the disparity heads on the fused fp32 head kernels (A/B knob: 0 = the
+# module under autocast, i.e. MIOpen's bf16 convolution + sigmoid)
+_AMP_HEADS = os.environ.get("MD2_AMP_FUSED_HEADS", "1") != "0"
+
 
 class DepthDecoder(nn.Module):
     """5-level skip decoder with sigmoid disparity heads (depth_decoder.py:14-65).
@@ -82,6 +88,13 @@ class DepthDecoder(nn.Module):
                 head = self.convs[("dispconv", i)].conv
                 if self.fused_heads and supports_disp_head(Ph, head) and not torch.is_autocast_enabled():
                     self.outputs[("disp", i)] = disp_head(Ph, head)
+                elif (self.fused_heads and _AMP_HEADS and torch.is_autocast_enabled()
+                        and supports_disp_head(Ph, head, bf16_input=True)):
+                    # bf16 autocast (config C5): the same fused head on the input cast up
+                    # (exact) with the fp32 weight, fp32 disparities out — instead of
+                    # MIOpen's C -> 1 bf16 convolution + a separate sigmoid each way
+                    with torch.autocast("cuda", enabled=False):
+                        self.outputs[("disp", i)] = disp_head(Ph.float(), head)
                 else:
                     self.outputs[("disp", i)] = self.sigmoid(head(Ph))
         return self.outputs
