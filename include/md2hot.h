@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MD2_ABI_VERSION 22
+#define MD2_ABI_VERSION 23
 #define MD2_MAX_SCALES 4
 #define MD2_MAX_SRC 3
 
@@ -260,6 +260,9 @@ int md2_disp_head_bwd(const md2_head_desc* desc, const float* padded, const floa
  * Replaces MIOpen's backward-weights convolution for this layer.
  */
 #define MD2_STEM_WEIGHT_CL (1u << 0)
+/* ABI 23: x and grad_y of md2_stem_wgrad are bf16 (uint16 storage behind the float
+ * pointers; config C5's bf16 autocast stem), channels 3 / 6; grad_weight stays fp32 */
+#define MD2_STEM_BF16 (1u << 1)
 
 typedef struct md2_stem_desc {
     int32_t batch, channels, height, width; /* of the input */

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("MD2_LIB", _BUILT_LIB)
 
 MAX_SCALES = 4
 MAX_SRC = 3
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 NO_SSIM = 1 << 0
 AVG_REPROJECTION = 1 << 1
@@ -150,6 +150,7 @@ class HeadDesc(ctypes.Structure):
 
 
 STEM_WEIGHT_CL = 1 << 0
+STEM_BF16 = 1 << 1   # ABI 23: md2_stem_wgrad on bf16 x / grad_y
 
 
 class StemDesc(ctypes.Structure):

@@ -357,7 +357,7 @@ __device__ __forceinline__ bf16x8 tr_pair(const __bf16* lo, const __bf16* hi) {
 }
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int C>
+template <int C, bool BF = false>
 __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs a) {
     // CP: channels per staged column — 3 padded to 4 (a column pair is then 8-byte
     // aligned for the tr read); 6 unpadded (24-byte column pairs are 8-byte aligned, a
@@ -365,8 +365,13 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
     // 48 instead of 64 n per kernel row for 42 real
     constexpr int CP = C == 3 ? 4 : 6, NB = (7 * CP + 15) / 16;   // n blocks of 16 per kernel row
     constexpr int XE = 7 * kTCols * CP, GE = kTSeg * kCo;
-    __shared__ __attribute__((aligned(16))) __bf16 xs[3][XE];
-    __shared__ __attribute__((aligned(16))) __bf16 gs[3][GE];
+    // BF (MD2_STEM_BF16): x and dy are bf16 (config C5's autocast stem) — staged as they
+    // are into one plane, one MFMA per fragment pair
+    constexpr int NPL = BF ? 1 : 3;
+    __shared__ __attribute__((aligned(16))) __bf16 xs[NPL][XE];
+    __shared__ __attribute__((aligned(16))) __bf16 gs[NPL][GE];
+    const uint16_t* xh = (const uint16_t*)a.x;
+    const uint16_t* gh = (const uint16_t*)a.gy;
     const int tid = threadIdx.x, lane = tid & 63, kh = tid >> 6;
     const int ks = blockIdx.x;
     const int t0 = ks * a.cps, n = min(a.cps, a.nchunks - t0);
@@ -388,6 +393,12 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
         // dy: 64 pixels x 16 channel quads
         for (int i = tid; i < kTSeg * 16; i += kTThreads) {
             const int px = i >> 4, co4 = i & 15, ow = ow0 + px;
+            if constexpr (BF) {
+                uint2 v = {0u, 0u};
+                if (ow < a.Wo) v = *(const uint2*)(gh + ((size_t)(b * a.Ho + oh) * a.Wo + ow) * kCo + 4 * co4);
+                *(u32x2*)&gs[0][tr_goff(px, co4)] = u32x2{v.x, v.y};
+                continue;
+            }
             float4 v = {0.f, 0.f, 0.f, 0.f};
             if (ow < a.Wo) v = *(const float4*)(a.gy + ((size_t)(b * a.Ho + oh) * a.Wo + ow) * kCo + 4 * co4);
             const float e[4] = {v.x, v.y, v.z, v.w};
@@ -401,7 +412,7 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
             }
             const int o = tr_goff(px, co4);
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) *(u32x2*)&gs[pl][o] = u32x2{hi16x2(c[pl][0], c[pl][1]), hi16x2(c[pl][2], c[pl][3])};
+            for (int pl = 0; pl < NPL; ++pl) *(u32x2*)&gs[pl][o] = u32x2{hi16x2(c[pl][0], c[pl][1]), hi16x2(c[pl][2], c[pl][3])};
         }
         if constexpr (CP == 4) {
             // the seven input rows, one column (3 channels + a zero) per task: three
@@ -409,6 +420,16 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
             for (int e = tid; e < 7 * (2 * kTSeg + 6); e += kTThreads) {
                 const int r = e / (2 * kTSeg + 6), col = e - r * (2 * kTSeg + 6);
                 const int ih = 2 * oh - 3 + r, iw = iw0 + col;
+                if constexpr (BF) {
+                    uint32_t h[4] = {0u, 0u, 0u, 0u};
+                    if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
+                        const uint16_t* px = xh + ((size_t)(b * H + ih) * W + iw) * C;
+#pragma unroll
+                        for (int ci = 0; ci < C; ++ci) h[ci] = px[ci];
+                    }
+                    *(u32x2*)&xs[0][(r * kTCols + col) * CP] = u32x2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
+                    continue;
+                }
                 float v[4] = {0.f, 0.f, 0.f, 0.f};
                 if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
                     const float* px = a.x + ((size_t)(b * H + ih) * W + iw) * C;
@@ -426,7 +447,7 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
                     pk[2][j / 2] = hi16x2(r0 - m0, r1 - m1);
                 }
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) *(u32x2*)&xs[pl][o] = pk[pl];
+                for (int pl = 0; pl < NPL; ++pl) *(u32x2*)&xs[pl][o] = pk[pl];
             }
         } else {
             // C = 6: each row's 134 columns x 6 channels are one contiguous run of the
@@ -435,6 +456,24 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
             for (int e = tid; e < 7 * RQ; e += kTThreads) {
                 const int r = e / RQ, k = 4 * (e - r * RQ);
                 const int ih = 2 * oh - 3 + r;
+                if constexpr (BF) {
+                    // four bf16 of the row run (element f0 is even: two 4-byte loads)
+                    uint32_t h[2] = {0u, 0u};
+                    if ((unsigned)ih < (unsigned)H) {
+                        const long long f0 = (long long)iw0 * C + k;
+                        const uint16_t* row = xh + (size_t)(b * H + ih) * W * C;
+                        if (f0 >= 0 && f0 + 4 <= (long long)W * C) {
+                            h[0] = *(const uint32_t*)(row + f0);
+                            h[1] = *(const uint32_t*)(row + f0 + 2);
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i)
+                                if (f0 + i >= 0 && f0 + i < (long long)W * C) h[i / 2] |= (uint32_t)row[f0 + i] << (16 * (i & 1));
+                        }
+                    }
+                    *(u32x2*)&xs[0][r * kTCols * CP + k] = u32x2{h[0], h[1]};
+                    continue;
+                }
                 float v[4] = {0.f, 0.f, 0.f, 0.f};
                 if ((unsigned)ih < (unsigned)H) {
                     const long long f0 = (long long)iw0 * C + k;   // element of the row, may be < 0
@@ -459,14 +498,14 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
                     pk[2][j / 2] = hi16x2(r0 - m0, r1 - m1);
                 }
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) *(u32x2*)&xs[pl][o] = pk[pl];
+                for (int pl = 0; pl < NPL; ++pl) *(u32x2*)&xs[pl][o] = pk[pl];
             }
         }
         __syncthreads();
 #pragma unroll
         for (int kk = 0; kk < kTSeg / 32; ++kk) {
             const int px = 32 * kk + 8 * g16 + q;   // this lane's pixel of the tr reads (and + 4)
-            bf16x8 fb[NB][3];
+            bf16x8 fb[NB][NPL];
 #pragma unroll
             for (int ni = 0; ni < NB; ++ni) {
                 // n0 = kw·CP + ci0: element (2 px + kw)·CP + ci0 = 2 px·CP + n0 of the row
@@ -474,16 +513,20 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
                 const int olo = (kh * kTCols + 2 * px) * CP + n0;
                 const int ohi = (kh * kTCols + 2 * (px + 4)) * CP + n0;
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) fb[ni][pl] = tr_pair(&xs[pl][olo], &xs[pl][ohi]);
+                for (int pl = 0; pl < NPL; ++pl) fb[ni][pl] = tr_pair(&xs[pl][olo], &xs[pl][ohi]);
             }
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi) {
-                bf16x8 fa[3];
+                bf16x8 fa[NPL];
                 const int glo = tr_goff(px, 4 * mi + p4), ghi = tr_goff(px + 4, 4 * mi + p4);
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) fa[pl] = tr_pair(&gs[pl][glo], &gs[pl][ghi]);
+                for (int pl = 0; pl < NPL; ++pl) fa[pl] = tr_pair(&gs[pl][glo], &gs[pl][ghi]);
 #pragma unroll
                 for (int ni = 0; ni < NB; ++ni) {
+                    if constexpr (BF) {
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[ni][0], acc[mi][ni], 0, 0, 0);
+                        continue;
+                    }
                     f32x4 c = acc[mi][ni];
                     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fb[ni][0], c, 0, 0, 0);
                     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[ni][1], c, 0, 0, 0);
@@ -772,6 +815,8 @@ int md2_stem_wgrad(const md2_stem_desc* d, const float* x, const float* grad_y, 
     if (!valid(d)) return md2_report_error(MD2_ERR_ARG, "stem_wgrad: channels 3/6/9, 32-bit element count");
     if (!x || !grad_y || !grad_weight || !workspace) return md2_report_error(MD2_ERR_ARG, "stem_wgrad: NULL operand");
     const bool tr = use_tr(d);
+    if ((d->flags & MD2_STEM_BF16) && !tr)
+        return md2_report_error(MD2_ERR_ARG, "stem_wgrad: bf16 operands (MD2_STEM_BF16) need channels 3 / 6");
     StemArgs a = tr ? plan_tr(d) : plan(d);
     a.x = x;
     a.gy = grad_y;
@@ -780,7 +825,9 @@ int md2_stem_wgrad(const md2_stem_desc* d, const float* x, const float* grad_y, 
     const int NG = a.C / kCG;
     const hipStream_t st = (hipStream_t)stream;
     if (tr) {
-        void (*k)(StemArgs) = a.C == 3 ? stem_x6_wgrad_tr_kernel<3> : stem_x6_wgrad_tr_kernel<6>;
+        const bool bf = (d->flags & MD2_STEM_BF16) != 0;
+        void (*k)(StemArgs) = a.C == 3 ? (bf ? stem_x6_wgrad_tr_kernel<3, true> : stem_x6_wgrad_tr_kernel<3>)
+                                       : (bf ? stem_x6_wgrad_tr_kernel<6, true> : stem_x6_wgrad_tr_kernel<6>);
         hipLaunchKernelGGL(k, dim3(a.splits), dim3(kTThreads), 0, st, a);
     } else {
         void (*k)(StemArgs) =

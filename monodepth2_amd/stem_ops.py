@@ -71,11 +71,14 @@ class _StemConv(torch.autograd.Function):
         return None, gw
 
 
+_WGRAD_BF16 = os.environ.get("MD2_STEM_WGRAD_BF16", "1") != "0"   # A/B knob: 0 = fp32 copies of the operands
+
+
 class _StemConvBF16(torch.autograd.Function):
     """The stem under bf16 autocast (config C5): the forward is autocast's — x and the
     weight cast to bf16, MIOpen's bf16 convolution — and the weight gradient, which MIOpen
-    computes non-deterministically in bf16, runs on md2_stem_wgrad (f32-class split-bf16
-    products, fixed-order reduction) over the exact fp32 values of the bf16 operands, then
+    computes non-deterministically in bf16, runs on md2_stem_wgrad (fixed-order reduction)
+    over the bf16 operands themselves (MD2_STEM_BF16; C = 9: their exact fp32 values), then
     rounded to bf16 as the autocast cast's backward would hand it to the parameter."""
 
     @staticmethod
@@ -90,10 +93,19 @@ class _StemConvBF16(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         xb, = ctx.saved_tensors
-        x = xb.float().contiguous(memory_format=_CL)
-        gy = gy.float().contiguous(memory_format=_CL)
-        B, C, H, W = x.shape
-        d = _lib.StemDesc(B, C, H, W, _lib.STEM_WEIGHT_CL if ctx.w_cl else 0)
+        B, C, H, W = xb.shape
+        flags = _lib.STEM_WEIGHT_CL if ctx.w_cl else 0
+        if C in (3, 6) and gy.dtype == torch.bfloat16 and _WGRAD_BF16:
+            # the bf16 operands as they are (MD2_STEM_BF16, ABI 23): one MFMA per fragment
+            # pair instead of six with five zero planes, no fp32 copies — bitwise the same
+            # sums (the zero planes add exact zeros; tests/test_stem_gpu.py)
+            x = xb.contiguous(memory_format=_CL)
+            gy = gy.contiguous(memory_format=_CL)
+            flags |= _lib.STEM_BF16
+        else:
+            x = xb.float().contiguous(memory_format=_CL)
+            gy = gy.float().contiguous(memory_format=_CL)
+        d = _lib.StemDesc(B, C, H, W, flags)
         gw = torch.empty(ctx.w_shape, device=x.device, dtype=torch.float32,
                          memory_format=_CL if ctx.w_cl else torch.contiguous_format)
         L = _lib.lib()

@@ -75,3 +75,34 @@ def test_stem_falls_back_when_the_input_needs_a_gradient():
     y = stem_conv(conv, x)
     gx, = torch.autograd.grad(y.sum(), x)
     assert gx.shape == x.shape
+
+
+@pytest.mark.parametrize("B,C,H,W", [(2, 3, 64, 128), (3, 6, 30, 50), (1, 6, 7, 9), (2, 6, 192, 640),
+                                     (1, 6, 9, 300), (2, 3, 192, 640)])
+@pytest.mark.parametrize("w_cl", [True, False])
+def test_stem_wgrad_bf16_operands_bitwise_the_fp32_path(B, C, H, W, w_cl):
+    """md2_stem_wgrad with MD2_STEM_BF16 (ABI 23: x and grad_y as bf16, config C5's
+    autocast stem) equals the fp32 path on the same values cast up, bit for bit: a bf16
+    value splits into itself and two zero planes, whose five products add exact zeros in
+    the same accumulation order."""
+    import ctypes
+    from monodepth2_amd import _lib
+    torch.manual_seed(11)
+    CL = torch.channels_last
+    xb = torch.randn(B, C, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    gb = torch.randn(B, 64, Ho, Wo, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    L = _lib.lib()
+    fmt = CL if w_cl else torch.contiguous_format
+
+    def run(x, g, flags):
+        d = _lib.StemDesc(B, C, H, W, flags | (_lib.STEM_WEIGHT_CL if w_cl else 0))
+        gw = torch.empty(64, C, 7, 7, device="cuda", memory_format=fmt)
+        ws = torch.empty(L.md2_stem_wgrad_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device="cuda")
+        _lib.check(L.md2_stem_wgrad(ctypes.byref(d), x.data_ptr(), g.data_ptr(), gw.data_ptr(), ws.data_ptr(),
+                                    _lib.stream(x.device)), "md2_stem_wgrad")
+        return gw
+
+    want = run(xb.float().contiguous(memory_format=CL), gb.float().contiguous(memory_format=CL), 0)
+    got = run(xb, gb, _lib.STEM_BF16)
+    assert torch.equal(got, want)
