@@ -260,8 +260,10 @@ int md2_disp_head_bwd(const md2_head_desc* desc, const float* padded, const floa
  * Replaces MIOpen's backward-weights convolution for this layer.
  */
 #define MD2_STEM_WEIGHT_CL (1u << 0)
-/* ABI 23: x and grad_y of md2_stem_wgrad are bf16 (uint16 storage behind the float
- * pointers; config C5's bf16 autocast stem), channels 3 / 6; grad_weight stays fp32 */
+/* ABI 23: bf16 operands (uint16 storage behind the float pointers; config C5's bf16
+ * autocast stem), channels 3 / 6: md2_stem_wgrad's x and grad_y (grad_weight stays
+ * fp32); md2_stem_fwd's x and y (the fp32 weight rounded to bf16, fp32 accumulation,
+ * y rounded to nearest even) */
 #define MD2_STEM_BF16 (1u << 1)
 
 typedef struct md2_stem_desc {

@@ -83,6 +83,13 @@ __device__ __forceinline__ float trunc16(float x) {
 __device__ __forceinline__ uint32_t hi16x2(float lo, float hi) {
     return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo), 0x07060302u);
 }
+// fp32 -> bf16 bits / the bf16 value as fp32, round to nearest even (torch's cast)
+__device__ __forceinline__ uint16_t f2bf16(float v) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, v);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf16_rne(float v) { return __builtin_bit_cast(float, (uint32_t)f2bf16(v) << 16); }
 // [rows][32 k] bf16 planes with 16-byte quads XOR-swizzled by (row >> 2) & 3 and rows
 // r, r ^ 1 swapped in odd row quads (conv.hip xidx2): conflict-free fragment reads
 // and conflict-free 8-byte stores from lanes covering two adjacent rows
@@ -611,13 +618,17 @@ struct StemFwdArgs {
 // the image or fragments crossing a row end (zeros), pixels past the row (not stored).
 // The (kernel row, k step) loop is unrolled with its fragment loads kPD steps ahead.
 constexpr int kPD = 3;
-template <int C, bool EDGE>
+// BF (MD2_STEM_BF16, config C5): x and y are bf16, the weight image one plane rounded to
+// nearest even (autocast's cast), one MFMA per fragment pair, y rounded once (RNE).
+template <int C, bool EDGE, bool BF = false>
 __device__ __forceinline__ void stem_fwd_tile(const StemFwdArgs& a, const u32x4* __restrict__ wf, int b, int oh,
                                               int ow0, int lane) {
     constexpr int KP = (7 * C + 15) / 16 * 16, S = KP / 16, NQ = 7 * S;
+    constexpr int NPL = BF ? 1 : 3;
     const int lr = lane & 31, h = lane >> 5;
     const int H = a.H, rowlen = a.W * C;
     const float* img = a.x + (size_t)b * H * rowlen;
+    const uint16_t* imgh = (const uint16_t*)a.x + (size_t)b * H * rowlen;
     int base[2];
 #pragma unroll
     for (int p = 0; p < 2; ++p) base[p] = (2 * (ow0 + 32 * p + lr) - 3) * C + 8 * h;
@@ -642,6 +653,39 @@ __device__ __forceinline__ void stem_fwd_tile(const StemFwdArgs& a, const u32x4*
             }
         }
     };
+    // BF: the eight bf16 k values of a pixel group as four packed pairs.  Their first
+    // element (2 ow - 3) C + 8 h + 16 s is odd at C = 3 (two dword-aligned loads, funnel
+    // shifted by 16 bits) and even at C = 6
+    auto load_bf = [&](int q, uint32_t (&r)[2][4]) {
+        const int kh = q / S, s = q - kh * S, ih = 2 * oh - 3 + kh;
+        const bool rowok = !EDGE || (unsigned)ih < (unsigned)H;
+        const uint16_t* rowp = imgh + (size_t)(rowok ? ih : 0) * rowlen;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int o = base[p] + 16 * s;
+            if (!EDGE || (rowok && o >= 1 && o + 9 <= rowlen)) {
+                const uint32_t* dp = (const uint32_t*)(rowp + (o & ~1));
+                const u32x4 d = *(const u32x4*)dp;
+                if constexpr (C % 2 == 1) {   // o odd
+                    const uint32_t d4 = dp[4];
+                    r[p][0] = __builtin_amdgcn_alignbyte(d[1], d[0], 2);
+                    r[p][1] = __builtin_amdgcn_alignbyte(d[2], d[1], 2);
+                    r[p][2] = __builtin_amdgcn_alignbyte(d[3], d[2], 2);
+                    r[p][3] = __builtin_amdgcn_alignbyte(d4, d[3], 2);
+                } else {
+                    r[p][0] = d[0]; r[p][1] = d[1]; r[p][2] = d[2]; r[p][3] = d[3];
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; i += 2) {
+                    const int f = o + i;
+                    const uint32_t lo = (rowok && f >= 0 && f < rowlen) ? rowp[f] : 0u;
+                    const uint32_t hi = (rowok && f + 1 >= 0 && f + 1 < rowlen) ? rowp[f + 1] : 0u;
+                    r[p][i / 2] = lo | (hi << 16);
+                }
+            }
+        }
+    };
     f32x16 acc[2][2];
 #pragma unroll
     for (int p = 0; p < 2; ++p)
@@ -649,6 +693,37 @@ __device__ __forceinline__ void stem_fwd_tile(const StemFwdArgs& a, const u32x4*
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[p][j][e] = 0.f;
+    if constexpr (BF) {
+        uint32_t rb[kPD + 1][2][4];
+#pragma unroll
+        for (int q = 0; q < kPD && q < NQ; ++q) load_bf(q, rb[q]);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            if (q + kPD < NQ) load_bf(q + kPD, rb[(q + kPD) % (kPD + 1)]);
+            const uint32_t (&cur)[2][4] = rb[q % (kPD + 1)];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const bf16x8 fb = __builtin_bit_cast(bf16x8, wf[(q * 2 + j) * 64 + lane]);
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    const bf16x8 fa = __builtin_bit_cast(bf16x8, u32x4{cur[p][0], cur[p][1], cur[p][2], cur[p][3]});
+                    acc[p][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[p][j], 0, 0, 0);
+                }
+            }
+        }
+        uint16_t* yrow = (uint16_t*)a.y + (size_t)(b * a.Ho + oh) * a.Wo * kCo;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int ow = ow0 + 32 * p + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (!EDGE || ow < a.Wo) {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) yrow[(size_t)ow * kCo + 32 * j + lr] = f2bf16(acc[p][j][e]);
+                }
+            }
+        return;
+    }
     float raw[kPD + 1][2][8];
 #pragma unroll
     for (int q = 0; q < kPD && q < NQ; ++q) load(q, raw[q]);
@@ -703,11 +778,12 @@ __device__ __forceinline__ void stem_fwd_tile(const StemFwdArgs& a, const u32x4*
         }
 }
 
-template <int C>
+template <int C, bool BF = false>
 __global__ __launch_bounds__(64 * kFwdWaves, 1) void stem_x6_fwd_kernel(StemFwdArgs a) {
     constexpr int KP = (7 * C + 15) / 16 * 16, S = KP / 16;
     constexpr int NQ = 7 * S;                       // (kernel row, k step) pairs
-    __shared__ u32x4 wf[NQ * 2 * 3 * 64];           // [kh][s][co half][plane][lane] x 8 bf16
+    constexpr int NPL = BF ? 1 : 3;
+    __shared__ u32x4 wf[NQ * 2 * NPL * 64];         // [kh][s][co half][plane][lane] x 8 bf16
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     // the weight fragment image: lane l of fragment (kh, s, j) holds W[kh][16 s + 8 h + i][32 j + l % 32]
 #pragma unroll
@@ -722,15 +798,16 @@ __global__ __launch_bounds__(64 * kFwdWaves, 1) void stem_x6_fwd_kernel(StemFwdA
             float v = 0.f;
             if (k < 7 * C)
                 v = a.w_cl ? a.w[((co * 7 + kh) * 7 + kw) * C + ci] : a.w[((co * C + ci) * 7 + kh) * 7 + kw];
+            if constexpr (BF) v = bf16_rne(v);   // autocast's cast of the weight: plane 0 alone
             const float a0 = trunc16(v), r1 = v - a0, a1 = trunc16(r1);
             c[0][i] = a0;
             c[1][i] = a1;
             c[2][i] = r1 - a1;
         }
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-            wf[((q * 2 + j) * 3 + pl) * 64 + l] = u32x4{hi16x2(c[pl][0], c[pl][1]), hi16x2(c[pl][2], c[pl][3]),
-                                                        hi16x2(c[pl][4], c[pl][5]), hi16x2(c[pl][6], c[pl][7])};
+        for (int pl = 0; pl < NPL; ++pl)
+            wf[((q * 2 + j) * NPL + pl) * 64 + l] = u32x4{hi16x2(c[pl][0], c[pl][1]), hi16x2(c[pl][2], c[pl][3]),
+                                                          hi16x2(c[pl][4], c[pl][5]), hi16x2(c[pl][6], c[pl][7])};
     }
     __syncthreads();
 
@@ -742,10 +819,12 @@ __global__ __launch_bounds__(64 * kFwdWaves, 1) void stem_x6_fwd_kernel(StemFwdA
         const int rr = t / a.nseg, seg = t - rr * a.nseg, b = rr / a.Ho, oh = rr - b * a.Ho;
         const int ow0 = seg * kFwdSeg;
         // interior tile: every window row in the image and every fragment inside its row
+        // (BF at odd C reads one element past a fragment: the funnel shift's extra half)
+        constexpr int XTRA = (BF && (C & 1)) ? 1 : 0;
         const bool inner = 2 * oh - 3 >= 0 && 2 * oh + 3 < a.H && ow0 >= 2 &&
-                           (2 * (ow0 + kFwdSeg - 1) - 3) * C + KP <= a.W * C && ow0 + kFwdSeg <= a.Wo;
-        if (inner) stem_fwd_tile<C, false>(a, wf, b, oh, ow0, lane);
-        else stem_fwd_tile<C, true>(a, wf, b, oh, ow0, lane);
+                           (2 * (ow0 + kFwdSeg - 1) - 3) * C + KP + XTRA <= a.W * C && ow0 + kFwdSeg <= a.Wo;
+        if (inner) stem_fwd_tile<C, false, BF>(a, wf, b, oh, ow0, lane);
+        else stem_fwd_tile<C, true, BF>(a, wf, b, oh, ow0, lane);
     }
 }
 
@@ -859,7 +938,9 @@ int md2_stem_fwd(const md2_stem_desc* d, const float* x, const float* weight, fl
     a.y = y;
     // one block per CU (the weight image fills most of the LDS), tiles walked persistently
     const int blocks = std::min(256, (a.tiles + kFwdWaves - 1) / kFwdWaves);
-    void (*k)(StemFwdArgs) = a.C == 3 ? stem_x6_fwd_kernel<3> : stem_x6_fwd_kernel<6>;
+    const bool bf = (d->flags & MD2_STEM_BF16) != 0;   // bf16 x / y (ABI 23)
+    void (*k)(StemFwdArgs) = a.C == 3 ? (bf ? stem_x6_fwd_kernel<3, true> : stem_x6_fwd_kernel<3>)
+                                      : (bf ? stem_x6_fwd_kernel<6, true> : stem_x6_fwd_kernel<6>);
     hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * kFwdWaves), 0, (hipStream_t)stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MD2_OK : md2_report_error(MD2_ERR_HIP, hipGetErrorString(e));

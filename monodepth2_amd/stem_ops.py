@@ -46,6 +46,24 @@ def _fwd(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     return y
 
 
+def _fwd_bf16(xb: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """The bf16 autocast stem convolution on md2_stem_fwd (MD2_STEM_BF16, ABI 23): bf16 x,
+    the weight rounded to bf16 in the kernel, fp32 accumulation, bf16 y (C = 3 / 6)."""
+    B, C, H, W = xb.shape
+    w_cl = weight.is_contiguous(memory_format=_CL)
+    if not (w_cl or weight.is_contiguous()):
+        weight = weight.contiguous()
+    d = _lib.StemDesc(B, C, H, W, (_lib.STEM_WEIGHT_CL if w_cl else 0) | _lib.STEM_BF16)
+    y = torch.empty((B, 64, (H - 1) // 2 + 1, (W - 1) // 2 + 1), device=xb.device, dtype=torch.bfloat16,
+                    memory_format=_CL)
+    _lib.check(_lib.lib().md2_stem_fwd(ctypes.byref(d), xb.data_ptr(), weight.data_ptr(), y.data_ptr(),
+                                       _lib.stream(xb.device)), "md2_stem_fwd")
+    return y
+
+
+_FWD_BF16 = os.environ.get("MD2_STEM_FWD_BF16", "1") != "0"   # A/B knob: 0 = MIOpen's bf16 forward
+
+
 class _StemConv(torch.autograd.Function):
 
     @staticmethod
@@ -75,8 +93,9 @@ _WGRAD_BF16 = os.environ.get("MD2_STEM_WGRAD_BF16", "1") != "0"   # A/B knob: 0 
 
 
 class _StemConvBF16(torch.autograd.Function):
-    """The stem under bf16 autocast (config C5): the forward is autocast's — x and the
-    weight cast to bf16, MIOpen's bf16 convolution — and the weight gradient, which MIOpen
+    """The stem under bf16 autocast (config C5): the forward is autocast's arithmetic — x
+    and the weight cast to bf16, fp32 accumulation, a bf16 output — on md2_stem_fwd's bf16
+    form (C = 3 / 6; else MIOpen's bf16 convolution), and the weight gradient, which MIOpen
     computes non-deterministically in bf16, runs on md2_stem_wgrad (fixed-order reduction)
     over the bf16 operands themselves (MD2_STEM_BF16; C = 9: their exact fp32 values), then
     rounded to bf16 as the autocast cast's backward would hand it to the parameter."""
@@ -87,6 +106,8 @@ class _StemConvBF16(torch.autograd.Function):
         ctx.save_for_backward(xb)
         ctx.w_cl = weight.is_contiguous(memory_format=_CL)
         ctx.w_shape = weight.shape
+        if _FWD_BF16 and FWD_ENABLED and xb.shape[1] in (3, 6) and xb.is_contiguous(memory_format=_CL):
+            return _fwd_bf16(xb, weight)
         with torch.autocast("cuda", enabled=False):
             return F.conv2d(xb, weight.to(torch.bfloat16), None, 2, 3)
 

@@ -106,3 +106,27 @@ def test_stem_wgrad_bf16_operands_bitwise_the_fp32_path(B, C, H, W, w_cl):
     want = run(xb.float().contiguous(memory_format=CL), gb.float().contiguous(memory_format=CL), 0)
     got = run(xb, gb, _lib.STEM_BF16)
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("B,C,H,W", [(2, 3, 64, 128), (3, 6, 30, 50), (1, 6, 7, 9), (2, 6, 192, 640),
+                                     (1, 3, 9, 300), (2, 3, 192, 640), (1, 3, 1, 1)])
+@pytest.mark.parametrize("w_cl", [True, False])
+def test_stem_fwd_bf16_operands(B, C, H, W, w_cl):
+    """md2_stem_fwd with MD2_STEM_BF16 (ABI 23): the bf16 autocast stem — bf16 x, the
+    weight rounded to bf16, fp32 accumulation, bf16 y — against an fp64 convolution of the
+    same bf16 operands: every element within one bf16 ulp (+ 1e-6 max|ref|) of it, relative
+    L2 within 2.5e-3 (the final rounding), bitwise repeatable."""
+    torch.manual_seed(13)
+    CL = torch.channels_last
+    w = (torch.randn(64, C, 7, 7, device="cuda") / (49 * C) ** 0.5)
+    w = w.contiguous(memory_format=CL) if w_cl else w.contiguous()
+    xb = torch.randn(B, C, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    y = stem_ops._fwd_bf16(xb, w)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=CL)
+    ref = torch.nn.functional.conv2d(xb.double(), w.to(torch.bfloat16).double(), None, 2, 3)
+    g = y.double()
+    rel = float((g - ref).norm() / ref.norm().clamp_min(1e-30))
+    assert rel <= 2.5e-3, rel
+    ulp = ref.abs() * 2.0 ** -7 + 1e-6 * ref.abs().max()
+    assert int(((g - ref).abs() > ulp).sum()) == 0, float((g - ref).abs().max())
+    assert torch.equal(y, stem_ops._fwd_bf16(xb, w))
