@@ -235,6 +235,10 @@ int md2_decoder_pad_bwd2(const md2_pad_desc* desc, const float* x, const float* 
  * Replaces the dispconv Conv3x3 + nn.Sigmoid of the reference decoder.
  */
 #define MD2_HEAD_WEIGHT_CL (1u << 0)
+/* ABI 23: padded / grad_padded are bf16 (uint16 storage behind the float pointers; config
+ * C5's bf16 decoder), widened exactly / rounded to nearest even; weight, bias, disp and
+ * the gradients of the parameters stay fp32 */
+#define MD2_HEAD_BF16 (1u << 1)
 
 typedef struct md2_head_desc {
     int32_t batch, channels, height, width; /* of the unpadded output */

@@ -142,6 +142,7 @@ class PoolDesc(ctypes.Structure):
 
 
 HEAD_WEIGHT_CL = 1 << 0
+HEAD_BF16 = 1 << 1   # ABI 23: bf16 padded input / its gradient
 
 
 class HeadDesc(ctypes.Structure):

@@ -780,6 +780,15 @@ def _bf_planes_for(x, w, stride, pad, need_dg: bool):
     return _bf16_weights(x, w, stride, pad, need_dg)
 
 
+def _w_bf16_view(x, w, stride, pad):
+    """The weight rounded to bf16 as autocast casts it, as a channels_last (N, C, kh, kw)
+    view of its forward plane ([N][kh][kw][C], md2_conv_bf16_weights; from the step's
+    bf16 PlaneBank when it holds this weight)."""
+    N, C, kh, kw = w.shape
+    pf = _bf_planes_for(x, w, stride, pad, False)[0]
+    return pf.view(N, kh, kw, C).permute(0, 3, 1, 2)
+
+
 def _fwd_bf(x, w, plane, stride, pad, flags):
     B, _, H, W = x.shape
     N, _, KH, KW = w.shape
@@ -817,7 +826,7 @@ class _ConvBF16(torch.autograd.Function):
         fl, nm = _bf_flags(Co, Ci, weight.shape[2], stride) if ours else ((), ())
         pf, pd = _bf_planes_for(x, weight, stride, pad, need_dg) if (ours or need_dg) else (None, None)
         cands = [(lambda f=f: _fwd_bf(x, weight, pf, stride, pad, f)) for f in fl] + \
-            [lambda: F.conv2d(x, weight.to(torch.bfloat16), None, stride, pad)]
+            [lambda: F.conv2d(x, _w_bf16_view(x, weight, stride, pad), None, stride, pad)]
         i = _fastest("fwd_bf16", ctx.key, cands, list(nm) + ["miopen"])
         y = cands[i]()
         ctx.save_for_backward(x, weight, pd)
@@ -829,7 +838,6 @@ class _ConvBF16(torch.autograd.Function):
         s, p = ctx.stride, ctx.pad
         gy = gy.contiguous(memory_format=_CL)
         gx = gw = None
-        wb = None
         if ctx.needs_input_grad[0]:
             if pd is not None and s == 1:
                 fl, nm = _bf_flags(w.shape[1], w.shape[0], w.shape[2], 1)
@@ -839,8 +847,9 @@ class _ConvBF16(torch.autograd.Function):
                 cands = [(lambda f=f: _dgrad_bf(gy, x, w, pd, p, f, s)) for f in fl]
             else:
                 fl, nm, cands = (), (), []
-            wb = w.to(torch.bfloat16)
-            cands.append(lambda: _miopen_bwd(gy, x, wb, s, p, (True, False, False))[0])
+            # MIOpen's candidate on the step's bf16 weight plane viewed as the channels_last
+            # bf16 weight (no cast launch per call; only built when it runs)
+            cands.append(lambda: _miopen_bwd(gy, x, _w_bf16_view(x, w, s, p), s, p, (True, False, False))[0])
             gx = cands[_fastest("dgrad_bf16", ctx.key, cands, list(nm) + ["miopen"])]()
         if ctx.needs_input_grad[1]:
             # ours only: MIOpen's bf16 weight gradients are not deterministic (atomics);

@@ -27,6 +27,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "md2_bf16.h"
 #include "md2hot.h"
 
 namespace {
@@ -58,6 +59,28 @@ __device__ __forceinline__ float4 wt_quad(const HeadArgs& a, int tap, int q) {
 }
 
 __device__ __forceinline__ float dot4(float4 u, float4 v) { return u.x * v.x + u.y * v.y + u.z * v.z + u.w * v.w; }
+
+// channel quad i of P (float4 units): fp32, or bf16 (MD2_HEAD_BF16: config C5's bf16
+// decoder activations, widened exactly); gP quads stored likewise (bf16: rounded to
+// nearest even, what autograd's cast of an fp32 gradient back to bf16 gives)
+template <bool BF>
+__device__ __forceinline__ float4 ld_quad(const float* P, unsigned i) {
+    if constexpr (BF) {
+        const uint2 u = reinterpret_cast<const uint2*>(P)[i];
+        return make_float4(md2::bf2f(u.x & 0xffffu), md2::bf2f(u.x >> 16), md2::bf2f(u.y & 0xffffu),
+                           md2::bf2f(u.y >> 16));
+    } else {
+        return reinterpret_cast<const float4*>(P)[i];
+    }
+}
+template <bool BF>
+__device__ __forceinline__ void st_quad(float* G, unsigned i, float4 g) {
+    if constexpr (BF)
+        reinterpret_cast<uint2*>(G)[i] =
+            make_uint2(md2::f2bf(g.x) | (md2::f2bf(g.y) << 16), md2::f2bf(g.z) | (md2::f2bf(g.w) << 16));
+    else
+        reinterpret_cast<float4*>(G)[i] = g;
+}
 
 // L lanes per pixel, QL quads per lane (C = 4·L·QL)
 template <int L, int QL>
@@ -124,7 +147,7 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(HeadArgs a) {
 // for R pixels instead of 9 per pixel — all of them before any arithmetic, then the
 // same tap-ordered dot products, shuffle reduction, bias and sigmoid as head_fwd_kernel
 // (bitwise the same outputs).  MD2_HEAD_ROWWALK=1 keeps the pixel-walk kernel above.
-template <int L, int QL>
+template <int L, int QL, bool BF = false>
 __global__ __launch_bounds__(kThreads) void head_fwd_col_kernel(HeadArgs a) {
     constexpr int Q = L * QL, GPB = kThreads / L, R = QL >= 4 ? 2 : 8 / QL;
     const int Wp = a.w + 2, Hp = a.h + 2;
@@ -143,16 +166,15 @@ __global__ __launch_bounds__(kThreads) void head_fwd_col_kernel(HeadArgs a) {
 #pragma unroll
         for (int k = 0; k < QL; ++k) wr[tap][k] = wt_quad(a, tap, sub + k * L);
     const float bias = a.bias[0];
-    const float4* P4 = reinterpret_cast<const float4*>(a.P) + sub;
     float4 v[R + 2][3][QL];
 #pragma unroll
     for (int r = 0; r < R + 2; ++r) {
         const int Y = y0 + r < Hp ? y0 + r : Hp - 1;   // rows past the image: loaded, not used
-        const unsigned base = ((unsigned)(b * Hp + Y) * Wp + x) * Q;
+        const unsigned base = ((unsigned)(b * Hp + Y) * Wp + x) * Q + sub;
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-            for (int k = 0; k < QL; ++k) v[r][kx][k] = P4[base + kx * Q + k * L];
+            for (int k = 0; k < QL; ++k) v[r][kx][k] = ld_quad<BF>(a.P, base + kx * Q + k * L);
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -173,15 +195,13 @@ __global__ __launch_bounds__(kThreads) void head_fwd_col_kernel(HeadArgs a) {
 // Blocks walk padded rows; a thread owns channel quad q = tid % Q and pixels
 // X = tid / Q + k·(256/Q) of the row.  Dynamic LDS: dz[3][Wp + 2] during the walk,
 // then the per-wave partials [4 waves][min(Q,64)][37].
-template <int Q>
+template <int Q, bool BF = false>
 __global__ __launch_bounds__(kThreads) void head_bwd_kernel(HeadArgs a) {
     extern __shared__ float lds[];
     constexpr int TP = kThreads / Q;            // pixels per pass
     const int Wp = a.w + 2, Hp = a.h + 2;
     const int Ws = Wp + 2;                      // dz row stride: x + 2 for x in [-2, Wp)
     const int q = threadIdx.x % Q, p0 = threadIdx.x / Q;
-    const float4* P4 = reinterpret_cast<const float4*>(a.P);
-    float4* G4 = reinterpret_cast<float4*>(a.gP);
     float4 wq[9];
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) wq[tap] = wt_quad(a, tap, q);
@@ -207,7 +227,7 @@ __global__ __launch_bounds__(kThreads) void head_bwd_kernel(HeadArgs a) {
         const int rowbase = r * Wp;
         for (int X = p0; X < Wp; X += TP) {
             const int i = (rowbase + X) * Q + q;
-            const float4 p = P4[i];
+            const float4 p = ld_quad<BF>(a.P, i);
             float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int ky = 0; ky < 3; ++ky)
@@ -225,7 +245,7 @@ __global__ __launch_bounds__(kThreads) void head_bwd_kernel(HeadArgs a) {
                     dw[tap].w += p.w * dz;
                 }
             if (q == 0) db += lds[Ws + X + 1];      // centre tap: each output pixel once
-            G4[i] = g;
+            st_quad<BF>(a.gP, i, g);
         }
     }
     // lanes with equal q inside a wave: xor-shuffle over the lane bits above Q
@@ -347,16 +367,18 @@ int md2_disp_head_fwd(const md2_head_desc* d, const float* padded, const float* 
         const char* e = getenv("MD2_HEAD_ROWWALK");
         return e && e[0] == '1';
     }();
-    if (!rowwalk) {
+    const bool bf = (d->flags & MD2_HEAD_BF16) != 0;   // bf16 P (ABI 23): the column walk only
+    if (!rowwalk || bf) {
         const int QL = Q > 16 ? Q / 16 : 1, R = QL >= 4 ? 2 : 8 / QL, GPB = kThreads / L;
         const long long tiles = (long long)((a.w + GPB - 1) / GPB) * ((a.h + R - 1) / R) * a.B;
-        void (*kc)(HeadArgs) = Q == 1    ? head_fwd_col_kernel<1, 1>
-                               : Q == 2  ? head_fwd_col_kernel<2, 1>
-                               : Q == 4  ? head_fwd_col_kernel<4, 1>
-                               : Q == 8  ? head_fwd_col_kernel<8, 1>
-                               : Q == 16 ? head_fwd_col_kernel<16, 1>
-                               : Q == 32 ? head_fwd_col_kernel<16, 2>
-                                         : head_fwd_col_kernel<16, 4>;
+        void (*kc)(HeadArgs) = Q == 1    ? (bf ? head_fwd_col_kernel<1, 1, true> : head_fwd_col_kernel<1, 1>)
+                               : Q == 2  ? (bf ? head_fwd_col_kernel<2, 1, true> : head_fwd_col_kernel<2, 1>)
+                               : Q == 4  ? (bf ? head_fwd_col_kernel<4, 1, true> : head_fwd_col_kernel<4, 1>)
+                               : Q == 8  ? (bf ? head_fwd_col_kernel<8, 1, true> : head_fwd_col_kernel<8, 1>)
+                               : Q == 16 ? (bf ? head_fwd_col_kernel<16, 1, true> : head_fwd_col_kernel<16, 1>)
+                               : Q == 32 ? (bf ? head_fwd_col_kernel<16, 2, true> : head_fwd_col_kernel<16, 2>)
+                                         : (bf ? head_fwd_col_kernel<16, 4, true> : head_fwd_col_kernel<16, 4>);
+        if (bf && tiles >= (1ll << 31)) return MD2_ERR_ARG;
         if (tiles < (1ll << 31)) {
             hipLaunchKernelGGL(kc, dim3((unsigned)tiles), dim3(kThreads), 0, (hipStream_t)stream, a);
             return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;
@@ -390,13 +412,14 @@ int md2_disp_head_bwd(const md2_head_desc* d, const float* padded, const float* 
     a.gb = grad_bias;
     const int G = bwd_grid(a);
     const int Q = a.C / 4;
-    void (*k)(HeadArgs) = Q == 1    ? head_bwd_kernel<1>
-                          : Q == 2  ? head_bwd_kernel<2>
-                          : Q == 4  ? head_bwd_kernel<4>
-                          : Q == 8  ? head_bwd_kernel<8>
-                          : Q == 16 ? head_bwd_kernel<16>
-                          : Q == 32 ? head_bwd_kernel<32>
-                                    : head_bwd_kernel<64>;
+    const bool bf = (d->flags & MD2_HEAD_BF16) != 0;
+    void (*k)(HeadArgs) = Q == 1    ? (bf ? head_bwd_kernel<1, true> : head_bwd_kernel<1>)
+                          : Q == 2  ? (bf ? head_bwd_kernel<2, true> : head_bwd_kernel<2>)
+                          : Q == 4  ? (bf ? head_bwd_kernel<4, true> : head_bwd_kernel<4>)
+                          : Q == 8  ? (bf ? head_bwd_kernel<8, true> : head_bwd_kernel<8>)
+                          : Q == 16 ? (bf ? head_bwd_kernel<16, true> : head_bwd_kernel<16>)
+                          : Q == 32 ? (bf ? head_bwd_kernel<32, true> : head_bwd_kernel<32>)
+                                    : (bf ? head_bwd_kernel<64, true> : head_bwd_kernel<64>);
     hipLaunchKernelGGL(k, dim3(G), dim3(kThreads), bwd_lds(a.C, a.w), (hipStream_t)stream, a);
     hipLaunchKernelGGL(head_wgrad_kernel, dim3(9 * a.C + 1), dim3(kThreads), 0, (hipStream_t)stream, a, G);
     return hipGetLastError() == hipSuccess ? MD2_OK : MD2_ERR_HIP;

@@ -104,7 +104,9 @@ class _DispHead(torch.autograd.Function):
         w_cl = weight.is_contiguous(memory_format=_CL)
         if not w_cl:
             weight = weight.contiguous()
-        d = _lib.HeadDesc(B, C, Hp - 2, Wp - 2, _lib.HEAD_WEIGHT_CL if w_cl else 0)
+        # bf16 P (config C5's bf16 decoder): read as is, its gradient written as bf16
+        flags = (_lib.HEAD_WEIGHT_CL if w_cl else 0) | (_lib.HEAD_BF16 if P.dtype == torch.bfloat16 else 0)
+        d = _lib.HeadDesc(B, C, Hp - 2, Wp - 2, flags)
         disp = torch.empty(B, 1, Hp - 2, Wp - 2, device=P.device, dtype=torch.float32)
         rc = _lib.lib().md2_disp_head_fwd(ctypes.byref(d), P.data_ptr(), weight.data_ptr(), bias.data_ptr(),
                                           disp.data_ptr(), _lib.stream(P.device))
@@ -118,7 +120,7 @@ class _DispHead(torch.autograd.Function):
         P, weight, disp = ctx.saved_tensors
         d = ctx.d
         gdisp = gdisp.float().contiguous()
-        gP = torch.empty_like(P, memory_format=_CL)
+        gP = torch.empty_like(P, memory_format=_CL)   # P's dtype: bf16 input, bf16 gradient
         gw = torch.empty_like(weight)        # keeps the weight's memory format
         gb = torch.empty(1, device=P.device, dtype=torch.float32)
         ws = torch.empty(_lib.lib().md2_disp_head_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8,
@@ -143,9 +145,10 @@ def supports_disp_head(P: torch.Tensor, conv: torch.nn.Conv2d, bf16_input: bool 
 
 def disp_head(P: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor:
     """sigmoid(conv(P)) for the decoder's Conv2d(C, 1, 3) disparity head in one HIP
-    pass each way (networks/depth_decoder.py:63-64 dispconv + sigmoid)."""
-    if not supports_disp_head(P, conv):
-        raise ValueError("disp_head: fp32 channels_last input, Conv2d(C, 1, 3) with bias, C/4 dividing 256")
+    pass each way (networks/depth_decoder.py:63-64 dispconv + sigmoid).  P fp32, or bf16
+    (config C5: read as is, fp32 arithmetic and weights, fp32 disparities)."""
+    if not supports_disp_head(P, conv, bf16_input=P.dtype == torch.bfloat16):
+        raise ValueError("disp_head: fp32 / bf16 channels_last input, Conv2d(C, 1, 3) with bias, C/4 dividing 256")
     return _DispHead.apply(P, conv.weight, conv.bias)
 
 

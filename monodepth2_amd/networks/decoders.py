@@ -90,11 +90,12 @@ class DepthDecoder(nn.Module):
                     self.outputs[("disp", i)] = disp_head(Ph, head)
                 elif (self.fused_heads and _AMP_HEADS and torch.is_autocast_enabled()
                         and supports_disp_head(Ph, head, bf16_input=True)):
-                    # bf16 autocast (config C5): the same fused head on the input cast up
-                    # (exact) with the fp32 weight, fp32 disparities out — instead of
-                    # MIOpen's C -> 1 bf16 convolution + a separate sigmoid each way
+                    # bf16 autocast (config C5): the same fused head reading the bf16 input
+                    # (widened exactly; fp32 weight and arithmetic, fp32 disparities, a bf16
+                    # input gradient) — instead of MIOpen's C -> 1 bf16 convolution + a
+                    # separate sigmoid each way
                     with torch.autocast("cuda", enabled=False):
-                        self.outputs[("disp", i)] = disp_head(Ph.float(), head)
+                        self.outputs[("disp", i)] = disp_head(Ph, head)
                 else:
                     self.outputs[("disp", i)] = self.sigmoid(head(Ph))
         return self.outputs

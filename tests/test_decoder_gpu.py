@@ -149,6 +149,31 @@ def test_disp_head_matches_conv_sigmoid(C, h, w, w_cl):
         assert e_ours <= 2 * e_ref + 2e-6 * exact.abs().max().item() + 1e-6, (e_ours, e_ref)
 
 
+@pytest.mark.parametrize("C,h,w", [(16, 96, 320), (32, 48, 160), (64, 24, 80), (128, 12, 40), (4, 5, 7)])
+@pytest.mark.parametrize("w_cl", [True, False])
+def test_disp_head_bf16_input_is_the_fp32_head_on_its_values(C, h, w, w_cl):
+    """MD2_HEAD_BF16 (ABI 23, config C5): the head reading a bf16 padded input equals the
+    fp32 head on the same values widened, bit for bit (disp, weight and bias gradients),
+    and its input gradient is that fp32 gradient rounded to bf16 (nearest even)."""
+    from monodepth2_amd.decoder_ops import disp_head
+    torch.manual_seed(6)
+    CL = torch.channels_last
+    conv = torch.nn.Conv2d(C, 1, 3).cuda()
+    if w_cl:
+        conv = conv.to(memory_format=CL)
+    Pb = torch.randn(3, C, h + 2, w + 2, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    Pb.requires_grad_(True)
+    Pf = Pb.detach().float().contiguous(memory_format=CL).requires_grad_(True)
+    db_, df_ = disp_head(Pb, conv), disp_head(Pf, conv)
+    assert db_.dtype == torch.float32 and torch.equal(db_, df_)
+    g = torch.randn_like(df_)
+    gPb, gwb, gbb = torch.autograd.grad(db_, (Pb, conv.weight, conv.bias), g)
+    gPf, gwf, gbf = torch.autograd.grad(df_, (Pf, conv.weight, conv.bias), g)
+    assert gPb.dtype == torch.bfloat16 and gPb.is_contiguous(memory_format=CL)
+    assert torch.equal(gPb, gPf.to(torch.bfloat16))
+    assert torch.equal(gwb, gwf) and torch.equal(gbb, gbf)
+
+
 @pytest.mark.parametrize("num_layers,H,W,cl", [(18, 64, 128, False), (18, 192, 640, False), (50, 64, 96, False),
                                                (18, 64, 128, True)])
 def test_fused_decoder_matches_eager(num_layers, H, W, cl):
