@@ -595,7 +595,9 @@ def _direct(a: torch.Tensor, wk: torch.Tensor, pad: int, cout: int, flags: int =
     """a (B, C, H, W) channels_last correlated with wk [3][3][C][cout], zero padding `pad`
     (flags X6: the split-bf16 MFMA form, else the f32 VALU form)."""
     B, C, H, W = a.shape
-    y = torch.empty(B, cout, H + 2 * pad - 2, W + 2 * pad - 2, device=a.device, memory_format=_CL)
+    # MD2_CONV_BF16 (with X6): bf16 a and y, the fp32 wk rounded to bf16 in the kernel
+    y = torch.empty(B, cout, H + 2 * pad - 2, W + 2 * pad - 2, device=a.device, memory_format=_CL,
+                    dtype=torch.bfloat16 if flags & BF else torch.float32)
     k = (tuple(a.shape), cout, pad, flags)
     d = _ddescs.get(k)
     if d is None:
@@ -810,6 +812,23 @@ def _wgrad_bf(gy, x, w, stride, pad, flags=BF):
     return gw
 
 
+def _dgrad_mm_bf16(gy: torch.Tensor, wv: torch.Tensor) -> torch.Tensor:
+    """The input gradient of a 1x1 stride-1 bf16 convolution (wv: the (N, C, 1, 1) bf16
+    weight) as one GEMM over the NHWC rows, gx[p][c] = sum_n gy[p][n] wv[n][c] (fp32 accumulation, one rounding), for the
+    shapes our GEMMs do not cover (out_channels % 8: the pose decoder's last layer,
+    256 -> 12).  MIOpen's bf16 input gradient there is not bitwise repeatable (a replay
+    and an eager run of C5's step from one state differed in the pose decoder's bias
+    gradients, tools/miopen_det_check.py); a K = out_channels GEMM has no K split."""
+    B, N, H, W = gy.shape
+    C = wv.shape[1]
+    g2 = gy.permute(0, 2, 3, 1).reshape(B * H * W, N)
+    return torch.mm(g2, wv.permute(0, 2, 3, 1).reshape(N, C)).view(B, H, W, C).permute(0, 3, 1, 2)
+
+
+# A/B knob: MD2_DGRAD_MM=0 leaves those input gradients on MIOpen
+_DGRAD_MM = os.environ.get("MD2_DGRAD_MM", "1") != "0"
+
+
 class _ConvBF16(torch.autograd.Function):
     """y = conv2d(x_bf16, bf16(weight)) with autocast's dtypes: x and y bf16, weight the
     fp32 parameter (its gradient fp32, holding bf16-rounded values)."""
@@ -825,9 +844,12 @@ class _ConvBF16(torch.autograd.Function):
         ours = Ci % 8 == 0
         fl, nm = _bf_flags(Co, Ci, weight.shape[2], stride) if ours else ((), ())
         pf, pd = _bf_planes_for(x, weight, stride, pad, need_dg) if (ours or need_dg) else (None, None)
+        # the decoder's 16-channel full-resolution layers: the direct form (md2_conv_direct)
+        direct = _direct_ok(Ci, Co, weight.shape[2], stride)
         cands = [(lambda f=f: _fwd_bf(x, weight, pf, stride, pad, f)) for f in fl] + \
+            ([lambda: _direct_fwd(x, weight, pad, X6 | BF)] if direct else []) + \
             [lambda: F.conv2d(x, _w_bf16_view(x, weight, stride, pad), None, stride, pad)]
-        i = _fastest("fwd_bf16", ctx.key, cands, list(nm) + ["miopen"])
+        i = _fastest("fwd_bf16", ctx.key, cands, list(nm) + (["direct_bf16"] if direct else []) + ["miopen"])
         y = cands[i]()
         ctx.save_for_backward(x, weight, pd)
         return y
@@ -842,15 +864,23 @@ class _ConvBF16(torch.autograd.Function):
             if pd is not None and s == 1:
                 fl, nm = _bf_flags(w.shape[1], w.shape[0], w.shape[2], 1)
                 cands = [(lambda f=f: _dgrad_bf(gy, x, w, pd, p, f)) for f in fl]
+                if _direct_ok(w.shape[0], w.shape[1], w.shape[2], 1):   # roles swapped
+                    cands.append(lambda: _direct_dgrad(gy, w, p, X6 | BF))
+                    nm = tuple(nm) + ("direct_bf16",)
             elif pd is not None:
                 fl, nm = (BF, BF | S2_ONE), ("bf16_s2", "bf16_s2one")
                 cands = [(lambda f=f: _dgrad_bf(gy, x, w, pd, p, f, s)) for f in fl]
             else:
                 fl, nm, cands = (), (), []
-            # MIOpen's candidate on the step's bf16 weight plane viewed as the channels_last
-            # bf16 weight (no cast launch per call; only built when it runs)
-            cands.append(lambda: _miopen_bwd(gy, x, _w_bf16_view(x, w, s, p), s, p, (True, False, False))[0])
-            gx = cands[_fastest("dgrad_bf16", ctx.key, cands, list(nm) + ["miopen"])]()
+            if not cands and _DGRAD_MM and s == 1 and p == 0 and w.shape[2] == 1 and w.shape[3] == 1:
+                # a 1x1 layer our GEMMs do not cover: the GEMM form only (MIOpen's is not
+                # bitwise repeatable there)
+                gx = _dgrad_mm_bf16(gy, _w_bf16_view(x, w, 1, 0))
+            else:
+                # MIOpen's candidate on the step's bf16 weight plane viewed as the channels_last
+                # bf16 weight (no cast launch per call; only built when it runs)
+                cands.append(lambda: _miopen_bwd(gy, x, _w_bf16_view(x, w, s, p), s, p, (True, False, False))[0])
+                gx = cands[_fastest("dgrad_bf16", ctx.key, cands, list(nm) + ["miopen"])]()
         if ctx.needs_input_grad[1]:
             # ours only: MIOpen's bf16 weight gradients are not deterministic (atomics);
             # a repeat check over a few timing runs does not always catch it (C5's
@@ -859,10 +889,13 @@ class _ConvBF16(torch.autograd.Function):
             # segment staged once for the nine taps), whichever is faster
             pw = w.shape[2] == 3 and w.shape[3] == 3 and s == 1
             w256 = w.shape[0] > 64   # the 256-wide warp-specialised tile (conv_x6wws256_kernel)
+            direct = _direct_ok(w.shape[1], w.shape[0], w.shape[2], s) and w.shape[0] == 16
             cands = [lambda: _wgrad_bf(gy, x, w, s, p)] + ([lambda: _wgrad_bf(gy, x, w, s, p, BF | PATCH)] if pw else []) + \
-                ([lambda: _wgrad_bf(gy, x, w, s, p, BF | WS | BM256)] if w256 else [])
+                ([lambda: _wgrad_bf(gy, x, w, s, p, BF | WS | BM256)] if w256 else []) + \
+                ([lambda: _direct_wgrad(gy, x, w, p, X6 | BF).to(torch.bfloat16).float()] if direct else [])
             gw = cands[_fastest("wgrad_bf16", ctx.key, cands,
-                                ["bf16"] + (["bf16pw"] if pw else []) + (["bf16ws_256"] if w256 else []))]()
+                                ["bf16"] + (["bf16pw"] if pw else []) + (["bf16ws_256"] if w256 else []) +
+                                (["direct_bf16"] if direct else []))]()
         return gx, gw, None, None
 
 

@@ -148,12 +148,21 @@ __device__ __forceinline__ float x6_trunc16(float x) {
 __device__ __forceinline__ uint32_t x6_hi16x2(float lo, float hi) {
     return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo), 0x07060302u);
 }
+// fp32 -> bf16 bits / the bf16 value as fp32, round to nearest even (torch's cast)
+__device__ __forceinline__ uint16_t x6_f2bf(float v) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, v);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float x6_rne(float v) { return __builtin_bit_cast(float, (uint32_t)x6_f2bf(v) << 16); }
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <int CIN, int COUT>
+// BF (MD2_CONV_BF16, config C5): x bf16, the tap-major fp32 weights rounded to bf16 (as
+// autocast casts them) into one plane, one MFMA per fragment pair, y written as bf16 (RNE)
+template <int CIN, int COUT, bool BF = false>
 __global__ __launch_bounds__(kThreads, 2) void conv3_x6_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ wk, float* __restrict__ y,
                                                                int B, int H, int W, int Ho, int Wo, int pad,
@@ -162,11 +171,12 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_kernel(const float* __re
     constexpr int KS = (9 * CIN + 31) / 32, NB = COUT / 16;
     constexpr int NQ = PE / 4;                                      // float4s per patch
     static_assert(kThreads == 64 * kXR, "one wave per output row of the tile");
-    __shared__ u32x2 patch[3][NQ];                                  // 4 bf16 per entry
+    constexpr int NPL = BF ? 1 : 3;
+    __shared__ u32x2 patch[NPL][NQ];                                // 4 bf16 per entry
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int col = lane & 15, g = lane >> 4;
     // the weight fragments: B[k = 32 s + 8 g + j][n = 16 nb + col] = wk[k][n] (k < 9 CIN)
-    bf16x8 wf[KS][NB][3];
+    bf16x8 wf[KS][NB][NPL];
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
@@ -175,14 +185,15 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_kernel(const float* __re
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int k = 32 * s + 8 * g + j;
-                const float v = k < 9 * CIN ? wk[k * COUT + 16 * nb + col] : 0.f;
+                float v = k < 9 * CIN ? wk[k * COUT + 16 * nb + col] : 0.f;
+                if constexpr (BF) v = x6_rne(v);
                 const float a0 = x6_trunc16(v), r1 = v - a0, a1 = x6_trunc16(r1);
                 c[0][j] = a0;
                 c[1][j] = a1;
                 c[2][j] = r1 - a1;
             }
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
+            for (int pl = 0; pl < NPL; ++pl)
                 wf[s][nb][pl] = __builtin_bit_cast(
                     bf16x8, u32x4{x6_hi16x2(c[pl][0], c[pl][1]), x6_hi16x2(c[pl][2], c[pl][3]),
                                   x6_hi16x2(c[pl][4], c[pl][5]), x6_hi16x2(c[pl][6], c[pl][7])});
@@ -195,6 +206,13 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_kernel(const float* __re
         for (int i = tid; i < NQ; i += kThreads) {
             const int pix = i / (CIN / 4), q = i - pix * (CIN / 4), pr = pix / PC, pc = pix - pr * PC;
             const int ih = oh0 - pad + pr, iw = ow0 - pad + pc;
+            if constexpr (BF) {
+                uint2 u = {0u, 0u};
+                if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+                    u = ((const uint2*)x)[((size_t)(b * H + ih) * W + iw) * (CIN / 4) + q];
+                patch[0][i] = u32x2{u.x, u.y};
+                continue;
+            }
             float4 v = {0.f, 0.f, 0.f, 0.f};
             if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
                 v = ((const float4*)x)[((size_t)(b * H + ih) * W + iw) * (CIN / 4) + q];
@@ -208,13 +226,13 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_kernel(const float* __re
                 c[2][j] = r1 - a1;
             }
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) patch[pl][i] = u32x2{x6_hi16x2(c[pl][0], c[pl][1]), x6_hi16x2(c[pl][2], c[pl][3])};
+            for (int pl = 0; pl < NPL; ++pl) patch[pl][i] = u32x2{x6_hi16x2(c[pl][0], c[pl][1]), x6_hi16x2(c[pl][2], c[pl][3])};
         }
         __syncthreads();
         const int oh = oh0 + wid;
         const __bf16* P0 = (const __bf16*)patch[0];
-        const __bf16* P1 = (const __bf16*)patch[1];
-        const __bf16* P2 = (const __bf16*)patch[2];
+        const __bf16* P1 = (const __bf16*)patch[BF ? 0 : 1];
+        const __bf16* P2 = (const __bf16*)patch[BF ? 0 : 2];
 #pragma unroll
         for (int m = 0; m < kXC / 16; ++m) {
             f32x4 acc[NB];
@@ -227,18 +245,24 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_kernel(const float* __re
                 const int k0 = 32 * s + 8 * g, tap = min(k0 / CIN, 8), ci0 = k0 - (k0 / CIN) * CIN;
                 const int kh = tap / 3, kw = tap - kh * 3;
                 const int e = ((wid + kh) * PC + 16 * m + col + kw) * CIN + ci0;
-                bf16x8 fa[3];
+                bf16x8 fa[NPL];
                 fa[0] = *(const bf16x8*)(P0 + e);
-                fa[1] = *(const bf16x8*)(P1 + e);
-                fa[2] = *(const bf16x8*)(P2 + e);
+                if constexpr (BF) {
 #pragma unroll
-                for (int nb = 0; nb < NB; ++nb) {
-                    acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], wf[s][nb][0], acc[nb], 0, 0, 0);
-                    acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wf[s][nb][1], acc[nb], 0, 0, 0);
-                    acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wf[s][nb][2], acc[nb], 0, 0, 0);
-                    acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wf[s][nb][0], acc[nb], 0, 0, 0);
-                    acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wf[s][nb][1], acc[nb], 0, 0, 0);
-                    acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wf[s][nb][0], acc[nb], 0, 0, 0);
+                    for (int nb = 0; nb < NB; ++nb)
+                        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wf[s][nb][0], acc[nb], 0, 0, 0);
+                } else {
+                    fa[1] = *(const bf16x8*)(P1 + e);
+                    fa[2] = *(const bf16x8*)(P2 + e);
+#pragma unroll
+                    for (int nb = 0; nb < NB; ++nb) {
+                        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], wf[s][nb][0], acc[nb], 0, 0, 0);
+                        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wf[s][nb][1], acc[nb], 0, 0, 0);
+                        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wf[s][nb][2], acc[nb], 0, 0, 0);
+                        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], wf[s][nb][0], acc[nb], 0, 0, 0);
+                        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wf[s][nb][1], acc[nb], 0, 0, 0);
+                        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], wf[s][nb][0], acc[nb], 0, 0, 0);
+                    }
                 }
             }
             // D[row = 4 g + i][col]: pixel ow0 + 16 m + 4 g + i, channel 16 nb + col
@@ -247,9 +271,12 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_kernel(const float* __re
                 for (int i = 0; i < 4; ++i) {
                     const int ow = ow0 + 16 * m + 4 * g + i;
                     if (ow < Wo) {
-                        float* yp = y + ((size_t)(b * Ho + oh) * Wo + ow) * COUT + col;
+                        const size_t o = ((size_t)(b * Ho + oh) * Wo + ow) * COUT + col;
 #pragma unroll
-                        for (int nb = 0; nb < NB; ++nb) yp[16 * nb] = acc[nb][i];
+                        for (int nb = 0; nb < NB; ++nb) {
+                            if constexpr (BF) ((uint16_t*)y)[o + 16 * nb] = x6_f2bf(acc[nb][i]);
+                            else y[o + 16 * nb] = acc[nb][i];
+                        }
                     }
                 }
             }
@@ -282,7 +309,8 @@ __device__ __forceinline__ s16x4 tr_read(const __bf16* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
 }
 
-template <int CIN, int TR>
+// BF (MD2_CONV_BF16): x and gy bf16, staged as they are into one plane, one MFMA per pair
+template <int CIN, int TR, bool BF = false>
 __global__ __launch_bounds__(kThreads, 2) void conv3_x6_wgrad_kernel(const float* __restrict__ x,
                                                                      const float* __restrict__ gy,
                                                                      float* __restrict__ part, int B, int H, int W,
@@ -295,8 +323,9 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_wgrad_kernel(const float
     // bf16 per plane; the pixel swizzle permutes within aligned groups of 16 pixels, so the
     // patch plane is padded to whole groups (396 -> 400 pixels)
     constexpr int XE = (PR * PC + 15) / 16 * 16 * CIN, GE = TR * kXC * COUT;
-    __shared__ __attribute__((aligned(16))) __bf16 xs[3][XE];
-    __shared__ __attribute__((aligned(16))) __bf16 gs[3][GE];
+    constexpr int NPL = BF ? 1 : 3;
+    __shared__ __attribute__((aligned(16))) __bf16 xs[BF ? 2 : 3][XE];   // (the wave reduction reuses 2 planes' worth)
+    __shared__ __attribute__((aligned(16))) __bf16 gs[NPL][GE];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int g16 = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
     f32x4 acc[9][CB];
@@ -315,9 +344,10 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_wgrad_kernel(const float
             c[2][j] = r1 - a1;
         }
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
+        for (int pl = 0; pl < NPL; ++pl)
             *(u32x2*)(base + pl * stride + off) = u32x2{x6_hi16x2(c[pl][0], c[pl][1]), x6_hi16x2(c[pl][2], c[pl][3])};
     };
+    auto put_bf = [&](__bf16* base, int off, uint2 u) { *(u32x2*)(base + off) = u32x2{u.x, u.y}; };
     const int ntiles = B * tiles_r * tiles_c;
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int tcb = t % tiles_c, rest = t / tiles_c, trb = rest % tiles_r, b = rest / tiles_r;
@@ -325,17 +355,28 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_wgrad_kernel(const float
         for (int i = tid; i < PR * PC * CIN / 4; i += kThreads) {   // input patch, zeros outside the image
             const int pix = i / (CIN / 4), q4 = i - pix * (CIN / 4), pr = pix / PC, pc = pix - pr * PC;
             const int ih = oh0 - pad + pr, iw = ow0 - pad + pc;
-            float4 v = {0.f, 0.f, 0.f, 0.f};
-            if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-                v = ((const float4*)x)[((size_t)(b * H + ih) * W + iw) * (CIN / 4) + q4];
-            put(&xs[0][0], XE, wg_off<CIN>(pix, q4), v);
+            const bool in = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+            const size_t o = ((size_t)(b * H + ih) * W + iw) * (CIN / 4) + q4;
+            if constexpr (BF) {
+                put_bf(&xs[0][0], wg_off<CIN>(pix, q4), in ? ((const uint2*)x)[o] : uint2{0u, 0u});
+            } else {
+                float4 v = {0.f, 0.f, 0.f, 0.f};
+                if (in) v = ((const float4*)x)[o];
+                put(&xs[0][0], XE, wg_off<CIN>(pix, q4), v);
+            }
         }
         for (int i = tid; i < GE / 4; i += kThreads) {   // output gradient, zeros past the output
             const int pix = i >> 2, q4 = i & 3, pr = pix / kXC, pc = pix - pr * kXC;
             const int oh = oh0 + pr, ow = ow0 + pc;
-            float4 v = {0.f, 0.f, 0.f, 0.f};
-            if (oh < Ho && ow < Wo) v = ((const float4*)gy)[((size_t)(b * Ho + oh) * Wo + ow) * 4 + q4];
-            put(&gs[0][0], GE, wg_off<16>(pix, q4), v);
+            const bool in = oh < Ho && ow < Wo;
+            const size_t o = ((size_t)(b * Ho + oh) * Wo + ow) * 4 + q4;
+            if constexpr (BF) {
+                put_bf(&gs[0][0], wg_off<16>(pix, q4), in ? ((const uint2*)gy)[o] : uint2{0u, 0u});
+            } else {
+                float4 v = {0.f, 0.f, 0.f, 0.f};
+                if (in) v = ((const float4*)gy)[o];
+                put(&gs[0][0], GE, wg_off<16>(pix, q4), v);
+            }
         }
         __syncthreads();
         const int wrow = TR == 4 ? wid : wid >> 1, ks0 = TR == 4 ? 0 : wid & 1;
@@ -343,10 +384,10 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_wgrad_kernel(const float
         for (int kk = 0; kk < KSW; ++kk) {
             const int ks = ks0 + kk;
             // A = gy^T: row co = lane & 15, k = pixel 8 g16 + j of this 32-pixel step
-            bf16x8 fa[3];
+            bf16x8 fa[NPL];
             const int gp = wrow * kXC + 32 * ks + 8 * g16 + q;
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) {
+            for (int pl = 0; pl < NPL; ++pl) {
                 const s16x4 lo = tr_read(&gs[pl][wg_off<16>(gp, p4)]), hi = tr_read(&gs[pl][wg_off<16>(gp + 4, p4)]);
                 fa[pl] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
             }
@@ -356,20 +397,24 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_wgrad_kernel(const float
                 const int xp = (wrow + kh) * PC + 32 * ks + 8 * g16 + q + kw;
 #pragma unroll
                 for (int cb = 0; cb < CB; ++cb) {
-                    bf16x8 fb[3];
+                    bf16x8 fb[NPL];
 #pragma unroll
-                    for (int pl = 0; pl < 3; ++pl) {
+                    for (int pl = 0; pl < NPL; ++pl) {
                         const s16x4 lo = tr_read(&xs[pl][wg_off<CIN>(xp, 4 * cb + p4)]),
                                     hi = tr_read(&xs[pl][wg_off<CIN>(xp + 4, 4 * cb + p4)]);
                         fb[pl] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
                     }
-                    f32x4 c = acc[tap][cb];
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fb[0], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[1], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[2], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[0], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[1], c, 0, 0, 0);
-                    acc[tap][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[0], c, 0, 0, 0);
+                    if constexpr (BF) {
+                        acc[tap][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[0], acc[tap][cb], 0, 0, 0);
+                    } else {
+                        f32x4 c = acc[tap][cb];
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fb[0], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[1], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[2], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[0], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[1], c, 0, 0, 0);
+                        acc[tap][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[0], c, 0, 0, 0);
+                    }
                 }
             }
         }
@@ -379,7 +424,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_wgrad_kernel(const float
     // ((w0 + w1) + w2) + w3, then this block's partial row [co][tap][ci]:
     // D[row = co = 4 g16 + e][col = ci = 16 cb + lane & 15]
     float* red = (float*)&xs[0][0];
-    static_assert(9 * CB * 256 * 4 <= 3 * XE * 2, "reduction buffer fits in the patch planes");
+    static_assert(9 * CB * 256 * 4 <= (BF ? 2 : 3) * XE * 2, "reduction buffer fits in the patch planes");
     for (int w = 0; w < 4; ++w) {
         if (wid == w) {
 #pragma unroll
@@ -564,15 +609,15 @@ int md2_conv_direct(const md2_conv_desc* d, const float* x, const float* wk, flo
         // persistent: as many blocks as fit on a CU (LDS / VGPRs: 4 for 16 -> 16, else 2)
         const long long cap = 256ll * ((ci == 16 && co == 16) ? 4 : 2);
         const dim3 g2((unsigned)(nt < cap ? nt : cap));
-        if (ci == 16 && co == 16)
-            hipLaunchKernelGGL((conv3_x6_kernel<16, 16>), g2, dim3(kThreads), 0, st, x, wk, y, d->batch, d->height,
-                               d->width, Ho, Wo, d->pad, tr, tc);
-        else if (ci == 32 && co == 16)
-            hipLaunchKernelGGL((conv3_x6_kernel<32, 16>), g2, dim3(kThreads), 0, st, x, wk, y, d->batch, d->height,
-                               d->width, Ho, Wo, d->pad, tr, tc);
-        else if (ci == 16 && co == 32)
-            hipLaunchKernelGGL((conv3_x6_kernel<16, 32>), g2, dim3(kThreads), 0, st, x, wk, y, d->batch, d->height,
-                               d->width, Ho, Wo, d->pad, tr, tc);
+        const bool bf = (d->flags & MD2_CONV_BF16) != 0;   // bf16 x / y (config C5)
+        void (*k)(const float*, const float*, float*, int, int, int, int, int, int, int, int) =
+            (ci == 16 && co == 16)   ? (bf ? conv3_x6_kernel<16, 16, true> : conv3_x6_kernel<16, 16>)
+            : (ci == 32 && co == 16) ? (bf ? conv3_x6_kernel<32, 16, true> : conv3_x6_kernel<32, 16>)
+            : (ci == 16 && co == 32) ? (bf ? conv3_x6_kernel<16, 32, true> : conv3_x6_kernel<16, 32>)
+                                     : nullptr;
+        if (k)
+            hipLaunchKernelGGL(k, g2, dim3(kThreads), 0, st, x, wk, y, d->batch, d->height, d->width, Ho, Wo, d->pad,
+                               tr, tc);
         else
             return md2_report_error(MD2_ERR_ARG, "conv_direct: (in, out) channels (16,16), (32,16) or (16,32)");
         const hipError_t e = hipGetLastError();
@@ -641,15 +686,13 @@ int md2_conv_wgrad_direct(const md2_conv_desc* d, const float* x, const float* g
         const long long nt = (long long)d->batch * tr * tc;
         const int nb = (int)(nt < kWBlocks ? nt : kWBlocks);
         float* part = (float*)workspace;
-        if (d->in_channels == 16 && TRW == 4)
-            hipLaunchKernelGGL((conv3_x6_wgrad_kernel<16, 4>), dim3(nb), dim3(kThreads), 0, st0, x, grad_y, part,
-                               d->batch, d->height, d->width, Ho, Wo, d->pad, tr, tc);
-        else if (d->in_channels == 16)
-            hipLaunchKernelGGL((conv3_x6_wgrad_kernel<16, 2>), dim3(nb), dim3(kThreads), 0, st0, x, grad_y, part,
-                               d->batch, d->height, d->width, Ho, Wo, d->pad, tr, tc);
-        else
-            hipLaunchKernelGGL((conv3_x6_wgrad_kernel<32, 2>), dim3(nb), dim3(kThreads), 0, st0, x, grad_y, part,
-                               d->batch, d->height, d->width, Ho, Wo, d->pad, tr, tc);
+        const bool bf = (d->flags & MD2_CONV_BF16) != 0;   // bf16 x / grad_y (config C5)
+        void (*k)(const float*, const float*, float*, int, int, int, int, int, int, int, int) =
+            (d->in_channels == 16 && TRW == 4) ? (bf ? conv3_x6_wgrad_kernel<16, 4, true> : conv3_x6_wgrad_kernel<16, 4>)
+            : d->in_channels == 16             ? (bf ? conv3_x6_wgrad_kernel<16, 2, true> : conv3_x6_wgrad_kernel<16, 2>)
+                                               : (bf ? conv3_x6_wgrad_kernel<32, 2, true> : conv3_x6_wgrad_kernel<32, 2>);
+        hipLaunchKernelGGL(k, dim3(nb), dim3(kThreads), 0, st0, x, grad_y, part, d->batch, d->height, d->width, Ho, Wo,
+                           d->pad, tr, tc);
         const int n = 16 * 9 * d->in_channels;
         hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3((n + kRedO - 1) / kRedO), dim3(kThreads), 0, st0, part,
                            grad_weight, n, nb);

@@ -95,7 +95,7 @@ def test_bf16_kernels_match_fp64(B, C, N, k, s, p, H, W):
     assert float((ym - y64).norm() / y64.norm()) <= 5e-3
 
 
-@pytest.mark.parametrize("B,C,N,k,s,p,H,W", [SHAPES[0], SHAPES[3], SHAPES[6], SHAPES[8]])
+@pytest.mark.parametrize("B,C,N,k,s,p,H,W", [SHAPES[0], SHAPES[3], SHAPES[6], SHAPES[8], SHAPES[9]])
 def test_bf16_autocast_conv_through_conv_ops(B, C, N, k, s, p, H, W, monkeypatch):
     """conv_ops.conv2d under bf16 autocast: the output and both gradients of the
     production path (autotuned against MIOpen; a non-repeatable candidate never kept)
@@ -123,3 +123,36 @@ def test_bf16_autocast_conv_through_conv_ops(B, C, N, k, s, p, H, W, monkeypatch
     _check(gx, gx64, "dgrad")   # the cast's backward: the bf16 gradient as fp32
     _check(gw, gw64, "wgrad")
     assert "fwd_bf16" in {k[0] for k in conv_ops._choice}
+    if k == 1 and N % 8:   # pose_2: the input gradient on the GEMM form (_dgrad_mm_bf16), not timed
+        assert ("dgrad_bf16", (B, C, H, W), (N, C, k, k), s, p) not in conv_ops._choice
+
+
+@pytest.mark.parametrize("B,C,N,p,H,W", [(2, 16, 16, 0, 18, 34), (2, 32, 16, 0, 18, 34), (2, 16, 32, 0, 18, 34),
+                                         (3, 16, 16, 1, 20, 70), (2, 32, 16, 1, 9, 11)])
+def test_bf16_direct_16_channel_forms(B, C, N, p, H, W):
+    """md2_conv_direct / md2_conv_wgrad_direct with MD2_CONV_X6 | MD2_CONV_BF16 (the
+    decoder's 16-channel full-resolution layers under autocast): forward, input gradient
+    (roles swapped, flipped weight) and weight gradient within the bars above of the fp64
+    convolution of the same bf16 operands; bitwise repeatable."""
+    from monodepth2_amd.conv_ops import _direct_dgrad, _direct_fwd, _direct_ok, _direct_wgrad, X6
+    x, w = _case(B, C, N, 3, 1, p, H, W)
+    wb = _rne(w)
+    x64, w64 = x.double(), wb.double()
+    if _direct_ok(C, N, 3, 1):
+        y = _direct_fwd(x, w, p, X6 | BF)
+        assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=CL)
+        _check(y, F.conv2d(x64, w64, None, 1, p), "fwd")
+        assert torch.equal(y, _direct_fwd(x, w, p, X6 | BF))
+    y64 = F.conv2d(x64, w64, None, 1, p)
+    gy = _rne(torch.randn(y64.shape, device="cuda")).contiguous(memory_format=CL)
+    gx64, gw64 = torch.ops.aten.convolution_backward(gy.double(), x64, w64, None, (1, 1), (p, p), (1, 1), False,
+                                                     (0, 0), 1, (True, True, False))[:2]
+    if _direct_ok(N, C, 3, 1):
+        gx = _direct_dgrad(gy, w, p, X6 | BF)
+        assert gx.dtype == torch.bfloat16
+        _check(gx, gx64, "dgrad")
+        assert torch.equal(gx, _direct_dgrad(gy, w, p, X6 | BF))
+    if _direct_ok(C, N, 3, 1) and N == 16:
+        gw = _direct_wgrad(gy, x, w, p, X6 | BF)
+        _check(gw.to(torch.bfloat16).float(), gw64, "wgrad")
+        assert torch.equal(gw, _direct_wgrad(gy, x, w, p, X6 | BF))

@@ -1,11 +1,15 @@
-# round 6: bf16 head input (ABI 23) + the bf16 weight plane for MIOpen candidates — tests + C5 line
+# round 6: bf16 direct convolutions for the decoder's 16-channel layers + the GEMM-form pose_2
+# input gradient (C5) — determinism check, tests, C5 A/B
 set -o pipefail
-OUT=gpurun_out/r6hb
+OUT=gpurun_out/r6db
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests/test_decoder_gpu.py tests/test_conv_bf16_gpu.py tests/test_trainer_gpu.py -x -q -k "head or bf16" --timeout 300 --timeout-method thread > $OUT/test.log 2>&1 || { tail -30 $OUT/test.log; exit 1; }
+
+
+timeout -k 10 700 python -u -m pytest tests/test_conv_bf16_gpu.py tests/test_trainer_gpu.py -x -q -k "bf16" --timeout 300 --timeout-method thread > $OUT/test.log 2>&1 || { tail -30 $OUT/test.log; exit 1; }
 tail -1 $OUT/test.log
 for r in 1 2; do
   timeout -k 10 300 python -u bench.py --amp bf16 --batch 32 --steps 20 --warmup 5 --no-cpu-baseline --pmc 0 --no-eager-aten > $OUT/on_$r.json 2>/dev/null || exit 1
+  MD2_CONV_EXCLUDE=direct_bf16 timeout -k 10 300 python -u bench.py --amp bf16 --batch 32 --steps 20 --warmup 5 --no-cpu-baseline --pmc 0 --no-eager-aten > $OUT/off_$r.json 2>/dev/null || exit 1
   python3 -c "import json,sys
-for f in sys.argv[1:]: d=json.loads(open(f).read().strip().splitlines()[-1]); print(f, d['ms_per_step'], d['loss_delta_vs_oracle'])" $OUT/on_$r.json
+for f in sys.argv[1:]: d=json.loads(open(f).read().strip().splitlines()[-1]); print(f, d['ms_per_step'], d['loss_delta_vs_oracle'])" $OUT/on_$r.json $OUT/off_$r.json
 done
