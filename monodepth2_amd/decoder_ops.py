@@ -187,6 +187,46 @@ class _BiasAct(torch.autograd.Function):
         return gz, gb, None
 
 
+class _BiasActBF16(torch.autograd.Function):
+    """[relu](z + bf16(b)) for config C5's bf16 pose decoder, autocast's arithmetic forward
+    (one bf16 add, the ReLU); backward on md2_bias_act_bwd over the exact fp32 widening of
+    the bf16 operands: the ReLU mask (bitwise torch's threshold_backward on the bf16 values)
+    and the bias gradient as a fixed-order fp32 sum, rounded to bf16 as autocast's bf16 sum
+    leaves it.  The bias gradient was ATen's bf16 sum before: inside C5's captured step its
+    value changed between replays of one state (~20 of pose_0's 256 channels by one bf16
+    ulp, 1 replay in 2; tools/c5_replay_diag.py), the only non-repeatable gradient there."""
+
+    @staticmethod
+    def forward(ctx, z, bias, relu: bool):
+        y = z + bias.to(torch.bfloat16).view(1, -1, 1, 1)
+        if relu:
+            y = torch.relu(y)
+        ctx.save_for_backward(y if relu else None)
+        ctx.relu = relu
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        y, = ctx.saved_tensors
+        relu = ctx.relu
+        B, C, H, W = gy.shape
+        g32 = gy.float().contiguous(memory_format=_CL)
+        y32 = y.float().contiguous(memory_format=_CL) if relu else None
+        d = _lib.BiasActDesc(B * H * W, C, _lib.BIAS_ACT_RELU if relu else 0)
+        gb = torch.empty(C, device=gy.device, dtype=torch.float32)
+        gz32 = torch.empty_like(g32, memory_format=_CL) if relu else None
+        L = _lib.lib()
+        ws = torch.empty(L.md2_bias_act_workspace_bytes(ctypes.byref(d)), dtype=torch.uint8, device=gy.device)
+        _lib.check(L.md2_bias_act_bwd(ctypes.byref(d), y32.data_ptr() if relu else None, g32.data_ptr(),
+                                      gz32.data_ptr() if relu else None, gb.data_ptr(), ws.data_ptr(),
+                                      _lib.stream(gy.device)), "md2_bias_act_bwd")
+        gz = gz32.to(torch.bfloat16) if relu else gy
+        return gz, gb.to(torch.bfloat16).float(), None
+
+
+_BF16_BIAS_ACT = os.environ.get("MD2_BF16_BIAS_ACT", "1") != "0"   # A/B knob: 0 = ATen's add / relu / sum
+
+
 def conv_bias_act(conv: torch.nn.Conv2d, x: torch.Tensor, relu: bool) -> torch.Tensor:
     """relu?(conv(x)) for the pose decoder (networks/pose_decoder.py:43-54): the
     convolution bias-free on conv_ops (split-bf16 MFMA kernels chosen per shape against
@@ -211,6 +251,8 @@ def conv_bias_act(conv: torch.nn.Conv2d, x: torch.Tensor, relu: bool) -> torch.T
         # deterministic weight gradient), the bf16-cast bias added as autocast's conv
         # would, then the ReLU
         z = conv_ops.conv2d_bf16(x, conv.weight, conv.stride[0], conv.padding[0])
+        if _BF16_BIAS_ACT and z.is_contiguous(memory_format=_CL) and conv.out_channels % 4 == 0:
+            return _BiasActBF16.apply(z, conv.bias, relu)
         z = z + conv.bias.to(torch.bfloat16).view(1, -1, 1, 1)
         return F.relu(z) if relu else z
     y = conv(x)

@@ -34,6 +34,12 @@ class _PoseToT(torch.autograd.Function):
     def backward(ctx, gT):
         aa, tr = ctx.saved_tensors
         gT = gT.contiguous()
+        # dL/dT comes from the loss backward on the main stream; this runs on the pose
+        # stream.  Mark its block in use here, or the allocator hands it back to the main
+        # stream once this node has been enqueued — inside a captured step a later
+        # main-stream allocation then shares its address with no order against this read
+        # (C5 replays' pose-decoder bias gradients differed by a bf16 ulp, 1 run in 2)
+        gT.record_stream(torch.cuda.current_stream(gT.device))
         gaa, gtr = torch.empty_like(aa), torch.empty_like(tr)
         st = _lib.stream(aa.device)
         _lib.check(_lib.lib().md2_pose_bwd(aa.shape[0], aa.shape[1], ctx.mask, aa.data_ptr(), tr.data_ptr(),
@@ -61,6 +67,12 @@ class _Pose6ToT(torch.autograd.Function):
     def backward(ctx, gT):
         aa, tr = ctx.saved_tensors
         gT = gT.contiguous()
+        # dL/dT comes from the loss backward on the main stream; this runs on the pose
+        # stream.  Mark its block in use here, or the allocator hands it back to the main
+        # stream once this node has been enqueued — inside a captured step a later
+        # main-stream allocation then shares its address with no order against this read
+        # (C5 replays' pose-decoder bias gradients differed by a bf16 ulp, 1 run in 2)
+        gT.record_stream(torch.cuda.current_stream(gT.device))
         gaa, gtr = torch.empty_like(aa), torch.empty_like(tr)
         st = _lib.stream(aa.device)
         _lib.check(_lib.lib().md2_pose_bwd(aa.shape[0], aa.shape[1], ctx.mask, aa.data_ptr(), tr.data_ptr(),

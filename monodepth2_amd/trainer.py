@@ -120,6 +120,12 @@ class _Networks(nn.Module):
         return trainer._run_networks(self.models, inputs)
 
 
+# diagnosis knobs (C5 graph-replay determinism): the logging maps on the main stream,
+# the pose stream joined to the main one before the backward, the pose network second
+_LOGMAPS_SIDE = os.environ.get("MD2_LOGMAPS_SIDE", "1") != "0"
+_JOIN_BEFORE_BWD = os.environ.get("MD2_JOIN_BEFORE_BWD", "0") == "1"
+_POSE_LAST = os.environ.get("MD2_POSE_LAST", "0") == "1"
+
 class Trainer:
     def __init__(self, options, device: Optional[torch.device] = None, rank: int = 0, world_size: int = 1):
         self.opt = options
@@ -289,7 +295,7 @@ class Trainer:
         # enqueued LAST has its backward enqueued FIRST.  pose_last: the pose network
         # goes second, its backward (needing only dL/dT from the loss) goes onto its
         # stream before the host spends its time enqueuing the depth backward.
-        pose_last = side is not None and getattr(self, "pose_last", False)
+        pose_last = side is not None and (getattr(self, "pose_last", False) or _POSE_LAST)
         inputs_ready = None
         if pose_last:   # the pose stream waits for the inputs only, not the depth forward
             inputs_ready = torch.cuda.Event()
@@ -485,7 +491,7 @@ class Trainer:
             # here until the hot path's backward hands it dL/dT, instead of delaying that
             # backward on the main stream (_step_body joins the pose stream after backward)
             C = self.hot.noise_channels()
-            side = self._pose_stream if (self._in_step and self.use_pose_net) else None
+            side = (self._pose_stream if (self._in_step and self.use_pose_net and _LOGMAPS_SIDE) else None)
             if side is not None:
                 main = torch.cuda.current_stream(self.device)
                 side.wait_stream(main)
@@ -532,6 +538,8 @@ class Trainer:
                 self.flat_sync.zero()
             else:
                 self.model_optimizer.zero_grad(set_to_none=True)
+            if _JOIN_BEFORE_BWD and self._pose_stream is not None and self.use_pose_net:
+                self._pose_stream.wait_stream(torch.cuda.current_stream(self.device))
             losses["loss"].backward()
             if self._pose_stream is not None and self.use_pose_net:
                 # the pose stream's work of this step (its backward, the logging maps of

@@ -260,3 +260,34 @@ def test_conv_bias_act_matches_eager(cin, cout, k, relu):
     exp = torch.autograd.grad(ref, (x, conv.weight, conv.bias), g)
     for a, b in zip(got, exp):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("relu,C", [(True, 256), (False, 12)])
+def test_bf16_bias_act_matches_autocast(relu, C):
+    """decoder_ops._BiasActBF16 (C5's pose decoder bias + ReLU): the forward bitwise
+    autocast's bf16 add + ReLU, the input gradient bitwise torch's threshold_backward, the
+    bias gradient within one bf16 ulp of the fp64 sum of the same bf16 gradient; bitwise
+    repeatable."""
+    from monodepth2_amd.decoder_ops import _BiasActBF16
+    torch.manual_seed(C)
+    z = torch.randn(4, C, 6, 20, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(C, device="cuda")
+    g = torch.randn(z.shape, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+    def ours():
+        zz, bb = z.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        y = _BiasActBF16.apply(zz, bb, relu)
+        gz, gb = torch.autograd.grad(y, [zz, bb], g)
+        return y, gz, gb
+
+    zz, bb = z.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = zz + bb.to(torch.bfloat16).view(1, -1, 1, 1)
+    yr = torch.relu(yr) if relu else yr
+    gzr, gbr = torch.autograd.grad(yr, [zz, bb], g)
+    y, gz, gb = ours()
+    assert torch.equal(y, yr) and torch.equal(gz, gzr)
+    ref = (g.double() * (yr.double() > 0) if relu else g.double()).sum((0, 2, 3))
+    assert bool(((gb.double() - ref).abs() <= ref.abs() * 2.0 ** -8 + 1e-6).all())
+    assert torch.equal(gb, gb.to(torch.bfloat16).float())
+    y2, gz2, gb2 = ours()
+    assert torch.equal(gb, gb2) and torch.equal(gz, gz2)

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--amp", default="bf16")
     ap.add_argument("--deterministic", type=int, default=0, help="MIOpen deterministic algorithms only")
+    ap.add_argument("--pose-streams", type=int, default=1, help="0: the pose network on the main stream")
+    ap.add_argument("--first", default="graph", choices=["graph", "eager"], help="the first run of the step")
     ap.add_argument("--second", default="eager", choices=["eager", "graph", "fp32"],
                     help="what the replay is compared with: the eager step, or a second replay")
     a = ap.parse_args()
@@ -28,7 +30,8 @@ def main():
     Hf, Wf, B = 192, 640, a.batch
     torch.manual_seed(0)
     tr = Trainer(default_options(batch_size=B, height=Hf, width=Wf, weights_init="scratch", log_dir="/tmp/md2_diag",
-                                 frame_ids=[0, -1, 1], amp=a.amp, hip_graph=True), device=torch.device("cuda", 0))
+                                 frame_ids=[0, -1, 1], amp=a.amp, hip_graph=True,
+                                 pose_streams=a.pose_streams), device=torch.device("cuda", 0))
     batch = synthetic_batch(B, Hf, Wf, tr.opt.frame_ids, 4, seed=3, device="cuda", eight_bit=True)
     gen = torch.Generator().manual_seed(7)
     tr.noise_override = {s: torch.randn(*tr.hot.noise_shape(s), generator=gen).cuda() for s in range(4)}
@@ -40,7 +43,7 @@ def main():
     p0 = [p.detach().clone() for p in tr.nets.parameters()]
     b0 = [b.detach().clone() for b in tr.nets.buffers()]
     seed0 = tr.seed_tensor.clone()
-    _, lg = tr.train_step(batch)
+    _, lg = tr.train_step(batch) if a.first == "graph" else tr.eager_step(tr.static_inputs)
     torch.cuda.synchronize()
     pg = [p.detach().clone() for p in tr.nets.parameters()]
     gg = [None if p.grad is None else p.grad.detach().clone() for p in tr.nets.parameters()]
@@ -88,6 +91,25 @@ def main():
     num = sum(float((g - e).double().square().sum()) for g, e in zip(gg, ge) if g is not None and e is not None)
     den = sum(float(e.double().square().sum()) for g, e in zip(gg, ge) if g is not None and e is not None)
     print("grad rel-L2 over all params: %.3e" % (num / den) ** 0.5)
+    # every parameter whose gradient differs at all, in module order (the last one in
+    # forward order sits closest to the op that differs), and the autotune's bf16 choices
+    for i, n in enumerate(names):
+        if gg[i] is not None and ge[i] is not None and not torch.equal(gg[i], ge[i]):
+            print("differs %-48s rel-L2 %.3e  |first| %.3e |second| %.3e" % (
+                n, float((gg[i] - ge[i]).norm() / ge[i].norm().clamp_min(1e-30)), float(gg[i].norm()),
+                float(ge[i].norm())))
+            dd = (gg[i] - ge[i]).flatten()
+            nz = torch.nonzero(dd).flatten()
+            print("   %d of %d elements differ; at %s: %s vs %s" % (
+                nz.numel(), dd.numel(), nz[:6].tolist(), gg[i].flatten()[nz[:6]].tolist(),
+                ge[i].flatten()[nz[:6]].tolist()))
+            if gg[i].numel() <= 16:
+                print("   graph", gg[i].flatten().tolist())
+                print("   eager", ge[i].flatten().tolist())
+    from monodepth2_amd import conv_ops
+    for k, i in conv_ops._choice.items():
+        if k in conv_ops._names and k[0].endswith("bf16"):
+            print("choice", k, conv_ops._names[k][i], "nondet" if k in conv_ops._nondet else "")
 
 
 if __name__ == "__main__":
