@@ -203,6 +203,13 @@ class Trainer:
         # gradient averaging: DDP (hooks, overlapped with backward) for eager steps, flat
         # buckets + one RCCL all-reduce each (graph-capturable) for --hip_graph
         self.use_graph = bool(getattr(self.opt, "hip_graph", False))
+        if (self.use_graph and self.device.type == "cuda" and self._pose_stream is None
+                and os.environ.get("MD2_ALLOW_ONESTREAM_GRAPH", "0") != "1"):
+            # open bug: a captured step with the pose network on the main
+            # stream replays with non-finite gradients for some parameters after one or more
+            # replays (tools/onestream_graph_check.py; fp32 and bf16); the default two-stream
+            # capture is bitwise the eager step.  Refused rather than trained on silently.
+            raise ValueError("--hip_graph needs the pose network on its own stream (--pose_streams 1)")
         sync = getattr(self.opt, "grad_sync", "auto")
         if sync == "auto":
             sync = "flat" if self.use_graph else "ddp"
