@@ -19,11 +19,28 @@ def main():
     ap.add_argument("--pose-streams", type=int, default=0)
     ap.add_argument("--amp", default="none")
     ap.add_argument("--batch", type=int, default=2)
+    ap.add_argument("--quiet", type=int, default=0, help="replays without host-side work between them")
+    ap.add_argument("--between", default="none", choices=["none", "gpu", "host"],
+                    help="with --quiet: GPU allocations (parameter clones) or host allocations between replays")
     a = ap.parse_args()
     torch.manual_seed(0)
     tr = Trainer(default_options(batch_size=a.batch, height=64, width=128, weights_init="scratch",
                                  log_dir="/tmp/md2_os", frame_ids=[0, -1, 1], amp=a.amp, hip_graph=True,
                                  pose_streams=a.pose_streams), device=torch.device("cuda", 0))
+    if a.quiet:
+        batch = synthetic_batch(a.batch, 64, 128, tr.opt.frame_ids, 4, seed=3, device="cuda", eight_bit=True)
+        keep = []
+        for k in range(6):
+            tr.train_step(batch)
+            if a.between == "gpu":
+                keep.append([p.detach().clone() for p in tr.nets.parameters()])
+            elif a.between == "host":
+                keep.append([bytearray(4096) for _ in range(2000)] + [object() for _ in range(20000)])
+        torch.cuda.synchronize()
+        bad = [n for n, p in tr.nets.named_parameters() if p.grad is not None and not bool(torch.isfinite(p.grad).all())]
+        badp = [n for n, p in tr.nets.named_parameters() if not bool(torch.isfinite(p).all())]
+        print("quiet: %d non-finite grads %s; %d non-finite params" % (len(bad), bad[:20], len(badp)), flush=True)
+        return
     for k in range(4):
         batch = synthetic_batch(a.batch, 64, 128, tr.opt.frame_ids, 4, seed=3 + k, device="cuda", eight_bit=True)
         p0 = [p.detach().clone() for p in tr.nets.parameters()]

@@ -1,13 +1,9 @@
-# round 6: C5 graph replays — with the pose decoder's bf16 bias + ReLU on md2_bias_act_bwd
+# round 6: one-stream captured step — GPU vs host allocations between replays
 set -o pipefail
 OUT=gpurun_out/r6det
 mkdir -p $OUT
-one() {  # tag, env...
-  local tag=$1; shift
-  timeout -k 10 300 env "$@" python -u tools/c5_replay_diag.py --batch 32 --first graph --second graph > $OUT/$tag.txt 2>&1 || { tail -20 $OUT/$tag.txt; return 1; }
-  echo "== $tag $(grep 'rel-L2 over' $OUT/$tag.txt) $(grep '^differs' $OUT/$tag.txt | head -2 | cut -c1-60 | tr '\n' ' ')"
-}
-timeout -k 10 300 python -u -m pytest tests/test_decoder_gpu.py -x -q -k "bias_act" --timeout 200 --timeout-method thread > $OUT/u.log 2>&1 || { tail -30 $OUT/u.log; exit 1; }
-tail -1 $OUT/u.log
-one ba1 A=1 && one ba2 A=1 && one ba3 A=1 && one ba4 A=1 && one ba5 A=1 && one ba6 A=1 &&
-timeout -k 10 400 python -u -m pytest tests/test_trainer_gpu.py -x -q -k "bf16_full_resolution" --timeout 300 --timeout-method thread > $OUT/t.log 2>&1; tail -1 $OUT/t.log
+export MD2_ALLOW_ONESTREAM_GRAPH=1
+for bt in gpu host gpu host; do
+  timeout -k 10 300 python -u tools/onestream_graph_check.py --pose-streams 0 --amp none --quiet 1 --between $bt > $OUT/osb.txt 2>&1 || { tail -20 $OUT/osb.txt; exit 1; }
+  echo "$bt: $(grep '^quiet' $OUT/osb.txt | cut -c1-300)"
+done
