@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--quiet", type=int, default=0, help="replays without host-side work between them")
     ap.add_argument("--between", default="none", choices=["none", "gpu", "host"],
                     help="with --quiet: GPU allocations (parameter clones) or host allocations between replays")
+    ap.add_argument("--vary", type=int, default=0, help="with --quiet: a new batch every replay")
     a = ap.parse_args()
     torch.manual_seed(0)
     tr = Trainer(default_options(batch_size=a.batch, height=64, width=128, weights_init="scratch",
@@ -30,8 +31,10 @@ def main():
     if a.quiet:
         batch = synthetic_batch(a.batch, 64, 128, tr.opt.frame_ids, 4, seed=3, device="cuda", eight_bit=True)
         keep = []
+        batches = [synthetic_batch(a.batch, 64, 128, tr.opt.frame_ids, 4, seed=3 + k, device="cuda", eight_bit=True)
+                   for k in range(6)] if a.vary else [batch] * 6
         for k in range(6):
-            tr.train_step(batch)
+            tr.train_step(batches[k])
             if a.between == "gpu":
                 keep.append([p.detach().clone() for p in tr.nets.parameters()])
             elif a.between == "host":

@@ -1,9 +1,9 @@
-# round 6: one-stream captured step — GPU vs host allocations between replays
+# round 6: one-stream captured step — a new batch every replay
 set -o pipefail
 OUT=gpurun_out/r6det
 mkdir -p $OUT
 export MD2_ALLOW_ONESTREAM_GRAPH=1
-for bt in gpu host gpu host; do
-  timeout -k 10 300 python -u tools/onestream_graph_check.py --pose-streams 0 --amp none --quiet 1 --between $bt > $OUT/osb.txt 2>&1 || { tail -20 $OUT/osb.txt; exit 1; }
-  echo "$bt: $(grep '^quiet' $OUT/osb.txt | cut -c1-300)"
+for ps in 0 0 1; do
+  timeout -k 10 300 python -u tools/onestream_graph_check.py --pose-streams $ps --amp none --quiet 1 --vary 1 > $OUT/osv.txt 2>&1 || { tail -20 $OUT/osv.txt; exit 1; }
+  echo "pose_streams $ps vary: $(grep '^quiet' $OUT/osv.txt | cut -c1-400)"
 done
