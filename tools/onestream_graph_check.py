@@ -44,23 +44,32 @@ def main():
         badp = [n for n, p in tr.nets.named_parameters() if not bool(torch.isfinite(p).all())]
         print("quiet: %d non-finite grads %s; %d non-finite params" % (len(bad), bad[:20], len(badp)), flush=True)
         return
-    for k in range(4):
-        batch = synthetic_batch(a.batch, 64, 128, tr.opt.frame_ids, 4, seed=3 + k, device="cuda", eight_bit=True)
-        p0 = [p.detach().clone() for p in tr.nets.parameters()]
+    parts = set(os.environ.get("MD2_OS_PARTS", "batch,clone,norm").split(","))
+    batch = synthetic_batch(a.batch, 64, 128, tr.opt.frame_ids, 4, seed=3, device="cuda", eight_bit=True)
+    for k in range(6):
+        if "batch" in parts:
+            batch = synthetic_batch(a.batch, 64, 128, tr.opt.frame_ids, 4, seed=3 + k, device="cuda", eight_bit=True)
+        p0 = [p.detach().clone() for p in tr.nets.parameters()] if "clone" in parts else \
+            [p.detach() for p in tr.nets.parameters()]
         _, l = tr.train_step(batch)
         torch.cuda.synchronize()
+        if "norm" not in parts:
+            continue
         moved = sum(int(not torch.equal(p0[i], p.detach())) for i, p in enumerate(tr.nets.parameters()))
         gn = sum(float(p.grad.float().norm()) ** 2 for p in tr.nets.parameters() if p.grad is not None) ** 0.5
         fin = all(bool(torch.isfinite(p).all()) for p in tr.nets.parameters())
         print("step %d loss %.9g params moved %d/%d grad norm %.4g params finite %s" % (
             k, float(l["loss"]), moved, len(p0), gn, fin), flush=True)
-        if k == 2:
+        if k == 5:
             for i, (n, p) in enumerate(tr.nets.named_parameters()):
                 bad = p.grad is not None and not bool(torch.isfinite(p.grad).all())
                 still = torch.equal(p0[i], p.detach())
                 if bad or still:
                     print("   %-55s grad finite %s  moved %s  grad ptr %x" % (
                         n, not bad, not still, p.grad.data_ptr() if p.grad is not None else 0), flush=True)
+
+    bad = [n for n, p in tr.nets.named_parameters() if p.grad is not None and not bool(torch.isfinite(p.grad).all())]
+    print("final: %d non-finite grads %s" % (len(bad), bad[:12]), flush=True)
 
 
 if __name__ == "__main__":
