@@ -69,30 +69,34 @@ def test_conv_input_folds_the_conv_bias(C, dtype, up, skip_ch):
     torch.testing.assert_close(gb, gbr, rtol=1e-4 if dtype == torch.float32 else 2e-2, atol=1e-3)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("up,skip_ch", [(False, 0), (True, 16)])
 @pytest.mark.parametrize("used", [(0, 1), (0,), (1,)])
-def test_conv_input_alias_sums_both_gradients(up, skip_ch, used):
+def test_conv_input_alias_sums_both_gradients(up, skip_ch, used, dtype):
     """conv_input(..., alias=True) -> (P, P'): the two consumers' gradients of the padded
     map are summed as the pad backward reads them (md2_decoder_pad_bwd2); grads w.r.t.
     x, skip and the folded bias match autograd's sum over the consumers."""
     torch.manual_seed(5)
     cl = torch.channels_last
-    x = torch.randn(2, 32, 12, 20, device="cuda").contiguous(memory_format=cl).requires_grad_(True)
+    x = torch.randn(2, 32, 12, 20, device="cuda").to(dtype).contiguous(memory_format=cl).requires_grad_(True)
     b = torch.randn(32, device="cuda", requires_grad=True)
     H, W = (24, 40) if up else (12, 20)
-    skip = (torch.randn(2, skip_ch, H, W, device="cuda").contiguous(memory_format=cl).requires_grad_(True)
+    skip = (torch.randn(2, skip_ch, H, W, device="cuda").to(dtype).contiguous(memory_format=cl).requires_grad_(True)
             if skip_ch else None)
     P, P2 = conv_input(x, skip, elu=True, upsample=up, nhwc=True, bias=b, alias=True)
     assert torch.equal(P, P2) and "ConvInput" in type(P2.grad_fn).__name__
-    gs = [torch.randn(P.shape, device="cuda").contiguous(memory_format=cl) for _ in range(2)]
+    gs = [torch.randn(P.shape, device="cuda").to(dtype).contiguous(memory_format=cl) for _ in range(2)]
     inputs = (x, b) + ((skip,) if skip is not None else ())
     got = torch.autograd.grad([(P, P2)[i] for i in used], inputs, [gs[i] for i in used])
     ref = conv_input(x, skip, elu=True, upsample=up, nhwc=True, bias=b)
     exp = torch.autograd.grad([ref] * len(used), inputs, [gs[i] for i in used])
-    torch.testing.assert_close(got[0], exp[0], rtol=1e-6, atol=1e-6)
-    torch.testing.assert_close(got[1], exp[1], rtol=1e-5, atol=1e-4)
+    # bf16: autograd rounds the two consumers' sum to bf16 before the pad backward, the
+    # fused path adds them in fp32 — one bf16 rounding apart
+    t0, t1 = ((1e-6, 1e-6), (1e-5, 1e-4)) if dtype == torch.float32 else ((2e-2, 2e-2), (2e-2, 2e-2))
+    torch.testing.assert_close(got[0].float(), exp[0].float(), rtol=t0[0], atol=t0[1])
+    torch.testing.assert_close(got[1], exp[1], rtol=t1[0], atol=t1[1] * (1 if dtype == torch.float32 else 50))
     if skip is not None:
-        torch.testing.assert_close(got[2], exp[2], rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(got[2].float(), exp[2].float(), rtol=t0[0], atol=t0[1])
 
 
 def test_conv_input_bf16_matches_eager():
