@@ -498,6 +498,109 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply8_kernel(const void* __r
     }
 }
 
+// The two reductions on eight channels per thread as well (bf16): Σx, Σx² and Σg', Σg'(x-μ)
+// per channel with the same block partial rows (two block_partials calls, one per
+// channel quad of the octet) — a different fixed order than the quad kernels (fp32
+// partials of twice as many pixels per block step), equally deterministic.
+template <bool UNUSED = false>
+__global__ void __launch_bounds__(kThreads) bn_stats8_kernel(const void* __restrict__ x, long long P, int C, int G,
+                                                             void* ws) {
+    const int Q8 = C / 8;
+    const Map m8 = {Q8, 1, kThreads / Q8};
+    const int NG = gridDim.y, grp = blockIdx.y;
+    const Work w = work(ws, G, C, NG);
+    x = (const char*)x + (size_t)grp * P * C * 2;
+    __shared__ float4 lds[2][kThreads];
+    const int q8 = threadIdx.x % Q8, pl = threadIdx.x / Q8;
+    float v[8], s[8], ss[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] = ss[e] = 0.f;
+    auto acc = [&]() {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            s[e] += v[e];
+            ss[e] += v[e] * v[e];
+        }
+    };
+    const long long stride = (long long)G * m8.PPB;
+    for (long long p = (long long)blockIdx.x * m8.PPB + pl; p < P; p += stride) {
+        ld8bf(x, p * C + 8 * q8, v);
+        acc();
+    }
+    block_partials(make_float4(s[0], s[1], s[2], s[3]), make_float4(ss[0], ss[1], ss[2], ss[3]), 2 * q8, pl, m8, C,
+                   NG * G, grp * G + blockIdx.x, w, lds);
+    block_partials(make_float4(s[4], s[5], s[6], s[7]), make_float4(ss[4], ss[5], ss[6], ss[7]), 2 * q8 + 1, pl, m8,
+                   C, NG * G, grp * G + blockIdx.x, w, lds);
+}
+
+template <bool RELU, bool MIN = false>
+__global__ void __launch_bounds__(kThreads) bn_bwd_reduce8_kernel(const void* __restrict__ x,
+                                                                  const void* __restrict__ y,
+                                                                  const void* __restrict__ g,
+                                                                  const void* __restrict__ g2,
+                                                                  const void* __restrict__ g3, long long P, int C,
+                                                                  int G, const float* __restrict__ smean, void* ws) {
+    const int Q8 = C / 8;
+    const Map m8 = {Q8, 1, kThreads / Q8};
+    const int NG = gridDim.y, grp = blockIdx.y;
+    const Work w = work(ws, G, C, NG);
+    const size_t base = (size_t)grp * P * C;
+    __shared__ float4 lds[2][kThreads];
+    const int q8 = threadIdx.x % Q8, pl = threadIdx.x / Q8;
+    float mu[8], s[8], sx[8];
+    ld8f(smean + grp * C + 8 * q8, mu);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] = sx[e] = 0.f;
+    const long long stride = (long long)G * m8.PPB;
+    for (long long p = (long long)blockIdx.x * m8.PPB + pl; p < P; p += stride) {
+        const size_t o = base + p * C + 8 * q8;   // element offset; o / 8 = octet index
+        float gv[8], v[8];
+        ld8bf(g, o, gv);
+        if (g2) {
+            float u[8];
+            ld8bf(g2, o, u);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) gv[e] += u[e];
+        }
+        if (g3) {
+            float u[8];
+            ld8bf(g3, o, u);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) gv[e] += u[e];
+        }
+        if (RELU) {
+            if constexpr (MIN) {
+                const uint32_t m = ((const uint16_t*)y)[o / 8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) gv[e] = ((m >> ((e & 3) + 8 * (e >> 2))) & 1u) ? gv[e] : 0.f;
+            } else {
+                float yv[8];
+                ld8bf(y, o, yv);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) gv[e] = yv[e] > 0.f ? gv[e] : 0.f;
+            }
+        }
+        ld8bf(x, o, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            s[e] += gv[e];
+            sx[e] += gv[e] * (v[e] - mu[e]);
+        }
+    }
+    block_partials(make_float4(s[0], s[1], s[2], s[3]), make_float4(sx[0], sx[1], sx[2], sx[3]), 2 * q8, pl, m8, C,
+                   NG * G, grp * G + blockIdx.x, w, lds);
+    block_partials(make_float4(s[4], s[5], s[6], s[7]), make_float4(sx[4], sx[5], sx[6], sx[7]), 2 * q8 + 1, pl, m8,
+                   C, NG * G, grp * G + blockIdx.x, w, lds);
+}
+
+bool reduce8_on() {   // A/B knob: MD2_BN_RED8=0 keeps the bf16 quad reductions
+    static const bool on = [] {
+        const char* e = getenv("MD2_BN_RED8");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 bool apply8_on() {   // A/B knob: MD2_BN_V8=0 keeps the bf16 quad elementwise kernels
     static const bool on = [] {
         const char* e = getenv("MD2_BN_V8");
@@ -537,7 +640,10 @@ void launch_fwd(const md2_bn_desc* d, const void* x, const float* gamma, const f
     const int NG = groups_of(d);
     const long long P = d->pixels / NG;   // per group
     const int C = d->channels, G = blocks_for_stats(P, C);
-    hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(G, NG), dim3(kThreads), 0, st, x, P, C, G, workspace);
+    if (sizeof(T) == 2 && C % 8 == 0 && C <= 8 * kThreads && reduce8_on())
+        hipLaunchKernelGGL(bn_stats8_kernel<>, dim3(G, NG), dim3(kThreads), 0, st, x, P, C, G, workspace);
+    else
+        hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(G, NG), dim3(kThreads), 0, st, x, P, C, G, workspace);
     hipLaunchKernelGGL(bn_stats_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, NG, d->eps, d->momentum,
                        running_mean, running_var, save_mean, save_invstd, workspace);
     const int n4g = (int)(P * C / 4);
@@ -569,6 +675,9 @@ void launch_bwd(const md2_bn_desc* d, const void* x, const void* y, const void* 
     // mask_in: y is the forward's ReLU mask (one byte per element quad), not y itself
     auto red = relu ? (mask_in ? bn_bwd_reduce_kernel<T, true, true> : bn_bwd_reduce_kernel<T, true>)
                     : bn_bwd_reduce_kernel<T, false>;
+    if (sizeof(T) == 2 && C % 8 == 0 && C <= 8 * kThreads && reduce8_on())
+        red = relu ? (mask_in ? bn_bwd_reduce8_kernel<true, true> : bn_bwd_reduce8_kernel<true>)
+                   : bn_bwd_reduce8_kernel<false>;
     hipLaunchKernelGGL(red, dim3(G, NG), dim3(kThreads), 0, st, x, y, grad_y, grad_y2, grad_y3, P, C, G, save_mean,
                        workspace);
     hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(C), dim3(kThreads), 0, st, P, C, G, NG, gamma, save_invstd,
