@@ -503,3 +503,14 @@ def test_resnet50_1024x320_losses_match_oracle():
     for s in range(4):
         assert abs(float(losses[f"loss/{s}"]) - float(ref[f"loss/{s}"])) < 1e-5, s
     assert abs(float(losses["loss"]) - float(ref["loss"])) < 1e-5
+
+
+def test_hip_graph_needs_the_pose_stream(monkeypatch):
+    """A captured step with the pose network on the main stream (--pose_streams 0) is
+    refused when the Trainer is built, before any capture (open bug: its replays produce non-finite gradients,
+    DESIGN.md §6; tools/onestream_graph_check.py reproduces it)."""
+    from monodepth2_amd.trainer import Trainer
+    monkeypatch.delenv("MD2_ALLOW_ONESTREAM_GRAPH", raising=False)
+    with pytest.raises(ValueError, match="pose_streams"):
+        Trainer(default_options(batch_size=2, height=64, width=128, weights_init="scratch", log_dir="/tmp/md2_test",
+                                hip_graph=True, pose_streams=0), device=torch.device("cuda", 0))
