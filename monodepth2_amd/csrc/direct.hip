@@ -21,6 +21,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -199,36 +201,54 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_kernel(const float* __re
                                   x6_hi16x2(c[pl][4], c[pl][5]), x6_hi16x2(c[pl][6], c[pl][7])});
         }
     const int ntiles = B * tiles_r * tiles_c;
+    // the tile's patch is loaded into registers one tile ahead (issued before the current
+    // tile's MFMAs, so the loads' latency hides behind them), then split into LDS
+    constexpr int NL = (NQ + kThreads - 1) / kThreads;
+    using RegT = typename std::conditional<BF, uint2, float4>::type;
+    RegT rg[NL];
+    auto fetch = [&](int t) {
+        const int tcb = t % tiles_c, rest = t / tiles_c, trb = rest % tiles_r, b = rest / tiles_r;
+        const int oh0 = trb * kXR, ow0 = tcb * kXC;
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            const int i = tid + k * kThreads;
+            const int pix = i / (CIN / 4), q = i - pix * (CIN / 4), pr = pix / PC, pc = pix - pr * PC;
+            const int ih = oh0 - pad + pr, iw = ow0 - pad + pc;
+            const bool in = i < NQ && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+            const size_t o = ((size_t)(b * H + ih) * W + iw) * (CIN / 4) + q;
+            if constexpr (BF) rg[k] = in ? ((const uint2*)x)[o] : uint2{0u, 0u};
+            else rg[k] = in ? ((const float4*)x)[o] : float4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    if (blockIdx.x < ntiles) fetch(blockIdx.x);
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int tcb = t % tiles_c, rest = t / tiles_c, trb = rest % tiles_r, b = rest / tiles_r;
         const int oh0 = trb * kXR, ow0 = tcb * kXC;
         // stage the patch: float4 i = (pixel, channel quad), split into three planes
-        for (int i = tid; i < NQ; i += kThreads) {
-            const int pix = i / (CIN / 4), q = i - pix * (CIN / 4), pr = pix / PC, pc = pix - pr * PC;
-            const int ih = oh0 - pad + pr, iw = ow0 - pad + pc;
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            const int i = tid + k * kThreads;
+            if (NQ % kThreads && i >= NQ) break;
             if constexpr (BF) {
-                uint2 u = {0u, 0u};
-                if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-                    u = ((const uint2*)x)[((size_t)(b * H + ih) * W + iw) * (CIN / 4) + q];
-                patch[0][i] = u32x2{u.x, u.y};
-                continue;
-            }
-            float4 v = {0.f, 0.f, 0.f, 0.f};
-            if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-                v = ((const float4*)x)[((size_t)(b * H + ih) * W + iw) * (CIN / 4) + q];
-            const float e[4] = {v.x, v.y, v.z, v.w};
-            float c[3][4];
+                patch[0][i] = u32x2{rg[k].x, rg[k].y};
+            } else {
+                const float4 v = rg[k];
+                const float e[4] = {v.x, v.y, v.z, v.w};
+                float c[3][4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float a0 = x6_trunc16(e[j]), r1 = e[j] - a0, a1 = x6_trunc16(r1);
-                c[0][j] = a0;
-                c[1][j] = a1;
-                c[2][j] = r1 - a1;
-            }
+                for (int j = 0; j < 4; ++j) {
+                    const float a0 = x6_trunc16(e[j]), r1 = e[j] - a0, a1 = x6_trunc16(r1);
+                    c[0][j] = a0;
+                    c[1][j] = a1;
+                    c[2][j] = r1 - a1;
+                }
 #pragma unroll
-            for (int pl = 0; pl < NPL; ++pl) patch[pl][i] = u32x2{x6_hi16x2(c[pl][0], c[pl][1]), x6_hi16x2(c[pl][2], c[pl][3])};
+                for (int pl = 0; pl < NPL; ++pl)
+                    patch[pl][i] = u32x2{x6_hi16x2(c[pl][0], c[pl][1]), x6_hi16x2(c[pl][2], c[pl][3])};
+            }
         }
         __syncthreads();
+        if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x);   // next tile's loads in flight
         const int oh = oh0 + wid;
         const __bf16* P0 = (const __bf16*)patch[0];
         const __bf16* P1 = (const __bf16*)patch[BF ? 0 : 1];
@@ -349,36 +369,56 @@ __global__ __launch_bounds__(kThreads, 2) void conv3_x6_wgrad_kernel(const float
     };
     auto put_bf = [&](__bf16* base, int off, uint2 u) { *(u32x2*)(base + off) = u32x2{u.x, u.y}; };
     const int ntiles = B * tiles_r * tiles_c;
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    // the next tile's input patch and output gradient are loaded into registers while
+    // the current tile's MFMAs run (as conv3_x6_kernel), then split / copied into LDS
+    constexpr int NX = PR * PC * CIN / 4, NG4 = GE / 4;
+    constexpr int LX = (NX + kThreads - 1) / kThreads, LG = (NG4 + kThreads - 1) / kThreads;
+    using RegT = typename std::conditional<BF, uint2, float4>::type;
+    RegT rx[LX], rgy[LG];
+    auto fetch = [&](int t) {
         const int tcb = t % tiles_c, rest = t / tiles_c, trb = rest % tiles_r, b = rest / tiles_r;
         const int oh0 = trb * TR, ow0 = tcb * kXC;
-        for (int i = tid; i < PR * PC * CIN / 4; i += kThreads) {   // input patch, zeros outside the image
+#pragma unroll
+        for (int k = 0; k < LX; ++k) {   // input patch, zeros outside the image
+            const int i = tid + k * kThreads;
             const int pix = i / (CIN / 4), q4 = i - pix * (CIN / 4), pr = pix / PC, pc = pix - pr * PC;
             const int ih = oh0 - pad + pr, iw = ow0 - pad + pc;
-            const bool in = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+            const bool in = i < NX && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
             const size_t o = ((size_t)(b * H + ih) * W + iw) * (CIN / 4) + q4;
-            if constexpr (BF) {
-                put_bf(&xs[0][0], wg_off<CIN>(pix, q4), in ? ((const uint2*)x)[o] : uint2{0u, 0u});
-            } else {
-                float4 v = {0.f, 0.f, 0.f, 0.f};
-                if (in) v = ((const float4*)x)[o];
-                put(&xs[0][0], XE, wg_off<CIN>(pix, q4), v);
-            }
+            if constexpr (BF) rx[k] = in ? ((const uint2*)x)[o] : uint2{0u, 0u};
+            else rx[k] = in ? ((const float4*)x)[o] : float4{0.f, 0.f, 0.f, 0.f};
         }
-        for (int i = tid; i < GE / 4; i += kThreads) {   // output gradient, zeros past the output
+#pragma unroll
+        for (int k = 0; k < LG; ++k) {   // output gradient, zeros past the output
+            const int i = tid + k * kThreads;
             const int pix = i >> 2, q4 = i & 3, pr = pix / kXC, pc = pix - pr * kXC;
             const int oh = oh0 + pr, ow = ow0 + pc;
-            const bool in = oh < Ho && ow < Wo;
+            const bool in = i < NG4 && oh < Ho && ow < Wo;
             const size_t o = ((size_t)(b * Ho + oh) * Wo + ow) * 4 + q4;
-            if constexpr (BF) {
-                put_bf(&gs[0][0], wg_off<16>(pix, q4), in ? ((const uint2*)gy)[o] : uint2{0u, 0u});
-            } else {
-                float4 v = {0.f, 0.f, 0.f, 0.f};
-                if (in) v = ((const float4*)gy)[o];
-                put(&gs[0][0], GE, wg_off<16>(pix, q4), v);
-            }
+            if constexpr (BF) rgy[k] = in ? ((const uint2*)gy)[o] : uint2{0u, 0u};
+            else rgy[k] = in ? ((const float4*)gy)[o] : float4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    if (blockIdx.x < ntiles) fetch(blockIdx.x);
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+#pragma unroll
+        for (int k = 0; k < LX; ++k) {
+            const int i = tid + k * kThreads;
+            if (NX % kThreads && i >= NX) break;
+            const int pix = i / (CIN / 4), q4 = i - pix * (CIN / 4);
+            if constexpr (BF) put_bf(&xs[0][0], wg_off<CIN>(pix, q4), rx[k]);
+            else put(&xs[0][0], XE, wg_off<CIN>(pix, q4), rx[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < LG; ++k) {
+            const int i = tid + k * kThreads;
+            if (NG4 % kThreads && i >= NG4) break;
+            const int pix = i >> 2, q4 = i & 3;
+            if constexpr (BF) put_bf(&gs[0][0], wg_off<16>(pix, q4), rgy[k]);
+            else put(&gs[0][0], GE, wg_off<16>(pix, q4), rgy[k]);
         }
         __syncthreads();
+        if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x);
         const int wrow = TR == 4 ? wid : wid >> 1, ks0 = TR == 4 ? 0 : wid & 1;
 #pragma unroll
         for (int kk = 0; kk < KSW; ++kk) {
@@ -606,10 +646,13 @@ int md2_conv_direct(const md2_conv_desc* d, const float* x, const float* wk, flo
     if (d->flags & MD2_CONV_X6) {
         const int tr = (Ho + kXR - 1) / kXR, tc = (Wo + kXC - 1) / kXC;
         const long long nt = (long long)d->batch * tr * tc;
-        // persistent: as many blocks as fit on a CU (LDS / VGPRs: 4 for 16 -> 16, else 2)
-        const long long cap = 256ll * ((ci == 16 && co == 16) ? 4 : 2);
-        const dim3 g2((unsigned)(nt < cap ? nt : cap));
         const bool bf = (d->flags & MD2_CONV_BF16) != 0;   // bf16 x / y (config C5)
+        // persistent: as many blocks as are resident per CU (the kernels' occupancy with
+        // the next tile's patch held in registers: fp32 3 / 2 / 2, bf16 4 / 3 / 4 for
+        // 16->16 / 32->16 / 16->32; a fourth fp32 16->16 block would only queue)
+        const int per_cu = bf ? ((ci == 32) ? 3 : 4) : ((ci == 16 && co == 16) ? 3 : 2);
+        const long long cap = 256ll * per_cu;
+        const dim3 g2((unsigned)(nt < cap ? nt : cap));
         void (*k)(const float*, const float*, float*, int, int, int, int, int, int, int, int) =
             (ci == 16 && co == 16)   ? (bf ? conv3_x6_kernel<16, 16, true> : conv3_x6_kernel<16, 16>)
             : (ci == 32 && co == 16) ? (bf ? conv3_x6_kernel<32, 16, true> : conv3_x6_kernel<32, 16>)
