@@ -1,6 +1,6 @@
 # kernel trace of config C5's eager step (bf16 autocast, B=32)
 set -o pipefail
-OUT=gpurun_out/r6c5t5
+OUT=gpurun_out/r6c5t6
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o c5 --output-format csv \
