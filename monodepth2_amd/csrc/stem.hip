@@ -389,6 +389,133 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
 #pragma unroll
         for (int ni = 0; ni < NB; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int H = a.H, W = a.W;
+    auto compute = [&]() {
+#pragma unroll
+        for (int kk = 0; kk < kTSeg / 32; ++kk) {
+            const int px = 32 * kk + 8 * g16 + q;   // this lane's pixel of the tr reads (and + 4)
+            bf16x8 fb[NB][NPL];
+#pragma unroll
+            for (int ni = 0; ni < NB; ++ni) {
+                // n0 = kw·CP + ci0: element (2 px + kw)·CP + ci0 = 2 px·CP + n0 of the row
+                const int n0 = 16 * ni + 4 * p4;
+                const int olo = (kh * kTCols + 2 * px) * CP + n0;
+                const int ohi = (kh * kTCols + 2 * (px + 4)) * CP + n0;
+#pragma unroll
+                for (int pl = 0; pl < NPL; ++pl) fb[ni][pl] = tr_pair(&xs[pl][olo], &xs[pl][ohi]);
+            }
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                bf16x8 fa[NPL];
+                const int glo = tr_goff(px, 4 * mi + p4), ghi = tr_goff(px + 4, 4 * mi + p4);
+#pragma unroll
+                for (int pl = 0; pl < NPL; ++pl) fa[pl] = tr_pair(&gs[pl][glo], &gs[pl][ghi]);
+#pragma unroll
+                for (int ni = 0; ni < NB; ++ni) {
+                    if constexpr (BF) {
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[ni][0], acc[mi][ni], 0, 0, 0);
+                        continue;
+                    }
+                    f32x4 c = acc[mi][ni];
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fb[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[ni][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[ni][2], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[ni][1], c, 0, 0, 0);
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[ni][0], c, 0, 0, 0);
+                }
+            }
+        }
+    };
+    if constexpr (BF) {
+        // bf16: the next chunk's dy and input rows are loaded into registers while this
+        // chunk's MFMAs run (stage -> barrier -> MFMAs -> barrier per chunk left the
+        // MFMAs waiting on every chunk's loads), then stored to LDS as the loop above does
+        constexpr int NGT = kTSeg * 16, LG = (NGT + kTThreads - 1) / kTThreads;
+        constexpr int NXT = CP == 4 ? 7 * (2 * kTSeg + 6) : 7 * ((2 * kTSeg + 6) * CP / 4);
+        constexpr int LX = (NXT + kTThreads - 1) / kTThreads;
+        uint2 rg[LG], rx[LX];
+        auto fetch = [&](int tt) {
+            const int per_img = a.nseg * a.Ho, b = tt / per_img, rem = tt - b * per_img;
+            const int seg = rem / a.Ho, oh = rem - seg * a.Ho;
+            const int ow0 = seg * kTSeg, iw0 = 2 * ow0 - 3;
+#pragma unroll
+            for (int k = 0; k < LG; ++k) {
+                const int i = tid + k * kTThreads;
+                const int px = i >> 4, co4 = i & 15, ow = ow0 + px;
+                uint2 v = {0u, 0u};
+                if (i < NGT && ow < a.Wo) v = *(const uint2*)(gh + ((size_t)(b * a.Ho + oh) * a.Wo + ow) * kCo + 4 * co4);
+                rg[k] = v;
+            }
+#pragma unroll
+            for (int k = 0; k < LX; ++k) {
+                const int e = tid + k * kTThreads;
+                uint32_t h0 = 0u, h1 = 0u;
+                if (e < NXT) {
+                    if constexpr (CP == 4) {
+                        const int r = e / (2 * kTSeg + 6), col = e - r * (2 * kTSeg + 6);
+                        const int ih = 2 * oh - 3 + r, iw = iw0 + col;
+                        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
+                            const uint16_t* px = xh + ((size_t)(b * H + ih) * W + iw) * C;
+                            uint32_t hh[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                            for (int ci = 0; ci < C; ++ci) hh[ci] = px[ci];
+                            h0 = hh[0] | (hh[1] << 16);
+                            h1 = hh[2] | (hh[3] << 16);
+                        }
+                    } else {
+                        constexpr int RQ = (2 * kTSeg + 6) * CP / 4;
+                        const int r = e / RQ, kq = 4 * (e - r * RQ);
+                        const int ih = 2 * oh - 3 + r;
+                        if ((unsigned)ih < (unsigned)H) {
+                            const long long f0 = (long long)iw0 * C + kq;
+                            const uint16_t* row = xh + (size_t)(b * H + ih) * W * C;
+                            if (f0 >= 0 && f0 + 4 <= (long long)W * C) {
+                                h0 = *(const uint32_t*)(row + f0);
+                                h1 = *(const uint32_t*)(row + f0 + 2);
+                            } else {
+                                uint32_t hh[2] = {0u, 0u};
+#pragma unroll
+                                for (int q2 = 0; q2 < 4; ++q2)
+                                    if (f0 + q2 >= 0 && f0 + q2 < (long long)W * C)
+                                        hh[q2 / 2] |= (uint32_t)row[f0 + q2] << (16 * (q2 & 1));
+                                h0 = hh[0];
+                                h1 = hh[1];
+                            }
+                        }
+                    }
+                }
+                rx[k] = uint2{h0, h1};
+            }
+        };
+        if (n > 0) fetch(t0);
+        for (int t = 0; t < n; ++t) {
+#pragma unroll
+            for (int k = 0; k < LG; ++k) {
+                const int i = tid + k * kTThreads;
+                if (NGT % kTThreads && i >= NGT) break;
+                *(u32x2*)&gs[0][tr_goff(i >> 4, i & 15)] = u32x2{rg[k].x, rg[k].y};
+            }
+#pragma unroll
+            for (int k = 0; k < LX; ++k) {
+                const int e = tid + k * kTThreads;
+                if (NXT % kTThreads && e >= NXT) break;
+                int o;
+                if constexpr (CP == 4) {
+                    const int r = e / (2 * kTSeg + 6), col = e - r * (2 * kTSeg + 6);
+                    o = (r * kTCols + col) * CP;
+                } else {
+                    constexpr int RQ = (2 * kTSeg + 6) * CP / 4;
+                    const int r = e / RQ;
+                    o = r * kTCols * CP + 4 * (e - r * RQ);
+                }
+                *(u32x2*)&xs[0][o] = u32x2{rx[k].x, rx[k].y};
+            }
+            __syncthreads();
+            if (t + 1 < n) fetch(t0 + t + 1);
+            compute();
+            __syncthreads();
+        }
+    } else {
     for (int t = 0; t < n; ++t) {
         // chunks column-major within an image (oh fastest, then the 64-pixel segment): a
         // block's consecutive chunks share 5 of their 7 input rows, so its working set in
@@ -545,6 +672,7 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
             }
         }
         __syncthreads();   // restaged next chunk
+    }
     }
     // D[row = co = 16 mi + 4 g16 + e][col = n = 16 ni + lane & 15], n = kw·CP + ci
 #pragma unroll
