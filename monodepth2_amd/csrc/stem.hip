@@ -31,6 +31,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <stdint.h>
 
 #include <algorithm>
@@ -364,7 +366,7 @@ __device__ __forceinline__ bf16x8 tr_pair(const __bf16* lo, const __bf16* hi) {
 }
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int C, bool BF = false>
+template <int C, bool BF = false, bool PF = BF>
 __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs a) {
     // CP: channels per staged column — 3 padded to 4 (a column pair is then 8-byte
     // aligned for the tr read); 6 unpadded (24-byte column pairs are 8-byte aligned, a
@@ -426,14 +428,30 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
             }
         }
     };
-    if constexpr (BF) {
-        // bf16: the next chunk's dy and input rows are loaded into registers while this
+    if constexpr (PF) {
+        // PF: the next chunk's dy and input rows are loaded into registers while this
         // chunk's MFMAs run (stage -> barrier -> MFMAs -> barrier per chunk left the
-        // MFMAs waiting on every chunk's loads), then stored to LDS as the loop above does
+        // MFMAs waiting on every chunk's loads), then stored to LDS (fp32: split into the
+        // three planes) as the loop below does
         constexpr int NGT = kTSeg * 16, LG = (NGT + kTThreads - 1) / kTThreads;
         constexpr int NXT = CP == 4 ? 7 * (2 * kTSeg + 6) : 7 * ((2 * kTSeg + 6) * CP / 4);
         constexpr int LX = (NXT + kTThreads - 1) / kTThreads;
-        uint2 rg[LG], rx[LX];
+        using RT = typename std::conditional<BF, uint2, float4>::type;
+        RT rg[LG], rx[LX];
+        auto put3 = [&](__bf16* base, int stride, int o, float4 v) {   // three exact planes
+            const float e[4] = {v.x, v.y, v.z, v.w};
+            float c[3][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float a0 = trunc16(e[j]), r1 = e[j] - a0, a1 = trunc16(r1);
+                c[0][j] = a0;
+                c[1][j] = a1;
+                c[2][j] = r1 - a1;
+            }
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                *(u32x2*)(base + pl * stride + o) = u32x2{hi16x2(c[pl][0], c[pl][1]), hi16x2(c[pl][2], c[pl][3])};
+        };
         auto fetch = [&](int tt) {
             const int per_img = a.nseg * a.Ho, b = tt / per_img, rem = tt - b * per_img;
             const int seg = rem / a.Ho, oh = rem - seg * a.Ho;
@@ -442,10 +460,11 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
             for (int k = 0; k < LG; ++k) {
                 const int i = tid + k * kTThreads;
                 const int px = i >> 4, co4 = i & 15, ow = ow0 + px;
-                uint2 v = {0u, 0u};
-                if (i < NGT && ow < a.Wo) v = *(const uint2*)(gh + ((size_t)(b * a.Ho + oh) * a.Wo + ow) * kCo + 4 * co4);
-                rg[k] = v;
+                const size_t go = ((size_t)(b * a.Ho + oh) * a.Wo + ow) * kCo + 4 * co4;
+                if constexpr (BF) rg[k] = (i < NGT && ow < a.Wo) ? *(const uint2*)(gh + go) : uint2{0u, 0u};
+                else rg[k] = (i < NGT && ow < a.Wo) ? *(const float4*)(a.gy + go) : float4{0.f, 0.f, 0.f, 0.f};
             }
+            if constexpr (BF) {
 #pragma unroll
             for (int k = 0; k < LX; ++k) {
                 const int e = tid + k * kTThreads;
@@ -486,6 +505,41 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
                 }
                 rx[k] = uint2{h0, h1};
             }
+            } else {
+#pragma unroll
+            for (int k = 0; k < LX; ++k) {
+                const int e = tid + k * kTThreads;
+                float v[4] = {0.f, 0.f, 0.f, 0.f};
+                if (e < NXT) {
+                    if constexpr (CP == 4) {
+                        const int r = e / (2 * kTSeg + 6), col = e - r * (2 * kTSeg + 6);
+                        const int ih = 2 * oh - 3 + r, iw = iw0 + col;
+                        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
+                            const float* px = a.x + ((size_t)(b * H + ih) * W + iw) * C;
+#pragma unroll
+                            for (int ci = 0; ci < C; ++ci) v[ci] = px[ci];
+                        }
+                    } else {
+                        constexpr int RQ = (2 * kTSeg + 6) * CP / 4;
+                        const int r = e / RQ, kq = 4 * (e - r * RQ);
+                        const int ih = 2 * oh - 3 + r;
+                        if ((unsigned)ih < (unsigned)H) {
+                            const long long f0 = (long long)iw0 * C + kq;
+                            const float* row = a.x + (size_t)(b * H + ih) * W * C;
+                            if (f0 >= 0 && f0 + 4 <= (long long)W * C) {
+                                const float4 q4 = *(const float4*)(row + f0);
+                                v[0] = q4.x; v[1] = q4.y; v[2] = q4.z; v[3] = q4.w;
+                            } else {
+#pragma unroll
+                                for (int q2 = 0; q2 < 4; ++q2)
+                                    if (f0 + q2 >= 0 && f0 + q2 < (long long)W * C) v[q2] = row[f0 + q2];
+                            }
+                        }
+                    }
+                }
+                rx[k] = float4{v[0], v[1], v[2], v[3]};
+            }
+            }
         };
         if (n > 0) fetch(t0);
         for (int t = 0; t < n; ++t) {
@@ -493,7 +547,8 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
             for (int k = 0; k < LG; ++k) {
                 const int i = tid + k * kTThreads;
                 if (NGT % kTThreads && i >= NGT) break;
-                *(u32x2*)&gs[0][tr_goff(i >> 4, i & 15)] = u32x2{rg[k].x, rg[k].y};
+                if constexpr (BF) *(u32x2*)&gs[0][tr_goff(i >> 4, i & 15)] = u32x2{rg[k].x, rg[k].y};
+                else put3(&gs[0][0], GE, tr_goff(i >> 4, i & 15), rg[k]);
             }
 #pragma unroll
             for (int k = 0; k < LX; ++k) {
@@ -508,7 +563,8 @@ __global__ __launch_bounds__(kTThreads, 2) void stem_x6_wgrad_tr_kernel(StemArgs
                     const int r = e / RQ;
                     o = r * kTCols * CP + 4 * (e - r * RQ);
                 }
-                *(u32x2*)&xs[0][o] = u32x2{rx[k].x, rx[k].y};
+                if constexpr (BF) *(u32x2*)&xs[0][o] = u32x2{rx[k].x, rx[k].y};
+                else put3(&xs[0][0], XE, o, rx[k]);
             }
             __syncthreads();
             if (t + 1 < n) fetch(t0 + t + 1);
@@ -1033,8 +1089,15 @@ int md2_stem_wgrad(const md2_stem_desc* d, const float* x, const float* grad_y, 
     const hipStream_t st = (hipStream_t)stream;
     if (tr) {
         const bool bf = (d->flags & MD2_STEM_BF16) != 0;
-        void (*k)(StemArgs) = a.C == 3 ? (bf ? stem_x6_wgrad_tr_kernel<3, true> : stem_x6_wgrad_tr_kernel<3>)
-                                       : (bf ? stem_x6_wgrad_tr_kernel<6, true> : stem_x6_wgrad_tr_kernel<6>);
+        static const bool pf32 = [] {   // A/B knob: MD2_STEM_PF32=1 prefetches in the fp32 form too
+            const char* e = getenv("MD2_STEM_PF32");
+            return e && e[0] == '1';
+        }();
+        void (*k)(StemArgs) =
+            a.C == 3 ? (bf ? stem_x6_wgrad_tr_kernel<3, true>
+                           : (pf32 ? stem_x6_wgrad_tr_kernel<3, false, true> : stem_x6_wgrad_tr_kernel<3>))
+                     : (bf ? stem_x6_wgrad_tr_kernel<6, true>
+                           : (pf32 ? stem_x6_wgrad_tr_kernel<6, false, true> : stem_x6_wgrad_tr_kernel<6>));
         hipLaunchKernelGGL(k, dim3(a.splits), dim3(kTThreads), 0, st, a);
     } else {
         void (*k)(StemArgs) =
