@@ -1,6 +1,6 @@
 # round-6 final tree: GPU suite, smoke, default bench line, C5 / C3 / C4 lines
 set -o pipefail
-OUT=gpurun_out/r6f4
+OUT=gpurun_out/r6f5
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
 tail -1 $OUT/gpu_tests.log
